@@ -1,0 +1,239 @@
+"""eds-bwt_amd — MI355X-native EDS-BWT backward search (host side, Python).
+
+Python mirror of the reference's MOVE_EDSBWTSearch path (riccardo-nozza/EDS-BWT):
+
+* :class:`MoveEDSBWT` mirrors ``MOVE_EDSBWT::MOVE_EDSBWT(base, patterns)``
+  (MOVE_EDSBWTSearch.cpp:23-176): load the index, search every line of the pattern
+  file, write ``<patterns>output_M_LF.csv`` and keep ``count_found`` /
+  ``count_not_found``.
+* :class:`Index` is the batch API over the C ABI of ``include/edsbwt.h``
+  (``libedsbwt.so``, hand-written gfx950 kernels).
+
+Everything computes on the GPU through ``libedsbwt.so``; there is no CPU fallback.
+A missing or unloadable library raises :class:`EdsBwtError`.  The package directory
+name contains a hyphen, so import it with ``importlib.import_module("eds-bwt_amd")``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import time
+from typing import Iterable, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD_DIR = os.path.join(_HERE, "_build")
+LIB_PATH = os.path.join(BUILD_DIR, "libedsbwt.so")
+
+COUNT_ONLY = 0x1
+LOCATE = 0x2
+LOCATE_TABLE = 0x4
+PROFILE = 0x8
+
+OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
+CSV_HEADER = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"  # MOVE_EDSBWTSearch.cpp:59 (note the trailing space)
+
+
+class EdsBwtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"edsbwt error {code}: {msg}")
+        self.code = code
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("n_rows", ctypes.c_uint64), ("n_words", ctypes.c_uint64), ("n_segments", ctypes.c_uint64),
+                ("sigma", ctypes.c_uint32), ("alphabet", ctypes.c_uint8 * 16), ("device_bytes", ctypes.c_uint64)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("patterns", ctypes.c_uint64), ("found", ctypes.c_uint64), ("not_found", ctypes.c_uint64),
+                ("occurrences", ctypes.c_uint64), ("depths", ctypes.c_uint64), ("trie_nodes", ctypes.c_uint64),
+                ("intervals_stepped", ctypes.c_uint64), ("link_hash_rows", ctypes.c_uint64),
+                ("link_ranges", ctypes.c_uint64), ("locate_lf_steps", ctypes.c_uint64), ("ms_total", ctypes.c_double),
+                ("ms_kernel", ctypes.c_double * 16), ("launches_kernel", ctypes.c_uint64 * 16),
+                ("bytes_kernel", ctypes.c_uint64 * 16)]
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libedsbwt.so (built in-tree by __graft_entry__.build()); raise if absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise EdsBwtError(-4, f"{LIB_PATH} not built: run __graft_entry__.build() (make -C eds-bwt_amd)")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    L.edsbwt_index_open.argtypes = [ctypes.c_char_p, i32, u32, ctypes.POINTER(vp)]
+    L.edsbwt_index_open.restype = i32
+    L.edsbwt_index_close.argtypes = [vp]
+    L.edsbwt_index_close.restype = None
+    L.edsbwt_index_get_info.argtypes = [vp, ctypes.POINTER(_Info)]
+    L.edsbwt_index_get_info.restype = i32
+    L.edsbwt_search.argtypes = [vp, vp, vp, u64, u32, u32, vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
+    L.edsbwt_search.restype = i32
+    L.edsbwt_search_device.argtypes = [vp, vp, vp, u64, u32, u32, vp, ctypes.POINTER(vp), ctypes.POINTER(u64), vp]
+    L.edsbwt_search_device.restype = i32
+    L.edsbwt_occ_free.argtypes = [vp]
+    L.edsbwt_occ_free.restype = None
+    L.edsbwt_last_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
+    L.edsbwt_last_stats.restype = i32
+    L.edsbwt_kernel_name.argtypes = [i32]
+    L.edsbwt_kernel_name.restype = ctypes.c_char_p
+    L.edsbwt_format_csv.argtypes = [vp, u64, vp, u64, i32]
+    L.edsbwt_format_csv.restype = u64
+    L.edsbwt_last_error.argtypes = []
+    L.edsbwt_last_error.restype = ctypes.c_char_p
+    L.edsbwt_abi_version.argtypes = []
+    L.edsbwt_abi_version.restype = i32
+    _LIB = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise EdsBwtError(rc, lib().edsbwt_last_error().decode(errors="replace"))
+
+
+def pack_patterns(patterns: Iterable[bytes | str]) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate patterns into (bytes u8[], offsets u64[npat+1])."""
+    pats = [p.encode() if isinstance(p, str) else bytes(p) for p in patterns]
+    offs = np.zeros(len(pats) + 1, dtype=np.uint64)
+    if pats:
+        offs[1:] = np.cumsum([len(p) for p in pats], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(pats), dtype=np.uint8) if pats else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(buf), offs
+
+
+def read_pattern_file(path: str) -> tuple[np.ndarray, np.ndarray]:
+    """std::getline semantics (MOVE_EDSBWTSearch.cpp:111): split at '\\n', keep '\\r',
+    a last line without '\\n' counts, a trailing '\\n' does not open a new line."""
+    data = np.fromfile(path, dtype=np.uint8)
+    nl = np.flatnonzero(data == 10)
+    starts = np.concatenate(([0], nl + 1))
+    ends = np.concatenate((nl, [data.size]))
+    if starts.size and starts[-1] >= data.size:  # file ends with '\n'
+        starts, ends = starts[:-1], ends[:-1]
+    lens = (ends - starts).astype(np.uint64)
+    offs = np.zeros(lens.size + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    keep = np.ones(data.size, dtype=bool)
+    keep[nl] = False
+    return np.ascontiguousarray(data[keep]), offs
+
+
+class Index:
+    """A loaded EDS-BWT index on one GPU (edsbwt_index_open)."""
+
+    def __init__(self, base: str, device: int = 0, a_balance: int = 8):
+        L = lib()
+        h = ctypes.c_void_p()
+        _check(L.edsbwt_index_open(base.encode(), int(device), int(a_balance), ctypes.byref(h)))
+        self._h = h
+        self.base = base
+        self.device = device
+        inf = _Info()
+        _check(L.edsbwt_index_get_info(self._h, ctypes.byref(inf)))
+        self.n_rows, self.n_words, self.n_segments = inf.n_rows, inf.n_words, inf.n_segments
+        self.sigma = inf.sigma
+        self.alphabet = bytes(inf.alphabet[: inf.sigma])
+        self.device_bytes = inf.device_bytes
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().edsbwt_index_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def search(self, patterns: Sequence[bytes | str] | tuple[np.ndarray, np.ndarray], *, first_pattern_id: int = 1,
+               locate: bool = True, table: bool = False, profile: bool = False):
+        """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc])."""
+        buf, offs = patterns if isinstance(patterns, tuple) else pack_patterns(patterns)
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        npat = offs.size - 1
+        counts = np.zeros(max(npat, 0), dtype=np.uint32)
+        flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
+        occ_p = ctypes.c_void_p()
+        nocc = ctypes.c_uint64()
+        bp = buf.ctypes.data if buf.size else None
+        _check(lib().edsbwt_search(self._h, bp, offs.ctypes.data, npat, first_pattern_id, flags,
+                                   counts.ctypes.data if npat else None, ctypes.byref(occ_p), ctypes.byref(nocc)))
+        n = nocc.value
+        occ = np.zeros(n, dtype=OCC_DTYPE)
+        if n:
+            ctypes.memmove(occ.ctypes.data, occ_p.value, n * OCC_DTYPE.itemsize)
+            lib().edsbwt_occ_free(occ_p)
+        return counts, occ
+
+    def search_device(self, d_bytes: int, d_offsets: int, npat: int, d_counts: int, *, first_pattern_id: int = 1,
+                      locate: bool = True, table: bool = False, profile: bool = False, stream: int = 0):
+        """Device-resident batch (pointers are device addresses, e.g. torch data_ptr()).
+        Returns (device pointer of the records, number of records)."""
+        flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
+        occ_p = ctypes.c_void_p()
+        nocc = ctypes.c_uint64()
+        _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,
+                                          ctypes.byref(occ_p), ctypes.byref(nocc), stream or None))
+        return occ_p.value or 0, nocc.value
+
+    def stats(self) -> dict:
+        s = _Stats()
+        _check(lib().edsbwt_last_stats(self._h, ctypes.byref(s)))
+        out = {k: getattr(s, k) for k, _ in _Stats._fields_ if k not in ("ms_kernel", "launches_kernel", "bytes_kernel")}
+        names = [lib().edsbwt_kernel_name(i).decode() for i in range(16)]
+        out["kernels"] = {n: {"ms": s.ms_kernel[i], "launches": s.launches_kernel[i], "bytes": s.bytes_kernel[i]}
+                          for i, n in enumerate(names) if n}
+        return out
+
+
+def format_csv(occ: np.ndarray, threads: int = 8) -> bytes:
+    """CSV body rows "%u\\t%u\\t%u\\t%u\\t%u\\n" (MOVE_EDSBWTSearch.cpp:365)."""
+    occ = np.ascontiguousarray(occ, dtype=OCC_DTYPE)
+    n = occ.size
+    if n == 0:
+        return b""
+    L = lib()
+    size = L.edsbwt_format_csv(occ.ctypes.data, n, None, 0, threads)
+    out = ctypes.create_string_buffer(int(size))
+    L.edsbwt_format_csv(occ.ctypes.data, n, out, size, threads)
+    return out.raw[:size]
+
+
+class MoveEDSBWT:
+    """Mirror of ``MOVE_EDSBWT(inputFileName, filepatterns)`` (MOVE_EDSBWTSearch.cpp:23-176):
+    the constructor does all the work.  Attributes ``count_found``, ``count_not_found``,
+    ``counts`` (per pattern) and ``seconds`` (the ``bs took:`` region, :109,:145)."""
+
+    def __init__(self, input_file_name: str, file_patterns: str, device: int = 0, *, table: bool = False):
+        with Index(input_file_name, device) as idx:
+            buf, offs = read_pattern_file(file_patterns)
+            t0 = time.perf_counter()
+            counts, occ = idx.search((buf, offs), first_pattern_id=1, locate=True, table=table)
+            out_path = file_patterns + "output_M_LF.csv"
+            try:
+                with open(out_path, "wb") as f:
+                    f.write(CSV_HEADER)
+                    f.write(format_csv(occ))
+            except OSError as e:  # :61-64
+                raise EdsBwtError(-1, f"ERROR opening file {out_path} to write output") from e
+            self.seconds = time.perf_counter() - t0
+            self.counts = counts
+            self.occ = occ
+            self.count_found = int((counts > 0).sum())
+            self.count_not_found = int(counts.size - self.count_found)
+            self.stats = idx.stats()

@@ -1,0 +1,691 @@
+// eds-bwt_amd/csrc/engine.hip — device index + batch search orchestrator + C ABI.
+//
+// Replaces, for the MOVE_EDSBWTSearch path of riccardo-nozza/EDS-BWT:
+//   recoverInfo / retrieve_MLF / bitvector load  MOVE_EDSBWTSearch.cpp:23-95,178-218,628-770
+//   build_MLF (M_LF + rank/select over L')        build_MLF.cpp:53-164
+//   the pattern loop + backwardSearch             MOVE_EDSBWTSearch.cpp:97-155,228-374
+//   link / dollars_in_interval / pdf              MOVE_EDSBWTSearch.cpp:512-625
+//   locate (position recovery)                    MOVE_EDSBWTSearch.cpp:328-369
+//
+// The state of backwardSearch after its last q steps depends only on the last q
+// pattern characters, so the batch is processed as a trie of reversed patterns,
+// one depth per launch group: every distinct pattern suffix is searched once.
+// DESIGN.md §Search walks through the phases and why each equals the reference.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "index_io.h"
+#include "kernels.hip"
+
+namespace edsbwt {
+
+static thread_local std::string g_err;
+
+struct Fail : std::runtime_error {
+    int code;
+    Fail(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                                 \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess)                                                                     \
+            throw Fail(EDSBWT_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap && p) return;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t c = std::max<size_t>(n, 1024);
+        if (hipMalloc(&p, c * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            throw Fail(EDSBWT_E_NOMEM, "hipMalloc of " + std::to_string(c * sizeof(T)) + " bytes failed");
+        }
+        cap = c;
+    }
+    // grow keeping contents (archive)
+    void grow_keep(size_t n, hipStream_t s) {
+        if (n <= cap && p) return;
+        size_t c = std::max<size_t>({n, cap + cap / 2, 1024});
+        T* q = nullptr;
+        if (hipMalloc(&q, c * sizeof(T)) != hipSuccess) throw Fail(EDSBWT_E_NOMEM, "hipMalloc (grow) failed");
+        if (p) {
+            HIPCHK(hipMemcpyAsync(q, p, cap * sizeof(T), hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+            (void)hipFree(p);
+        }
+        p = q;
+        cap = c;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+enum KClass { KC_TRIE = 0, KC_NODES, KC_EXPAND, KC_LINK, KC_STEP, KC_MERGE, KC_FINISH, KC_LOCATE, KC_SCAN, KC_TABLE, KC_COUNT };
+static const char* kKNames[KC_COUNT] = {"trie_sort", "trie_nodes", "expand", "link", "step", "merge", "finish", "locate", "scan", "table"};
+
+struct Engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* pinned = nullptr;  // host scalars
+    // index
+    uint32_t N = 0, W = 0, S = 0, sigma = 0;
+    uint8_t alpha[16] = {0};
+    uint32_t C[8] = {0};
+    uint64_t device_bytes = 0;
+    DBuf<OccBlock> occ;
+    DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt;
+    DBuf<uint8_t> code_of;
+    uint8_t h_code_of[256];
+    bool have_table = false;
+    // workspace
+    DBuf<uint32_t> len, perm, perm2, slen, lcp, nid[2], flag, scan, node_first, node_parent, child_first, child_end;
+    DBuf<uint8_t> node_char;
+    DBuf<uint64_t> keys, kc, kc2;
+    DBuf<uint32_t> ib[2], ie[2], iu[2], ioff[2], iend[2], iocb, ioce;
+    DBuf<uint32_t> hcnt, hoff, rflag, rscan, rb, re, ru, doff, dend, docb, doce;
+    DBuf<uint64_t> lkeys, lkeys2;
+    DBuf<uint32_t> tcnt, toff, tb, te, tu, tflag, tscan, cb, ce, cu, mflag, mscan;
+    DBuf<uint32_t> fcnt, foff, node_occ;
+    DBuf<uint32_t> ab, ae, res_cnt, res_occ;
+    DBuf<uint64_t> res_off, occ64, oscan, tc64, tscan64, tout;
+    DBuf<uint32_t> trow, tpat;
+    DBuf<edsbwt_occ> rec;
+    DBuf<unsigned long long> counters;
+    DBuf<uint8_t> tmp;      // hipcub temp storage
+    DBuf<uint8_t> hbytes;   // host-API pattern staging
+    DBuf<uint64_t> hoffs;
+    DBuf<uint32_t> hcounts;
+    edsbwt_stats st{};
+    // profiling
+    bool prof = false;
+    struct Ev { int k; hipEvent_t a, b; };
+    std::vector<Ev> evs, ev_pool;
+
+    KIdx kidx() const {
+        KIdx X;
+        X.occ = occ.p;
+        X.eof_seg = eof_seg.p;
+        X.eof_word = eof_word.p;
+        X.seg_of_word = seg_of_word.p;
+        X.seg_start = seg_start.p;
+        X.seg_lo = seg_lo.p;
+        X.da = da.p;
+        X.offt = offt.p;
+        X.N = N; X.W = W; X.S = S; X.sigma = sigma;
+        for (int c = 0; c < 8; c++) X.C[c] = C[c];
+        return X;
+    }
+
+    // ------------------------------------------------------------ helpers
+    static unsigned grid_for(size_t n) { return (unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 16384)); }
+
+    Ev ev_get(int k) {
+        Ev e;
+        if (!ev_pool.empty()) { e = ev_pool.back(); ev_pool.pop_back(); }
+        else { HIPCHK(hipEventCreate(&e.a)); HIPCHK(hipEventCreate(&e.b)); }
+        e.k = k;
+        return e;
+    }
+    template <typename F>
+    void timed(int k, F&& f) {
+        if (!prof) { f(); return; }
+        Ev e = ev_get(k);
+        HIPCHK(hipEventRecord(e.a, stream));
+        f();
+        HIPCHK(hipEventRecord(e.b, stream));
+        evs.push_back(e);
+    }
+    template <typename K, typename... A>
+    void launch(int k, K kern, size_t n, A... a) {
+        if (!n) return;
+        timed(k, [&] { hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(256), 0, stream, a...); });
+        HIPCHK(hipGetLastError());
+        st.launches_kernel[k]++;
+    }
+    uint32_t read_u32(const uint32_t* d) {
+        HIPCHK(hipMemcpyAsync(pinned, d, 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        return pinned[0];
+    }
+    uint64_t read_u64(const void* d) {
+        HIPCHK(hipMemcpyAsync(pinned, d, 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        uint64_t v;
+        std::memcpy(&v, pinned, 8);
+        return v;
+    }
+    void zero(void* p, size_t bytes) { if (bytes) HIPCHK(hipMemsetAsync(p, 0, bytes, stream)); }
+
+    // out[0..n] = exclusive prefix sum of in[0..n); returns out[n]
+    uint32_t scan_u32(const uint32_t* in, DBuf<uint32_t>& out, size_t n) {
+        out.ensure(n + 1);
+        zero(out.p, 4);
+        if (n) {
+            if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+            size_t tb = 0;
+            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
+            tmp.ensure(tb);
+            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+        }
+        return read_u32(out.p + n);
+    }
+    uint64_t scan_u64(const uint64_t* in, DBuf<uint64_t>& out, size_t n) {
+        out.ensure(n + 1);
+        zero(out.p, 8);
+        if (n) {
+            if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+            size_t tb = 0;
+            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
+            tmp.ensure(tb);
+            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+        }
+        return read_u64(out.p + n);
+    }
+
+    // ------------------------------------------------------------ index
+    void open(const std::string& base, int dev) {
+        device = dev;
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHK(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
+        HostIndex H;
+        std::string err;
+        int rc = read_host_index(base, H, err);
+        if (rc) throw Fail(rc, err);
+        if (H.sigma > 8)
+            throw Fail(EDSBWT_E_UNSUPPORTED, "alphabet of " + std::to_string(H.sigma) + " symbols (incl. '#'): the device layout supports 8");
+        N = H.N; W = H.W; S = H.S; sigma = H.sigma;
+        for (uint32_t j = 0; j < sigma; j++) alpha[j] = H.alpha[j];
+        std::memcpy(h_code_of, H.code_of, 256);
+        if (W > N) throw Fail(EDSBWT_E_FORMAT, "more words than rows");
+        // occ blocks (parallel over block ranges)
+        const size_t nblk = (size_t)N / 256 + 1;
+        std::vector<OccBlock> hb(nblk);
+        std::vector<uint32_t> tot(8, 0);
+        {
+            unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+            std::vector<std::vector<uint32_t>> part(T, std::vector<uint32_t>(8, 0));
+            auto rng = [&](unsigned t) { return std::make_pair(nblk * t / T, nblk * (t + 1) / T); };
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < T; t++)
+                th.emplace_back([&, t] {
+                    auto [b0, b1] = rng(t);
+                    for (size_t b = b0; b < b1; b++) {
+                        OccBlock& B = hb[b];
+                        std::memset(&B, 0, sizeof B);
+                        for (uint32_t r = 0; r < 256; r++) {
+                            size_t x = b * 256 + r;
+                            uint32_t c = x < N ? H.code_of[H.L[x]] : 7u;
+                            if (x < N) part[t][c]++;
+                            B.plane[0][r >> 6] |= (uint64_t)(c & 1) << (r & 63);
+                            B.plane[1][r >> 6] |= (uint64_t)((c >> 1) & 1) << (r & 63);
+                            B.plane[2][r >> 6] |= (uint64_t)((c >> 2) & 1) << (r & 63);
+                        }
+                    }
+                });
+            for (auto& x : th) x.join();
+            // block-start counts: sequential prefix over blocks within each part, offset by previous parts
+            std::vector<uint32_t> run(8, 0);
+            for (unsigned t = 0; t < T; t++) {
+                auto [b0, b1] = rng(t);
+                for (size_t b = b0; b < b1; b++) {
+                    for (int c = 0; c < 8; c++) hb[b].cnt[c] = run[c];
+                    for (uint32_t r = 0; r < 256; r++) {
+                        size_t x = b * 256 + r;
+                        if (x < N) run[H.code_of[H.L[x]]]++;
+                    }
+                }
+            }
+            tot = run;
+        }
+        uint32_t acc = 0;
+        for (uint32_t c = 0; c < 8; c++) { C[c] = acc; acc += tot[c]; }
+        if (tot[0] != W) throw Fail(EDSBWT_E_FORMAT, "number of '#' rows != nText");
+        // segments
+        std::vector<uint32_t> sow(W), sst(S + 2, 0), slo(S + 2, 0), eseg(W);
+        std::vector<uint8_t> has_empty(S + 2, 0);
+        {
+            uint32_t s = 0;
+            for (uint32_t w = 0; w < W; w++) {
+                if ((H.bv[w >> 6] >> (w & 63)) & 1) { s++; sst[s] = w; }
+                sow[w] = s;
+                if (H.L[w] == '#') has_empty[s] = 1;  // row w is the '#'-suffix of word w
+            }
+            sst[S + 1] = W;
+            // link from a word of segment s >= 2 covers segments [seg_lo[s], s-1]: the
+            // chain of dollars_in_interval pushes through empty words (:557,:620)
+            for (uint32_t t = 2; t <= S; t++) {
+                uint32_t v = t - 1;
+                slo[t] = (v >= 2 && has_empty[v]) ? slo[v] : v;
+            }
+            for (uint32_t k = 0; k < W; k++) {
+                uint32_t sg = sow[H.eof_id[k]];
+                eseg[k] = sg >= 2 ? sg : 0;
+            }
+        }
+        auto up = [&](auto& buf, const auto& v) {
+            using T = typename std::decay_t<decltype(v)>::value_type;
+            buf.ensure(v.size());
+            HIPCHK(hipMemcpy(buf.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+            device_bytes += v.size() * sizeof(T);
+        };
+        up(occ, hb);
+        up(eof_seg, eseg);
+        up(eof_word, H.eof_id);
+        up(seg_of_word, sow);
+        up(seg_start, sst);
+        up(seg_lo, slo);
+        std::vector<uint8_t> co(H.code_of, H.code_of + 256);
+        up(code_of, co);
+        counters.ensure(8);
+    }
+
+    void build_table() {
+        if (have_table) return;
+        da.ensure(N);
+        offt.ensure(N);
+        DBuf<uint32_t> wl;
+        wl.ensure(W);
+        device_bytes += (size_t)N * 8;
+        KIdx X = kidx();
+        launch(KC_TABLE, k_table_walk, W, W, X, da.p, offt.p, wl.p);
+        launch(KC_TABLE, k_table_finish, N, N, (const uint32_t*)da.p, (const uint32_t*)wl.p, offt.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        wl.release();
+        have_table = true;
+    }
+
+    // ------------------------------------------------------------ search
+    // d_bytes/d_off/d_counts are device pointers; returns number of records
+    uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
+        st = edsbwt_stats{};
+        prof = (flags & EDSBWT_PROFILE) != 0;
+        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
+        const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
+        if (use_table) build_table();
+        st.patterns = P;
+        if (P == 0) return 0;
+        if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, stream));
+        const KIdx X = kidx();
+        // ---- A. lengths, keys, reversed-pattern sort (trie order)
+        len.ensure(P);
+        launch(KC_TRIE, k_lens, P, d_off, P, len.p);
+        uint32_t Lmax = 0;
+        {
+            size_t tb = 0;
+            counters.ensure(8);
+            HIPCHK(hipcub::DeviceReduce::Max(nullptr, tb, len.p, (uint32_t*)counters.p, (int)P, stream));
+            tmp.ensure(tb);
+            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceReduce::Max(tmp.p, tb, len.p, (uint32_t*)counters.p, (int)P, stream)); });
+            Lmax = read_u32((const uint32_t*)counters.p);
+        }
+        res_off.ensure(P);
+        res_cnt.ensure(P);
+        res_occ.ensure(P);
+        zero(res_cnt.p, P * 4);
+        zero(res_occ.p, P * 4);
+        if (Lmax == 0) {
+            HIPCHK(hipMemsetAsync(d_counts, 0, P * 4, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+            st.not_found = P;
+            return 0;
+        }
+        const uint32_t nch = (Lmax + 15) / 16;
+        keys.ensure((size_t)nch * P);
+        launch(KC_TRIE, k_keys, P, d_bytes, d_off, (const uint32_t*)len.p, P, (const uint8_t*)code_of.p, sigma, nch, keys.p);
+        perm.ensure(P);
+        perm2.ensure(P);
+        kc.ensure(P);
+        kc2.ensure(P);
+        launch(KC_TRIE, k_iota, P, perm.p, P);
+        for (int c = (int)nch - 1; c >= 0; c--) {
+            launch(KC_TRIE, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, kc.p);
+            size_t tb = 0;
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kc.p, kc2.p, perm.p, perm2.p, (int)P, 0, 64, stream));
+            tmp.ensure(tb);
+            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kc.p, kc2.p, perm.p, perm2.p, (int)P, 0, 64, stream)); });
+            std::swap(perm.p, perm2.p);
+            std::swap(perm.cap, perm2.cap);
+        }
+        slen.ensure(P);
+        lcp.ensure(P);
+        launch(KC_TRIE, k_slen_lcp, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)keys.p, nch, P, slen.p, lcp.p);
+        // ---- B. root state [(0, N-1)] (init_backward_search, :220-225)
+        nid[0].ensure(P);
+        nid[1].ensure(P);
+        zero(nid[0].p, P * 4);
+        int cur = 0;
+        uint32_t Mcur = 1;  // nodes at the current depth
+        uint32_t ncur = 1;  // intervals at the current depth
+        ib[0].ensure(1); ie[0].ensure(1); iu[0].ensure(1); ioff[0].ensure(1); iend[0].ensure(1);
+        {
+            uint32_t h[5] = {0, N - 1, 0, 0, 1};
+            HIPCHK(hipMemcpyAsync(ib[0].p, &h[0], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(ie[0].p, &h[1], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(iu[0].p, &h[2], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(ioff[0].p, &h[3], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(iend[0].p, &h[4], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+        }
+        uint64_t abase = 0;
+        uint64_t depths = 0;
+        // ---- C. depth loop
+        for (uint32_t d = 0; d < Lmax; d++) {
+            const uint32_t D = d + 1;
+            const int nxt = cur ^ 1;
+            depths++;
+            // children nodes at depth D
+            flag.ensure(P);
+            launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
+            const uint32_t M = scan_u32(flag.p, scan, P);
+            if (M == 0) break;
+            st.trie_nodes += M;
+            node_first.ensure(M);
+            node_parent.ensure(M);
+            node_char.ensure(M);
+            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, (const uint32_t*)perm.p,
+                   (const uint32_t*)len.p, d_off, d_bytes, (const uint8_t*)code_of.p, sigma, (const uint32_t*)flag.p,
+                   (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
+            child_first.ensure(Mcur);
+            child_end.ensure(Mcur);
+            zero(child_first.p, (size_t)Mcur * 4);
+            zero(child_end.p, (size_t)Mcur * 4);
+            launch(KC_NODES, k_child_links, M, (const uint32_t*)node_parent.p, M, child_first.p, child_end.p);
+            // expand current intervals: rank of every symbol at both ends
+            iocb.ensure((size_t)ncur * 8);
+            ioce.ensure((size_t)ncur * 8);
+            launch(KC_EXPAND, k_expand, ncur, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p, (uint64_t)ncur, X, iocb.p, ioce.p);
+            st.bytes_kernel[KC_EXPAND] += (uint64_t)ncur * (2 * 128 + 8 + 64);
+            // LINK (not before the first step, :246-258)
+            uint32_t R = 0;
+            doff.ensure(Mcur);
+            dend.ensure(Mcur);
+            zero(doff.p, (size_t)Mcur * 4);
+            zero(dend.p, (size_t)Mcur * 4);
+            if (d > 0) {
+                hcnt.ensure(ncur);
+                launch(KC_LINK, k_hash_counts, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)iocb.p, (const uint32_t*)ioce.p,
+                       (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (uint64_t)ncur, hcnt.p);
+                const uint32_t Hn = scan_u32(hcnt.p, hoff, ncur);
+                st.link_hash_rows += Hn;
+                if (Hn) {
+                    lkeys.ensure(Hn);
+                    lkeys2.ensure(Hn);
+                    zero(counters.p, 8);
+                    launch(KC_LINK, k_link_emit, Hn, (uint64_t)Hn, (const uint32_t*)hoff.p, (uint64_t)ncur, (const uint32_t*)iocb.p,
+                           (const uint32_t*)iu[cur].p, (const uint32_t*)eof_seg.p, lkeys.p, counters.p);
+                    st.bytes_kernel[KC_LINK] += (uint64_t)Hn * 12;
+                    const uint32_t V = (uint32_t)read_u64(counters.p);
+                    if (V) {
+                        size_t tb = 0;
+                        // sentinels (~0) sort last; only the first V keys are used
+                        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream));
+                        tmp.ensure(tb);
+                        timed(KC_LINK, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream)); });
+                        rflag.ensure(V);
+                        launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, rflag.p);
+                        R = scan_u32(rflag.p, rscan, V);
+                        rb.ensure(R); re.ensure(R); ru.ensure(R);
+                        launch(KC_LINK, k_run_build, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
+                               (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p);
+                        launch(KC_LINK, k_bounds, R, (const uint32_t*)ru.p, (uint64_t)R, doff.p, dend.p);
+                        docb.ensure((size_t)R * 8);
+                        doce.ensure((size_t)R * 8);
+                        launch(KC_EXPAND, k_expand, R, (const uint32_t*)rb.p, (const uint32_t*)re.p, (uint64_t)R, X, docb.p, doce.p);
+                        st.bytes_kernel[KC_EXPAND] += (uint64_t)R * (2 * 128 + 8 + 64);
+                        st.link_ranges += R;
+                    }
+                }
+            }
+            // STEP every child over [dollar ranges, own intervals] of its parent
+            tcnt.ensure(M);
+            launch(KC_STEP, k_task_counts, M, M, (const uint32_t*)node_parent.p, (const uint32_t*)doff.p, (const uint32_t*)dend.p,
+                   (const uint32_t*)ioff[cur].p, (const uint32_t*)iend[cur].p, tcnt.p);
+            const uint32_t T = scan_u32(tcnt.p, toff, M);
+            st.intervals_stepped += T;
+            uint32_t R2 = 0;
+            if (T) {
+                tb.ensure(T); te.ensure(T); tu.ensure(T); tflag.ensure(T);
+                launch(KC_STEP, k_step, T, (uint64_t)T, (const uint32_t*)toff.p, M, (const uint32_t*)node_parent.p, (const uint8_t*)node_char.p,
+                       (const uint32_t*)doff.p, (const uint32_t*)dend.p, (const uint32_t*)ioff[cur].p, (const uint32_t*)docb.p,
+                       (const uint32_t*)doce.p, (const uint32_t*)iocb.p, (const uint32_t*)ioce.p, X, tb.p, te.p, tu.p, tflag.p);
+                st.bytes_kernel[KC_STEP] += (uint64_t)T * (8 + 16 + 16);
+                const uint32_t V2 = scan_u32(tflag.p, tscan, T);
+                if (V2) {
+                    cb.ensure(V2); ce.ensure(V2); cu.ensure(V2);
+                    launch(KC_MERGE, k_compact3, T, (uint64_t)T, (const uint32_t*)tflag.p, (const uint32_t*)tscan.p, (const uint32_t*)tb.p,
+                           (const uint32_t*)te.p, (const uint32_t*)tu.p, cb.p, ce.p, cu.p);
+                    mflag.ensure(V2);
+                    launch(KC_MERGE, k_merge_flags, V2, (uint64_t)V2, (const uint32_t*)cb.p, (const uint32_t*)ce.p, (const uint32_t*)cu.p, mflag.p);
+                    R2 = scan_u32(mflag.p, mscan, V2);
+                    ib[nxt].ensure(R2); ie[nxt].ensure(R2); iu[nxt].ensure(R2);
+                    launch(KC_MERGE, k_merge_build, V2, (uint64_t)V2, (const uint32_t*)mflag.p, (const uint32_t*)mscan.p, (const uint32_t*)cb.p,
+                           (const uint32_t*)ce.p, (const uint32_t*)cu.p, ib[nxt].p, ie[nxt].p, iu[nxt].p);
+                }
+            }
+            ioff[nxt].ensure(M);
+            iend[nxt].ensure(M);
+            zero(ioff[nxt].p, (size_t)M * 4);
+            zero(iend[nxt].p, (size_t)M * 4);
+            launch(KC_MERGE, k_bounds, R2, (const uint32_t*)iu[nxt].p, (uint64_t)R2, ioff[nxt].p, iend[nxt].p);
+            // FINISH patterns of length D: archive their node's list
+            fcnt.ensure(M);
+            launch(KC_FINISH, k_fin_counts, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, (const uint32_t*)ioff[nxt].p,
+                   (const uint32_t*)iend[nxt].p, fcnt.p);
+            const uint32_t F = scan_u32(fcnt.p, foff, M);
+            node_occ.ensure(M);
+            zero(node_occ.p, (size_t)M * 4);
+            if (F) {
+                ab.grow_keep(abase + F, stream);
+                ae.grow_keep(abase + F, stream);
+                launch(KC_FINISH, k_archive, R2, (uint64_t)R2, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
+                       (const uint32_t*)ioff[nxt].p, (const uint32_t*)fcnt.p, (const uint32_t*)foff.p, abase, ab.p, ae.p, node_occ.p);
+            }
+            launch(KC_FINISH, k_finish, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
+                   (const uint32_t*)foff.p, (const uint32_t*)fcnt.p, (const uint32_t*)node_occ.p, abase, res_off.p, res_cnt.p, res_occ.p);
+            abase += F;
+            cur = nxt;
+            Mcur = M;
+            ncur = R2;
+            if (R2 == 0) break;  // every deeper suffix has an empty list
+        }
+        st.depths = depths;
+        // ---- D. counts (backwardSearch's return value) and locate
+        HIPCHK(hipMemcpyAsync(d_counts, res_occ.p, P * 4, hipMemcpyDeviceToDevice, stream));
+        zero(counters.p + 1, 8);
+        launch(KC_FINISH, k_count_found, P, (const uint32_t*)res_occ.p, P, counters.p + 1);
+        st.found = read_u64(counters.p + 1);
+        st.not_found = P - st.found;
+        uint64_t OCC = 0;
+        if (locate) {
+            occ64.ensure(P);
+            launch(KC_LOCATE, k_u32_to_u64, P, (const uint32_t*)res_occ.p, P, occ64.p);
+            OCC = scan_u64(occ64.p, oscan, P);
+            tc64.ensure(P);
+            launch(KC_LOCATE, k_u32_to_u64, P, (const uint32_t*)res_cnt.p, P, tc64.p);
+            const uint64_t TT = scan_u64(tc64.p, tscan64, P);
+            if (OCC) {
+                trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
+                launch(KC_LOCATE, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
+                       (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p);
+                rec.ensure(OCC);
+                zero(counters.p, 8);
+                launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
+                       X, use_table ? 1 : 0, rec.p, counters.p);
+                st.locate_lf_steps = read_u64(counters.p);
+                st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * 128 + OCC * (128 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
+            }
+        }
+        HIPCHK(hipEventRecord(e1, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        st.ms_total = ms;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (prof) {
+            for (auto& e : evs) {
+                float t = 0;
+                HIPCHK(hipEventElapsedTime(&t, e.a, e.b));
+                st.ms_kernel[e.k] += t;
+                ev_pool.push_back(e);
+            }
+            evs.clear();
+        }
+        st.occurrences = OCC;
+        return OCC;
+    }
+
+    ~Engine() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+        if (pinned) (void)hipHostFree(pinned);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+}  // namespace edsbwt
+
+using edsbwt::Engine;
+using edsbwt::Fail;
+
+struct edsbwt_index {
+    std::unique_ptr<Engine> eng;
+};
+
+#define ABI_TRY try {
+#define ABI_CATCH                                                        \
+    }                                                                    \
+    catch (const Fail& f) {                                              \
+        edsbwt::g_err = f.what();                                        \
+        return f.code;                                                   \
+    }                                                                    \
+    catch (const std::bad_alloc&) {                                      \
+        edsbwt::g_err = "host allocation failed";                        \
+        return EDSBWT_E_NOMEM;                                           \
+    }                                                                    \
+    catch (const std::exception& e) {                                    \
+        edsbwt::g_err = e.what();                                        \
+        return EDSBWT_E_DEVICE;                                          \
+    }
+
+extern "C" {
+
+int edsbwt_abi_version(void) { return EDSBWT_ABI_VERSION; }
+const char* edsbwt_last_error(void) { return edsbwt::g_err.c_str(); }
+const char* edsbwt_kernel_name(int k) { return (k >= 0 && k < edsbwt::KC_COUNT) ? edsbwt::kKNames[k] : ""; }
+
+int edsbwt_index_open(const char* base, int device, uint32_t a_balance, edsbwt_index** out) {
+    (void)a_balance;
+    if (!base || !out) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    *out = nullptr;
+    ABI_TRY
+    auto h = std::make_unique<edsbwt_index>();
+    h->eng = std::make_unique<Engine>();
+    h->eng->open(base, device);
+    *out = h.release();
+    return 0;
+    ABI_CATCH
+}
+
+void edsbwt_index_close(edsbwt_index* idx) {
+    if (!idx) return;
+    try { delete idx; } catch (...) {}
+}
+
+int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
+    if (!idx || !info) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    const Engine& E = *idx->eng;
+    std::memset(info, 0, sizeof *info);
+    info->n_rows = E.N;
+    info->n_words = E.W;
+    info->n_segments = E.S;
+    info->sigma = E.sigma;
+    std::memcpy(info->alphabet, E.alpha, sizeof info->alphabet);
+    info->device_bytes = E.device_bytes;
+    return 0;
+}
+
+int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t npat,
+                         uint32_t first_pattern_id, uint32_t flags, uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc,
+                         void* stream) {
+    if (!idx || (!d_counts && npat) || (npat && (!d_bytes || !d_offsets))) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    Engine& E = *idx->eng;
+    HIPCHK(hipSetDevice(E.device));
+    hipStream_t user = (hipStream_t)stream;
+    if (user) {  // order after the caller's stream
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(ev, user));
+        HIPCHK(hipStreamWaitEvent(E.stream, ev, 0));
+        (void)hipEventDestroy(ev);
+    }
+    uint64_t n = E.search(d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts);
+    if (d_occ) *d_occ = n ? E.rec.p : nullptr;
+    if (nocc) *nocc = n;
+    return 0;
+    ABI_CATCH
+}
+
+int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_offsets, uint64_t npat, uint32_t first_pattern_id,
+                  uint32_t flags, uint32_t* counts, edsbwt_occ** occ, uint64_t* nocc) {
+    if (!idx || (npat && (!pat_offsets || !counts))) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    if (occ) *occ = nullptr;
+    if (nocc) *nocc = 0;
+    ABI_TRY
+    Engine& E = *idx->eng;
+    HIPCHK(hipSetDevice(E.device));
+    const uint64_t nb = npat ? pat_offsets[npat] : 0;
+    if (npat && pat_offsets[0] != 0) throw Fail(EDSBWT_E_ARG, "pat_offsets[0] must be 0");
+    E.hbytes.ensure(nb + 1);
+    E.hoffs.ensure(npat + 1);
+    E.hcounts.ensure(npat + 1);
+    if (nb) HIPCHK(hipMemcpyAsync(E.hbytes.p, pat_bytes, nb, hipMemcpyHostToDevice, E.stream));
+    if (npat) HIPCHK(hipMemcpyAsync(E.hoffs.p, pat_offsets, (npat + 1) * 8, hipMemcpyHostToDevice, E.stream));
+    uint64_t n = E.search(E.hbytes.p, E.hoffs.p, npat, first_pattern_id, flags, E.hcounts.p);
+    if (npat) HIPCHK(hipMemcpyAsync(counts, E.hcounts.p, npat * 4, hipMemcpyDeviceToHost, E.stream));
+    edsbwt_occ* h = nullptr;
+    if (n && occ) {
+        h = (edsbwt_occ*)std::malloc(n * sizeof(edsbwt_occ));
+        if (!h) throw Fail(EDSBWT_E_NOMEM, "host allocation of occurrence records failed");
+        HIPCHK(hipMemcpyAsync(h, E.rec.p, n * sizeof(edsbwt_occ), hipMemcpyDeviceToHost, E.stream));
+    }
+    HIPCHK(hipStreamSynchronize(E.stream));
+    if (occ) *occ = h;
+    if (nocc) *nocc = n;
+    return 0;
+    ABI_CATCH
+}
+
+void edsbwt_occ_free(edsbwt_occ* occ) { std::free(occ); }
+
+int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st) {
+    if (!idx || !st) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    *st = idx->eng->st;
+    return 0;
+}
+
+}  // extern "C"

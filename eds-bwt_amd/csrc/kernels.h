@@ -1,0 +1,31 @@
+// eds-bwt_amd/csrc/kernels.h — device data layout shared by kernels.hip and engine.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "../../include/edsbwt.h"
+
+namespace edsbwt {
+
+// 128-B rank block over 256 BWT rows
+struct alignas(128) OccBlock {
+    uint32_t cnt[8];
+    uint64_t plane[3][4];
+};
+static_assert(sizeof(OccBlock) == 128, "occ block must be one 128-B line");
+
+// kernel-side view of the device index (passed by value)
+struct KIdx {
+    const OccBlock* occ;       // ceil((N+1)/256) blocks
+    const uint32_t* eof_seg;   // [W] segment (1-based) of the word of the k-th '#' row, 0 if segment 1
+    const uint32_t* eof_word;  // [W] EOF_ID_Copy
+    const uint32_t* seg_of_word;  // [W] 1-based segment of each word
+    const uint32_t* seg_start;    // [S+2] first word of segment s (1-based), seg_start[S+1] = W
+    const uint32_t* seg_lo;       // [S+2] lowest segment reached by link from segment s (empty-word chains)
+    const uint32_t* da;        // [N] optional DA per row
+    const uint32_t* offt;      // [N] optional offset-in-word per row
+    uint32_t N, W, S, sigma;
+    uint32_t C[8];             // first row of each pile
+};
+
+}  // namespace edsbwt

@@ -1,0 +1,486 @@
+// eds-bwt_amd/csrc/kernels.hip — hand-written gfx950 kernels of the EDS-BWT
+// backward search (MOVE_EDSBWTSearch.cpp:228-625 re-designed as a level-synchronous
+// walk over a trie of reversed patterns).
+//
+// Rank/LF layout ("occ block", 128 B = one L2 line, 256 BWT rows):
+//   u32 cnt[8]      rank of code c before the block's first row
+//   u64 plane[3][4] the 3-bit code of each of the 256 rows, bit-sliced
+// rank_c(L, x) = cnt[c] + popcount of rows < x&255 whose 3 bits equal c.
+// One 128-B line answers the rank of every symbol at once, so the backward step
+// LF_c([b,e]) of MOVE_EDSBWTSearch.cpp:424-510 costs two line reads, and the
+// '#'-rank of dollars_in_interval (:607-625) comes out of the same two lines.
+#include "kernels.h"
+
+namespace edsbwt {
+
+// ---------------------------------------------------------------- occ blocks
+__device__ __forceinline__ void load_block(const OccBlock* __restrict__ occ, uint32_t blk, uint4 (&v)[8]) {
+    const uint4* p = reinterpret_cast<const uint4*>(occ + blk);
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = p[i];
+}
+
+__device__ __forceinline__ uint64_t u64_of(uint4 v, int hi) {
+    return hi ? ((uint64_t)v.w << 32 | v.z) : ((uint64_t)v.y << 32 | v.x);
+}
+
+// rank of every code < sigma at row x (rows [0,x) counted)
+__device__ __forceinline__ void rank_all(const OccBlock* __restrict__ occ, uint32_t x, uint32_t sigma, uint32_t* out) {
+    uint4 v[8];
+    load_block(occ, x >> 8, v);
+    const uint32_t r = x & 255u;
+    const uint32_t wq = r >> 6, bit = r & 63u;
+    uint64_t p0[4], p1[4], p2[4], m[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        p0[q] = u64_of(v[2 + (q >> 1)], q & 1);
+        p1[q] = u64_of(v[4 + (q >> 1)], q & 1);
+        p2[q] = u64_of(v[6 + (q >> 1)], q & 1);
+        m[q] = (uint32_t)q < wq ? ~0ull : ((uint32_t)q == wq ? ((1ull << bit) - 1ull) : 0ull);
+    }
+    const uint32_t cnt[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+    for (uint32_t c = 0; c < 8; c++) {
+        if (c < sigma) {
+            uint32_t acc = cnt[c];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint64_t e = ((c & 1) ? p0[q] : ~p0[q]) & ((c & 2) ? p1[q] : ~p1[q]) & ((c & 4) ? p2[q] : ~p2[q]);
+                acc += (uint32_t)__popcll(e & m[q]);
+            }
+            out[c] = acc;
+        } else {
+            out[c] = 0;
+        }
+    }
+}
+
+// symbol code at row x and its rank (one line): LF(x) = C[code] + rank
+__device__ __forceinline__ uint32_t sym_rank(const OccBlock* __restrict__ occ, uint32_t x, uint32_t* rank) {
+    uint4 v[8];
+    load_block(occ, x >> 8, v);
+    const uint32_t r = x & 255u;
+    const uint32_t wq = r >> 6, bit = r & 63u;
+    uint64_t p0[4], p1[4], p2[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        p0[q] = u64_of(v[2 + (q >> 1)], q & 1);
+        p1[q] = u64_of(v[4 + (q >> 1)], q & 1);
+        p2[q] = u64_of(v[6 + (q >> 1)], q & 1);
+    }
+    uint64_t w0 = p0[0], w1 = p1[0], w2 = p2[0];
+#pragma unroll
+    for (int q = 1; q < 4; q++)
+        if ((uint32_t)q == wq) { w0 = p0[q]; w1 = p1[q]; w2 = p2[q]; }
+    const uint32_t c = (uint32_t)((w0 >> bit) & 1) | (uint32_t)(((w1 >> bit) & 1) << 1) | (uint32_t)(((w2 >> bit) & 1) << 2);
+    const uint32_t cnt[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t cc = 0; cc < 8; cc++)
+        if (cc == c) acc = cnt[cc];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint64_t mq = (uint32_t)q < wq ? ~0ull : ((uint32_t)q == wq ? ((1ull << bit) - 1ull) : 0ull);
+        uint64_t e = ((c & 1) ? p0[q] : ~p0[q]) & ((c & 2) ? p1[q] : ~p1[q]) & ((c & 4) ? p2[q] : ~p2[q]);
+        acc += (uint32_t)__popcll(e & mq);
+    }
+    *rank = acc;
+    return c;
+}
+
+#define GRID_STRIDE(i, n) for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(n); i += (size_t)gridDim.x * blockDim.x)
+
+template <typename T>
+__device__ __forceinline__ size_t upper_bound_dev(const T* __restrict__ a, size_t n, T key) {
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+        size_t mid = (lo + hi) >> 1;
+        if (a[mid] <= key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// ------------------------------------------------------------ pattern trie
+__global__ void k_lens(const uint64_t* __restrict__ off, uint64_t P, uint32_t* __restrict__ len) {
+    GRID_STRIDE(i, P) len[i] = (uint32_t)(off[i + 1] - off[i]);
+}
+
+// 4-bit sort codes of the reversed pattern, 16 per u64, most significant first:
+// 0 = end of pattern, 1+code for alphabet symbols, sigma+1 for bytes outside it.
+__global__ void k_keys(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                       uint64_t P, const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t nch, uint64_t* __restrict__ keys) {
+    GRID_STRIDE(i, P) {
+        const uint32_t L = len[i];
+        const uint8_t* s = bytes + off[i];
+        for (uint32_t c = 0; c < nch; c++) {
+            uint64_t key = 0;
+            for (uint32_t t = 0; t < 16; t++) {
+                uint32_t pos = c * 16 + t;
+                uint64_t v = 0;
+                if (pos < L) {
+                    uint32_t code = code_of[s[L - 1 - pos]];
+                    v = code < sigma ? code + 1 : sigma + 1;
+                }
+                key = (key << 4) | v;
+            }
+            keys[(size_t)c * P + i] = key;
+        }
+    }
+}
+
+__global__ void k_iota(uint32_t* __restrict__ a, uint64_t n) { GRID_STRIDE(i, n) a[i] = (uint32_t)i; }
+
+__global__ void k_gather_key(const uint64_t* __restrict__ keys_c, const uint32_t* __restrict__ perm, uint64_t P, uint64_t* __restrict__ out) {
+    GRID_STRIDE(i, P) out[i] = keys_c[perm[i]];
+}
+
+__global__ void k_slen_lcp(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len, const uint64_t* __restrict__ keys,
+                           uint32_t nch, uint64_t P, uint32_t* __restrict__ slen, uint32_t* __restrict__ lcp) {
+    GRID_STRIDE(i, P) {
+        const uint32_t a = perm[i];
+        slen[i] = len[a];
+        if (i == 0) { lcp[0] = 0; continue; }
+        const uint32_t b = perm[i - 1];
+        uint32_t l = 16 * nch;
+        for (uint32_t c = 0; c < nch; c++) {
+            uint64_t x = keys[(size_t)c * P + a] ^ keys[(size_t)c * P + b];
+            if (x) { l = c * 16 + (uint32_t)__clzll(x) / 4; break; }
+        }
+        uint32_t la = len[a], lb = len[b];
+        l = l < la ? l : la;
+        l = l < lb ? l : lb;
+        lcp[i] = l;
+    }
+}
+
+// node starts at depth D: pattern i is the first member of a depth-D node
+__global__ void k_node_flags(const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp, uint64_t P, uint32_t D, uint32_t* __restrict__ flag) {
+    GRID_STRIDE(i, P) flag[i] = (slen[i] >= D && lcp[i] < D) ? 1u : 0u;
+}
+
+// nscan = exclusive scan of flags (P+1 entries)
+__global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp,
+                             const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len, const uint64_t* __restrict__ off,
+                             const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of, uint32_t sigma,
+                             const uint32_t* __restrict__ flag, const uint32_t* __restrict__ nscan,
+                             const uint32_t* __restrict__ nid_prev, uint32_t* __restrict__ nid_cur,
+                             uint32_t* __restrict__ node_first, uint32_t* __restrict__ node_parent, uint8_t* __restrict__ node_char) {
+    GRID_STRIDE(i, P) {
+        if (slen[i] < D) { nid_cur[i] = 0xFFFFFFFFu; continue; }
+        const uint32_t id = nscan[i] + flag[i] - 1;
+        nid_cur[i] = id;
+        if (flag[i]) {
+            node_first[id] = (uint32_t)i;
+            node_parent[id] = nid_prev[i];
+            const uint32_t a = perm[i];
+            const uint32_t code = code_of[bytes[off[a] + len[a] - D]];
+            node_char[id] = (uint8_t)(code < sigma ? code : 0xFF);
+        }
+    }
+}
+
+// children of each parent are contiguous: [child_first[p], child_end[p])
+__global__ void k_child_links(const uint32_t* __restrict__ node_parent, uint32_t M, uint32_t* __restrict__ child_first, uint32_t* __restrict__ child_end) {
+    GRID_STRIDE(u, M) {
+        const uint32_t p = node_parent[u];
+        if (u == 0 || node_parent[u - 1] != p) child_first[p] = (uint32_t)u;
+        if (u + 1 == M || node_parent[u + 1] != p) child_end[p] = (uint32_t)u + 1;
+    }
+}
+
+// ---------------------------------------------------------- interval lists
+// owner-sorted list → [off[u], end[u]) per owner (arrays zeroed by the caller)
+__global__ void k_bounds(const uint32_t* __restrict__ owner, uint64_t n, uint32_t* __restrict__ off, uint32_t* __restrict__ end) {
+    GRID_STRIDE(t, n) {
+        const uint32_t u = owner[t];
+        if (t == 0 || owner[t - 1] != u) off[u] = (uint32_t)t;
+        if (t + 1 == n || owner[t + 1] != u) end[u] = (uint32_t)t + 1;
+    }
+}
+
+// EXPAND: rank of every symbol at b and at e+1 (2 occ-block lines per interval)
+__global__ void __launch_bounds__(256) k_expand(const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, uint64_t n, KIdx X,
+                                                uint32_t* __restrict__ ocb, uint32_t* __restrict__ oce) {
+    GRID_STRIDE(j, n) {
+        uint32_t rb[8], re[8];
+        rank_all(X.occ, ib[j], X.sigma, rb);
+        rank_all(X.occ, ie[j] + 1, X.sigma, re);
+        uint4* pb = reinterpret_cast<uint4*>(ocb + j * 8);
+        uint4* pe = reinterpret_cast<uint4*>(oce + j * 8);
+        pb[0] = make_uint4(rb[0], rb[1], rb[2], rb[3]);
+        pb[1] = make_uint4(rb[4], rb[5], rb[6], rb[7]);
+        pe[0] = make_uint4(re[0], re[1], re[2], re[3]);
+        pe[1] = make_uint4(re[4], re[5], re[6], re[7]);
+    }
+}
+
+// LINK step 1: number of '#' rows in each interval whose node has children
+// (dollars_in_interval, MOVE_EDSBWTSearch.cpp:607-625)
+__global__ void k_hash_counts(const uint32_t* __restrict__ owner, const uint32_t* __restrict__ ocb, const uint32_t* __restrict__ oce,
+                              const uint32_t* __restrict__ child_first, const uint32_t* __restrict__ child_end, uint64_t n,
+                              uint32_t* __restrict__ h) {
+    GRID_STRIDE(j, n) {
+        const uint32_t u = owner[j];
+        h[j] = (child_end[u] > child_first[u]) ? oce[j * 8] - ocb[j * 8] : 0u;
+    }
+}
+
+// LINK step 2: one key per '#' row: (owner << 32 | segment of its word) when the
+// word is past segment 1 (index > first_symbol_index, :620), else a sentinel.
+__global__ void k_link_emit(uint64_t H, const uint32_t* __restrict__ hoff, uint64_t n, const uint32_t* __restrict__ ocb,
+                            const uint32_t* __restrict__ owner, const uint32_t* __restrict__ eof_seg,
+                            uint64_t* __restrict__ keys, unsigned long long* __restrict__ nvalid) {
+    GRID_STRIDE(t, H) {
+        const size_t j = upper_bound_dev<uint32_t>(hoff, n, (uint32_t)t) - 1;
+        const uint32_t k = ocb[j * 8] + ((uint32_t)t - hoff[j]);
+        const uint32_t s = eof_seg[k];
+        uint64_t key = ~0ull;
+        if (s) {
+            key = ((uint64_t)owner[j] << 32) | s;
+            atomicAdd(nvalid, 1ull);
+        }
+        keys[t] = key;
+    }
+}
+
+// LINK step 3: union of previous-segment ranges [seg_lo[s], s-1] per owner
+// (the deque walk of link(), :533-561, yields exactly these maximal runs, ascending)
+__global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ seg_lo, uint32_t* __restrict__ flag) {
+    GRID_STRIDE(t, V) {
+        const uint64_t k = keys[t];
+        uint32_t f = 1;
+        if (t) {
+            const uint64_t kp = keys[t - 1];
+            if ((kp >> 32) == (k >> 32) && seg_lo[(uint32_t)k] <= (uint32_t)kp) f = 0;
+        }
+        flag[t] = f;
+    }
+}
+
+__global__ void k_run_build(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rscan,
+                            const uint32_t* __restrict__ seg_lo, const uint32_t* __restrict__ seg_start,
+                            uint32_t* __restrict__ rb, uint32_t* __restrict__ re, uint32_t* __restrict__ rown) {
+    GRID_STRIDE(t, V) {
+        const uint64_t k = keys[t];
+        const uint32_t s = (uint32_t)k;
+        const uint32_t r = rscan[t] + flag[t] - 1;
+        if (flag[t]) {
+            rb[r] = seg_start[seg_lo[s]];
+            rown[r] = (uint32_t)(k >> 32);
+        }
+        if (t + 1 == V || flag[t + 1]) re[r] = seg_start[s] - 1;
+    }
+}
+
+// STEP: per child node, its parent's list [dollar ranges..., own intervals...]
+// stepped by the child's symbol (backward_search_step + updateSingleInterval,
+// :376-510; concatenation order of :300).
+__global__ void k_task_counts(uint32_t M, const uint32_t* __restrict__ node_parent, const uint32_t* __restrict__ doff, const uint32_t* __restrict__ dend,
+                              const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend, uint32_t* __restrict__ tcnt) {
+    GRID_STRIDE(u, M) {
+        const uint32_t p = node_parent[u];
+        tcnt[u] = (dend[p] - doff[p]) + (iend[p] - ioff[p]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_step(uint64_t T, const uint32_t* __restrict__ toff, uint32_t M,
+                                              const uint32_t* __restrict__ node_parent, const uint8_t* __restrict__ node_char,
+                                              const uint32_t* __restrict__ doff, const uint32_t* __restrict__ dend,
+                                              const uint32_t* __restrict__ ioff,
+                                              const uint32_t* __restrict__ docb, const uint32_t* __restrict__ doce,
+                                              const uint32_t* __restrict__ iocb, const uint32_t* __restrict__ ioce, KIdx X,
+                                              uint32_t* __restrict__ ob, uint32_t* __restrict__ oe, uint32_t* __restrict__ ou,
+                                              uint32_t* __restrict__ flag) {
+    GRID_STRIDE(t, T) {
+        const uint32_t u = (uint32_t)(upper_bound_dev<uint32_t>(toff, M, (uint32_t)t) - 1);
+        const uint32_t p = node_parent[u];
+        const uint32_t j = (uint32_t)t - toff[u];
+        const uint32_t nd = dend[p] - doff[p];
+        const uint32_t c = node_char[u];
+        uint32_t f = 0, b = 0, e = 0;
+        if (c < X.sigma) {
+            uint32_t lo, hi;
+            if (j < nd) {
+                const size_t s = (size_t)(doff[p] + j) * 8 + c;
+                lo = docb[s];
+                hi = doce[s];
+            } else {
+                const size_t s = (size_t)(ioff[p] + j - nd) * 8 + c;
+                lo = iocb[s];
+                hi = ioce[s];
+            }
+            if (hi > lo) {
+                f = 1;
+                b = X.C[c] + lo;
+                e = X.C[c] + hi - 1;
+            }
+        }
+        ob[t] = b;
+        oe[t] = e;
+        ou[t] = u;
+        flag[t] = f;
+    }
+}
+
+// stream compaction (order-preserving): fscan = exclusive scan of flag
+__global__ void k_compact3(uint64_t n, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ fscan,
+                           const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, const uint32_t* __restrict__ c,
+                           uint32_t* __restrict__ oa, uint32_t* __restrict__ ob, uint32_t* __restrict__ oc) {
+    GRID_STRIDE(t, n) {
+        if (flag[t]) {
+            const uint32_t d = fscan[t];
+            oa[d] = a[t];
+            ob[d] = b[t];
+            oc[d] = c[t];
+        }
+    }
+}
+
+// adjacency merge inside each child (:309-324): a new run unless start == last.end+1
+__global__ void k_merge_flags(uint64_t n, const uint32_t* __restrict__ cb, const uint32_t* __restrict__ ce, const uint32_t* __restrict__ cu,
+                              uint32_t* __restrict__ flag) {
+    GRID_STRIDE(t, n) {
+        uint32_t f = 1;
+        if (t && cu[t] == cu[t - 1] && cb[t] == ce[t - 1] + 1) f = 0;
+        flag[t] = f;
+    }
+}
+
+__global__ void k_merge_build(uint64_t n, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ mscan,
+                              const uint32_t* __restrict__ cb, const uint32_t* __restrict__ ce, const uint32_t* __restrict__ cu,
+                              uint32_t* __restrict__ nb, uint32_t* __restrict__ ne, uint32_t* __restrict__ nu) {
+    GRID_STRIDE(t, n) {
+        const uint32_t r = mscan[t] + flag[t] - 1;
+        if (flag[t]) {
+            nb[r] = cb[t];
+            nu[r] = cu[t];
+        }
+        if (t + 1 == n || flag[t + 1]) ne[r] = ce[t];
+    }
+}
+
+// ------------------------------------------------------------- finishing
+__global__ void k_fin_counts(uint32_t M, uint32_t D, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ slen,
+                             const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend, uint32_t* __restrict__ fcnt) {
+    GRID_STRIDE(u, M) fcnt[u] = (slen[node_first[u]] == D) ? iend[u] - ioff[u] : 0u;
+}
+
+__global__ void k_archive(uint64_t n, const uint32_t* __restrict__ nu, const uint32_t* __restrict__ nb, const uint32_t* __restrict__ ne,
+                          const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ fcnt, const uint32_t* __restrict__ foff,
+                          uint64_t abase, uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, uint32_t* __restrict__ node_occ) {
+    GRID_STRIDE(r, n) {
+        const uint32_t u = nu[r];
+        if (fcnt[u]) {
+            const uint64_t d = abase + foff[u] + (r - ioff[u]);
+            ab[d] = nb[r];
+            ae[d] = ne[r];
+            atomicAdd(node_occ + u, ne[r] - nb[r] + 1);
+        }
+    }
+}
+
+__global__ void k_finish(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ nid,
+                         const uint32_t* __restrict__ perm, const uint32_t* __restrict__ foff, const uint32_t* __restrict__ fcnt,
+                         const uint32_t* __restrict__ node_occ, uint64_t abase,
+                         uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ) {
+    GRID_STRIDE(i, P) {
+        if (slen[i] != D) continue;
+        const uint32_t u = nid[i];
+        const uint32_t o = perm[i];
+        res_off[o] = abase + foff[u];
+        res_cnt[o] = fcnt[u];
+        res_occ[o] = node_occ[u];
+    }
+}
+
+// --------------------------------------------------------------- locate
+__global__ void k_u32_to_u64(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ b) { GRID_STRIDE(i, n) b[i] = a[i]; }
+
+__global__ void k_tasks(uint64_t P, const uint64_t* __restrict__ res_off, const uint32_t* __restrict__ res_cnt,
+                        const uint64_t* __restrict__ tscan, const uint64_t* __restrict__ oscan,
+                        const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
+                        uint32_t* __restrict__ trow, uint64_t* __restrict__ tout, uint32_t* __restrict__ tpat) {
+    GRID_STRIDE(i, P) {
+        uint64_t base = oscan[i];
+        const uint64_t t0 = tscan[i];
+        const uint32_t n = res_cnt[i];
+        for (uint32_t q = 0; q < n; q++) {
+            const uint64_t a = res_off[i] + q;
+            trow[t0 + q] = ab[a];
+            tout[t0 + q] = base;
+            tpat[t0 + q] = (uint32_t)i;
+            base += (uint64_t)(ae[a] - ab[a]) + 1;
+        }
+    }
+}
+
+// locate (:328-369): walk LF until L = '#'; the walk length is the offset in the
+// word, the '#'-rank gives EOF_ID, the segment bitvector gives (D, S_j).
+__global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
+                                                const uint32_t* __restrict__ tpat, uint32_t first_id, KIdx X, int use_table,
+                                                edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ steps) {
+    unsigned long long my_steps = 0;
+    GRID_STRIDE(o, OCC) {
+        const size_t t = upper_bound_dev<uint64_t>(tout, TT, (uint64_t)o) - 1;
+        uint32_t x = trow[t] + (uint32_t)(o - tout[t]);
+        uint32_t word, off;
+        if (use_table) {
+            word = X.da[x];
+            off = X.offt[x];
+        } else {
+            off = 0;
+            for (;;) {
+                uint32_t rk;
+                const uint32_t c = sym_rank(X.occ, x, &rk);
+                if (c == 0) { word = X.eof_word[rk]; break; }
+                x = X.C[c] + rk;
+                off++;
+            }
+            my_steps += off;
+        }
+        const uint32_t seg = X.seg_of_word[word];
+        edsbwt_occ r;
+        r.pat = first_id + tpat[t];
+        r.word = word;
+        r.seg = seg;
+        r.word_in_seg = word - X.seg_start[seg];
+        r.offset = off;
+        rec[o] = r;
+    }
+    if (my_steps) atomicAdd(steps, my_steps);
+}
+
+// ------------------------------------------------- DA/OFF table (index open)
+// For every word w, walk LF from row w (its '#'-suffix) to the row with L='#'
+// (position 0): rows visited get DA = w and their distance from the word end.
+__global__ void k_table_walk(uint32_t W, KIdx X, uint32_t* __restrict__ da, uint32_t* __restrict__ dist, uint32_t* __restrict__ wlen) {
+    GRID_STRIDE(w, W) {
+        uint32_t x = (uint32_t)w, t = 0;
+        da[x] = (uint32_t)w;
+        dist[x] = 0;
+        for (;;) {
+            uint32_t rk;
+            const uint32_t c = sym_rank(X.occ, x, &rk);
+            if (c == 0) break;
+            x = X.C[c] + rk;
+            t++;
+            da[x] = (uint32_t)w;
+            dist[x] = t;
+        }
+        wlen[w] = t;
+    }
+}
+
+__global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, const uint32_t* __restrict__ wlen, uint32_t* __restrict__ off) {
+    GRID_STRIDE(x, N) off[x] = wlen[da[x]] - off[x];
+}
+
+__global__ void k_count_found(const uint32_t* __restrict__ occ, uint64_t P, unsigned long long* __restrict__ found) {
+    unsigned long long f = 0;
+    GRID_STRIDE(i, P) f += occ[i] > 0;
+    if (f) atomicAdd(found, f);
+}
+
+__global__ void k_fill_u32(uint32_t* __restrict__ a, uint64_t n, uint32_t v) { GRID_STRIDE(i, n) a[i] = v; }
+
+}  // namespace edsbwt

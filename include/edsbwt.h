@@ -1,0 +1,120 @@
+/*
+ * include/edsbwt.h — C ABI of the MI355X-native EDS-BWT backward-search engine.
+ *
+ * Drop-in boundary for riccardo-nozza/EDS-BWT's MOVE_EDSBWTSearch path.  The
+ * reference has no FFI: its boundary is the process `MOVE_EDSBWTSearch <base>
+ * <patterns>` (mainMove_EDSBWT.cpp:17-62) and, inside it, the class
+ * MOVE_EDSBWT (MOVE_EDSBWTSearch.hpp:54-136).  Each entry point below names the
+ * reference interface it replaces.  Plain pointers and sizes only.
+ *
+ * Conventions: 0 on success, a negative EDSBWT_E_* code on failure (never exit());
+ * the message is in edsbwt_last_error() (thread-local).  One index per device;
+ * calls on distinct handles are thread-safe, calls on one handle are serialized
+ * by the caller.
+ */
+#ifndef EDSBWT_H
+#define EDSBWT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EDSBWT_ABI_VERSION 1
+
+enum {
+    EDSBWT_OK = 0,
+    EDSBWT_E_IO = -1,          /* cannot open / short read of an index file */
+    EDSBWT_E_FORMAT = -2,      /* index file contents inconsistent */
+    EDSBWT_E_UNSUPPORTED = -3, /* e.g. alphabet larger than the device layout supports */
+    EDSBWT_E_DEVICE = -4,      /* HIP runtime error */
+    EDSBWT_E_ARG = -5,         /* bad argument */
+    EDSBWT_E_NOMEM = -6        /* host or device allocation failed */
+};
+
+/* search flags */
+#define EDSBWT_COUNT_ONLY   0x1u /* counts only; RECOVERBW=0 of the legacy engine (README.md:42-45) */
+#define EDSBWT_LOCATE       0x2u /* counts + occurrence records (MOVE engine default, MOVE_EDSBWTSearch.cpp:328-369) */
+#define EDSBWT_LOCATE_TABLE 0x4u /* with LOCATE: read (word, offset) from the per-row table
+                                    instead of walking LF to '#'; identical records */
+#define EDSBWT_PROFILE      0x8u /* record per-kernel HIP-event times into edsbwt_stats */
+
+typedef struct edsbwt_index edsbwt_index;
+
+/* One output row of <patterns>output_M_LF.csv (MOVE_EDSBWTSearch.cpp:365):
+ * #Pat, $_i (word id), D[i] (1-based segment), S_j (word in segment), S_j[r] (offset). */
+typedef struct {
+    uint32_t pat, word, seg, word_in_seg, offset;
+} edsbwt_occ;
+
+/* Loaded-index facts (recoverInfo, MOVE_EDSBWTSearch.cpp:628-770). */
+typedef struct {
+    uint64_t n_rows;      /* lengthTot_plus_eof */
+    uint64_t n_words;     /* nText */
+    uint64_t n_segments;  /* ones in <base>.bitvector */
+    uint32_t sigma;       /* sizeAlpha */
+    uint8_t alphabet[16]; /* alphaInverse[0..sigma) */
+    uint64_t device_bytes;/* HBM held by the index */
+} edsbwt_index_info;
+
+/* Per-call counters and timings (filled by every edsbwt_search*). */
+typedef struct {
+    uint64_t patterns, found, not_found, occurrences;
+    uint64_t depths;          /* trie depths processed */
+    uint64_t trie_nodes;      /* Σ nodes over depths */
+    uint64_t intervals_stepped;/* backward_search_step work items (each = 2 rank queries) */
+    uint64_t link_hash_rows;  /* '#' rows read by link (dollars_in_interval) */
+    uint64_t link_ranges;     /* merged previous-segment ranges produced by link */
+    uint64_t locate_lf_steps; /* LF steps of the locate walk (0 with LOCATE_TABLE) */
+    double ms_total;          /* device time of the call (hipEvent) */
+    double ms_kernel[16];     /* EDSBWT_PROFILE: per kernel class, see edsbwt_kernel_name */
+    uint64_t launches_kernel[16];
+    uint64_t bytes_kernel[16];/* algorithmic bytes per kernel class */
+} edsbwt_stats;
+
+/* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,
+ * 178-218, 628-770) and build_MLF (build_MLF.cpp:53-164): reads <base>_info.aux,
+ * <base>.ebwt (or the _bwt_<j>.aux piles) and <base>.bitvector, builds the device
+ * rank/LF table and segment tables on `device`.  a_balance is the build_MLF `a`
+ * parameter (kept for CLI compatibility; the device LF table does not need it). */
+int edsbwt_index_open(const char* base, int device, uint32_t a_balance, edsbwt_index** out);
+void edsbwt_index_close(edsbwt_index* idx);
+int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info);
+
+/* Replaces the pattern loop + backwardSearch (MOVE_EDSBWTSearch.cpp:97-155, 228-374).
+ * Patterns are pat_bytes[pat_offsets[i] .. pat_offsets[i+1]) (host memory, no
+ * terminator), i < npat; pattern i is reported as #Pat = first_pattern_id + i.
+ * counts[npat] (caller-owned) receives backwardSearch's return value per pattern.
+ * With EDSBWT_LOCATE, *occ (library-owned, free with edsbwt_occ_free) receives
+ * *nocc records in reference order: pattern-major, then interval order, rows
+ * ascending — the order of <patterns>output_M_LF.csv. */
+int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_offsets,
+                  uint64_t npat, uint32_t first_pattern_id, uint32_t flags,
+                  uint32_t* counts, edsbwt_occ** occ, uint64_t* nocc);
+void edsbwt_occ_free(edsbwt_occ* occ);
+
+/* Device-resident variant (benchmarks, multi-GPU shards): d_bytes / d_offsets /
+ * d_counts are device pointers on the index's device; occurrence records stay in
+ * a library-owned device buffer returned through *d_occ (valid until the next
+ * call on this index).  `stream` is a hipStream_t (NULL = the index's stream). */
+int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                         uint64_t npat, uint32_t first_pattern_id, uint32_t flags,
+                         uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc, void* stream);
+
+/* Counters/timings of the last search on this index. */
+int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st);
+const char* edsbwt_kernel_name(int k);
+
+/* Format records as the reference CSV body (no header), one row per record:
+ * "%u\t%u\t%u\t%u\t%u\n" (MOVE_EDSBWTSearch.cpp:365).  Returns bytes written, or
+ * the size needed when buf is NULL.  Multi-threaded. */
+uint64_t edsbwt_format_csv(const edsbwt_occ* occ, uint64_t nocc, char* buf, uint64_t cap, int threads);
+
+const char* edsbwt_last_error(void);
+int edsbwt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,50 @@
+"""The C-ABI library loads and exports every symbol include/edsbwt.h declares
+(no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def _declared():
+    hdr = open(os.path.join(ROOT, "include", "edsbwt.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(edsbwt_[a-z_]+)\s*\(", hdr)))
+
+
+def test_header_symbols_exported(edsbwt):
+    L = edsbwt.lib()
+    names = _declared()
+    assert "edsbwt_search" in names and "edsbwt_index_open" in names
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.edsbwt_abi_version() == 1
+
+
+def test_open_missing_index_fails_cleanly(edsbwt, tmp_path):
+    import pytest
+    with pytest.raises(edsbwt.EdsBwtError) as e:
+        edsbwt.Index(str(tmp_path / "nope"))
+    assert e.value.code in (-1, -4)
+
+
+def test_format_csv(edsbwt):
+    import numpy as np
+    occ = np.zeros(3, edsbwt.OCC_DTYPE)
+    occ["pat"] = [1, 1, 12]
+    occ["word"] = [3, 4000000000, 0]
+    occ["seg"] = [2, 3, 1]
+    occ["offset"] = [0, 1, 99]
+    assert edsbwt.format_csv(occ, threads=2) == b"1\t3\t2\t0\t0\n1\t4000000000\t3\t0\t1\n12\t0\t1\t0\t99\n"
+
+
+def test_read_pattern_file_getline(edsbwt, tmp_path):
+    p = tmp_path / "p.txt"
+    p.write_bytes(b"ACG\nT\r\n\nGG")
+    buf, offs = edsbwt.read_pattern_file(str(p))
+    pats = [bytes(buf[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+    assert pats == [b"ACG", b"T\r", b"", b"GG"]
+    p.write_bytes(b"A\nC\n")
+    buf, offs = edsbwt.read_pattern_file(str(p))
+    assert len(offs) == 3

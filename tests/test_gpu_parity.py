@@ -1,0 +1,93 @@
+"""GPU parity: libedsbwt.so (hand-written gfx950 kernels) vs the oracle, bit-exact.
+
+Counts per pattern and the occurrence records — including their order, which is
+the order of <patterns>output_M_LF.csv — must equal the oracle's on the same index."""
+import os
+import random
+import shutil
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+import edsgen
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(pats):
+    bs = [p.encode() if isinstance(p, str) else p for p in pats]
+    buf = np.frombuffer(b"".join(bs), np.uint8) if bs else np.zeros(0, np.uint8)
+    offs = np.concatenate(([0], np.cumsum([len(p) for p in bs]))).astype(np.uint64)
+    return buf, offs
+
+
+def _build(oracle, tmp_path, text, name="idx"):
+    (tmp_path / f"{name}.eds").write_text(text)
+    base = str(tmp_path / name)
+    oracle.transform(str(tmp_path / f"{name}.eds"), base)
+    return base
+
+
+def _compare(oracle, edsbwt, base, pats, table_too=True):
+    buf, offs = _pack(pats)
+    eng = oracle.Engine(base, 8)
+    oc, oo, _ = eng.search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc)
+        assert np.array_equal(go, oo), (go[:10], oo[:10])
+        gc2, go2 = idx.search((buf, offs), locate=False)
+        assert np.array_equal(gc2, oc) and go2.size == 0
+        if table_too:
+            gc3, go3 = idx.search((buf, offs), table=True)
+            assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)
+        st = idx.stats()
+        assert st["found"] == int((oc > 0).sum())
+    return oc, oo
+
+
+def test_readme_kat_gpu(oracle, edsbwt, tmp_path):
+    base = _build(oracle, tmp_path, open(os.path.join(GOLDEN, "test.eds")).read(), "test")
+    oc, oo = _compare(oracle, edsbwt, base, ["TATT", "ACT", "TTAT"])
+    assert [tuple(int(x) for x in r) for r in oo] == [(1, 3, 2, 0, 0), (1, 4, 3, 0, 1), (1, 7, 4, 0, 1), (1, 1, 1, 1, 0),
+                                                      (3, 0, 1, 0, 1), (3, 4, 3, 0, 0), (3, 7, 4, 0, 0)]
+
+
+def test_move_edsbwt_mirror_csv(oracle, edsbwt, tmp_path):
+    base = _build(oracle, tmp_path, open(os.path.join(GOLDEN, "test.eds")).read(), "test")
+    shutil.copy(os.path.join(GOLDEN, "kmers.txt"), tmp_path / "kmers.txt")
+    m = edsbwt.MoveEDSBWT(base, str(tmp_path / "kmers.txt"))
+    assert (m.count_found, m.count_not_found) == (1, 6)
+    assert open(tmp_path / "kmers.txtoutput_M_LF.csv", "rb").read() == \
+        b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n1\t0\t1\t0\t1\n1\t4\t3\t0\t0\n1\t7\t4\t0\t0\n"
+
+
+def test_example_paper_gpu(oracle, edsbwt, tmp_path):
+    base = _build(oracle, tmp_path, open(os.path.join(GOLDEN, "examplePaper.eds")).read(), "ex")
+    _compare(oracle, edsbwt, base, ["TAC", "A", "CTA", "GTCT", "ACTAC", "Q", "", "T"])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_eds_gpu(oracle, edsbwt, tmp_path, seed):
+    rng = random.Random(100 + seed)
+    segs = edsgen.random_eds(rng, rng.randint(20, 400), alphabet="ACGT" if seed % 3 else "ACGTN",
+                             lmax=3 + seed, p_empty=0.0 if seed % 4 == 0 else 0.25)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = []
+    for _ in range(400):
+        m = rng.randint(1, 24)
+        p = edsgen.planted(rng, segs, m) if rng.random() < 0.6 else None
+        pats.append(p or "".join(rng.choice("ACGT") for _ in range(m)))
+    pats += pats[:40]                     # duplicates share trie nodes
+    pats += ["ACGTX", "NNNN", "#A", "A#", "AC\r"]  # bytes outside / the end-marker itself
+    _compare(oracle, edsbwt, base, pats)
+
+
+def test_larger_eds_gpu(oracle, edsbwt, tmp_path):
+    rng = random.Random(5)
+    segs = edsgen.random_eds(rng, 6000, lmax=7, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.choice([8, 12, 20, 31])) or "ACGT" for _ in range(3000)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(20)) for _ in range(3000)]
+    _compare(oracle, edsbwt, base, pats)
