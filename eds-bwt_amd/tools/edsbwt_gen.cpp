@@ -1,0 +1,163 @@
+// eds-bwt_amd/tools/edsbwt_gen.cpp — synthetic EDS and pattern generators for the
+// benchmark configurations of SURVEY.md §8(d) (seeded, reproducible).
+//
+//   edsbwt_gen eds --config c2|c3|c5 --chars N --seed S --out file.eds
+//     c2: segments of k~U{1..5} strings, each of length U{1..7}, uniform ACGT
+//     c3: "COVID-like": a solid segment (1 string, length U{50..150}) then a variant
+//         segment (k~U{2..4} strings, each empty with p=0.1, else length U{1..3})
+//     c5: c2 where 20% of the segments with k>=2 replace one string by the empty word
+//   edsbwt_gen patterns --eds file.eds --count P --seed S --out file.txt
+//                       [--len L | --lens 8,16,32,64] [--mode random|planted|mixed]
+//     planted: spelled along a random path (start segment, word and offset uniform,
+//     then a uniform word of each following segment; empty words add nothing), as
+//     extract_patterns_from_msa.py:30-60 samples k-mers from real sequences.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "eds_common.h"
+
+using namespace edsbwt_tools;
+
+static const char ACGT[4] = {'A', 'C', 'G', 'T'};
+
+static int gen_eds(const std::string& cfg, uint64_t chars, uint64_t seed, const std::string& out) {
+    Rng R(seed);
+    std::string s;
+    s.reserve(chars + chars / 2 + 64);
+    uint64_t n = 0;
+    bool solid = true;
+    auto word = [&](uint64_t len) { for (uint64_t i = 0; i < len; i++) s.push_back(ACGT[R.below(4)]); n += len; };
+    while (n < chars) {
+        s.push_back('{');
+        if (cfg == "c3") {
+            if (solid) {
+                word(R.uni(50, 150));
+            } else {
+                const uint64_t k = R.uni(2, 4);
+                for (uint64_t i = 0; i < k; i++) {
+                    if (i) s.push_back(',');
+                    if (R.unit() >= 0.1) word(R.uni(1, 3));
+                }
+            }
+            solid = !solid;
+        } else {
+            const uint64_t k = R.uni(1, 5);
+            uint64_t empty_at = ~0ull;
+            if (cfg == "c5" && k >= 2 && R.unit() < 0.2) empty_at = R.below(k);
+            for (uint64_t i = 0; i < k; i++) {
+                if (i) s.push_back(',');
+                const uint64_t len = R.uni(1, 7);
+                if (i == empty_at) continue;
+                word(len);
+            }
+        }
+        s.push_back('}');
+    }
+    FILE* f = std::fopen(out.c_str(), "wb");
+    if (!f) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
+    std::fwrite(s.data(), 1, s.size(), f);
+    std::fclose(f);
+    std::fprintf(stderr, "edsbwt_gen: %s with %llu chars (%zu bytes)\n", out.c_str(), (unsigned long long)n, s.size());
+    return 0;
+}
+
+static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t seed, const std::vector<uint64_t>& lens,
+                        const std::string& mode, const std::string& out) {
+    Rng R(seed);
+    Eds E;
+    std::vector<uint64_t> seg_first;  // first word of each segment
+    if (mode != "random") {
+        E = parse_eds(read_all(eds_path));
+        for (uint64_t w = 0; w < E.wstart.size(); w++)
+            if (E.first[w]) seg_first.push_back(w);
+        seg_first.push_back(E.wstart.size());
+    }
+    const uint64_t S = seg_first.empty() ? 0 : seg_first.size() - 1;
+    auto wlen = [&](uint64_t w) {
+        const uint64_t e = (w + 1 < E.wstart.size() ? E.wstart[w + 1] : E.text.size()) - 1;
+        uint64_t l = e - E.wstart[w];
+        if (l == 1 && E.text[E.wstart[w]] == 'Z') l = 0;  // the empty word
+        return l;
+    };
+    std::string s;
+    s.reserve(count * (lens.back() + 1));
+    std::string p;
+    for (uint64_t i = 0; i < count; i++) {
+        const uint64_t m = lens[R.below(lens.size())];
+        bool plant = (mode == "planted") || (mode == "mixed" && (R.next() & 1));
+        p.clear();
+        if (plant) {
+            for (int attempt = 0; attempt < 1000 && p.size() < m; attempt++) {
+                p.clear();
+                uint64_t sg = R.below(S);
+                uint64_t w = seg_first[sg] + R.below(seg_first[sg + 1] - seg_first[sg]);
+                uint64_t l = wlen(w);
+                if (!l) continue;
+                uint64_t o = R.below(l);
+                for (;;) {
+                    for (uint64_t t = o; t < l && p.size() < m; t++) p.push_back((char)E.text[E.wstart[w] + t]);
+                    if (p.size() >= m || ++sg >= S) break;
+                    w = seg_first[sg] + R.below(seg_first[sg + 1] - seg_first[sg]);
+                    l = wlen(w);
+                    o = 0;
+                }
+            }
+        }
+        if (p.size() < m) {
+            p.clear();
+            for (uint64_t t = 0; t < m; t++) p.push_back(ACGT[R.below(4)]);
+        }
+        s += p;
+        s.push_back('\n');
+    }
+    FILE* f = std::fopen(out.c_str(), "wb");
+    if (!f) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
+    std::fwrite(s.data(), 1, s.size(), f);
+    std::fclose(f);
+    std::fprintf(stderr, "edsbwt_gen: %llu patterns (%s) -> %s\n", (unsigned long long)count, mode.c_str(), out.c_str());
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s eds --config c2|c3|c5 --chars N --seed S --out F\n"
+                             "       %s patterns --eds F --count P --seed S --out F [--len L|--lens a,b,..] [--mode random|planted|mixed]\n",
+                     argv[0], argv[0]);
+        return 1;
+    }
+    std::string cmd = argv[1], cfg = "c2", out, eds, mode = "random";
+    uint64_t chars = 1000000, seed = 1, count = 1000;
+    std::vector<uint64_t> lens{20};
+    for (int i = 2; i + 1 < argc; i += 2) {
+        std::string k = argv[i], v = argv[i + 1];
+        if (k == "--config") cfg = v;
+        else if (k == "--chars") chars = std::stoull(v);
+        else if (k == "--seed") seed = std::stoull(v);
+        else if (k == "--out") out = v;
+        else if (k == "--eds") eds = v;
+        else if (k == "--count") count = std::stoull(v);
+        else if (k == "--len") lens = {std::stoull(v)};
+        else if (k == "--lens") {
+            lens.clear();
+            size_t a = 0;
+            while (a < v.size()) {
+                size_t b = v.find(',', a);
+                if (b == std::string::npos) b = v.size();
+                lens.push_back(std::stoull(v.substr(a, b - a)));
+                a = b + 1;
+            }
+        } else if (k == "--mode") mode = v;
+        else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 1; }
+    }
+    try {
+        if (cmd == "eds") return gen_eds(cfg, chars, seed, out);
+        if (cmd == "patterns") return gen_patterns(eds, count, seed, lens, mode, out);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        return 1;
+    }
+    std::fprintf(stderr, "unknown command %s\n", cmd.c_str());
+    return 1;
+}

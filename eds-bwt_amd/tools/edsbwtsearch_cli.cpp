@@ -1,0 +1,125 @@
+// eds-bwt_amd/tools/edsbwtsearch_cli.cpp — the EDSBWTsearch / MOVE_EDSBWTSearch CLI.
+//
+//   EDSBWTsearch <index_base> <pattern_file> [--device D] [--quiet] [--count-only] [--table]
+//
+// Same argv, files and console contract as mainMove_EDSBWT.cpp:17-62 driving
+// MOVE_EDSBWT::MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:23-176):
+//   * wrong argc → usage on stderr, exit 1 (:19-25); success also exits 1 (:61);
+//   * writes <pattern_file>output_M_LF.csv with header "#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n" (:55-64);
+//   * stdout: banner, index summary, per pattern "Pattern: <p> of length <n>" and
+//     "num occ <k>" (:113,:371), then "bs took:<secs>" without a newline (:145);
+//   * stderr: "OCCORRENZA DI: <p> TROVATA|NON TROVATA" per pattern (:124,:129), then
+//     "count_found = N" / "count_not_found = M" (:154-155) — the lines the
+//     reference's scripts grep (launch_COVID.sh:106-108).
+// --quiet drops the per-pattern lines (they dominate console time at 10^7 patterns).
+// The search itself runs on the GPU through libedsbwt.so (include/edsbwt.h).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/edsbwt.h"
+
+int main(int argc, char** argv) {
+    std::vector<std::string> pos;
+    int device = 0;
+    bool quiet = false, count_only = false, table = false;
+    for (int i = 1; i < argc; i++) {
+        if (!std::strcmp(argv[i], "--quiet")) quiet = true;
+        else if (!std::strcmp(argv[i], "--count-only")) count_only = true;
+        else if (!std::strcmp(argv[i], "--table")) table = true;
+        else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+        else pos.push_back(argv[i]);
+    }
+    if (pos.size() != 2) {
+        std::fprintf(stderr, "usage: %s inputEBWTfileName inputPATTERNfile\n", argv[0]);
+        std::fprintf(stderr, "where:\n");
+        std::fprintf(stderr, "  inputEBWTfile is the BWT filename without the extension .ebwt (and .ebwt.qs for the QS string)\n");
+        std::fprintf(stderr, "  inputPATTERNfile is the pattern file\n");
+        return 1;
+    }
+    const std::string base = pos[0], pfile = pos[1];
+    std::printf("BCR_eds: %s\nBCR_eds: The input ebwt file is %s\nBCR_eds: The pattern file is %s\n", argv[0], base.c_str(), pfile.c_str());
+    std::fprintf(stderr, "Backward Search\n");
+    edsbwt_index* idx = nullptr;
+    int rc = edsbwt_index_open(base.c_str(), device, 8, &idx);
+    if (rc) {
+        std::fprintf(stderr, "%s\n", edsbwt_last_error());
+        return 1;
+    }
+    edsbwt_index_info info;
+    edsbwt_index_get_info(idx, &info);
+    std::printf("\nFrom %s_info.aux file:\n\tNumber of sequences: %llu\n\tTotal length (with $): %llu\n\tSize alpha: %u\n\tAlphabet: ",
+                base.c_str(), (unsigned long long)info.n_words, (unsigned long long)info.n_rows, info.sigma);
+    for (uint32_t j = 0; j < info.sigma; j++) std::printf("%c\t", info.alphabet[j]);
+    std::printf("\nBitVector size: %llu\n", (unsigned long long)info.n_words);
+    // patterns: std::getline semantics (:111)
+    FILE* f = std::fopen(pfile.c_str(), "rb");
+    if (!f) {
+        std::fprintf(stderr, "Error opening %s\n", pfile.c_str());
+        return 1;
+    }
+    std::vector<char> raw;
+    {
+        char buf[1 << 16];
+        size_t n;
+        while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + n);
+        std::fclose(f);
+    }
+    std::vector<char> bytes;
+    std::vector<uint64_t> offs{0};
+    bytes.reserve(raw.size());
+    for (size_t s = 0; s < raw.size();) {
+        size_t e = s;
+        while (e < raw.size() && raw[e] != '\n') e++;
+        bytes.insert(bytes.end(), raw.begin() + s, raw.begin() + e);
+        offs.push_back(bytes.size());
+        s = e + 1;
+    }
+    const uint64_t npat = offs.size() - 1;
+    const std::string out = pfile + "output_M_LF.csv";
+    FILE* fo = std::fopen(out.c_str(), "wb");
+    if (!fo) {
+        std::fprintf(stderr, "ERROR opening file %s to write output\n", out.c_str());
+        return 1;
+    }
+    std::fputs("#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n", fo);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint32_t> counts(npat + 1, 0);
+    edsbwt_occ* occ = nullptr;
+    uint64_t nocc = 0;
+    uint32_t flags = count_only ? EDSBWT_COUNT_ONLY : (EDSBWT_LOCATE | (table ? EDSBWT_LOCATE_TABLE : 0));
+    rc = edsbwt_search(idx, bytes.data(), offs.data(), npat, 1, flags, counts.data(), &occ, &nocc);
+    if (rc) {
+        std::fprintf(stderr, "%s\n", edsbwt_last_error());
+        return 1;
+    }
+    if (nocc) {
+        const uint64_t sz = edsbwt_format_csv(occ, nocc, nullptr, 0, 16);
+        std::vector<char> csv(sz);
+        edsbwt_format_csv(occ, nocc, csv.data(), sz, 16);
+        std::fwrite(csv.data(), 1, sz, fo);
+    }
+    std::fclose(fo);
+    uint64_t found = 0;
+    for (uint64_t i = 0; i < npat; i++) {
+        const bool ok = counts[i] > 0;
+        found += ok;
+        if (!quiet) {
+            const std::string p(bytes.data() + offs[i], bytes.data() + offs[i + 1]);
+            std::printf("Pattern: %s of length %zu\nnum occ %u\n", p.c_str(), p.size(), counts[i]);
+            std::fprintf(stderr, "OCCORRENZA DI: %s %s\n", p.c_str(), ok ? "TROVATA" : "NON TROVATA");
+        }
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("bs took:%g", secs);
+    std::fflush(stdout);
+    std::fprintf(stderr, "\ncount_found = %llu\ncount_not_found = %llu\n", (unsigned long long)found, (unsigned long long)(npat - found));
+    std::fprintf(stderr, count_only ? "\nThe search is finished! \n" : "\nThe csv file is ready! \n");
+    std::fprintf(stderr, "The End!\n");
+    edsbwt_occ_free(occ);
+    edsbwt_index_close(idx);
+    return 1;  // mainMove_EDSBWT.cpp:61
+}
