@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -78,8 +79,16 @@ struct DBuf {
     }
 };
 
-enum KClass { KC_TRIE = 0, KC_NODES, KC_EXPAND, KC_LINK, KC_STEP, KC_MERGE, KC_FINISH, KC_LOCATE, KC_SCAN, KC_TABLE, KC_COUNT };
-static const char* kKNames[KC_COUNT] = {"trie_sort", "trie_nodes", "expand", "link", "step", "merge", "finish", "locate", "scan", "table"};
+enum KClass { KC_TRIE = 0, KC_NODES, KC_EXPAND, KC_LINK, KC_LINKSORT, KC_STEP, KC_MERGE, KC_FINISH, KC_DEEP, KC_LOCPREP, KC_LOCATE, KC_SCAN,
+              KC_TABLE, KC_COUNT };
+static const char* kKNames[KC_COUNT] = {"trie_sort", "trie_nodes", "expand", "link", "link_sort", "step", "merge", "finish",
+                                        "deep", "locate_prep", "locate", "scan", "table"};
+// k_deep keeps at most kDeepK intervals per list in registers
+constexpr int kDeepK = 8;
+// switch to k_deep once depth-D nodes >= kDeepShare x patterns of length >= D
+constexpr double kDeepShare = 0.7;
+// ... and once a depth's lists average at most kDeepItems intervals per node
+constexpr double kDeepItems = 2.0;
 
 struct Engine {
     int device = 0;
@@ -110,12 +119,21 @@ struct Engine {
     DBuf<edsbwt_occ> rec;
     DBuf<unsigned long long> counters;
     DBuf<uint8_t> tmp;      // hipcub temp storage
+    DBuf<unsigned long long> lhist;
+    DBuf<uint32_t> ovf_orig, ovf_scan, sub_map, sub_rcnt, sub_rocc;
+    DBuf<uint64_t> sub_len, sub_off, sub_roff;
+    DBuf<uint8_t> sub_bytes, fin;
+    DBuf<uint32_t> lcnt, ck_u, ck_k, ck_e, gcnt, gfill, goff, gend, gb, gee, fv, fv2, fend, hterm;
+    DBuf<uint64_t> fk, fk2, ekeys, efk;
+    DBuf<uint32_t> eu, eb, ee, eck_u, eck_k, eck_e, efv, shpre;
+    uint32_t* pinned_big = nullptr;  // host shard counters + prefix
     DBuf<uint8_t> hbytes;   // host-API pattern staging
     DBuf<uint64_t> hoffs;
     DBuf<uint32_t> hcounts;
     edsbwt_stats st{};
     // profiling
     bool prof = false;
+    bool trace = std::getenv("EDSBWT_TRACE") != nullptr;
     struct Ev { int k; hipEvent_t a, b; };
     std::vector<Ev> evs, ev_pool;
 
@@ -174,6 +192,68 @@ struct Engine {
     }
     void zero(void* p, size_t bytes) { if (bytes) HIPCHK(hipMemsetAsync(p, 0, bytes, stream)); }
 
+    // ---- sharded appends (kernels.hip NSHARD): per-shard counters on the host
+    std::vector<uint32_t> hsh = std::vector<uint32_t>(NSHARD * 32, 0);
+    void fetch_shards() {
+        HIPCHK(hipMemcpyAsync(pinned_big, lcnt.p, NSHARD * 32 * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        std::memcpy(hsh.data(), pinned_big, NSHARD * 32 * 4);
+    }
+    std::vector<uint32_t> shard_counts(int k) const {
+        std::vector<uint32_t> v(NSHARD);
+        for (uint32_t sh = 0; sh < NSHARD; sh++) v[sh] = hsh[sh * 32 + k];
+        return v;
+    }
+    // most items one shard can receive from a launch over n inputs (<= fanout each)
+    static size_t shard_bound(size_t n, size_t fanout) {
+        const size_t G = grid_for(n), iters = (n + G * 256 - 1) / (G * 256);
+        return ((G + NSHARD - 1) / NSHARD) * 256 * iters * fanout;
+    }
+    uint32_t shard_max(int k) const {
+        uint32_t m = 0;
+        for (uint32_t sh = 0; sh < NSHARD; sh++) m = std::max(m, hsh[sh * 32 + k]);
+        return m;
+    }
+    uint32_t shard_total(int k) const {
+        uint64_t t = 0;
+        for (uint32_t sh = 0; sh < NSHARD; sh++) t += hsh[sh * 32 + k];
+        if (t > 0xffffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^32 items at one depth");
+        return (uint32_t)t;
+    }
+    void upload_prefix(int k) {
+        uint32_t* pre = pinned_big + NSHARD * 32;
+        pre[0] = 0;
+        for (uint32_t sh = 0; sh < NSHARD; sh++) pre[sh + 1] = pre[sh] + hsh[sh * 32 + k];
+        shpre.ensure(NSHARD + 1);
+        HIPCHK(hipMemcpyAsync(shpre.p, pre, (NSHARD + 1) * 4, hipMemcpyHostToDevice, stream));
+    }
+    template <typename A, typename B, typename C>
+    void unshard3(int k, size_t cap, const A* a, const B* b, const C* c, A* oa, B* ob, C* oc, uint32_t total) {
+        upload_prefix(k);
+        launch(KC_MERGE, k_unshard<A, B, C>, total, total, (const uint32_t*)shpre.p, (uint32_t)cap, a, b, c, oa, ob, oc);
+    }
+    template <typename A, typename B>
+    void unshard2(int k, size_t cap, const A* a, const B* b, A* oa, B* ob, uint32_t total) {
+        unshard3<A, B, uint8_t>(k, cap, a, b, (const uint8_t*)nullptr, oa, ob, (uint8_t*)nullptr, total);
+    }
+    template <typename A>
+    void unshard1(int k, size_t cap, const A* a, A* oa, uint32_t total) {
+        unshard3<A, uint8_t, uint8_t>(k, cap, a, (const uint8_t*)nullptr, (const uint8_t*)nullptr, oa, (uint8_t*)nullptr, (uint8_t*)nullptr, total);
+    }
+    // grow three sharded buffers from cap to ncap per shard, keeping keep[sh] items of each shard
+    void regrow3(DBuf<uint32_t>& a, DBuf<uint32_t>& b, DBuf<uint32_t>& c, size_t cap, size_t ncap, const std::vector<uint32_t>& keep) {
+        for (DBuf<uint32_t>* x : {&a, &b, &c}) {
+            DBuf<uint32_t> n;
+            n.ensure(ncap * NSHARD);
+            for (uint32_t sh = 0; sh < NSHARD; sh++)
+                HIPCHK(hipMemcpyAsync(n.p + sh * ncap, x->p + sh * cap, (size_t)keep[sh] * 4, hipMemcpyDeviceToDevice, stream));
+            std::swap(n.p, x->p);
+            std::swap(n.cap, x->cap);
+            HIPCHK(hipStreamSynchronize(stream));
+            n.release();
+        }
+    }
+
     // out[0..n] = exclusive prefix sum of in[0..n); returns out[n]
     uint32_t scan_u32(const uint32_t* in, DBuf<uint32_t>& out, size_t n) {
         out.ensure(n + 1);
@@ -206,6 +286,7 @@ struct Engine {
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         HIPCHK(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&pinned_big, (NSHARD * 32 + NSHARD + 8) * 4, hipHostMallocDefault));
         HostIndex H;
         std::string err;
         int rc = read_host_index(base, H, err);
@@ -295,7 +376,7 @@ struct Engine {
         up(seg_lo, slo);
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
-        counters.ensure(8);
+        counters.ensure(16);
     }
 
     void build_table() {
@@ -314,44 +395,35 @@ struct Engine {
     }
 
     // ------------------------------------------------------------ search
-    // d_bytes/d_off/d_counts are device pointers; returns number of records
-    uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
-        st = edsbwt_stats{};
-        prof = (flags & EDSBWT_PROFILE) != 0;
-        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
-        const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
-        if (use_table) build_table();
-        st.patterns = P;
-        if (P == 0) return 0;
+    // Reversed-pattern trie order: patterns radix-sorted by their reversed symbol
+    // codes, with the common-suffix length of neighbours (lcp).  Nodes of depth D
+    // are then maximal runs with lcp >= D.  Returns false when every pattern is empty.
+    bool build_trie(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t& Lmax, std::vector<unsigned long long>& hist,
+                    std::vector<uint64_t>& ge) {
         if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
-        hipEvent_t e0, e1;
-        HIPCHK(hipEventCreate(&e0));
-        HIPCHK(hipEventCreate(&e1));
-        HIPCHK(hipEventRecord(e0, stream));
-        const KIdx X = kidx();
         // ---- A. lengths, keys, reversed-pattern sort (trie order)
         len.ensure(P);
         launch(KC_TRIE, k_lens, P, d_off, P, len.p);
-        uint32_t Lmax = 0;
+        Lmax = 0;
         {
             size_t tb = 0;
-            counters.ensure(8);
             HIPCHK(hipcub::DeviceReduce::Max(nullptr, tb, len.p, (uint32_t*)counters.p, (int)P, stream));
             tmp.ensure(tb);
             timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceReduce::Max(tmp.p, tb, len.p, (uint32_t*)counters.p, (int)P, stream)); });
             Lmax = read_u32((const uint32_t*)counters.p);
         }
-        res_off.ensure(P);
-        res_cnt.ensure(P);
-        res_occ.ensure(P);
-        zero(res_cnt.p, P * 4);
-        zero(res_occ.p, P * 4);
-        if (Lmax == 0) {
-            HIPCHK(hipMemsetAsync(d_counts, 0, P * 4, stream));
+        if (Lmax == 0) return false;
+        // patterns per length (decides when the trie stops sharing)
+        hist.assign(Lmax + 1, 0);
+        {
+            lhist.ensure(Lmax + 1);
+            zero(lhist.p, (Lmax + 1) * 8);
+            launch(KC_TRIE, k_len_hist, P, (const uint32_t*)len.p, P, Lmax, lhist.p);
+            HIPCHK(hipMemcpyAsync(hist.data(), lhist.p, (Lmax + 1) * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
-            st.not_found = P;
-            return 0;
         }
+        ge.assign(Lmax + 2, 0);  // patterns with length >= l
+        for (int l = (int)Lmax; l >= 0; l--) ge[l] = ge[l + 1] + hist[l];
         const uint32_t nch = (Lmax + 15) / 16;
         keys.ensure((size_t)nch * P);
         launch(KC_TRIE, k_keys, P, d_bytes, d_off, (const uint32_t*)len.p, P, (const uint8_t*)code_of.p, sigma, nch, keys.p);
@@ -372,6 +444,24 @@ struct Engine {
         slen.ensure(P);
         lcp.ensure(P);
         launch(KC_TRIE, k_slen_lcp, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)keys.p, nch, P, slen.p, lcp.p);
+        return true;
+    }
+
+    // Ordered level-synchronous walk over the reversed-pattern trie for the batch (d_bytes,
+    // d_off, P).  Writes res_off/res_cnt/res_occ per pattern (original order) and
+    // appends the final interval lists to the archive.  With allow_deep, switches
+    // to k_deep once the trie stops sharing; patterns k_deep cannot hold are
+    // flagged in ovf_orig (original order) and their number returned.
+    // This path keeps every list in the reference's order (concatenation of the
+    // stepped dollar pile and other pile, adjacent merge, :300-324) and is used for
+    // patterns holding the end-marker '#', whose lists may overlap.
+    uint32_t levels(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, uint64_t* r_off, uint32_t* r_cnt,
+                    uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
+        const KIdx X = kidx();
+        uint32_t Lmax = 0;
+        std::vector<unsigned long long> hist;
+        std::vector<uint64_t> ge;
+        if (!build_trie(d_bytes, d_off, P, Lmax, hist, ge)) return 0;
         // ---- B. root state [(0, N-1)] (init_backward_search, :220-225)
         nid[0].ensure(P);
         nid[1].ensure(P);
@@ -382,26 +472,33 @@ struct Engine {
         ib[0].ensure(1); ie[0].ensure(1); iu[0].ensure(1); ioff[0].ensure(1); iend[0].ensure(1);
         {
             uint32_t h[5] = {0, N - 1, 0, 0, 1};
-            HIPCHK(hipMemcpyAsync(ib[0].p, &h[0], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(ie[0].p, &h[1], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(iu[0].p, &h[2], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(ioff[0].p, &h[3], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(iend[0].p, &h[4], 4, hipMemcpyHostToDevice, stream));
+            std::memcpy(pinned, h, sizeof h);
+            HIPCHK(hipMemcpyAsync(ib[0].p, &pinned[0], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(ie[0].p, &pinned[1], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(iu[0].p, &pinned[2], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(ioff[0].p, &pinned[3], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(iend[0].p, &pinned[4], 4, hipMemcpyHostToDevice, stream));
             HIPCHK(hipStreamSynchronize(stream));
         }
-        uint64_t abase = 0;
-        uint64_t depths = 0;
+        uint32_t novf = 0;
         // ---- C. depth loop
         for (uint32_t d = 0; d < Lmax; d++) {
             const uint32_t D = d + 1;
             const int nxt = cur ^ 1;
-            depths++;
             // children nodes at depth D
             flag.ensure(P);
             launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
             const uint32_t M = scan_u32(flag.p, scan, P);
             if (M == 0) break;
+            // the trie stopped sharing below depth d: finish every pattern alone (k_deep)
+            if (allow_deep && d >= 1 && (double)M >= kDeepShare * (double)ge[D]) {
+                novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, ioff[cur].p, iend[cur].p, ib[cur].p, ie[cur].p, r_off, r_cnt,
+                                r_occ, abase, ovf_orig);
+                break;
+            }
+            st.depths++;
             st.trie_nodes += M;
+            if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, parent intervals %u\n", D, M, ncur);
             node_first.ensure(M);
             node_parent.ensure(M);
             node_char.ensure(M);
@@ -443,7 +540,7 @@ struct Engine {
                         // sentinels (~0) sort last; only the first V keys are used
                         HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream));
                         tmp.ensure(tb);
-                        timed(KC_LINK, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream)); });
+                        timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream)); });
                         rflag.ensure(V);
                         launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, rflag.p);
                         R = scan_u32(rflag.p, rscan, V);
@@ -465,6 +562,7 @@ struct Engine {
                    (const uint32_t*)ioff[cur].p, (const uint32_t*)iend[cur].p, tcnt.p);
             const uint32_t T = scan_u32(tcnt.p, toff, M);
             st.intervals_stepped += T;
+            if (trace) std::fprintf(stderr, "[edsbwt]   link ranges %u, step tasks %u\n", R, T);
             uint32_t R2 = 0;
             if (T) {
                 tb.ensure(T); te.ensure(T); tu.ensure(T); tflag.ensure(T);
@@ -503,15 +601,307 @@ struct Engine {
                 launch(KC_FINISH, k_archive, R2, (uint64_t)R2, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
                        (const uint32_t*)ioff[nxt].p, (const uint32_t*)fcnt.p, (const uint32_t*)foff.p, abase, ab.p, ae.p, node_occ.p);
             }
-            launch(KC_FINISH, k_finish, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
-                   (const uint32_t*)foff.p, (const uint32_t*)fcnt.p, (const uint32_t*)node_occ.p, abase, res_off.p, res_cnt.p, res_occ.p);
+            if (hist[D])
+                launch(KC_FINISH, k_finish, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
+                       (const uint32_t*)foff.p, (const uint32_t*)fcnt.p, (const uint32_t*)node_occ.p, abase, r_off, r_cnt, r_occ);
             abase += F;
             cur = nxt;
             Mcur = M;
             ncur = R2;
             if (R2 == 0) break;  // every deeper suffix has an empty list
         }
-        st.depths = depths;
+        return novf;
+    }
+
+    // Finish every pattern longer than d with k_deep, starting from the lists of its
+    // depth-d node ([goff[u], gend[u]) in gb/ge).  Returns the overflow count.
+    uint32_t run_deep(uint32_t d, uint32_t M, uint64_t P, uint64_t active, const uint8_t* d_bytes, const uint64_t* d_off,
+                      const uint32_t* nid_d, const uint32_t* goff, const uint32_t* gend, const uint32_t* gb, const uint32_t* gee,
+                      uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
+        const KIdx X = kidx();
+        const uint32_t D = d + 1;
+        DBuf<uint32_t>& ovf = tflag;  // per sorted pattern
+        ovf.ensure(P);
+        zero(ovf.p, P * 4);
+        ab.grow_keep(abase + (uint64_t)P * kDeepK, stream);
+        ae.grow_keep(abase + (uint64_t)P * kDeepK, stream);
+        zero(counters.p + 2, 16);
+        launch(KC_DEEP, k_deep<kDeepK>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, (const uint32_t*)len.p, d_off, d_bytes,
+               (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, counters.p);
+        abase += (uint64_t)P * kDeepK;
+        st.deep_from_depth = D;
+        if (trace) std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu\n", D, M, (unsigned long long)active);
+        HIPCHK(hipMemcpyAsync(pinned, counters.p + 2, 16, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        uint64_t dv[2];
+        std::memcpy(dv, pinned, 16);
+        st.intervals_stepped += dv[0];
+        st.link_hash_rows += dv[1];
+        st.bytes_kernel[KC_DEEP] += dv[0] * (2 * 128) + dv[1] * 4 + (uint64_t)P * 24;
+        zero(ovf_orig, P * 4);
+        launch(KC_DEEP, k_ovf_lens, P, P, (const uint32_t*)ovf.p, (const uint32_t*)perm.p, (const uint32_t*)len.p, ovf_orig);
+        const uint32_t novf = scan_u32(ovf.p, tscan, P);
+        st.deep_overflow += novf;
+        return novf;
+    }
+
+    // Order-free level walk (default): a depth's lists are unordered (node, b, e)
+    // items; k_lvl_items steps every item by every child symbol and emits its
+    // '#' rows in the same pass; link keys are sorted per node into previous-segment
+    // runs (k_run_*), which k_lvl_dollar steps.  Same outputs as levels() for
+    // patterns without '#' (finished lists are sorted by row before archiving).
+    uint32_t levels2(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, uint64_t* r_off, uint32_t* r_cnt,
+                     uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
+        const KIdx X = kidx();
+        uint32_t Lmax = 0;
+        std::vector<unsigned long long> hist;
+        std::vector<uint64_t> ge;
+        if (!build_trie(d_bytes, d_off, P, Lmax, hist, ge)) return 0;
+        nid[0].ensure(P);
+        nid[1].ensure(P);
+        zero(nid[0].p, P * 4);
+        int cur = 0;
+        uint32_t Mcur = 1, ncur = 1;
+        ib[0].ensure(1); ie[0].ensure(1); iu[0].ensure(1);
+        {
+            uint32_t h[3] = {0, N - 1, 0};
+            std::memcpy(pinned, h, sizeof h);
+            HIPCHK(hipMemcpyAsync(ib[0].p, &pinned[0], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(ie[0].p, &pinned[1], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(iu[0].p, &pinned[2], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+        }
+        lcnt.ensure(NSHARD * 32);
+        uint32_t novf = 0;
+        for (uint32_t d = 0; d < Lmax; d++) {
+            const uint32_t D = d + 1;
+            const int nxt = cur ^ 1;
+            flag.ensure(P);
+            launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
+            const uint32_t M = scan_u32(flag.p, scan, P);
+            if (M == 0) break;
+            if (allow_deep && d >= 1 && (double)M >= kDeepShare * (double)ge[D] && (double)ncur <= kDeepItems * (double)Mcur) {
+                // group the unordered items by node, then finish patterns one per thread
+                gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur);
+                zero(gcnt.p, (size_t)Mcur * 4);
+                zero(gfill.p, (size_t)Mcur * 4);
+                launch(KC_DEEP, k_group_count, ncur, ncur, (const uint32_t*)iu[cur].p, gcnt.p);
+                scan_u32(gcnt.p, goff, Mcur);
+                gb.ensure(ncur); gee.ensure(ncur);
+                launch(KC_DEEP, k_group_scatter, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p,
+                       (const uint32_t*)goff.p, gfill.p, gb.p, gee.p);
+                launch(KC_DEEP, k_group_end, Mcur, Mcur, (const uint32_t*)goff.p, (const uint32_t*)gcnt.p, gend.p);
+                novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, goff.p, gend.p, gb.p, gee.p, r_off, r_cnt, r_occ, abase, ovf_orig);
+                break;
+            }
+            st.depths++;
+            st.trie_nodes += M;
+            node_first.ensure(M);
+            node_parent.ensure(M);
+            node_char.ensure(M);
+            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, (const uint32_t*)perm.p,
+                   (const uint32_t*)len.p, d_off, d_bytes, (const uint8_t*)code_of.p, sigma, (const uint32_t*)flag.p,
+                   (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
+            child_first.ensure(Mcur);
+            child_end.ensure(Mcur);
+            zero(child_first.p, (size_t)Mcur * 4);
+            zero(child_end.p, (size_t)Mcur * 4);
+            launch(KC_NODES, k_child_links, M, (const uint32_t*)node_parent.p, M, child_first.p, child_end.p);
+            // fused step + '#'-row emission over the current items (sharded appends)
+            size_t cap_next = std::max<size_t>(shard_bound(ncur, 2), 4096);
+            size_t cap_keys = std::max<size_t>(shard_bound(ncur, 1), 4096);
+            size_t cap_chunks = std::max<size_t>(shard_bound(ncur, 1) / 8, 1024);
+            for (;;) {
+                eu.ensure(cap_next * NSHARD); eb.ensure(cap_next * NSHARD); ee.ensure(cap_next * NSHARD);
+                ekeys.ensure(cap_keys * NSHARD);
+                eck_u.ensure(cap_chunks * NSHARD); eck_k.ensure(cap_chunks * NSHARD); eck_e.ensure(cap_chunks * NSHARD);
+                zero(lcnt.p, NSHARD * 32 * 4);
+                if (d > 0)
+                    launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
+                           (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
+                           X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
+                           (uint32_t)cap_chunks);
+                else  // no link before the first step (:246-258)
+                    launch(KC_STEP, k_lvl_items<false>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
+                           (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
+                           X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
+                           (uint32_t)cap_chunks);
+                fetch_shards();
+                const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
+                if (m0 <= cap_next && m1 <= cap_keys && m2 <= cap_chunks) break;
+                cap_next = std::max<size_t>(cap_next, m0 + m0 / 4 + 1024);
+                cap_keys = std::max<size_t>(cap_keys, m1 + m1 / 4 + 1024);
+                cap_chunks = std::max<size_t>(cap_chunks, m2 + m2 / 4 + 256);
+            }
+            uint32_t nchunks = shard_total(2);
+            st.intervals_stepped += ncur;
+            const std::vector<uint32_t> keep_keys = shard_counts(1);
+            if (nchunks) {  // long '#'-row ranges: pack, then one chunk per thread
+                ck_u.ensure(nchunks); ck_k.ensure(nchunks); ck_e.ensure(nchunks);
+                unshard3(2, cap_chunks, eck_u.p, eck_k.p, eck_e.p, ck_u.p, ck_k.p, ck_e.p, nchunks);
+                for (;;) {
+                    launch(KC_LINK, k_lvl_chunks, nchunks, nchunks, (const uint32_t*)ck_u.p, (const uint32_t*)ck_k.p, (const uint32_t*)ck_e.p, X,
+                           lcnt.p, ekeys.p, (uint32_t)cap_keys);
+                    fetch_shards();
+                    const uint32_t m1 = shard_max(1);
+                    if (m1 <= cap_keys) break;
+                    // grow the key shards keeping what k_lvl_items wrote, then redo the chunks
+                    DBuf<uint64_t> nk;
+                    const size_t ncap = m1 + m1 / 4 + 1024;
+                    nk.ensure(ncap * NSHARD);
+                    for (uint32_t sh = 0; sh < NSHARD; sh++)
+                        HIPCHK(hipMemcpyAsync(nk.p + sh * ncap, ekeys.p + sh * cap_keys, (size_t)keep_keys[sh] * 8, hipMemcpyDeviceToDevice, stream));
+                    HIPCHK(hipStreamSynchronize(stream));
+                    std::swap(nk.p, ekeys.p);
+                    std::swap(nk.cap, ekeys.cap);
+                    nk.release();
+                    for (uint32_t sh = 0; sh < NSHARD; sh++) hsh[sh * 32 + 1] = keep_keys[sh];
+                    std::memcpy(pinned_big, hsh.data(), NSHARD * 32 * 4);
+                    HIPCHK(hipMemcpyAsync(lcnt.p, pinned_big, NSHARD * 32 * 4, hipMemcpyHostToDevice, stream));
+                    cap_keys = ncap;
+                }
+            }
+            const uint32_t nkeys = shard_total(1);
+            st.link_hash_rows += nkeys;
+            uint32_t R = 0;
+            if (nkeys) {
+                lkeys.ensure(nkeys);
+                lkeys2.ensure(nkeys);
+                unshard1(1, cap_keys, ekeys.p, lkeys.p, nkeys);
+                int endbit = 33;
+                while (endbit < 64 && ((uint64_t)Mcur >> (endbit - 32))) endbit++;
+                size_t tb = 0;
+                HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream));
+                tmp.ensure(tb);
+                timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream)); });
+                rflag.ensure(nkeys);
+                launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, rflag.p);
+                R = scan_u32(rflag.p, rscan, nkeys);
+                rb.ensure(R); re.ensure(R); ru.ensure(R);
+                launch(KC_LINK, k_run_build, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
+                       (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p);
+                st.link_ranges += R;
+                st.intervals_stepped += R;
+                const std::vector<uint32_t> keep_items = shard_counts(0);
+                for (;;) {
+                    launch(KC_STEP, k_lvl_dollar, R, R, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
+                           (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p, X, eu.p, eb.p, ee.p,
+                           (uint32_t)cap_next, lcnt.p);
+                    fetch_shards();
+                    const uint32_t m0 = shard_max(0);
+                    if (m0 <= cap_next) break;
+                    // grow the item shards keeping k_lvl_items' output, then redo the dollar step
+                    const size_t ncap = m0 + m0 / 4 + 1024;
+                    regrow3(eu, eb, ee, cap_next, ncap, keep_items);
+                    for (uint32_t sh = 0; sh < NSHARD; sh++) hsh[sh * 32 + 0] = keep_items[sh];
+                    std::memcpy(pinned_big, hsh.data(), NSHARD * 32 * 4);
+                    HIPCHK(hipMemcpyAsync(lcnt.p, pinned_big, NSHARD * 32 * 4, hipMemcpyHostToDevice, stream));
+                    cap_next = ncap;
+                }
+                st.bytes_kernel[KC_STEP] += (uint64_t)R * (12 + 2 * 128);
+            }
+            const uint32_t nnext = shard_total(0);
+            st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * 128) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
+            ib[nxt].ensure(nnext); ie[nxt].ensure(nnext); iu[nxt].ensure(nnext);
+            if (nnext) unshard3(0, cap_next, eu.p, eb.p, ee.p, iu[nxt].p, ib[nxt].p, ie[nxt].p, nnext);
+            if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
+                                    ncur, nkeys, R, nnext);
+            // finish patterns of length D: their node's items, sorted by row
+            if (hist[D]) {
+                fin.ensure(M);
+                launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
+                node_occ.ensure(M);
+                zero(node_occ.p, (size_t)M * 4);
+                const size_t cap_fin = shard_bound(nnext, 1);
+                efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD);
+                zero(lcnt.p, NSHARD * 32 * 4);
+                launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
+                       (const uint8_t*)fin.p, lcnt.p, efk.p, efv.p, (uint32_t)cap_fin, node_occ.p);
+                fetch_shards();
+                if (shard_max(4) > cap_fin) throw Fail(EDSBWT_E_DEVICE, "finisher shard overflow");  // cap_fin >= items per shard
+                const uint32_t F = shard_total(4);
+                fk.ensure(F); fv.ensure(F);
+                if (F) unshard2(4, cap_fin, efk.p, efv.p, fk.p, fv.p, F);
+                foff.ensure(M);
+                fend.ensure(M);
+                zero(foff.p, (size_t)M * 4);
+                zero(fend.p, (size_t)M * 4);
+                if (F) {
+                    fk2.ensure(F); fv2.ensure(F);
+                    int endbit = 33;
+                    while (endbit < 64 && ((uint64_t)M >> (endbit - 32))) endbit++;
+                    size_t tb = 0;
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream));
+                    tmp.ensure(tb);
+                    timed(KC_FINISH, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream)); });
+                    launch(KC_FINISH, k_fin_bounds, F, F, (const uint64_t*)fk2.p, foff.p, fend.p);
+                    ab.grow_keep(abase + F, stream);
+                    ae.grow_keep(abase + F, stream);
+                    launch(KC_FINISH, k_fin_archive, F, F, (const uint64_t*)fk2.p, (const uint32_t*)fv2.p, abase, ab.p, ae.p);
+                }
+                launch(KC_FINISH, k_finish2, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
+                       (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r_off, r_cnt, r_occ);
+                abase += F;
+            }
+            cur = nxt;
+            Mcur = M;
+            ncur = nnext;
+            if (ncur == 0) break;
+        }
+        return novf;
+    }
+
+    // d_bytes/d_off/d_counts are device pointers; returns number of records
+    uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
+        st = edsbwt_stats{};
+        prof = (flags & EDSBWT_PROFILE) != 0;
+        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
+        const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
+        const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
+        if (use_table) build_table();
+        st.patterns = P;
+        if (P == 0) return 0;
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, stream));
+        const KIdx X = kidx();
+        res_off.ensure(P);
+        res_cnt.ensure(P);
+        res_occ.ensure(P);
+        zero(res_cnt.p, P * 4);
+        zero(res_occ.p, P * 4);
+        ovf_orig.ensure(P);
+        uint64_t abase = 0;
+        // patterns holding '#' make the reference's lists overlap: ordered path for the batch
+        bool ordered = (flags & EDSBWT_ORDERED) != 0;
+        if (!ordered) {
+            hterm.ensure(P);
+            zero(counters.p + 4, 8);
+            launch(KC_TRIE, k_has_term, P, P, d_off, d_bytes, hterm.p, (uint32_t*)(counters.p + 4));
+            ordered = read_u32((const uint32_t*)(counters.p + 4)) != 0;
+        }
+        const uint32_t novf = ordered ? levels(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p)
+                                      : levels2(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
+        if (novf) {
+            // patterns k_deep could not hold: gather them and run the unbounded level path
+            const uint32_t n = scan_u32(ovf_orig.p, ovf_scan, P);
+            sub_map.ensure(n);
+            sub_len.ensure(n + 1);
+            launch(KC_DEEP, k_sub_build, P, P, (const uint32_t*)ovf_orig.p, (const uint32_t*)ovf_scan.p, (const uint32_t*)len.p, sub_map.p, sub_len.p);
+            const uint64_t nbytes = scan_u64(sub_len.p, sub_off, n);
+            sub_bytes.ensure(nbytes + 1);
+            launch(KC_DEEP, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)sub_map.p, d_off, (const uint64_t*)sub_off.p, d_bytes, sub_bytes.p);
+            sub_roff.ensure(n);
+            sub_rcnt.ensure(n);
+            sub_rocc.ensure(n);
+            zero(sub_rcnt.p, (size_t)n * 4);
+            zero(sub_rocc.p, (size_t)n * 4);
+            if (ordered) levels(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
+            else levels2(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
+            launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const uint64_t*)sub_roff.p, (const uint32_t*)sub_rcnt.p,
+                   (const uint32_t*)sub_rocc.p, res_off.p, res_cnt.p, res_occ.p);
+        }
         // ---- D. counts (backwardSearch's return value) and locate
         HIPCHK(hipMemcpyAsync(d_counts, res_occ.p, P * 4, hipMemcpyDeviceToDevice, stream));
         zero(counters.p + 1, 8);
@@ -521,21 +911,21 @@ struct Engine {
         uint64_t OCC = 0;
         if (locate) {
             occ64.ensure(P);
-            launch(KC_LOCATE, k_u32_to_u64, P, (const uint32_t*)res_occ.p, P, occ64.p);
+            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_occ.p, P, occ64.p);
             OCC = scan_u64(occ64.p, oscan, P);
             tc64.ensure(P);
-            launch(KC_LOCATE, k_u32_to_u64, P, (const uint32_t*)res_cnt.p, P, tc64.p);
+            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_cnt.p, P, tc64.p);
             const uint64_t TT = scan_u64(tc64.p, tscan64, P);
             if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
-                launch(KC_LOCATE, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
+                launch(KC_LOCPREP, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
                        (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p);
                 rec.ensure(OCC);
                 zero(counters.p, 8);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
                        X, use_table ? 1 : 0, rec.p, counters.p);
                 st.locate_lf_steps = read_u64(counters.p);
-                st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * 128 + OCC * (128 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
+                st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * 128 + OCC * (128 + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
             }
         }
         HIPCHK(hipEventRecord(e1, stream));
@@ -562,6 +952,7 @@ struct Engine {
         if (stream) (void)hipStreamSynchronize(stream);
         for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
         if (pinned) (void)hipHostFree(pinned);
+        if (pinned_big) (void)hipHostFree(pinned_big);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };

@@ -359,6 +359,535 @@ __global__ void k_merge_build(uint64_t n, const uint32_t* __restrict__ flag, con
     }
 }
 
+// ------------------------------------------------------------- deep phase
+// rank of '#' (code 0) and of code c at row x from one occ-block line
+__device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
+    uint4 v[8];
+    load_block(occ, x >> 8, v);
+    const uint32_t r = x & 255u;
+    const uint32_t wq = r >> 6, bit = r & 63u;
+    const uint32_t cnt[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    uint32_t a0 = cnt[0], ac = 0;
+#pragma unroll
+    for (uint32_t cc = 1; cc < 8; cc++)
+        if (cc == c) ac = cnt[cc];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint64_t p0 = u64_of(v[2 + (q >> 1)], q & 1);
+        const uint64_t p1 = u64_of(v[4 + (q >> 1)], q & 1);
+        const uint64_t p2 = u64_of(v[6 + (q >> 1)], q & 1);
+        const uint64_t mq = (uint32_t)q < wq ? ~0ull : ((uint32_t)q == wq ? ((1ull << bit) - 1ull) : 0ull);
+        a0 += (uint32_t)__popcll(~p0 & ~p1 & ~p2 & mq);
+        const uint64_t e = ((c & 1) ? p0 : ~p0) & ((c & 2) ? p1 : ~p1) & ((c & 4) ? p2 : ~p2);
+        ac += (uint32_t)__popcll(e & mq);
+    }
+    r0 = a0;
+    rc = (c == 0) ? a0 : ac;
+}
+
+// One thread per pattern whose trie node stopped sharing work: the rest of
+// backwardSearch (link → step both piles → merge, MOVE_EDSBWTSearch.cpp:254-325)
+// runs with the interval lists in registers (at most K each).  A pattern whose
+// lists outgrow K, or whose link reads more than K '#' rows at once, is flagged and
+// re-run by the level-synchronous path, which has no size limit.
+template <int K>
+__global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
+                                              const uint32_t* __restrict__ len, const uint64_t* __restrict__ off,
+                                              const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of,
+                                              const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
+                                              const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
+                                              const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
+                                              uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, uint64_t* __restrict__ res_off,
+                                              uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
+                                              uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr) {
+    unsigned long long n_steps = 0, n_hash = 0;
+    GRID_STRIDE(i, P) {
+        const uint32_t L = slen[i];
+        if (L <= D0) continue;
+        const uint32_t u = nid[i];
+        const uint32_t n0 = iend[u] - ioff[u];
+        if (n0 == 0) continue;  // dead suffix: count 0
+        if (n0 > K) { ovf[i] = 1; continue; }
+        uint32_t cb[K], ce[K];
+        uint32_t cn = n0;
+#pragma unroll
+        for (int t = 0; t < K; t++) {
+            cb[t] = (uint32_t)t < cn ? ib[ioff[u] + t] : 0u;
+            ce[t] = (uint32_t)t < cn ? ie[ioff[u] + t] : 0u;
+        }
+        const uint32_t a = perm[i];
+        const uint8_t* pat = bytes + off[a];
+        bool over = false;
+        for (uint32_t d = D0; d < L && cn; d++) {
+            const uint32_t code = code_of[pat[L - 1 - d]];
+            if (code >= X.sigma) { cn = 0; break; }
+            const uint32_t c = code;
+            // ranks at both ends of every current interval: '#'-rows (link) and c (step)
+            uint32_t sb[K], se[K], raw[K];
+            uint32_t rn = 0;
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                sb[j] = se[j] = 0;
+                raw[j] = 0;
+            }
+#pragma unroll
+            for (int j = 0; j < K; j++) {
+                if ((uint32_t)j < cn) {
+                    uint32_t h0, h1;
+                    rank2(X.occ, cb[j], c, h0, sb[j]);
+                    rank2(X.occ, ce[j] + 1, c, h1, se[j]);
+                    n_hash += h1 - h0;
+                    for (uint32_t k = h0; k < h1; k++) {  // dollars_in_interval (:607-625)
+                        const uint32_t s = X.eof_seg[k];
+                        if (!s) continue;
+                        // insert s into raw[0..rn) ascending, dropping duplicates
+                        bool dup = false;
+#pragma unroll
+                        for (int t = 0; t < K; t++)
+                            if ((uint32_t)t < rn && raw[t] == s) dup = true;
+                        if (dup) continue;
+                        if (rn == K) { over = true; break; }
+                        uint32_t vv = s;
+#pragma unroll
+                        for (int t = 0; t < K; t++) {
+                            if ((uint32_t)t < rn) {
+                                if (raw[t] > vv) { const uint32_t tmp = raw[t]; raw[t] = vv; vv = tmp; }
+                            } else if ((uint32_t)t == rn) {
+                                raw[t] = vv;
+                            }
+                        }
+                        rn++;
+                    }
+                }
+            }
+            if (over) break;
+            // step: [dollar runs (ascending), own intervals] by c, adjacent merged (:275-324)
+            uint32_t nb[K], ne[K];
+            uint32_t nn = 0, last_e = 0;
+#pragma unroll
+            for (int t = 0; t < K; t++) nb[t] = ne[t] = 0;
+            auto push = [&](uint32_t b, uint32_t e) {
+                if (nn && b == last_e + 1) {
+#pragma unroll
+                    for (int t = 0; t < K; t++)
+                        if ((uint32_t)t + 1 == nn) ne[t] = e;
+                    last_e = e;
+                    return;
+                }
+                if (nn == K) { over = true; return; }
+#pragma unroll
+                for (int t = 0; t < K; t++)
+                    if ((uint32_t)t == nn) { nb[t] = b; ne[t] = e; }
+                nn++;
+                last_e = e;
+            };
+            uint32_t run_lo = 0, run_s = 0;
+            bool have = false;
+            auto close_run = [&]() {
+                const uint32_t r0 = X.seg_start[run_lo], r1 = X.seg_start[run_s] - 1;
+                uint32_t x0, x1, y0, y1;
+                rank2(X.occ, r0, c, x0, x1);
+                rank2(X.occ, r1 + 1, c, y0, y1);
+                if (y1 > x1) push(X.C[c] + x1, X.C[c] + y1 - 1);
+                n_steps++;
+            };
+#pragma unroll
+            for (int t = 0; t < K; t++) {
+                if ((uint32_t)t < rn) {
+                    const uint32_t s = raw[t];
+                    const uint32_t lo = X.seg_lo[s];
+                    if (have && lo > run_s) { close_run(); have = false; }
+                    if (!have) { run_lo = lo; have = true; }
+                    run_s = s;
+                }
+            }
+            if (have) close_run();
+#pragma unroll
+            for (int j = 0; j < K; j++)
+                if ((uint32_t)j < cn && se[j] > sb[j]) push(X.C[c] + sb[j], X.C[c] + se[j] - 1);
+            n_steps += cn;
+            if (over) break;
+            cn = nn;
+#pragma unroll
+            for (int t = 0; t < K; t++) { cb[t] = nb[t]; ce[t] = ne[t]; }
+        }
+        if (over) { ovf[i] = 1; continue; }
+        // ascending rows (the input lists may be unordered sets)
+#pragma unroll
+        for (int a = 0; a < K; a++)
+#pragma unroll
+            for (int b2 = 0; b2 + 1 < K - a; b2++)
+                if ((uint32_t)(b2 + 1) < cn && cb[b2] > cb[b2 + 1]) {
+                    uint32_t t0 = cb[b2]; cb[b2] = cb[b2 + 1]; cb[b2 + 1] = t0;
+                    t0 = ce[b2]; ce[b2] = ce[b2 + 1]; ce[b2 + 1] = t0;
+                }
+        const uint32_t o = perm[i];
+        uint32_t occ = 0;
+        const uint64_t at = abase + (uint64_t)i * K;
+#pragma unroll
+        for (int t = 0; t < K; t++)
+            if ((uint32_t)t < cn) {
+                ab[at + t] = cb[t];
+                ae[at + t] = ce[t];
+                occ += ce[t] - cb[t] + 1;
+            }
+        res_off[o] = at;
+        res_cnt[o] = cn;
+        res_occ[o] = occ;
+    }
+    if (n_steps) atomicAdd(ctr + 2, n_steps);
+    if (n_hash) atomicAdd(ctr + 3, n_hash);
+}
+
+// pattern-length histogram: per-block LDS bins, one global atomic per bin per block
+__global__ void __launch_bounds__(256) k_len_hist(const uint32_t* __restrict__ len, uint64_t P, uint32_t Lmax,
+                                                  unsigned long long* __restrict__ hist) {
+    __shared__ unsigned int h[1024];
+    const uint32_t nb = Lmax + 1 < 1024 ? Lmax + 1 : 1024;
+    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) h[t] = 0;
+    __syncthreads();
+    GRID_STRIDE(i, P) {
+        const uint32_t l = len[i];
+        if (l < nb) atomicAdd(&h[l], 1u);
+        else atomicAdd(hist + (l < Lmax ? l : Lmax), 1ull);
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x)
+        if (h[t]) atomicAdd(hist + t, (unsigned long long)h[t]);
+}
+
+// overflowed patterns → a compact sub-batch (original ids kept in `map`)
+__global__ void k_ovf_lens(uint64_t P, const uint32_t* __restrict__ ovf, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len,
+                           uint32_t* __restrict__ flag_orig) {
+    GRID_STRIDE(i, P) if (ovf[i]) flag_orig[perm[i]] = 1;
+}
+
+__global__ void k_sub_build(uint64_t P, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ fscan, const uint32_t* __restrict__ len,
+                            uint32_t* __restrict__ map, uint64_t* __restrict__ sublen) {
+    GRID_STRIDE(o, P) if (flag[o]) { map[fscan[o]] = (uint32_t)o; sublen[fscan[o]] = len[o]; }
+}
+
+__global__ void k_sub_bytes(uint64_t n, const uint32_t* __restrict__ map, const uint64_t* __restrict__ off, const uint64_t* __restrict__ suboff,
+                            const uint8_t* __restrict__ bytes, uint8_t* __restrict__ subbytes) {
+    GRID_STRIDE(j, n) {
+        const uint64_t s = off[map[j]], d = suboff[j], l = suboff[j + 1] - d;
+        for (uint64_t t = 0; t < l; t++) subbytes[d + t] = bytes[s + t];
+    }
+}
+
+__global__ void k_sub_scatter(uint64_t n, const uint32_t* __restrict__ map, const uint64_t* __restrict__ so, const uint32_t* __restrict__ sc,
+                              const uint32_t* __restrict__ socc, uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt,
+                              uint32_t* __restrict__ res_occ) {
+    GRID_STRIDE(j, n) {
+        const uint32_t o = map[j];
+        res_off[o] = so[j];
+        res_cnt[o] = sc[j];
+        res_occ[o] = socc[j];
+    }
+}
+
+// ------------------------------------------- order-free level step (default path)
+// A node's interval list is kept as an unordered set of (node, b, e) items: merging
+// adjacent intervals and the order of the list never change the rows locate emits
+// (LF_c is monotone on each pile and the reference's lists are ascending and
+// disjoint for patterns without '#'), so every level is one fused pass that reads
+// each item's two occ-block lines and appends only the non-empty children.
+// Appends are wave-aggregated: one atomic per wave per buffer.  Call with every
+// lane of the wave active.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* __restrict__ counter, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(counter, total);
+    base = __shfl(base, 63, 64);
+    return base + x - n;
+}
+
+// Appends go to NSHARD independent regions (counter k of shard s at cnt[s*32+k],
+// one 128-B line per shard) so that no single address takes every wave's atomic;
+// k_unshard packs the regions afterwards.
+constexpr uint32_t NSHARD = 64;
+
+// grid-stride loop whose trip count is uniform across each block (so wave-wide
+// shuffles inside it see every lane); `valid` marks the lanes past the end
+#define UNIFORM_STRIDE(i, valid, n)                                                                                     \
+    for (size_t i##_b = (size_t)blockIdx.x * blockDim.x; i##_b < (size_t)(n); i##_b += (size_t)gridDim.x * blockDim.x) \
+        if (const size_t i = i##_b + threadIdx.x; true)                                                                  \
+            if (const bool valid = i < (size_t)(n); true)
+
+// children of node u: [child_first[u], child_end[u]) at the next depth, symbol node_char
+template <bool LINK>
+__global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* __restrict__ iu, const uint32_t* __restrict__ ib,
+                                                   const uint32_t* __restrict__ ie, const uint32_t* __restrict__ child_first,
+                                                   const uint32_t* __restrict__ child_end, const uint8_t* __restrict__ node_char, KIdx X,
+                                                   uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
+                                                   uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
+                                                   uint32_t cap_keys, uint32_t* __restrict__ ck_u, uint32_t* __restrict__ ck_k,
+                                                   uint32_t* __restrict__ ck_e, uint32_t cap_chunks) {
+    const uint32_t sh = blockIdx.x % NSHARD;
+    uint32_t* cnt = cnt_all + sh * 32;
+    nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
+    keys += (size_t)sh * cap_keys;
+    ck_u += (size_t)sh * cap_chunks; ck_k += (size_t)sh * cap_chunks; ck_e += (size_t)sh * cap_chunks;
+    UNIFORM_STRIDE(i, valid, n) {
+        uint32_t u = 0, cf = 0, nch = 0;
+        uint32_t rb[8], re[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
+        if (valid) {
+            u = iu[i];
+            cf = child_first[u];
+            nch = child_end[u] - cf;
+            if (nch) {
+                rank_all(X.occ, ib[i], X.sigma, rb);
+                rank_all(X.occ, ie[i] + 1, X.sigma, re);
+            }
+        }
+        // backward step of every child symbol (updateSingleInterval, :424-510)
+        uint32_t nk = 0;
+        uint32_t cc[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            cc[t] = 0xFF;
+            if ((uint32_t)t < nch) {
+                const uint32_t c = node_char[cf + t];
+                if (c < 8 && re[c] > rb[c]) { cc[t] = c; nk++; }
+            }
+        }
+        uint32_t at = wave_append(cnt + 0, nk);
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            if (cc[t] != 0xFF) {
+                if (at < cap_next) {
+                    const uint32_t c = cc[t];
+                    nu[at] = cf + t;
+                    nb[at] = X.C[c] + rb[c];
+                    ne[at] = X.C[c] + re[c] - 1;
+                }
+                at++;
+            }
+        }
+        if (LINK) {
+            // '#' rows of the item (dollars_in_interval, :607-625): short ranges inline,
+            // long ones as chunks of 256 rows for k_lvl_chunks
+            const uint32_t h = nch ? re[0] - rb[0] : 0u;
+            uint32_t nz = 0;
+            if (h && h <= 16)
+                for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
+            uint32_t kat = wave_append(cnt + 1, nz);
+            if (nz)
+                for (uint32_t k = rb[0]; k < re[0]; k++) {
+                    const uint32_t s = X.eof_seg[k];
+                    if (s) {
+                        if (kat < cap_keys) keys[kat] = ((uint64_t)u << 32) | s;
+                        kat++;
+                    }
+                }
+            const uint32_t nc = h > 16 ? (h + 255) / 256 : 0u;
+            uint32_t cat = wave_append(cnt + 2, nc);
+            for (uint32_t q = 0; q < nc; q++, cat++)
+                if (cat < cap_chunks) {
+                    ck_u[cat] = u;
+                    ck_k[cat] = rb[0] + 256 * q;
+                    ck_e[cat] = min(rb[0] + 256 * (q + 1), re[0]);
+                }
+        }
+    }
+}
+
+// long '#'-row ranges: one chunk (<= 256 rows, clipped to the item's end) per thread
+__global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* __restrict__ ck_u, const uint32_t* __restrict__ ck_k,
+                                                    const uint32_t* __restrict__ ck_end, KIdx X, uint32_t* __restrict__ cnt_all,
+                                                    uint64_t* __restrict__ keys, uint32_t cap_keys) {
+    const uint32_t sh = blockIdx.x % NSHARD;
+    uint32_t* cnt = cnt_all + sh * 32;
+    keys += (size_t)sh * cap_keys;
+    UNIFORM_STRIDE(i, valid, n) {
+        uint32_t k0 = 0, k1 = 0, u = 0, nz = 0;
+        if (valid) {
+            u = ck_u[i];
+            k0 = ck_k[i];
+            k1 = ck_end[i];
+            for (uint32_t k = k0; k < k1; k++) nz += X.eof_seg[k] != 0;
+        }
+        uint32_t kat = wave_append(cnt + 1, nz);
+        if (nz)
+            for (uint32_t k = k0; k < k1; k++) {
+                const uint32_t s = X.eof_seg[k];
+                if (s) {
+                    if (kat < cap_keys) keys[kat] = ((uint64_t)u << 32) | s;
+                    kat++;
+                }
+            }
+    }
+}
+
+// dollar items (previous-segment word ranges of a node) stepped by each child
+__global__ void __launch_bounds__(256) k_lvl_dollar(uint32_t n, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
+                                                    const uint32_t* __restrict__ de, const uint32_t* __restrict__ child_first,
+                                                    const uint32_t* __restrict__ child_end, const uint8_t* __restrict__ node_char, KIdx X,
+                                                    uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
+                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all) {
+    const uint32_t sh = blockIdx.x % NSHARD;
+    uint32_t* cnt = cnt_all + sh * 32;
+    nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
+    UNIFORM_STRIDE(i, valid, n) {
+        uint32_t cf = 0, nch = 0;
+        uint32_t rb[8], re[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
+        if (valid) {
+            const uint32_t u = du[i];
+            cf = child_first[u];
+            nch = child_end[u] - cf;
+            if (nch) {
+                rank_all(X.occ, db[i], X.sigma, rb);
+                rank_all(X.occ, de[i] + 1, X.sigma, re);
+            }
+        }
+        uint32_t nk = 0;
+        uint32_t cc[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            cc[t] = 0xFF;
+            if ((uint32_t)t < nch) {
+                const uint32_t c = node_char[cf + t];
+                if (c < 8 && re[c] > rb[c]) { cc[t] = c; nk++; }
+            }
+        }
+        uint32_t at = wave_append(cnt + 0, nk);
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            if (cc[t] != 0xFF) {
+                if (at < cap_next) {
+                    const uint32_t c = cc[t];
+                    nu[at] = cf + t;
+                    nb[at] = X.C[c] + rb[c];
+                    ne[at] = X.C[c] + re[c] - 1;
+                }
+                at++;
+            }
+        }
+    }
+}
+
+// finishing nodes (patterns of length D): (node << 32 | b, e) pairs, sorted later
+__global__ void __launch_bounds__(256) k_fin_emit(uint32_t n, const uint32_t* __restrict__ nu, const uint32_t* __restrict__ nb,
+                                                  const uint32_t* __restrict__ ne, const uint8_t* __restrict__ fin, uint32_t* __restrict__ cnt_all,
+                                                  uint64_t* __restrict__ fk, uint32_t* __restrict__ fv, uint32_t cap,
+                                                  uint32_t* __restrict__ node_occ) {
+    const uint32_t sh = blockIdx.x % NSHARD;
+    uint32_t* cnt = cnt_all + sh * 32;
+    fk += (size_t)sh * cap; fv += (size_t)sh * cap;
+    UNIFORM_STRIDE(i, valid, n) {
+        uint32_t f = 0, u = 0;
+        if (valid) {
+            u = nu[i];
+            f = fin[u];
+        }
+        uint32_t at = wave_append(cnt + 4, f);
+        if (f) {
+            if (at < cap) {
+                fk[at] = ((uint64_t)u << 32) | nb[i];
+                fv[at] = ne[i];
+            }
+            atomicAdd(node_occ + u, ne[i] - nb[i] + 1);
+        }
+    }
+}
+
+// pack shard regions: item t of the packed array lives in shard s = last with
+// pre[s] <= t, at s*cap + (t - pre[s])
+template <typename A, typename B, typename C3>
+__global__ void k_unshard(uint32_t total, const uint32_t* __restrict__ pre, uint32_t cap, const A* __restrict__ a, const B* __restrict__ b,
+                          const C3* __restrict__ c, A* __restrict__ oa, B* __restrict__ ob, C3* __restrict__ oc) {
+    __shared__ uint32_t sp[NSHARD + 1];
+    for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) sp[t] = pre[t];
+    __syncthreads();
+    GRID_STRIDE(t, total) {
+        uint32_t lo = 0, hi = NSHARD;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sp[mid] <= (uint32_t)t) lo = mid; else hi = mid;
+        }
+        const size_t src = (size_t)lo * cap + ((uint32_t)t - sp[lo]);
+        oa[t] = a[src];
+        if (ob) ob[t] = b[src];
+        if (oc) oc[t] = c[src];
+    }
+}
+
+__global__ void k_fin_flags(uint32_t M, uint32_t D, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ slen,
+                            uint8_t* __restrict__ fin) {
+    GRID_STRIDE(u, M) fin[u] = slen[node_first[u]] == D;
+}
+
+// per node [off, end) in the sorted finisher keys
+__global__ void k_fin_bounds(uint32_t F, const uint64_t* __restrict__ fk, uint32_t* __restrict__ foff, uint32_t* __restrict__ fend) {
+    GRID_STRIDE(t, F) {
+        const uint32_t u = (uint32_t)(fk[t] >> 32);
+        if (t == 0 || (uint32_t)(fk[t - 1] >> 32) != u) foff[u] = (uint32_t)t;
+        if (t + 1 == F || (uint32_t)(fk[t + 1] >> 32) != u) fend[u] = (uint32_t)t + 1;
+    }
+}
+
+__global__ void k_fin_archive(uint32_t F, const uint64_t* __restrict__ fk, const uint32_t* __restrict__ fv, uint64_t abase,
+                              uint32_t* __restrict__ ab, uint32_t* __restrict__ ae) {
+    GRID_STRIDE(t, F) {
+        ab[abase + t] = (uint32_t)fk[t];
+        ae[abase + t] = fv[t];
+    }
+}
+
+__global__ void k_finish2(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ nid,
+                          const uint32_t* __restrict__ perm, const uint32_t* __restrict__ foff, const uint32_t* __restrict__ fend,
+                          const uint32_t* __restrict__ node_occ, uint64_t abase, uint64_t* __restrict__ res_off,
+                          uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ) {
+    GRID_STRIDE(i, P) {
+        if (slen[i] != D) continue;
+        const uint32_t u = nid[i];
+        const uint32_t o = perm[i];
+        res_off[o] = abase + foff[u];
+        res_cnt[o] = fend[u] - foff[u];
+        res_occ[o] = node_occ[u];
+    }
+}
+
+// group unordered items by node (deep cut-over): count, scan, scatter
+__global__ void k_group_count(uint32_t n, const uint32_t* __restrict__ iu, uint32_t* __restrict__ gcnt) {
+    GRID_STRIDE(i, n) atomicAdd(gcnt + iu[i], 1u);
+}
+__global__ void k_group_scatter(uint32_t n, const uint32_t* __restrict__ iu, const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie,
+                                const uint32_t* __restrict__ goff, uint32_t* __restrict__ gfill, uint32_t* __restrict__ ob,
+                                uint32_t* __restrict__ oe) {
+    GRID_STRIDE(i, n) {
+        const uint32_t u = iu[i];
+        const uint32_t at = goff[u] + atomicAdd(gfill + u, 1u);
+        ob[at] = ib[i];
+        oe[at] = ie[i];
+    }
+}
+__global__ void k_group_end(uint32_t M, const uint32_t* __restrict__ goff, const uint32_t* __restrict__ gcnt, uint32_t* __restrict__ gend) {
+    GRID_STRIDE(u, M) gend[u] = goff[u] + gcnt[u];
+}
+
+// patterns holding the end-marker byte take the ordered (reference list) path
+__global__ void k_has_term(uint64_t P, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes, uint32_t* __restrict__ flag,
+                           uint32_t* __restrict__ count) {
+    GRID_STRIDE(i, P) {
+        uint32_t f = 0;
+        for (uint64_t t = off[i]; t < off[i + 1]; t++) f |= bytes[t] == '#';
+        flag[i] = f;
+        if (f) atomicAdd(count, 1u);
+    }
+}
+
 // ------------------------------------------------------------- finishing
 __global__ void k_fin_counts(uint32_t M, uint32_t D, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ slen,
                              const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend, uint32_t* __restrict__ fcnt) {

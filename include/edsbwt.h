@@ -39,6 +39,10 @@ enum {
 #define EDSBWT_LOCATE_TABLE 0x4u /* with LOCATE: read (word, offset) from the per-row table
                                     instead of walking LF to '#'; identical records */
 #define EDSBWT_PROFILE      0x8u /* record per-kernel HIP-event times into edsbwt_stats */
+#define EDSBWT_NO_DEEP      0x10u/* level-synchronous trie walk for every depth (no per-pattern
+                                    finishing kernel); same results, used by tests */
+#define EDSBWT_ORDERED      0x20u/* keep every interval list in the reference's order at every
+                                    depth (the path patterns holding '#' take); same results */
 
 typedef struct edsbwt_index edsbwt_index;
 
@@ -67,6 +71,8 @@ typedef struct {
     uint64_t link_hash_rows;  /* '#' rows read by link (dollars_in_interval) */
     uint64_t link_ranges;     /* merged previous-segment ranges produced by link */
     uint64_t locate_lf_steps; /* LF steps of the locate walk (0 with LOCATE_TABLE) */
+    uint64_t deep_from_depth; /* depth at which patterns were finished one per thread (0: never) */
+    uint64_t deep_overflow;   /* patterns re-run by the level path because their lists outgrew registers */
     double ms_total;          /* device time of the call (hipEvent) */
     double ms_kernel[16];     /* EDSBWT_PROFILE: per kernel class, see edsbwt_kernel_name */
     uint64_t launches_kernel[16];

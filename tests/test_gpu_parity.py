@@ -44,6 +44,11 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
             assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)
         st = idx.stats()
         assert st["found"] == int((oc > 0).sum())
+        gc4, go4 = idx.search((buf, offs), deep=False)   # level-synchronous path only
+        assert np.array_equal(gc4, oc) and np.array_equal(go4, oo)
+        for deep in (True, False):                       # reference-ordered lists at every depth
+            gc5, go5 = idx.search((buf, offs), ordered=True, deep=deep)
+            assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
     return oc, oo
 
 
@@ -91,3 +96,23 @@ def test_larger_eds_gpu(oracle, edsbwt, tmp_path):
     pats = [edsgen.planted(rng, segs, rng.choice([8, 12, 20, 31])) or "ACGT" for _ in range(3000)]
     pats += ["".join(rng.choice("ACGT") for _ in range(20)) for _ in range(3000)]
     _compare(oracle, edsbwt, base, pats)
+
+
+def test_deep_overflow_rerun(oracle, edsbwt, tmp_path):
+    """Lists longer than k_deep's registers (many '#' rows / many intervals) fall back
+    to the level path: force it with an EDS whose segments repeat one motif."""
+    rng = random.Random(9)
+    motif = ["AC", "ACA", "CA", "A", ""]
+    segs = [[rng.choice(motif) or "A" for _ in range(rng.randint(1, 5))] for _ in range(3000)]
+    for s in segs:
+        if rng.random() < 0.3 and len(s) > 1:
+            s[0] = ""
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = ["".join(rng.choice("AC") for _ in range(rng.randint(6, 30))) for _ in range(2000)]
+    pats += [edsgen.planted(rng, segs, 25) or "ACA" for _ in range(2000)]
+    _compare(oracle, edsbwt, base, pats, table_too=False)
+    with edsbwt.Index(base) as idx:
+        buf, offs = _pack(pats)
+        idx.search((buf, offs))
+        st = idx.stats()
+    assert st["deep_from_depth"] > 0 and st["deep_overflow"] > 0, st
