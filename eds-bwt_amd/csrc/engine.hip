@@ -86,7 +86,7 @@ static const char* kKNames[KC_COUNT] = {"trie_sort", "trie_nodes", "expand", "li
 // k_deep keeps at most kDeepK intervals per list in registers
 constexpr int kDeepK = 8;
 // switch to k_deep once depth-D nodes >= kDeepShare x patterns of length >= D
-constexpr double kDeepShare = 0.7;
+constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
 
@@ -107,7 +107,7 @@ struct Engine {
     // workspace
     DBuf<uint32_t> len, perm, perm2, slen, lcp, nid[2], flag, scan, node_first, node_parent, child_first, child_end;
     DBuf<uint8_t> node_char;
-    DBuf<uint64_t> keys, kc, kc2;
+    DBuf<uint64_t> keys, kc, kc2, skey;
     DBuf<uint32_t> ib[2], ie[2], iu[2], ioff[2], iend[2], iocb, ioce;
     DBuf<uint32_t> hcnt, hoff, rflag, rscan, rb, re, ru, doff, dend, docb, doce;
     DBuf<uint64_t> lkeys, lkeys2;
@@ -191,6 +191,20 @@ struct Engine {
         return v;
     }
     void zero(void* p, size_t bytes) { if (bytes) HIPCHK(hipMemsetAsync(p, 0, bytes, stream)); }
+
+    // reversed-code chunk of depth D for the patterns in trie order (chunk 0 is the
+    // last radix pass's output; later chunks are gathered once when first needed)
+    int skey_chunk = -1;
+    const uint64_t* sorted_chunk(uint32_t D, uint64_t P) {
+        const int c = (int)((D - 1) >> 4);
+        if (c == 0) return kc2.p;
+        if (c != skey_chunk) {
+            skey.ensure(P);
+            launch(KC_NODES, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, skey.p);
+            skey_chunk = c;
+        }
+        return skey.p;
+    }
 
     // ---- sharded appends (kernels.hip NSHARD): per-shard counters on the host
     std::vector<uint32_t> hsh = std::vector<uint32_t>(NSHARD * 32, 0);
@@ -441,6 +455,7 @@ struct Engine {
             std::swap(perm.p, perm2.p);
             std::swap(perm.cap, perm2.cap);
         }
+        skey_chunk = -1;
         slen.ensure(P);
         lcp.ensure(P);
         launch(KC_TRIE, k_slen_lcp, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)keys.p, nch, P, slen.p, lcp.p);
@@ -502,8 +517,7 @@ struct Engine {
             node_first.ensure(M);
             node_parent.ensure(M);
             node_char.ensure(M);
-            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, (const uint32_t*)perm.p,
-                   (const uint32_t*)len.p, d_off, d_bytes, (const uint8_t*)code_of.p, sigma, (const uint32_t*)flag.p,
+            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             child_first.ensure(Mcur);
             child_end.ensure(Mcur);
@@ -699,8 +713,7 @@ struct Engine {
             node_first.ensure(M);
             node_parent.ensure(M);
             node_char.ensure(M);
-            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, (const uint32_t*)perm.p,
-                   (const uint32_t*)len.p, d_off, d_bytes, (const uint8_t*)code_of.p, sigma, (const uint32_t*)flag.p,
+            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             child_first.ensure(Mcur);
             child_end.ensure(Mcur);

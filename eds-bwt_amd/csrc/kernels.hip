@@ -158,13 +158,13 @@ __global__ void k_node_flags(const uint32_t* __restrict__ slen, const uint32_t* 
     GRID_STRIDE(i, P) flag[i] = (slen[i] >= D && lcp[i] < D) ? 1u : 0u;
 }
 
-// nscan = exclusive scan of flags (P+1 entries)
-__global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp,
-                             const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len, const uint64_t* __restrict__ off,
-                             const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of, uint32_t sigma,
+// nscan = exclusive scan of flags (P+1 entries); skey = the sorted patterns'
+// reversed-code chunk holding depth D (4 bits per symbol, most significant first)
+__global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint64_t* __restrict__ skey, uint32_t sigma,
                              const uint32_t* __restrict__ flag, const uint32_t* __restrict__ nscan,
                              const uint32_t* __restrict__ nid_prev, uint32_t* __restrict__ nid_cur,
                              uint32_t* __restrict__ node_first, uint32_t* __restrict__ node_parent, uint8_t* __restrict__ node_char) {
+    const uint32_t sh = 4 * (15 - ((D - 1) & 15));
     GRID_STRIDE(i, P) {
         if (slen[i] < D) { nid_cur[i] = 0xFFFFFFFFu; continue; }
         const uint32_t id = nscan[i] + flag[i] - 1;
@@ -172,9 +172,8 @@ __global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict_
         if (flag[i]) {
             node_first[id] = (uint32_t)i;
             node_parent[id] = nid_prev[i];
-            const uint32_t a = perm[i];
-            const uint32_t code = code_of[bytes[off[a] + len[a] - D]];
-            node_char[id] = (uint8_t)(code < sigma ? code : 0xFF);
+            const uint32_t v = (uint32_t)(skey[i] >> sh) & 15u;
+            node_char[id] = (uint8_t)((v >= 1 && v <= sigma) ? v - 1 : 0xFF);
         }
     }
 }
