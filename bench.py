@@ -170,7 +170,7 @@ def main():
     total_occ = 0
     lf_steps = 0
     for i in range(args.steps):
-        _, nocc = step(profile=True)
+        _, nocc = step(profile="light")
         exchange()
         st = idx.stats()
         total_occ += nocc
@@ -225,7 +225,7 @@ def main():
                          "bytes_per_launch": int(d["bytes"] / max(1, d["launches"]))},
             "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items())},
             "index_open_s": round(t_open, 2),
-            "engine": {k: last[k] for k in ("depths", "deep_from_depth", "deep_overflow", "trie_nodes", "intervals_stepped",
+            "engine": {k: last[k] for k in ("depths", "deep_from_depth", "deep_overflow", "deep_level_rerun", "trie_nodes", "intervals_stepped",
                                               "link_hash_rows", "link_ranges", "locate_lf_steps")},
             "found_per_step": int(last["found"]),
         }

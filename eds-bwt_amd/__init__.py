@@ -32,6 +32,8 @@ LOCATE_TABLE = 0x4
 PROFILE = 0x8
 NO_DEEP = 0x10
 ORDERED = 0x20
+PROFILE_LIGHT = 0x40
+NO_WIDE = 0x80
 
 OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
 CSV_HEADER = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"  # MOVE_EDSBWTSearch.cpp:59 (note the trailing space)
@@ -53,7 +55,8 @@ class _Stats(ctypes.Structure):
                 ("occurrences", ctypes.c_uint64), ("depths", ctypes.c_uint64), ("trie_nodes", ctypes.c_uint64),
                 ("intervals_stepped", ctypes.c_uint64), ("link_hash_rows", ctypes.c_uint64),
                 ("link_ranges", ctypes.c_uint64), ("locate_lf_steps", ctypes.c_uint64),
-                ("deep_from_depth", ctypes.c_uint64), ("deep_overflow", ctypes.c_uint64), ("ms_total", ctypes.c_double),
+                ("deep_from_depth", ctypes.c_uint64), ("deep_overflow", ctypes.c_uint64),
+                ("deep_level_rerun", ctypes.c_uint64), ("ms_total", ctypes.c_double),
                 ("ms_kernel", ctypes.c_double * 16), ("launches_kernel", ctypes.c_uint64 * 16),
                 ("bytes_kernel", ctypes.c_uint64 * 16)]
 
@@ -164,7 +167,7 @@ class Index:
 
     def search(self, patterns: Sequence[bytes | str] | tuple[np.ndarray, np.ndarray], *, first_pattern_id: int = 1,
                locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
-               ordered: bool = False):
+               ordered: bool = False, wide: bool = True):
         """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc])."""
         buf, offs = patterns if isinstance(patterns, tuple) else pack_patterns(patterns)
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
@@ -172,7 +175,7 @@ class Index:
         npat = offs.size - 1
         counts = np.zeros(max(npat, 0), dtype=np.uint32)
         flags = ((LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
-                 | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0))
+                 | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0) | (0 if wide else NO_WIDE))
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         bp = buf.ctypes.data if buf.size else None
@@ -190,8 +193,8 @@ class Index:
                       stream: int = 0):
         """Device-resident batch (pointers are device addresses, e.g. torch data_ptr()).
         Returns (device pointer of the records, number of records)."""
-        flags = ((LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
-                 | (0 if deep else NO_DEEP))
+        pflag = {False: 0, True: PROFILE, "light": PROFILE_LIGHT}[profile]
+        flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | pflag | (0 if deep else NO_DEEP)
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,

@@ -89,6 +89,10 @@ constexpr int kDeepK = 8;
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
+// patterns k_deep<kDeepK> cannot hold retry with lists of up to kDeepWide intervals
+constexpr int kDeepWide = 64;
+// levels2() result meaning "the batch needs the ordered path"
+constexpr uint32_t kNeedOrdered = 0xFFFFFFFFu;
 
 struct Engine {
     int device = 0;
@@ -133,6 +137,8 @@ struct Engine {
     edsbwt_stats st{};
     // profiling
     bool prof = false;
+    bool no_wide = false;  // EDSBWT_NO_WIDE (tests): overflowed deep patterns go straight to the level path
+    uint32_t prof_mask = ~0u;  // kernel classes timed with events when profiling
     bool trace = std::getenv("EDSBWT_TRACE") != nullptr;
     struct Ev { int k; hipEvent_t a, b; };
     std::vector<Ev> evs, ev_pool;
@@ -164,7 +170,7 @@ struct Engine {
     }
     template <typename F>
     void timed(int k, F&& f) {
-        if (!prof) { f(); return; }
+        if (!prof || !((prof_mask >> k) & 1)) { f(); return; }
         Ev e = ev_get(k);
         HIPCHK(hipEventRecord(e.a, stream));
         f();
@@ -195,6 +201,7 @@ struct Engine {
     // reversed-code chunk of depth D for the patterns in trie order (chunk 0 is the
     // last radix pass's output; later chunks are gathered once when first needed)
     int skey_chunk = -1;
+    std::vector<uint64_t> nodes_at;  // trie nodes per depth of the current batch
     const uint64_t* sorted_chunk(uint32_t D, uint64_t P) {
         const int c = (int)((D - 1) >> 4);
         if (c == 0) return kc2.p;
@@ -207,11 +214,12 @@ struct Engine {
     }
 
     // ---- sharded appends (kernels.hip NSHARD): per-shard counters on the host
-    std::vector<uint32_t> hsh = std::vector<uint32_t>(NSHARD * 32, 0);
+    static constexpr uint32_t kCnt = NSHARD * 32 + 32;  // shard counters + device scalars (link runs)
+    std::vector<uint32_t> hsh = std::vector<uint32_t>(kCnt, 0);
     void fetch_shards() {
-        HIPCHK(hipMemcpyAsync(pinned_big, lcnt.p, NSHARD * 32 * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(pinned_big, lcnt.p, kCnt * 4, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        std::memcpy(hsh.data(), pinned_big, NSHARD * 32 * 4);
+        std::memcpy(hsh.data(), pinned_big, kCnt * 4);
     }
     std::vector<uint32_t> shard_counts(int k) const {
         std::vector<uint32_t> v(NSHARD);
@@ -235,7 +243,7 @@ struct Engine {
         return (uint32_t)t;
     }
     void upload_prefix(int k) {
-        uint32_t* pre = pinned_big + NSHARD * 32;
+        uint32_t* pre = pinned_big + kCnt;
         pre[0] = 0;
         for (uint32_t sh = 0; sh < NSHARD; sh++) pre[sh + 1] = pre[sh] + hsh[sh * 32 + k];
         shpre.ensure(NSHARD + 1);
@@ -266,6 +274,28 @@ struct Engine {
             HIPCHK(hipStreamSynchronize(stream));
             n.release();
         }
+    }
+
+    // out[0..n) = exclusive prefix sum of in[0..n) (no read-back)
+    void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n) {
+        if (!n) return;
+        if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, stream));
+        tmp.ensure(tb);
+        timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, out, (int)n, stream)); });
+    }
+
+    // out[0..n] = exclusive prefix sum (out[0] = 0, out[n] = total), no read-back
+    void inclusive_scan_u64(const uint64_t* in, DBuf<uint64_t>& out, size_t n) {
+        out.ensure(n + 1);
+        zero(out.p, 8);
+        if (!n) return;
+        if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
+        tmp.ensure(tb);
+        timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
     }
 
     // out[0..n] = exclusive prefix sum of in[0..n); returns out[n]
@@ -300,7 +330,7 @@ struct Engine {
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         HIPCHK(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc((void**)&pinned_big, (NSHARD * 32 + NSHARD + 8) * 4, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&pinned_big, (kCnt + NSHARD + 8) * 4, hipHostMallocDefault));
         HostIndex H;
         std::string err;
         int rc = read_host_index(base, H, err);
@@ -411,33 +441,20 @@ struct Engine {
     // ------------------------------------------------------------ search
     // Reversed-pattern trie order: patterns radix-sorted by their reversed symbol
     // codes, with the common-suffix length of neighbours (lcp).  Nodes of depth D
-    // are then maximal runs with lcp >= D.  Returns false when every pattern is empty.
+    // are the maximal runs with lcp >= D; nodes_at[D] counts them for every depth.
+    // Returns false when every pattern is empty.
     bool build_trie(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t& Lmax, std::vector<unsigned long long>& hist,
-                    std::vector<uint64_t>& ge) {
+                    std::vector<uint64_t>& ge, uint32_t* n_term = nullptr) {
         if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
-        // ---- A. lengths, keys, reversed-pattern sort (trie order)
+        // ---- A. lengths, longest pattern, patterns holding '#': one launch, one read
         len.ensure(P);
-        launch(KC_TRIE, k_lens, P, d_off, P, len.p);
-        Lmax = 0;
-        {
-            size_t tb = 0;
-            HIPCHK(hipcub::DeviceReduce::Max(nullptr, tb, len.p, (uint32_t*)counters.p, (int)P, stream));
-            tmp.ensure(tb);
-            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceReduce::Max(tmp.p, tb, len.p, (uint32_t*)counters.p, (int)P, stream)); });
-            Lmax = read_u32((const uint32_t*)counters.p);
-        }
+        zero(counters.p + 6, 8);
+        launch(KC_TRIE, k_prep, P, d_off, d_bytes, P, len.p, (unsigned int*)(counters.p + 6));
+        const uint64_t pv = read_u64(counters.p + 6);
+        Lmax = (uint32_t)pv;
+        if (n_term) *n_term = (uint32_t)(pv >> 32);
         if (Lmax == 0) return false;
-        // patterns per length (decides when the trie stops sharing)
-        hist.assign(Lmax + 1, 0);
-        {
-            lhist.ensure(Lmax + 1);
-            zero(lhist.p, (Lmax + 1) * 8);
-            launch(KC_TRIE, k_len_hist, P, (const uint32_t*)len.p, P, Lmax, lhist.p);
-            HIPCHK(hipMemcpyAsync(hist.data(), lhist.p, (Lmax + 1) * 8, hipMemcpyDeviceToHost, stream));
-            HIPCHK(hipStreamSynchronize(stream));
-        }
-        ge.assign(Lmax + 2, 0);  // patterns with length >= l
-        for (int l = (int)Lmax; l >= 0; l--) ge[l] = ge[l + 1] + hist[l];
+        // ---- B. reversed-pattern sort (trie order) and neighbours' common suffix
         const uint32_t nch = (Lmax + 15) / 16;
         keys.ensure((size_t)nch * P);
         launch(KC_TRIE, k_keys, P, d_bytes, d_off, (const uint32_t*)len.p, P, (const uint8_t*)code_of.p, sigma, nch, keys.p);
@@ -459,17 +476,28 @@ struct Engine {
         slen.ensure(P);
         lcp.ensure(P);
         launch(KC_TRIE, k_slen_lcp, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)keys.p, nch, P, slen.p, lcp.p);
+        // ---- C. nodes per depth and patterns per length, read once
+        lhist.ensure(2 * (size_t)(Lmax + 2));
+        zero(lhist.p, 2 * (size_t)(Lmax + 2) * 8);
+        if (Lmax + 2 <= 1024)
+            launch(KC_TRIE, k_trie_counts, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, Lmax, lhist.p, lhist.p + (Lmax + 2));
+        else
+            launch(KC_TRIE, k_trie_counts_global, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, lhist.p, lhist.p + (Lmax + 2));
+        std::vector<unsigned long long> hv(2 * (size_t)(Lmax + 2));
+        HIPCHK(hipMemcpyAsync(hv.data(), lhist.p, hv.size() * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        hist.assign(hv.begin() + (Lmax + 2), hv.begin() + (Lmax + 2) + (Lmax + 1));
+        nodes_at.assign(Lmax + 2, 0);
+        int64_t run = 0;
+        for (uint32_t D = 0; D <= Lmax + 1; D++) {
+            run += (int64_t)hv[D];
+            nodes_at[D] = (uint64_t)run;
+        }
+        ge.assign(Lmax + 2, 0);  // patterns with length >= l
+        for (int l = (int)Lmax; l >= 0; l--) ge[l] = ge[l + 1] + hist[l];
         return true;
     }
 
-    // Ordered level-synchronous walk over the reversed-pattern trie for the batch (d_bytes,
-    // d_off, P).  Writes res_off/res_cnt/res_occ per pattern (original order) and
-    // appends the final interval lists to the archive.  With allow_deep, switches
-    // to k_deep once the trie stops sharing; patterns k_deep cannot hold are
-    // flagged in ovf_orig (original order) and their number returned.
-    // This path keeps every list in the reference's order (concatenation of the
-    // stepped dollar pile and other pile, adjacent merge, :300-324) and is used for
-    // patterns holding the end-marker '#', whose lists may overlap.
     uint32_t levels(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, uint64_t* r_off, uint32_t* r_cnt,
                     uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
         const KIdx X = kidx();
@@ -560,7 +588,7 @@ struct Engine {
                         R = scan_u32(rflag.p, rscan, V);
                         rb.ensure(R); re.ensure(R); ru.ensure(R);
                         launch(KC_LINK, k_run_build, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
-                               (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p);
+                               (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p, (uint32_t*)nullptr);
                         launch(KC_LINK, k_bounds, R, (const uint32_t*)ru.p, (uint64_t)R, doff.p, dend.p);
                         docb.ensure((size_t)R * 8);
                         doce.ensure((size_t)R * 8);
@@ -652,10 +680,28 @@ struct Engine {
         st.intervals_stepped += dv[0];
         st.link_hash_rows += dv[1];
         st.bytes_kernel[KC_DEEP] += dv[0] * (2 * 128) + dv[1] * 4 + (uint64_t)P * 24;
+        // lists that outgrew k_deep's registers: retry those patterns with wide lists
+        uint32_t nw = scan_u32(ovf.p, tscan, P);
+        if (nw && !no_wide) {
+            DBuf<uint32_t>& todo = sub_map;
+            todo.ensure(nw);
+            launch(KC_DEEP, k_list_flagged, P, P, (const uint32_t*)ovf.p, (const uint32_t*)tscan.p, todo.p);
+            DBuf<uint32_t>& ovf2 = hcnt;
+            ovf2.ensure(P);
+            zero(ovf2.p, P * 4);
+            ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
+            ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
+            launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, (const uint32_t*)todo.p, nw, (const uint32_t*)slen.p, (const uint32_t*)perm.p,
+                   d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf2.p);
+            abase += (uint64_t)nw * kDeepWide;
+            st.deep_overflow += nw;
+            HIPCHK(hipMemcpyAsync(ovf.p, ovf2.p, P * 4, hipMemcpyDeviceToDevice, stream));
+        }
         zero(ovf_orig, P * 4);
         launch(KC_DEEP, k_ovf_lens, P, P, (const uint32_t*)ovf.p, (const uint32_t*)perm.p, (const uint32_t*)len.p, ovf_orig);
-        const uint32_t novf = scan_u32(ovf.p, tscan, P);
-        st.deep_overflow += novf;
+        const uint32_t novf = nw ? (no_wide ? nw : scan_u32(ovf.p, tscan, P)) : 0u;
+        if (no_wide) st.deep_overflow += nw;
+        st.deep_level_rerun += novf;
         return novf;
     }
 
@@ -667,40 +713,44 @@ struct Engine {
     uint32_t levels2(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, uint64_t* r_off, uint32_t* r_cnt,
                      uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
         const KIdx X = kidx();
-        uint32_t Lmax = 0;
+        uint32_t Lmax = 0, n_term = 0;
         std::vector<unsigned long long> hist;
         std::vector<uint64_t> ge;
-        if (!build_trie(d_bytes, d_off, P, Lmax, hist, ge)) return 0;
+        if (!build_trie(d_bytes, d_off, P, Lmax, hist, ge, &n_term)) return 0;
+        if (n_term) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
         nid[0].ensure(P);
         nid[1].ensure(P);
+        flag.ensure(P);
+        scan.ensure(P + 1);
+        node_first.ensure(P);
+        node_parent.ensure(P);
+        node_char.ensure(P);
+        lcnt.ensure(NSHARD * 32 + 32);
+        uint32_t* d_runs = lcnt.p + NSHARD * 32;  // link runs of the current depth (device count)
         zero(nid[0].p, P * 4);
         int cur = 0;
         uint32_t Mcur = 1, ncur = 1;
         ib[0].ensure(1); ie[0].ensure(1); iu[0].ensure(1);
         {
-            uint32_t h[3] = {0, N - 1, 0};
-            std::memcpy(pinned, h, sizeof h);
-            HIPCHK(hipMemcpyAsync(ib[0].p, &pinned[0], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(ie[0].p, &pinned[1], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(iu[0].p, &pinned[2], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipStreamSynchronize(stream));
+            uint32_t* h = pinned;
+            h[0] = 0; h[1] = N - 1; h[2] = 0;
+            HIPCHK(hipMemcpyAsync(ib[0].p, &h[0], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(ie[0].p, &h[1], 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(iu[0].p, &h[2], 4, hipMemcpyHostToDevice, stream));
         }
-        lcnt.ensure(NSHARD * 32);
         uint32_t novf = 0;
         for (uint32_t d = 0; d < Lmax; d++) {
             const uint32_t D = d + 1;
             const int nxt = cur ^ 1;
-            flag.ensure(P);
-            launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
-            const uint32_t M = scan_u32(flag.p, scan, P);
+            const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
             if (allow_deep && d >= 1 && (double)M >= kDeepShare * (double)ge[D] && (double)ncur <= kDeepItems * (double)Mcur) {
                 // group the unordered items by node, then finish patterns one per thread
-                gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur);
-                zero(gcnt.p, (size_t)Mcur * 4);
-                zero(gfill.p, (size_t)Mcur * 4);
+                gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur); goff.ensure(Mcur);
+                launch(KC_DEEP, k_zero4, 2 * (size_t)Mcur, gcnt.p, (uint64_t)Mcur, gfill.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0,
+                       (uint32_t*)nullptr, (uint64_t)0);
                 launch(KC_DEEP, k_group_count, ncur, ncur, (const uint32_t*)iu[cur].p, gcnt.p);
-                scan_u32(gcnt.p, goff, Mcur);
+                exclusive_scan(gcnt.p, goff.p, Mcur);
                 gb.ensure(ncur); gee.ensure(ncur);
                 launch(KC_DEEP, k_group_scatter, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p,
                        (const uint32_t*)goff.p, gfill.p, gb.p, gee.p);
@@ -710,25 +760,31 @@ struct Engine {
             }
             st.depths++;
             st.trie_nodes += M;
-            node_first.ensure(M);
-            node_parent.ensure(M);
-            node_char.ensure(M);
-            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
-                   (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
+            const bool finishing = hist[D] != 0;
+            // one zeroing launch: shard counters, child links of the parents, finisher tables
             child_first.ensure(Mcur);
             child_end.ensure(Mcur);
-            zero(child_first.p, (size_t)Mcur * 4);
-            zero(child_end.p, (size_t)Mcur * 4);
+            if (finishing) { node_occ.ensure(M); foff.ensure(M); fend.ensure(M); fin.ensure(M); }
+            launch(KC_NODES, k_zero4, (size_t)NSHARD * 32 + 32 + 2 * (size_t)Mcur, lcnt.p, (uint64_t)NSHARD * 32 + 32, child_first.p,
+                   (uint64_t)Mcur, child_end.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0);
+            if (finishing)
+                launch(KC_NODES, k_zero4, 3 * (size_t)M, node_occ.p, (uint64_t)M, foff.p, (uint64_t)M, fend.p, (uint64_t)M, (uint32_t*)nullptr,
+                       (uint64_t)0);
+            // children nodes at depth D (node count known from build_trie: no read-back)
+            launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
+            exclusive_scan(flag.p, scan.p, P);
+            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
+                   (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             launch(KC_NODES, k_child_links, M, (const uint32_t*)node_parent.p, M, child_first.p, child_end.p);
             // fused step + '#'-row emission over the current items (sharded appends)
             size_t cap_next = std::max<size_t>(shard_bound(ncur, 2), 4096);
             size_t cap_keys = std::max<size_t>(shard_bound(ncur, 1), 4096);
             size_t cap_chunks = std::max<size_t>(shard_bound(ncur, 1) / 8, 1024);
-            for (;;) {
+            for (bool first = true;; first = false) {
                 eu.ensure(cap_next * NSHARD); eb.ensure(cap_next * NSHARD); ee.ensure(cap_next * NSHARD);
                 ekeys.ensure(cap_keys * NSHARD);
                 eck_u.ensure(cap_chunks * NSHARD); eck_k.ensure(cap_chunks * NSHARD); eck_e.ensure(cap_chunks * NSHARD);
-                zero(lcnt.p, NSHARD * 32 * 4);
+                if (!first) zero(lcnt.p, NSHARD * 32 * 4);
                 if (d > 0)
                     launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
                            (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
@@ -739,14 +795,14 @@ struct Engine {
                            (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
                            X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
                            (uint32_t)cap_chunks);
-                fetch_shards();
+                fetch_shards();  // sync A
                 const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
                 if (m0 <= cap_next && m1 <= cap_keys && m2 <= cap_chunks) break;
                 cap_next = std::max<size_t>(cap_next, m0 + m0 / 4 + 1024);
                 cap_keys = std::max<size_t>(cap_keys, m1 + m1 / 4 + 1024);
                 cap_chunks = std::max<size_t>(cap_chunks, m2 + m2 / 4 + 256);
             }
-            uint32_t nchunks = shard_total(2);
+            const uint32_t nchunks = shard_total(2);
             st.intervals_stepped += ncur;
             const std::vector<uint32_t> keep_keys = shard_counts(1);
             if (nchunks) {  // long '#'-row ranges: pack, then one chunk per thread
@@ -776,8 +832,9 @@ struct Engine {
             }
             const uint32_t nkeys = shard_total(1);
             st.link_hash_rows += nkeys;
-            uint32_t R = 0;
+            uint32_t nnext = shard_total(0);
             if (nkeys) {
+                // link: sort (node, segment), maximal runs of previous-segment ranges, step them
                 lkeys.ensure(nkeys);
                 lkeys2.ensure(nkeys);
                 unshard1(1, cap_keys, ekeys.p, lkeys.p, nkeys);
@@ -788,19 +845,18 @@ struct Engine {
                 tmp.ensure(tb);
                 timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream)); });
                 rflag.ensure(nkeys);
+                rscan.ensure(nkeys);
                 launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, rflag.p);
-                R = scan_u32(rflag.p, rscan, nkeys);
-                rb.ensure(R); re.ensure(R); ru.ensure(R);
+                exclusive_scan(rflag.p, rscan.p, nkeys);
+                rb.ensure(nkeys); re.ensure(nkeys); ru.ensure(nkeys);
                 launch(KC_LINK, k_run_build, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
-                       (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p);
-                st.link_ranges += R;
-                st.intervals_stepped += R;
+                       (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p, d_runs);
                 const std::vector<uint32_t> keep_items = shard_counts(0);
                 for (;;) {
-                    launch(KC_STEP, k_lvl_dollar, R, R, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
+                    launch(KC_STEP, k_lvl_dollar, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
                            (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p, X, eu.p, eb.p, ee.p,
                            (uint32_t)cap_next, lcnt.p);
-                    fetch_shards();
+                    fetch_shards();  // sync B
                     const uint32_t m0 = shard_max(0);
                     if (m0 <= cap_next) break;
                     // grow the item shards keeping k_lvl_items' output, then redo the dollar step
@@ -811,35 +867,29 @@ struct Engine {
                     HIPCHK(hipMemcpyAsync(lcnt.p, pinned_big, NSHARD * 32 * 4, hipMemcpyHostToDevice, stream));
                     cap_next = ncap;
                 }
+                const uint32_t R = hsh[NSHARD * 32];
+                st.link_ranges += R;
+                st.intervals_stepped += R;
                 st.bytes_kernel[KC_STEP] += (uint64_t)R * (12 + 2 * 128);
+                nnext = shard_total(0);
             }
-            const uint32_t nnext = shard_total(0);
             st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * 128) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
+            if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
+                                    ncur, nkeys, nkeys ? hsh[NSHARD * 32] : 0u, nnext);
             ib[nxt].ensure(nnext); ie[nxt].ensure(nnext); iu[nxt].ensure(nnext);
             if (nnext) unshard3(0, cap_next, eu.p, eb.p, ee.p, iu[nxt].p, ib[nxt].p, ie[nxt].p, nnext);
-            if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
-                                    ncur, nkeys, R, nnext);
             // finish patterns of length D: their node's items, sorted by row
-            if (hist[D]) {
-                fin.ensure(M);
+            if (finishing) {
                 launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
-                node_occ.ensure(M);
-                zero(node_occ.p, (size_t)M * 4);
                 const size_t cap_fin = shard_bound(nnext, 1);
                 efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD);
-                zero(lcnt.p, NSHARD * 32 * 4);
                 launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
                        (const uint8_t*)fin.p, lcnt.p, efk.p, efv.p, (uint32_t)cap_fin, node_occ.p);
                 fetch_shards();
-                if (shard_max(4) > cap_fin) throw Fail(EDSBWT_E_DEVICE, "finisher shard overflow");  // cap_fin >= items per shard
                 const uint32_t F = shard_total(4);
                 fk.ensure(F); fv.ensure(F);
-                if (F) unshard2(4, cap_fin, efk.p, efv.p, fk.p, fv.p, F);
-                foff.ensure(M);
-                fend.ensure(M);
-                zero(foff.p, (size_t)M * 4);
-                zero(fend.p, (size_t)M * 4);
                 if (F) {
+                    unshard2(4, cap_fin, efk.p, efv.p, fk.p, fv.p, F);
                     fk2.ensure(F); fv2.ensure(F);
                     int endbit = 33;
                     while (endbit < 64 && ((uint64_t)M >> (endbit - 32))) endbit++;
@@ -867,10 +917,12 @@ struct Engine {
     // d_bytes/d_off/d_counts are device pointers; returns number of records
     uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
         st = edsbwt_stats{};
-        prof = (flags & EDSBWT_PROFILE) != 0;
+        prof = (flags & (EDSBWT_PROFILE | EDSBWT_PROFILE_LIGHT)) != 0;
+        prof_mask = (flags & EDSBWT_PROFILE) ? ~0u : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_LOCATE) | (1u << KC_LINKSORT));
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
         const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
+        no_wide = (flags & EDSBWT_NO_WIDE) != 0;
         if (use_table) build_table();
         st.patterns = P;
         if (P == 0) return 0;
@@ -886,16 +938,14 @@ struct Engine {
         zero(res_occ.p, P * 4);
         ovf_orig.ensure(P);
         uint64_t abase = 0;
-        // patterns holding '#' make the reference's lists overlap: ordered path for the batch
+        // patterns holding '#' make the reference's lists overlap: they take the ordered path
         bool ordered = (flags & EDSBWT_ORDERED) != 0;
+        uint32_t novf = 0;
         if (!ordered) {
-            hterm.ensure(P);
-            zero(counters.p + 4, 8);
-            launch(KC_TRIE, k_has_term, P, P, d_off, d_bytes, hterm.p, (uint32_t*)(counters.p + 4));
-            ordered = read_u32((const uint32_t*)(counters.p + 4)) != 0;
+            novf = levels2(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
+            if (novf == kNeedOrdered) ordered = true;
         }
-        const uint32_t novf = ordered ? levels(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p)
-                                      : levels2(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
+        if (ordered) novf = levels(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
         if (novf) {
             // patterns k_deep could not hold: gather them and run the unbounded level path
             const uint32_t n = scan_u32(ovf_orig.p, ovf_scan, P);
@@ -915,20 +965,30 @@ struct Engine {
             launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const uint64_t*)sub_roff.p, (const uint32_t*)sub_rcnt.p,
                    (const uint32_t*)sub_rocc.p, res_off.p, res_cnt.p, res_occ.p);
         }
-        // ---- D. counts (backwardSearch's return value) and locate
+        // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
         HIPCHK(hipMemcpyAsync(d_counts, res_occ.p, P * 4, hipMemcpyDeviceToDevice, stream));
         zero(counters.p + 1, 8);
         launch(KC_FINISH, k_count_found, P, (const uint32_t*)res_occ.p, P, counters.p + 1);
-        st.found = read_u64(counters.p + 1);
+        if (locate) {
+            occ64.ensure(P);
+            tc64.ensure(P);
+            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_occ.p, P, occ64.p);
+            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_cnt.p, P, tc64.p);
+            inclusive_scan_u64(occ64.p, oscan, P);
+            inclusive_scan_u64(tc64.p, tscan64, P);
+            HIPCHK(hipMemcpyAsync(pinned + 2, oscan.p + P, 8, hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipMemcpyAsync(pinned + 4, tscan64.p + P, 8, hipMemcpyDeviceToHost, stream));
+        }
+        HIPCHK(hipMemcpyAsync(pinned, counters.p + 1, 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        uint64_t rb3[3];
+        std::memcpy(rb3, pinned, 24);
+        st.found = rb3[0];
         st.not_found = P - st.found;
         uint64_t OCC = 0;
         if (locate) {
-            occ64.ensure(P);
-            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_occ.p, P, occ64.p);
-            OCC = scan_u64(occ64.p, oscan, P);
-            tc64.ensure(P);
-            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_cnt.p, P, tc64.p);
-            const uint64_t TT = scan_u64(tc64.p, tscan64, P);
+            OCC = rb3[1];
+            const uint64_t TT = rb3[2];
             if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
                 launch(KC_LOCPREP, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
@@ -937,12 +997,15 @@ struct Engine {
                 zero(counters.p, 8);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
                        X, use_table ? 1 : 0, rec.p, counters.p);
-                st.locate_lf_steps = read_u64(counters.p);
-                st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * 128 + OCC * (128 + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
+                HIPCHK(hipMemcpyAsync(pinned, counters.p, 8, hipMemcpyDeviceToHost, stream));
             }
         }
         HIPCHK(hipEventRecord(e1, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        if (locate && OCC) {
+            std::memcpy(&st.locate_lf_steps, pinned, 8);
+            st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * 128 + OCC * (128 + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
+        }
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         st.ms_total = ms;

@@ -258,8 +258,10 @@ __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const
 
 __global__ void k_run_build(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rscan,
                             const uint32_t* __restrict__ seg_lo, const uint32_t* __restrict__ seg_start,
-                            uint32_t* __restrict__ rb, uint32_t* __restrict__ re, uint32_t* __restrict__ rown) {
+                            uint32_t* __restrict__ rb, uint32_t* __restrict__ re, uint32_t* __restrict__ rown,
+                            uint32_t* __restrict__ nruns) {
     GRID_STRIDE(t, V) {
+        if (nruns && t + 1 == V) *nruns = rscan[t] + flag[t];
         const uint64_t k = keys[t];
         const uint32_t s = (uint32_t)k;
         const uint32_t r = rscan[t] + flag[t] - 1;
@@ -538,6 +540,98 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
     if (n_hash) atomicAdd(ctr + 3, n_hash);
 }
 
+// Patterns k_deep<8> could not hold: the same walk with lists of up to KW intervals
+// in private (scratch) arrays, one thread per flagged pattern.  Rare, so plain loops.
+template <int KW>
+__global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, const uint32_t* __restrict__ todo, uint32_t ntodo,
+                                                  const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
+                                                  const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                                                  const uint8_t* __restrict__ code_of, const uint32_t* __restrict__ nid,
+                                                  const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
+                                                  const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
+                                                  uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, uint64_t* __restrict__ res_off,
+                                                  uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
+                                                  uint32_t* __restrict__ ovf2) {
+    (void)P;
+    GRID_STRIDE(j, ntodo) {
+        const uint32_t i = todo[j];
+        const uint32_t L = slen[i];
+        const uint32_t u = nid[i];
+        const uint32_t n0 = iend[u] - ioff[u];
+        if (n0 > KW) { ovf2[i] = 1; continue; }
+        uint32_t cb[KW], ce[KW], nb[KW], ne[KW], sb[KW], se[KW], raw[KW];
+        uint32_t cn = n0;
+        for (uint32_t t = 0; t < cn; t++) { cb[t] = ib[ioff[u] + t]; ce[t] = ie[ioff[u] + t]; }
+        const uint32_t a = perm[i];
+        const uint8_t* pat = bytes + off[a];
+        bool over = false;
+        for (uint32_t d = D0; d < L && cn && !over; d++) {
+            const uint32_t code = code_of[pat[L - 1 - d]];
+            if (code >= X.sigma) { cn = 0; break; }
+            const uint32_t c = code;
+            uint32_t rn = 0;
+            for (uint32_t q = 0; q < cn && !over; q++) {
+                uint32_t h0, h1;
+                rank2(X.occ, cb[q], c, h0, sb[q]);
+                rank2(X.occ, ce[q] + 1, c, h1, se[q]);
+                for (uint32_t k = h0; k < h1; k++) {
+                    const uint32_t s = X.eof_seg[k];
+                    if (!s) continue;
+                    uint32_t pos = 0;
+                    while (pos < rn && raw[pos] < s) pos++;
+                    if (pos < rn && raw[pos] == s) continue;
+                    if (rn == KW) { over = true; break; }
+                    for (uint32_t t = rn; t > pos; t--) raw[t] = raw[t - 1];
+                    raw[pos] = s;
+                    rn++;
+                }
+            }
+            if (over) break;
+            uint32_t nn = 0;
+            auto push = [&](uint32_t b, uint32_t e) {
+                if (nn && b == ne[nn - 1] + 1) { ne[nn - 1] = e; return; }
+                if (nn == KW) { over = true; return; }
+                nb[nn] = b; ne[nn] = e; nn++;
+            };
+            for (uint32_t t = 0; t < rn && !over;) {
+                // a maximal run of [seg_lo[s], s-1] ranges (link(), :533-561)
+                const uint32_t lo = X.seg_lo[raw[t]];
+                uint32_t hi = raw[t];
+                uint32_t t2 = t + 1;
+                while (t2 < rn && X.seg_lo[raw[t2]] <= hi) { hi = raw[t2]; t2++; }
+                uint32_t x0, x1, y0, y1;
+                rank2(X.occ, X.seg_start[lo], c, x0, x1);
+                rank2(X.occ, X.seg_start[hi], c, y0, y1);  // one past the last word of segment hi-1
+                if (y1 > x1) push(X.C[c] + x1, X.C[c] + y1 - 1);
+                t = t2;
+            }
+            for (uint32_t q = 0; q < cn && !over; q++)
+                if (se[q] > sb[q]) push(X.C[c] + sb[q], X.C[c] + se[q] - 1);
+            if (over) break;
+            cn = nn;
+            for (uint32_t t = 0; t < cn; t++) { cb[t] = nb[t]; ce[t] = ne[t]; }
+        }
+        if (over) { ovf2[i] = 1; continue; }
+        for (uint32_t t = 1; t < cn; t++) {  // ascending rows
+            const uint32_t xb = cb[t], xe = ce[t];
+            uint32_t q = t;
+            while (q && cb[q - 1] > xb) { cb[q] = cb[q - 1]; ce[q] = ce[q - 1]; q--; }
+            cb[q] = xb; ce[q] = xe;
+        }
+        const uint32_t o = perm[i];
+        uint32_t occ = 0;
+        const uint64_t at = abase + (uint64_t)j * KW;
+        for (uint32_t t = 0; t < cn; t++) { ab[at + t] = cb[t]; ae[at + t] = ce[t]; occ += ce[t] - cb[t] + 1; }
+        res_off[o] = at;
+        res_cnt[o] = cn;
+        res_occ[o] = occ;
+    }
+}
+
+__global__ void k_list_flagged(uint64_t P, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ fscan, uint32_t* __restrict__ out) {
+    GRID_STRIDE(i, P) if (flag[i]) out[fscan[i]] = (uint32_t)i;
+}
+
 // pattern-length histogram: per-block LDS bins, one global atomic per bin per block
 __global__ void __launch_bounds__(256) k_len_hist(const uint32_t* __restrict__ len, uint64_t P, uint32_t Lmax,
                                                   unsigned long long* __restrict__ hist) {
@@ -728,11 +822,12 @@ __global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* 
 }
 
 // dollar items (previous-segment word ranges of a node) stepped by each child
-__global__ void __launch_bounds__(256) k_lvl_dollar(uint32_t n, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
+__global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__ dn, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
                                                     const uint32_t* __restrict__ de, const uint32_t* __restrict__ child_first,
                                                     const uint32_t* __restrict__ child_end, const uint8_t* __restrict__ node_char, KIdx X,
                                                     uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                     uint32_t cap_next, uint32_t* __restrict__ cnt_all) {
+    const uint32_t n = *dn;  // link runs, counted on the device by k_run_build
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
     nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
@@ -1003,10 +1098,86 @@ __global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, cons
     GRID_STRIDE(x, N) off[x] = wlen[da[x]] - off[x];
 }
 
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
 __global__ void k_count_found(const uint32_t* __restrict__ occ, uint64_t P, unsigned long long* __restrict__ found) {
     unsigned long long f = 0;
     GRID_STRIDE(i, P) f += occ[i] > 0;
-    if (f) atomicAdd(found, f);
+    f = wave_sum(f);
+    if ((threadIdx.x & 63) == 0 && f) atomicAdd(found, f);
+}
+
+// one launch: lengths, longest pattern, patterns holding the end-marker '#'
+__global__ void k_prep(const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes, uint64_t P, uint32_t* __restrict__ len,
+                       unsigned int* __restrict__ out /* [0] Lmax, [1] patterns with '#' */) {
+    uint32_t mx = 0;
+    unsigned long long nt = 0;
+    GRID_STRIDE(i, P) {
+        const uint64_t a = off[i], b = off[i + 1];
+        len[i] = (uint32_t)(b - a);
+        mx = max(mx, (uint32_t)(b - a));
+        uint32_t f = 0;
+        for (uint64_t t = a; t < b; t++) f |= bytes[t] == '#';
+        nt += f;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+    nt = wave_sum(nt);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(out + 0, mx);
+        if (nt) atomicAdd(out + 1, (unsigned int)nt);
+    }
+}
+
+// per depth D: trie nodes M_D = #{i : lcp[i] < D <= slen[i]} (difference array over D)
+// and patterns per length, in one pass (LDS bins, Lmax < 1023)
+__global__ void __launch_bounds__(256) k_trie_counts(const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp, uint64_t P,
+                                                     uint32_t Lmax, unsigned long long* __restrict__ diff, unsigned long long* __restrict__ hist) {
+    __shared__ unsigned int sd[1024], sh[1024];
+    const uint32_t nb = Lmax + 2;
+    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) sd[t] = sh[t] = 0;
+    __syncthreads();
+    GRID_STRIDE(i, P) {
+        const uint32_t l = slen[i], c = lcp[i];
+        atomicAdd(&sh[l], 1u);
+        if (c < l) {
+            atomicAdd(&sd[c + 1], 1u);
+            atomicSub(&sd[l + 1], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < nb; t += blockDim.x) {
+        if (sd[t]) atomicAdd(diff + t, (unsigned long long)(int)sd[t]);
+        if (sh[t]) atomicAdd(hist + t, (unsigned long long)sh[t]);
+    }
+}
+
+__global__ void k_trie_counts_global(const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp, uint64_t P,
+                                     unsigned long long* __restrict__ diff, unsigned long long* __restrict__ hist) {
+    GRID_STRIDE(i, P) {
+        const uint32_t l = slen[i], c = lcp[i];
+        atomicAdd(hist + l, 1ull);
+        if (c < l) {
+            atomicAdd(diff + c + 1, 1ull);
+            atomicAdd(diff + l + 1, ~0ull);  // -1 mod 2^64
+        }
+    }
+}
+
+// zero up to four buffers in one launch
+__global__ void k_zero4(uint32_t* __restrict__ a, uint64_t na, uint32_t* __restrict__ b, uint64_t nb, uint32_t* __restrict__ c, uint64_t nc,
+                        uint32_t* __restrict__ d, uint64_t nd) {
+    const uint64_t n = na + nb + nc + nd;
+    GRID_STRIDE(i, n) {
+        if (i < na) a[i] = 0;
+        else if (i < na + nb) b[i - na] = 0;
+        else if (i < na + nb + nc) c[i - na - nb] = 0;
+        else d[i - na - nb - nc] = 0;
+    }
 }
 
 __global__ void k_fill_u32(uint32_t* __restrict__ a, uint64_t n, uint32_t v) { GRID_STRIDE(i, n) a[i] = v; }

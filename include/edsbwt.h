@@ -41,6 +41,9 @@ enum {
 #define EDSBWT_PROFILE      0x8u /* record per-kernel HIP-event times into edsbwt_stats */
 #define EDSBWT_NO_DEEP      0x10u/* level-synchronous trie walk for every depth (no per-pattern
                                     finishing kernel); same results, used by tests */
+#define EDSBWT_PROFILE_LIGHT 0x40u/* events only around the few large launches (fused step, deep,
+                                    locate, link sort): what bench.py uses inside its timed region */
+#define EDSBWT_NO_WIDE      0x80u/* tests: skip the wide-list retry of k_deep overflows */
 #define EDSBWT_ORDERED      0x20u/* keep every interval list in the reference's order at every
                                     depth (the path patterns holding '#' take); same results */
 
@@ -72,7 +75,8 @@ typedef struct {
     uint64_t link_ranges;     /* merged previous-segment ranges produced by link */
     uint64_t locate_lf_steps; /* LF steps of the locate walk (0 with LOCATE_TABLE) */
     uint64_t deep_from_depth; /* depth at which patterns were finished one per thread (0: never) */
-    uint64_t deep_overflow;   /* patterns re-run by the level path because their lists outgrew registers */
+    uint64_t deep_overflow;   /* patterns whose lists outgrew k_deep's registers (retried with wide lists) */
+    uint64_t deep_level_rerun;/* of those, patterns re-run by the level path (lists beyond the wide limit) */
     double ms_total;          /* device time of the call (hipEvent) */
     double ms_kernel[16];     /* EDSBWT_PROFILE: per kernel class, see edsbwt_kernel_name */
     uint64_t launches_kernel[16];

@@ -110,9 +110,13 @@ def test_deep_overflow_rerun(oracle, edsbwt, tmp_path):
     base = _build(oracle, tmp_path, edsgen.eds_text(segs))
     pats = ["".join(rng.choice("AC") for _ in range(rng.randint(6, 30))) for _ in range(2000)]
     pats += [edsgen.planted(rng, segs, 25) or "ACA" for _ in range(2000)]
-    _compare(oracle, edsbwt, base, pats, table_too=False)
+    oc, oo = _compare(oracle, edsbwt, base, pats, table_too=False)
     with edsbwt.Index(base) as idx:
         buf, offs = _pack(pats)
         idx.search((buf, offs))
         st = idx.stats()
-    assert st["deep_from_depth"] > 0 and st["deep_overflow"] > 0, st
+        assert st["deep_from_depth"] > 0 and st["deep_overflow"] > 0, st
+        gc, go = idx.search((buf, offs), wide=False)   # overflows straight to the level path
+        st2 = idx.stats()
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert st2["deep_level_rerun"] > 0, st2
