@@ -24,7 +24,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(_HERE, "_build")
-LIB_PATH = os.path.join(BUILD_DIR, "libedsbwt.so")
+LIB_PATH = os.environ.get("EDSBWT_LIB") or os.path.join(BUILD_DIR, "libedsbwt.so")
 
 COUNT_ONLY = 0x1
 LOCATE = 0x2

@@ -342,7 +342,7 @@ struct Engine {
         std::memcpy(h_code_of, H.code_of, 256);
         if (W > N) throw Fail(EDSBWT_E_FORMAT, "more words than rows");
         // occ blocks (parallel over block ranges)
-        const size_t nblk = (size_t)N / 256 + 1;
+        const size_t nblk = (size_t)N / kOccRows + 1;
         std::vector<OccBlock> hb(nblk);
         std::vector<uint32_t> tot(8, 0);
         {
@@ -356,8 +356,8 @@ struct Engine {
                     for (size_t b = b0; b < b1; b++) {
                         OccBlock& B = hb[b];
                         std::memset(&B, 0, sizeof B);
-                        for (uint32_t r = 0; r < 256; r++) {
-                            size_t x = b * 256 + r;
+                        for (uint32_t r = 0; r < kOccRows; r++) {
+                            size_t x = b * kOccRows + r;
                             uint32_t c = x < N ? H.code_of[H.L[x]] : 7u;
                             if (x < N) part[t][c]++;
                             B.plane[0][r >> 6] |= (uint64_t)(c & 1) << (r & 63);
@@ -367,19 +367,25 @@ struct Engine {
                     }
                 });
             for (auto& x : th) x.join();
-            // block-start counts: sequential prefix over blocks within each part, offset by previous parts
-            std::vector<uint32_t> run(8, 0);
-            for (unsigned t = 0; t < T; t++) {
-                auto [b0, b1] = rng(t);
-                for (size_t b = b0; b < b1; b++) {
-                    for (int c = 0; c < 8; c++) hb[b].cnt[c] = run[c];
-                    for (uint32_t r = 0; r < 256; r++) {
-                        size_t x = b * 256 + r;
-                        if (x < N) run[H.code_of[H.L[x]]]++;
+            // block-start counts: each part's running counts start from the parts before it
+            std::vector<std::vector<uint32_t>> base(T, std::vector<uint32_t>(8, 0));
+            for (unsigned t = 1; t < T; t++)
+                for (int c = 0; c < 8; c++) base[t][c] = base[t - 1][c] + part[t - 1][c];
+            std::vector<std::thread> th2;
+            for (unsigned t = 0; t < T; t++)
+                th2.emplace_back([&, t] {
+                    auto [b0, b1] = rng(t);
+                    std::vector<uint32_t> run = base[t];
+                    for (size_t b = b0; b < b1; b++) {
+                        for (int c = 0; c < 8; c++) hb[b].cnt[c] = run[c];
+                        for (uint32_t r = 0; r < kOccRows; r++) {
+                            size_t x = b * kOccRows + r;
+                            if (x < N) run[H.code_of[H.L[x]]]++;
+                        }
                     }
-                }
-            }
-            tot = run;
+                });
+            for (auto& x : th2) x.join();
+            for (int c = 0; c < 8; c++) tot[c] = base[T - 1][c] + part[T - 1][c];
         }
         uint32_t acc = 0;
         for (uint32_t c = 0; c < 8; c++) { C[c] = acc; acc += tot[c]; }
@@ -556,7 +562,7 @@ struct Engine {
             iocb.ensure((size_t)ncur * 8);
             ioce.ensure((size_t)ncur * 8);
             launch(KC_EXPAND, k_expand, ncur, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p, (uint64_t)ncur, X, iocb.p, ioce.p);
-            st.bytes_kernel[KC_EXPAND] += (uint64_t)ncur * (2 * 128 + 8 + 64);
+            st.bytes_kernel[KC_EXPAND] += (uint64_t)ncur * (2 * sizeof(OccBlock) + 8 + 64);
             // LINK (not before the first step, :246-258)
             uint32_t R = 0;
             doff.ensure(Mcur);
@@ -593,7 +599,7 @@ struct Engine {
                         docb.ensure((size_t)R * 8);
                         doce.ensure((size_t)R * 8);
                         launch(KC_EXPAND, k_expand, R, (const uint32_t*)rb.p, (const uint32_t*)re.p, (uint64_t)R, X, docb.p, doce.p);
-                        st.bytes_kernel[KC_EXPAND] += (uint64_t)R * (2 * 128 + 8 + 64);
+                        st.bytes_kernel[KC_EXPAND] += (uint64_t)R * (2 * sizeof(OccBlock) + 8 + 64);
                         st.link_ranges += R;
                     }
                 }
@@ -679,7 +685,7 @@ struct Engine {
         std::memcpy(dv, pinned, 16);
         st.intervals_stepped += dv[0];
         st.link_hash_rows += dv[1];
-        st.bytes_kernel[KC_DEEP] += dv[0] * (2 * 128) + dv[1] * 4 + (uint64_t)P * 24;
+        st.bytes_kernel[KC_DEEP] += dv[0] * (2 * sizeof(OccBlock)) + dv[1] * 4 + (uint64_t)P * 24;
         // lists that outgrew k_deep's registers: retry those patterns with wide lists
         uint32_t nw = scan_u32(ovf.p, tscan, P);
         if (nw && !no_wide) {
@@ -870,10 +876,10 @@ struct Engine {
                 const uint32_t R = hsh[NSHARD * 32];
                 st.link_ranges += R;
                 st.intervals_stepped += R;
-                st.bytes_kernel[KC_STEP] += (uint64_t)R * (12 + 2 * 128);
+                st.bytes_kernel[KC_STEP] += (uint64_t)R * (12 + 2 * sizeof(OccBlock));
                 nnext = shard_total(0);
             }
-            st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * 128) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
+            st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * sizeof(OccBlock)) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
             if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
                                     ncur, nkeys, nkeys ? hsh[NSHARD * 32] : 0u, nnext);
             ib[nxt].ensure(nnext); ie[nxt].ensure(nnext); iu[nxt].ensure(nnext);
@@ -1004,7 +1010,7 @@ struct Engine {
         HIPCHK(hipStreamSynchronize(stream));
         if (locate && OCC) {
             std::memcpy(&st.locate_lf_steps, pinned, 8);
-            st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * 128 + OCC * (128 + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
+            st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * sizeof(OccBlock) + OCC * (sizeof(OccBlock) + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
         }
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));

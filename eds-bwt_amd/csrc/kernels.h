@@ -7,12 +7,30 @@
 
 namespace edsbwt {
 
-// 128-B rank block over 256 BWT rows
+#ifndef EDSBWT_OCC_ROWS
+#define EDSBWT_OCC_ROWS 64
+#endif
+#if EDSBWT_OCC_ROWS == 256
+// 128-B rank block over 256 BWT rows: 0.5 B/row
+constexpr uint32_t kOccShift = 8;
 struct alignas(128) OccBlock {
     uint32_t cnt[8];
     uint64_t plane[3][4];
 };
 static_assert(sizeof(OccBlock) == 128, "occ block must be one 128-B line");
+#elif EDSBWT_OCC_ROWS == 64
+// 64-B rank block over 64 BWT rows: 1 B/row, one half-line per rank query
+constexpr uint32_t kOccShift = 6;
+struct alignas(64) OccBlock {
+    uint32_t cnt[8];
+    uint64_t plane[3][1];
+    uint64_t pad;
+};
+static_assert(sizeof(OccBlock) == 64, "occ block must be 64 B");
+#else
+#error "EDSBWT_OCC_ROWS must be 64 or 256"
+#endif
+constexpr uint32_t kOccRows = 1u << kOccShift;
 
 // kernel-side view of the device index (passed by value)
 struct KIdx {

@@ -14,6 +14,7 @@
 namespace edsbwt {
 
 // ---------------------------------------------------------------- occ blocks
+#if EDSBWT_OCC_ROWS == 256
 __device__ __forceinline__ void load_block(const OccBlock* __restrict__ occ, uint32_t blk, uint4 (&v)[8]) {
     const uint4* p = reinterpret_cast<const uint4*>(occ + blk);
 #pragma unroll
@@ -87,6 +88,85 @@ __device__ __forceinline__ uint32_t sym_rank(const OccBlock* __restrict__ occ, u
     *rank = acc;
     return c;
 }
+
+// rank of '#' (code 0) and of code c at row x from one occ-block line
+__device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
+    uint4 v[8];
+    load_block(occ, x >> 8, v);
+    const uint32_t r = x & 255u;
+    const uint32_t wq = r >> 6, bit = r & 63u;
+    const uint32_t cnt[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    uint32_t a0 = cnt[0], ac = 0;
+#pragma unroll
+    for (uint32_t cc = 1; cc < 8; cc++)
+        if (cc == c) ac = cnt[cc];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint64_t p0 = u64_of(v[2 + (q >> 1)], q & 1);
+        const uint64_t p1 = u64_of(v[4 + (q >> 1)], q & 1);
+        const uint64_t p2 = u64_of(v[6 + (q >> 1)], q & 1);
+        const uint64_t mq = (uint32_t)q < wq ? ~0ull : ((uint32_t)q == wq ? ((1ull << bit) - 1ull) : 0ull);
+        a0 += (uint32_t)__popcll(~p0 & ~p1 & ~p2 & mq);
+        const uint64_t e = ((c & 1) ? p0 : ~p0) & ((c & 2) ? p1 : ~p1) & ((c & 4) ? p2 : ~p2);
+        ac += (uint32_t)__popcll(e & mq);
+    }
+    r0 = a0;
+    rc = (c == 0) ? a0 : ac;
+}
+#else  // 64 rows per 64-B block
+struct OccV {
+    uint32_t cnt[8];
+    uint64_t p0, p1, p2;
+};
+__device__ __forceinline__ OccV load_block(const OccBlock* __restrict__ occ, uint32_t blk) {
+    const uint4* p = reinterpret_cast<const uint4*>(occ + blk);
+    const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    OccV o;
+    o.cnt[0] = a.x; o.cnt[1] = a.y; o.cnt[2] = a.z; o.cnt[3] = a.w;
+    o.cnt[4] = b.x; o.cnt[5] = b.y; o.cnt[6] = b.z; o.cnt[7] = b.w;
+    o.p0 = (uint64_t)c.y << 32 | c.x;
+    o.p1 = (uint64_t)c.w << 32 | c.z;
+    o.p2 = (uint64_t)d.y << 32 | d.x;
+    (void)d;
+    return o;
+}
+
+__device__ __forceinline__ void rank_all(const OccBlock* __restrict__ occ, uint32_t x, uint32_t sigma, uint32_t* out) {
+    const OccV v = load_block(occ, x >> 6);
+    const uint64_t m = (1ull << (x & 63u)) - 1ull;
+#pragma unroll
+    for (uint32_t c = 0; c < 8; c++) {
+        const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
+        out[c] = c < sigma ? v.cnt[c] + (uint32_t)__popcll(e & m) : 0u;
+    }
+}
+
+__device__ __forceinline__ uint32_t sym_rank(const OccBlock* __restrict__ occ, uint32_t x, uint32_t* rank) {
+    const OccV v = load_block(occ, x >> 6);
+    const uint32_t bit = x & 63u;
+    const uint64_t m = (1ull << bit) - 1ull;
+    const uint32_t c = (uint32_t)((v.p0 >> bit) & 1) | (uint32_t)(((v.p1 >> bit) & 1) << 1) | (uint32_t)(((v.p2 >> bit) & 1) << 2);
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t cc = 0; cc < 8; cc++)
+        if (cc == c) acc = v.cnt[cc];
+    const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
+    *rank = acc + (uint32_t)__popcll(e & m);
+    return c;
+}
+
+__device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
+    const OccV v = load_block(occ, x >> 6);
+    const uint64_t m = (1ull << (x & 63u)) - 1ull;
+    uint32_t ac = 0;
+#pragma unroll
+    for (uint32_t cc = 1; cc < 8; cc++)
+        if (cc == c) ac = v.cnt[cc];
+    r0 = v.cnt[0] + (uint32_t)__popcll(~v.p0 & ~v.p1 & ~v.p2 & m);
+    const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
+    rc = (c == 0) ? r0 : ac + (uint32_t)__popcll(e & m);
+}
+#endif
 
 #define GRID_STRIDE(i, n) for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(n); i += (size_t)gridDim.x * blockDim.x)
 
@@ -361,31 +441,6 @@ __global__ void k_merge_build(uint64_t n, const uint32_t* __restrict__ flag, con
 }
 
 // ------------------------------------------------------------- deep phase
-// rank of '#' (code 0) and of code c at row x from one occ-block line
-__device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
-    uint4 v[8];
-    load_block(occ, x >> 8, v);
-    const uint32_t r = x & 255u;
-    const uint32_t wq = r >> 6, bit = r & 63u;
-    const uint32_t cnt[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
-    uint32_t a0 = cnt[0], ac = 0;
-#pragma unroll
-    for (uint32_t cc = 1; cc < 8; cc++)
-        if (cc == c) ac = cnt[cc];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint64_t p0 = u64_of(v[2 + (q >> 1)], q & 1);
-        const uint64_t p1 = u64_of(v[4 + (q >> 1)], q & 1);
-        const uint64_t p2 = u64_of(v[6 + (q >> 1)], q & 1);
-        const uint64_t mq = (uint32_t)q < wq ? ~0ull : ((uint32_t)q == wq ? ((1ull << bit) - 1ull) : 0ull);
-        a0 += (uint32_t)__popcll(~p0 & ~p1 & ~p2 & mq);
-        const uint64_t e = ((c & 1) ? p0 : ~p0) & ((c & 2) ? p1 : ~p1) & ((c & 4) ? p2 : ~p2);
-        ac += (uint32_t)__popcll(e & mq);
-    }
-    r0 = a0;
-    rc = (c == 0) ? a0 : ac;
-}
-
 // One thread per pattern whose trie node stopped sharing work: the rest of
 // backwardSearch (link → step both piles → merge, MOVE_EDSBWTSearch.cpp:254-325)
 // runs with the interval lists in registers (at most K each).  A pattern whose

@@ -120,3 +120,27 @@ def test_deep_overflow_rerun(oracle, edsbwt, tmp_path):
         st2 = idx.stats()
         assert np.array_equal(gc, oc) and np.array_equal(go, oo)
         assert st2["deep_level_rerun"] > 0, st2
+
+
+def test_cli_matches_oracle_csv(oracle, tmp_path):
+    """EDSBWTsearch (C++ CLI over the C ABI) vs the oracle's MOVE_EDSBWTSearch restatement:
+    identical <patterns>output_M_LF.csv bytes, count lines on stderr, exit code 1."""
+    import subprocess
+    from conftest import ROOT
+    rng = random.Random(77)
+    segs = edsgen.random_eds(rng, 500, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(4, 18)) or "ACGT" for _ in range(300)] + ["GATTACA", "N"]
+    p1 = tmp_path / "p1.txt"
+    p1.write_text("\n".join(pats) + "\n")
+    p2 = tmp_path / "p2.txt"
+    p2.write_text("\n".join(pats) + "\n")
+    cli = os.path.join(ROOT, "eds-bwt_amd", "_build", "EDSBWTsearch")
+    r = subprocess.run([cli, base, str(p1), "--quiet"], capture_output=True, text=True)
+    assert r.returncode == 1, r.stderr   # mainMove_EDSBWT.cpp:61 returns 1 on success
+    assert "bs took:" in r.stdout and not r.stdout.endswith("\n")
+    ctr, _ = oracle.Engine(base).search_file(str(p2), str(tmp_path / "p2.txtoutput_M_LF.csv"))
+    assert f"count_found = {ctr['found']}" in r.stderr and f"count_not_found = {ctr['not_found']}" in r.stderr
+    assert (tmp_path / "p1.txtoutput_M_LF.csv").read_bytes() == (tmp_path / "p2.txtoutput_M_LF.csv").read_bytes()
+    r = subprocess.run([cli, base], capture_output=True, text=True)
+    assert r.returncode == 1 and "usage" in r.stderr
