@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=0)
     ap.add_argument("--workdir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "edsbwt_bench"))
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -119,10 +120,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev  # rehearsal: several ranks may share one GPU (gloo)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
         barrier = lambda: dist.barrier()  # noqa: E731
     else:
         torch.cuda.set_device(0)
@@ -154,11 +160,14 @@ def main():
                                  first_pattern_id=first_id, locate=locate, table=args.table, profile=profile,
                                  stream=stream)
 
-    gathered = torch.zeros(npat * world, dtype=torch.int32, device=dev) if world > 1 else None
+    gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    gathered = torch.zeros(npat * world, dtype=torch.int32, device=gdev) if world > 1 else None
 
     def exchange():
+        # the path's one exchange: every rank's per-pattern counts, gathered over RCCL/xGMI
         if world > 1:
-            dist.all_gather_into_tensor(gathered, d_counts)
+            src = d_counts if args.dist_backend == "nccl" else d_counts.cpu()
+            dist.all_gather_into_tensor(gathered, src)
 
     for _ in range(args.warmup):
         step()
@@ -184,10 +193,10 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        agg = torch.tensor([lf_steps, total_occ], dtype=torch.float64, device=dev)
+        agg = torch.tensor([lf_steps, total_occ], dtype=torch.float64, device=gdev)
         dist.all_reduce(agg)
         lf_steps, total_occ = float(agg[0].item()), float(agg[1].item())
     last = idx.stats()
