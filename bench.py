@@ -41,6 +41,10 @@ WORKLOAD = {
     "c5": "C5: 1 Gchar synthetic EDS with 20% empty-string segments, 10M mixed 8-64-mers per GPU, full locate",
 }
 MI355X_HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
+# Practical ceiling of the rank queries' access shape — one random 64-B line per lane
+# from a table of the C3 index's size (100 MB, Infinity-Cache resident): measured on
+# MI355X by tools/calib_gather.hip (profiles/r01_calib_gather.json), 3.4-3.5 TB/s.
+GATHER64_CEILING_LINES_PER_S = 5.48e10
 
 
 def log(*a):
@@ -74,6 +78,19 @@ def prepare(cfg: str, workdir: str, rank: int, world: int, npat: int, barrier):
              "--seed", pseed * 1000003 + rank, "--out", pats])
     barrier()
     return base, pats
+
+
+def traffic_from_profile(cfg: str, kernel: str, locate: bool):
+    """HBM-side bytes per launch of `kernel` from the committed rocprofv3 PMC summary of
+    this same command (profiles/traffic_<cfg>.json, written by tools/profile_summary.py
+    from separate --pmc FETCH_SIZE / WRITE_SIZE passes); None when there is none."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    try:
+        t = json.load(open(path))
+        c = t["classes"][kernel]
+        return int(c["pmc_hbm_bytes_per_launch"]), f"profiles/traffic_{cfg}.json ({t.get('source', '')})"
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def cpu_baseline(base: str, pats_path: str, sample: int, threads: int) -> dict:
@@ -185,10 +202,11 @@ def main():
         total_occ += nocc
         lf_steps += 2 * st["intervals_stepped"] + st["locate_lf_steps"]
         for k, v in st["kernels"].items():
-            a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0})
+            a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
             a["ms"] += v["ms"]
             a["launches"] += v["launches"]
             a["bytes"] += v["bytes"]
+            a["lines"] += v["lines"]
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -209,6 +227,8 @@ def main():
         d = kstats[dom]
         avg_ms = d["ms"] / max(1, d["launches"])
         achieved = (d["bytes"] / d["launches"]) / (avg_ms * 1e-3) / 1e9 if d["launches"] and avg_ms > 0 else 0.0
+        line_rate = (d["lines"] / d["launches"]) / (avg_ms * 1e-3) if d["launches"] and avg_ms > 0 else 0.0
+        traffic, traffic_src = traffic_from_profile(cfg, dom, locate)
         out = {
             "metric": "patterns/sec + LF-steps/sec, 100 Mchar EDS, 10M 31-mers, 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -229,9 +249,17 @@ def main():
             "lf_steps_per_sec": round(lf_steps / elapsed, 1),
             "occurrences_per_step": int(total_occ / args.steps / max(1, world)) if world == 1 else int(total_occ / args.steps),
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": MI355X_HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / MI355X_HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / MI355X_HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "avg_launch_ms": round(avg_ms, 4), "launches": d["launches"],
-                         "bytes_per_launch": int(d["bytes"] / max(1, d["launches"]))},
+                         "bytes_per_launch": int(d["bytes"] / max(1, d["launches"])),
+                         # random 64-B lines: the rate the access shape is actually bound by
+                         "lines_per_launch": int(d["lines"] / max(1, d["launches"])),
+                         "lines_per_s": round(line_rate, 1),
+                         "gather_ceiling_lines_per_s": GATHER64_CEILING_LINES_PER_S,
+                         "frac_of_gather_ceiling": round(line_rate / GATHER64_CEILING_LINES_PER_S, 4)},
+            "kernel_lines_per_s": {k: round((v["lines"] / (v["ms"] * 1e-3)) if v["ms"] > 0 else 0.0, 1)
+                                   for k, v in sorted(kstats.items()) if v["lines"]},
             "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items())},
             "index_open_s": round(t_open, 2),
             "engine": {k: last[k] for k in ("depths", "deep_from_depth", "deep_overflow", "deep_level_rerun", "trie_nodes", "intervals_stepped",

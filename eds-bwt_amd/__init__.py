@@ -58,7 +58,8 @@ class _Stats(ctypes.Structure):
                 ("deep_from_depth", ctypes.c_uint64), ("deep_overflow", ctypes.c_uint64),
                 ("deep_level_rerun", ctypes.c_uint64), ("ms_total", ctypes.c_double),
                 ("ms_kernel", ctypes.c_double * 16), ("launches_kernel", ctypes.c_uint64 * 16),
-                ("bytes_kernel", ctypes.c_uint64 * 16)]
+                ("bytes_kernel", ctypes.c_uint64 * 16),
+                ("lines_kernel", ctypes.c_uint64 * 16)]
 
 
 _LIB = None
@@ -204,9 +205,10 @@ class Index:
     def stats(self) -> dict:
         s = _Stats()
         _check(lib().edsbwt_last_stats(self._h, ctypes.byref(s)))
-        out = {k: getattr(s, k) for k, _ in _Stats._fields_ if k not in ("ms_kernel", "launches_kernel", "bytes_kernel")}
+        out = {k: getattr(s, k) for k, _ in _Stats._fields_ if k not in ("ms_kernel", "launches_kernel", "bytes_kernel", "lines_kernel")}
         names = [lib().edsbwt_kernel_name(i).decode() for i in range(16)]
-        out["kernels"] = {n: {"ms": s.ms_kernel[i], "launches": s.launches_kernel[i], "bytes": s.bytes_kernel[i]}
+        out["kernels"] = {n: {"ms": s.ms_kernel[i], "launches": s.launches_kernel[i], "bytes": s.bytes_kernel[i],
+                              "lines": s.lines_kernel[i]}
                           for i, n in enumerate(names) if n}
         return out
 

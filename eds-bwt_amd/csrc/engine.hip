@@ -131,6 +131,15 @@ struct Engine {
     DBuf<uint64_t> fk, fk2, ekeys, efk;
     DBuf<uint32_t> eu, eb, ee, eck_u, eck_k, eck_e, efv, shpre;
     uint32_t* pinned_big = nullptr;  // host shard counters + prefix
+    DBuf<unsigned long long> stats;  // kStatSlots sharded statistics counters (stat_add)
+    unsigned long long* pinned_stats = nullptr;
+    // sum of the kStatShards shards of each statistic, from pinned_stats (already copied)
+    std::vector<uint64_t> fold_pinned_stats() const {
+        std::vector<uint64_t> v(kStatStride, 0);
+        for (uint32_t s = 0; s < kStatShards; s++)
+            for (uint32_t k = 0; k < kStatStride; k++) v[k] += pinned_stats[s * kStatStride + k];
+        return v;
+    }
     DBuf<uint8_t> hbytes;   // host-API pattern staging
     DBuf<uint64_t> hoffs;
     DBuf<uint32_t> hcounts;
@@ -177,6 +186,14 @@ struct Engine {
         HIPCHK(hipEventRecord(e.b, stream));
         evs.push_back(e);
     }
+    // reductions: a fixed small grid, one global atomic per block
+    static constexpr unsigned kReduceBlocks = 1024;
+    template <typename K, typename... A>
+    void launch_reduce(int k, K kern, A... a) {
+        timed(k, [&] { hipLaunchKernelGGL(kern, dim3(kReduceBlocks), dim3(256), 0, stream, a...); });
+        HIPCHK(hipGetLastError());
+        st.launches_kernel[k]++;
+    }
     template <typename K, typename... A>
     void launch(int k, K kern, size_t n, A... a) {
         if (!n) return;
@@ -199,18 +216,12 @@ struct Engine {
     void zero(void* p, size_t bytes) { if (bytes) HIPCHK(hipMemsetAsync(p, 0, bytes, stream)); }
 
     // reversed-code chunk of depth D for the patterns in trie order (chunk 0 is the
-    // last radix pass's output; later chunks are gathered once when first needed)
-    int skey_chunk = -1;
+    // last radix pass's output, chunks 1.. were gathered by build_trie)
+    uint32_t bps = 4;                // bits per symbol code of the current batch (3 or 4)
     std::vector<uint64_t> nodes_at;  // trie nodes per depth of the current batch
     const uint64_t* sorted_chunk(uint32_t D, uint64_t P) {
-        const int c = (int)((D - 1) >> 4);
-        if (c == 0) return kc2.p;
-        if (c != skey_chunk) {
-            skey.ensure(P);
-            launch(KC_NODES, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, skey.p);
-            skey_chunk = c;
-        }
-        return skey.p;
+        const uint32_t c = (D - 1) / (64 / bps);
+        return c == 0 ? kc2.p : skey.p + (size_t)(c - 1) * P;
     }
 
     // ---- sharded appends (kernels.hip NSHARD): per-shard counters on the host
@@ -331,6 +342,8 @@ struct Engine {
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         HIPCHK(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
         HIPCHK(hipHostMalloc((void**)&pinned_big, (kCnt + NSHARD + 8) * 4, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&pinned_stats, kStatSlots * 8, hipHostMallocDefault));
+        stats.ensure(kStatSlots);
         HostIndex H;
         std::string err;
         int rc = read_host_index(base, H, err);
@@ -452,46 +465,71 @@ struct Engine {
     bool build_trie(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t& Lmax, std::vector<unsigned long long>& hist,
                     std::vector<uint64_t>& ge, uint32_t* n_term = nullptr) {
         if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
-        // ---- A. lengths, longest pattern, patterns holding '#': one launch, one read
-        len.ensure(P);
+        // ---- A. longest pattern, from the offsets: one small launch, one read
         zero(counters.p + 6, 8);
-        launch(KC_TRIE, k_prep, P, d_off, d_bytes, P, len.p, (unsigned int*)(counters.p + 6));
-        const uint64_t pv = read_u64(counters.p + 6);
-        Lmax = (uint32_t)pv;
-        if (n_term) *n_term = (uint32_t)(pv >> 32);
+        launch_reduce(KC_TRIE, k_lmax, d_off, P, counters.p + 6);
+        Lmax = (uint32_t)read_u64(counters.p + 6);
         if (Lmax == 0) return false;
         // ---- B. reversed-pattern sort (trie order) and neighbours' common suffix
-        const uint32_t nch = (Lmax + 15) / 16;
+        bps = sigma + 2 <= 8 ? 3u : 4u;
+        const uint32_t spc = 64 / bps;
+        const uint32_t nch = (Lmax + spc - 1) / spc;
+        lhist.ensure(2 * (size_t)(Lmax + 2) + 1);
+        zero(lhist.p, (2 * (size_t)(Lmax + 2) + 1) * 8);
+        unsigned long long* d_nterm = lhist.p + 2 * (size_t)(Lmax + 2);
+        len.ensure(P);
         keys.ensure((size_t)nch * P);
-        launch(KC_TRIE, k_keys, P, d_bytes, d_off, (const uint32_t*)len.p, P, (const uint8_t*)code_of.p, sigma, nch, keys.p);
+        if (bps == 3)
+            launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
+        else
+            launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
         perm.ensure(P);
         perm2.ensure(P);
         kc.ensure(P);
         kc2.ensure(P);
         launch(KC_TRIE, k_iota, P, perm.p, P);
+        // LSD over the chunks, last (least significant) first; only the bits that hold
+        // symbols are sorted (the last chunk is partly empty)
         for (int c = (int)nch - 1; c >= 0; c--) {
-            launch(KC_TRIE, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, kc.p);
+            const uint32_t nsym = std::min(spc, Lmax - (uint32_t)c * spc);
+            const int begin_bit = (int)(bps * (spc - nsym)), end_bit = (int)(bps * spc);
+            const uint64_t* kin = keys.p + (size_t)c * P;
+            if (c != (int)nch - 1) {  // the first pass sorts the chunk in place order (perm = identity)
+                launch(KC_TRIE, k_gather_key, P, kin, (const uint32_t*)perm.p, P, kc.p);
+                kin = kc.p;
+            }
             size_t tb = 0;
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kc.p, kc2.p, perm.p, perm2.p, (int)P, 0, 64, stream));
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
             tmp.ensure(tb);
-            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kc.p, kc2.p, perm.p, perm2.p, (int)P, 0, 64, stream)); });
+            timed(KC_TRIE, [&] {
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
+            });
             std::swap(perm.p, perm2.p);
             std::swap(perm.cap, perm2.cap);
         }
-        skey_chunk = -1;
+        // sorted chunks 1.. (chunk 0 is the last pass's output, kc2)
+        if (nch > 1) {
+            skey.ensure((size_t)(nch - 1) * P);
+            for (uint32_t c = 1; c < nch; c++)
+                launch(KC_TRIE, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, skey.p + (size_t)(c - 1) * P);
+        }
         slen.ensure(P);
         lcp.ensure(P);
-        launch(KC_TRIE, k_slen_lcp, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)keys.p, nch, P, slen.p, lcp.p);
+        if (bps == 3)
+            launch(KC_TRIE, k_slen_lcp<3>, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)kc2.p, (const uint64_t*)skey.p,
+                   nch, P, slen.p, lcp.p);
+        else
+            launch(KC_TRIE, k_slen_lcp<4>, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)kc2.p, (const uint64_t*)skey.p,
+                   nch, P, slen.p, lcp.p);
         // ---- C. nodes per depth and patterns per length, read once
-        lhist.ensure(2 * (size_t)(Lmax + 2));
-        zero(lhist.p, 2 * (size_t)(Lmax + 2) * 8);
         if (Lmax + 2 <= 1024)
-            launch(KC_TRIE, k_trie_counts, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, Lmax, lhist.p, lhist.p + (Lmax + 2));
+            launch_reduce(KC_TRIE, k_trie_counts, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, Lmax, lhist.p, lhist.p + (Lmax + 2));
         else
             launch(KC_TRIE, k_trie_counts_global, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, lhist.p, lhist.p + (Lmax + 2));
-        std::vector<unsigned long long> hv(2 * (size_t)(Lmax + 2));
+        std::vector<unsigned long long> hv(2 * (size_t)(Lmax + 2) + 1);
         HIPCHK(hipMemcpyAsync(hv.data(), lhist.p, hv.size() * 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        if (n_term) *n_term = (uint32_t)hv.back();
         hist.assign(hv.begin() + (Lmax + 2), hv.begin() + (Lmax + 2) + (Lmax + 1));
         nodes_at.assign(Lmax + 2, 0);
         int64_t run = 0;
@@ -551,7 +589,7 @@ struct Engine {
             node_first.ensure(M);
             node_parent.ensure(M);
             node_char.ensure(M);
-            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
+            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             child_first.ensure(Mcur);
             child_end.ensure(Mcur);
@@ -673,19 +711,12 @@ struct Engine {
         zero(ovf.p, P * 4);
         ab.grow_keep(abase + (uint64_t)P * kDeepK, stream);
         ae.grow_keep(abase + (uint64_t)P * kDeepK, stream);
-        zero(counters.p + 2, 16);
         launch(KC_DEEP, k_deep<kDeepK>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, (const uint32_t*)len.p, d_off, d_bytes,
-               (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, counters.p);
+               (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
         abase += (uint64_t)P * kDeepK;
         st.deep_from_depth = D;
         if (trace) std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu\n", D, M, (unsigned long long)active);
-        HIPCHK(hipMemcpyAsync(pinned, counters.p + 2, 16, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipStreamSynchronize(stream));
-        uint64_t dv[2];
-        std::memcpy(dv, pinned, 16);
-        st.intervals_stepped += dv[0];
-        st.link_hash_rows += dv[1];
-        st.bytes_kernel[KC_DEEP] += dv[0] * (2 * sizeof(OccBlock)) + dv[1] * 4 + (uint64_t)P * 24;
+        st.bytes_kernel[KC_DEEP] += (uint64_t)P * 24;  // + interval steps and '#' rows, folded at the end of search()
         // lists that outgrew k_deep's registers: retry those patterns with wide lists
         uint32_t nw = scan_u32(ovf.p, tscan, P);
         if (nw && !no_wide) {
@@ -779,13 +810,17 @@ struct Engine {
             // children nodes at depth D (node count known from build_trie: no read-back)
             launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
             exclusive_scan(flag.p, scan.p, P);
-            launch(KC_NODES, k_node_build, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
+            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             launch(KC_NODES, k_child_links, M, (const uint32_t*)node_parent.p, M, child_first.p, child_end.p);
             // fused step + '#'-row emission over the current items (sharded appends)
             size_t cap_next = std::max<size_t>(shard_bound(ncur, 2), 4096);
             size_t cap_keys = std::max<size_t>(shard_bound(ncur, 1), 4096);
             size_t cap_chunks = std::max<size_t>(shard_bound(ncur, 1) / 8, 1024);
+            // use what earlier depths / calls already allocated: no regrow-and-redo in steady state
+            cap_next = std::max(cap_next, std::min({eu.cap, eb.cap, ee.cap}) / NSHARD);
+            cap_keys = std::max(cap_keys, ekeys.cap / NSHARD);
+            cap_chunks = std::max(cap_chunks, std::min({eck_u.cap, eck_k.cap, eck_e.cap}) / NSHARD);
             for (bool first = true;; first = false) {
                 eu.ensure(cap_next * NSHARD); eb.ensure(cap_next * NSHARD); ee.ensure(cap_next * NSHARD);
                 ekeys.ensure(cap_keys * NSHARD);
@@ -795,12 +830,12 @@ struct Engine {
                     launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
                            (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
                            X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
-                           (uint32_t)cap_chunks);
+                           (uint32_t)cap_chunks, stats.p);
                 else  // no link before the first step (:246-258)
                     launch(KC_STEP, k_lvl_items<false>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
                            (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
                            X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
-                           (uint32_t)cap_chunks);
+                           (uint32_t)cap_chunks, stats.p);
                 fetch_shards();  // sync A
                 const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
                 if (m0 <= cap_next && m1 <= cap_keys && m2 <= cap_chunks) break;
@@ -861,7 +896,7 @@ struct Engine {
                 for (;;) {
                     launch(KC_STEP, k_lvl_dollar, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
                            (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p, X, eu.p, eb.p, ee.p,
-                           (uint32_t)cap_next, lcnt.p);
+                           (uint32_t)cap_next, lcnt.p, stats.p);
                     fetch_shards();  // sync B
                     const uint32_t m0 = shard_max(0);
                     if (m0 <= cap_next) break;
@@ -879,6 +914,8 @@ struct Engine {
                 st.bytes_kernel[KC_STEP] += (uint64_t)R * (12 + 2 * sizeof(OccBlock));
                 nnext = shard_total(0);
             }
+            // two 64-B lines per interval step, plus the item streams
+            // (the lines actually read are counted by the kernels: lines_kernel)
             st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * sizeof(OccBlock)) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
             if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
                                     ncur, nkeys, nkeys ? hsh[NSHARD * 32] : 0u, nnext);
@@ -942,6 +979,7 @@ struct Engine {
         res_occ.ensure(P);
         zero(res_cnt.p, P * 4);
         zero(res_occ.p, P * 4);
+        zero(stats.p, kStatSlots * 8);
         ovf_orig.ensure(P);
         uint64_t abase = 0;
         // patterns holding '#' make the reference's lists overlap: they take the ordered path
@@ -974,7 +1012,7 @@ struct Engine {
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
         HIPCHK(hipMemcpyAsync(d_counts, res_occ.p, P * 4, hipMemcpyDeviceToDevice, stream));
         zero(counters.p + 1, 8);
-        launch(KC_FINISH, k_count_found, P, (const uint32_t*)res_occ.p, P, counters.p + 1);
+        launch_reduce(KC_FINISH, k_count_found, (const uint32_t*)res_occ.p, P, counters.p + 1);
         if (locate) {
             occ64.ensure(P);
             tc64.ensure(P);
@@ -1000,16 +1038,24 @@ struct Engine {
                 launch(KC_LOCPREP, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
                        (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p);
                 rec.ensure(OCC);
-                zero(counters.p, 8);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
-                       X, use_table ? 1 : 0, rec.p, counters.p);
-                HIPCHK(hipMemcpyAsync(pinned, counters.p, 8, hipMemcpyDeviceToHost, stream));
+                       X, use_table ? 1 : 0, rec.p, stats.p);
             }
         }
+        HIPCHK(hipMemcpyAsync(pinned_stats, stats.p, kStatSlots * 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipEventRecord(e1, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        {
+            const std::vector<uint64_t> sv = fold_pinned_stats();
+            st.intervals_stepped += sv[ST_DEEP_STEPS];
+            st.link_hash_rows += sv[ST_DEEP_HASH];
+            st.bytes_kernel[KC_DEEP] += sv[ST_DEEP_STEPS] * (2 * sizeof(OccBlock)) + sv[ST_DEEP_HASH] * 4;
+            st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
+            st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
+            st.locate_lf_steps = sv[ST_LOC_STEPS];
+            if (locate && !use_table) st.lines_kernel[KC_LOCATE] += st.locate_lf_steps + OCC;  // one line per walk position
+        }
         if (locate && OCC) {
-            std::memcpy(&st.locate_lf_steps, pinned, 8);
             st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * sizeof(OccBlock) + OCC * (sizeof(OccBlock) + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
         }
         float ms = 0;
@@ -1035,6 +1081,7 @@ struct Engine {
         for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
         if (pinned) (void)hipHostFree(pinned);
         if (pinned_big) (void)hipHostFree(pinned_big);
+        if (pinned_stats) (void)hipHostFree(pinned_stats);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };

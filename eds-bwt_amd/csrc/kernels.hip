@@ -113,6 +113,20 @@ __device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t
     r0 = a0;
     rc = (c == 0) ? a0 : ac;
 }
+
+__device__ __forceinline__ uint32_t rank_all_pair(const OccBlock* __restrict__ occ, uint32_t x0, uint32_t x1, uint32_t sigma, uint32_t* o0,
+                                                  uint32_t* o1) {
+    rank_all(occ, x0, sigma, o0);
+    rank_all(occ, x1, sigma, o1);
+    return 0;  // two block reads
+}
+
+__device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ, uint32_t x0, uint32_t x1, uint32_t c, uint32_t& h0, uint32_t& r0,
+                                               uint32_t& h1, uint32_t& r1) {
+    rank2(occ, x0, c, h0, r0);
+    rank2(occ, x1, c, h1, r1);
+    return 0;  // two block reads
+}
 #else  // 64 rows per 64-B block
 struct OccV {
     uint32_t cnt[8];
@@ -131,14 +145,30 @@ __device__ __forceinline__ OccV load_block(const OccBlock* __restrict__ occ, uin
     return o;
 }
 
-__device__ __forceinline__ void rank_all(const OccBlock* __restrict__ occ, uint32_t x, uint32_t sigma, uint32_t* out) {
-    const OccV v = load_block(occ, x >> 6);
+__device__ __forceinline__ void rank_all_v(const OccV& v, uint32_t x, uint32_t sigma, uint32_t* out) {
     const uint64_t m = (1ull << (x & 63u)) - 1ull;
 #pragma unroll
     for (uint32_t c = 0; c < 8; c++) {
         const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
         out[c] = c < sigma ? v.cnt[c] + (uint32_t)__popcll(e & m) : 0u;
     }
+}
+
+__device__ __forceinline__ void rank_all(const OccBlock* __restrict__ occ, uint32_t x, uint32_t sigma, uint32_t* out) {
+    rank_all_v(load_block(occ, x >> 6), x, sigma, out);
+}
+
+// ranks at x0 <= x1 (an interval's b and e+1): narrow intervals share one block, so
+// the second block is read only by lanes whose ends fall in different blocks.
+// Returns 1 when one block served both.
+__device__ __forceinline__ uint32_t rank_all_pair(const OccBlock* __restrict__ occ, uint32_t x0, uint32_t x1, uint32_t sigma, uint32_t* o0,
+                                                  uint32_t* o1) {
+    OccV v = load_block(occ, x0 >> 6);
+    rank_all_v(v, x0, sigma, o0);
+    const bool same = (x1 >> 6) == (x0 >> 6);
+    if (!same) v = load_block(occ, x1 >> 6);
+    rank_all_v(v, x1, sigma, o1);
+    return same;
 }
 
 __device__ __forceinline__ uint32_t sym_rank(const OccBlock* __restrict__ occ, uint32_t x, uint32_t* rank) {
@@ -155,8 +185,7 @@ __device__ __forceinline__ uint32_t sym_rank(const OccBlock* __restrict__ occ, u
     return c;
 }
 
-__device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
-    const OccV v = load_block(occ, x >> 6);
+__device__ __forceinline__ void rank2_v(const OccV& v, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
     const uint64_t m = (1ull << (x & 63u)) - 1ull;
     uint32_t ac = 0;
 #pragma unroll
@@ -166,9 +195,53 @@ __device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t
     const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
     rc = (c == 0) ? r0 : ac + (uint32_t)__popcll(e & m);
 }
+
+__device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t x, uint32_t c, uint32_t& r0, uint32_t& rc) {
+    rank2_v(load_block(occ, x >> 6), x, c, r0, rc);
+}
+
+__device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ, uint32_t x0, uint32_t x1, uint32_t c, uint32_t& h0, uint32_t& r0,
+                                               uint32_t& h1, uint32_t& r1) {
+    OccV v = load_block(occ, x0 >> 6);
+    rank2_v(v, x0, c, h0, r0);
+    const bool same = (x1 >> 6) == (x0 >> 6);
+    if (!same) v = load_block(occ, x1 >> 6);
+    rank2_v(v, x1, c, h1, r1);
+    return same;
+}
 #endif
 
 #define GRID_STRIDE(i, n) for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(n); i += (size_t)gridDim.x * blockDim.x)
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+// block-wide sum (256 threads), result valid in thread 0
+__device__ __forceinline__ unsigned long long block_sum(unsigned long long x, unsigned long long* sh) {
+    x = wave_sum(x);
+    __syncthreads();  // sh may still be read by a previous block_sum
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    unsigned long long t = 0;
+    if (threadIdx.x == 0)
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) t += sh[w];
+    return t;
+}
+
+
+// statistics counters: block-reduced, then one atomic per block into one of kStatShards
+// 128-B lines (the host folds the shards), so no address takes every block's add.
+// Every thread of the block must call it.
+constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards * kStatStride;
+// statistic slots (zeroed once per search, folded at its end)
+enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4 };
+__device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats, uint32_t k, unsigned long long v, unsigned long long* sh) {
+    v = block_sum(v, sh);
+    if (threadIdx.x == 0 && v) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + k, v);
+}
 
 template <typename T>
 __device__ __forceinline__ size_t upper_bound_dev(const T* __restrict__ a, size_t n, T key) {
@@ -185,27 +258,65 @@ __global__ void k_lens(const uint64_t* __restrict__ off, uint64_t P, uint32_t* _
     GRID_STRIDE(i, P) len[i] = (uint32_t)(off[i + 1] - off[i]);
 }
 
-// 4-bit sort codes of the reversed pattern, 16 per u64, most significant first:
-// 0 = end of pattern, 1+code for alphabet symbols, sigma+1 for bytes outside it.
-__global__ void k_keys(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-                       uint64_t P, const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t nch, uint64_t* __restrict__ keys) {
-    GRID_STRIDE(i, P) {
-        const uint32_t L = len[i];
-        const uint8_t* s = bytes + off[i];
-        for (uint32_t c = 0; c < nch; c++) {
-            uint64_t key = 0;
-            for (uint32_t t = 0; t < 16; t++) {
-                uint32_t pos = c * 16 + t;
-                uint64_t v = 0;
-                if (pos < L) {
-                    uint32_t code = code_of[s[L - 1 - pos]];
-                    v = code < sigma ? code + 1 : sigma + 1;
+// Sort codes of the reversed pattern, BPS bits each (3 when sigma+2 <= 8, else 4),
+// SPC = 64/BPS per u64 chunk, most significant first: 0 = end of pattern, 1+code
+// for alphabet symbols, sigma+1 for bytes outside it.  Chunk c of pattern i at
+// keys[c*P + i].  A block's patterns are contiguous in `bytes`, so the block stages
+// their bytes in LDS with coalesced 4-B loads (spans over kKeySpan bytes read global
+// memory directly).  Also writes len[] and counts patterns holding the end-marker '#'.
+constexpr uint32_t kKeySpan = 24576;
+template <int BPS>
+__global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
+                                              const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t nch, uint64_t* __restrict__ keys,
+                                              uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term) {
+    constexpr uint32_t SPC = 64 / BPS;
+    __shared__ uint32_t sbuf[kKeySpan / 4 + 2];
+    __shared__ uint8_t scode[256];
+    __shared__ unsigned long long sh[4];
+    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) {
+        const uint32_t c = code_of[t];
+        scode[t] = (uint8_t)(c < sigma ? c + 1 : sigma + 1);
+    }
+    unsigned long long nt = 0;
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < P; base += (size_t)gridDim.x * blockDim.x) {
+        const size_t nb = min((size_t)blockDim.x, (size_t)P - base);
+        const uint64_t s0 = off[base], s1 = off[base + nb];
+        const uint64_t w0 = s0 & ~3ull;
+        const bool staged = s1 - w0 <= kKeySpan && ((uintptr_t)bytes & 3) == 0;
+        __syncthreads();  // previous round's readers are done with sbuf (and scode is ready)
+        if (staged) {
+            const uint32_t nw = (uint32_t)((s1 - w0 + 3) / 4);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(bytes + w0);
+            for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x) sbuf[t] = src[t];
+        }
+        __syncthreads();
+        const size_t i = base + threadIdx.x;
+        if (i < P) {
+            const uint64_t a = off[i];
+            const uint32_t L = (uint32_t)(off[i + 1] - a);
+            len[i] = L;
+            const uint8_t* sg = bytes + a;
+            const uint8_t* sl = reinterpret_cast<const uint8_t*>(sbuf) + (a - w0);
+            uint32_t term = 0;
+            for (uint32_t c = 0; c < nch; c++) {
+                uint64_t key = 0;
+                for (uint32_t t = 0; t < SPC; t++) {
+                    const uint32_t pos = c * SPC + t;
+                    uint64_t v = 0;
+                    if (pos < L) {
+                        const uint8_t ch = staged ? sl[L - 1 - pos] : sg[L - 1 - pos];
+                        v = scode[ch];
+                        term |= ch == '#';
+                    }
+                    key = (key << BPS) | v;
                 }
-                key = (key << 4) | v;
+                keys[(size_t)c * P + i] = key;
             }
-            keys[(size_t)c * P + i] = key;
+            nt += term;
         }
     }
+    nt = block_sum(nt, sh);
+    if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
 }
 
 __global__ void k_iota(uint32_t* __restrict__ a, uint64_t n) { GRID_STRIDE(i, n) a[i] = (uint32_t)i; }
@@ -214,23 +325,41 @@ __global__ void k_gather_key(const uint64_t* __restrict__ keys_c, const uint32_t
     GRID_STRIDE(i, P) out[i] = keys_c[perm[i]];
 }
 
-__global__ void k_slen_lcp(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len, const uint64_t* __restrict__ keys,
-                           uint32_t nch, uint64_t P, uint32_t* __restrict__ slen, uint32_t* __restrict__ lcp) {
+// sorted order: slen[i] = len[perm[i]]; lcp[i] = common reversed prefix (= common
+// suffix) of sorted neighbours i-1, i, from the sorted key chunks (chunk 0 in k0,
+// chunks 1.. in krest[(c-1)*P + i]) — neighbours are adjacent, so reads coalesce
+template <int BPS>
+__global__ void k_slen_lcp(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len, const uint64_t* __restrict__ k0,
+                           const uint64_t* __restrict__ krest, uint32_t nch, uint64_t P, uint32_t* __restrict__ slen, uint32_t* __restrict__ lcp) {
+    constexpr uint32_t SPC = 64 / BPS, LEAD = 64 - SPC * BPS;
     GRID_STRIDE(i, P) {
-        const uint32_t a = perm[i];
-        slen[i] = len[a];
+        const uint32_t la = len[perm[i]];
+        slen[i] = la;
         if (i == 0) { lcp[0] = 0; continue; }
-        const uint32_t b = perm[i - 1];
-        uint32_t l = 16 * nch;
+        const uint32_t lb = len[perm[i - 1]];
+        uint32_t l = SPC * nch;
         for (uint32_t c = 0; c < nch; c++) {
-            uint64_t x = keys[(size_t)c * P + a] ^ keys[(size_t)c * P + b];
-            if (x) { l = c * 16 + (uint32_t)__clzll(x) / 4; break; }
+            const uint64_t x = c == 0 ? (k0[i] ^ k0[i - 1]) : (krest[(size_t)(c - 1) * P + i] ^ krest[(size_t)(c - 1) * P + i - 1]);
+            if (x) { l = c * SPC + ((uint32_t)__clzll(x) - LEAD) / BPS; break; }
         }
-        uint32_t la = len[a], lb = len[b];
         l = l < la ? l : la;
         l = l < lb ? l : lb;
         lcp[i] = l;
     }
+}
+
+// longest pattern, from the offsets alone (small grid, one atomic per block)
+__global__ void __launch_bounds__(256) k_lmax(const uint64_t* __restrict__ off, uint64_t P, unsigned long long* __restrict__ out) {
+    __shared__ unsigned int smx;
+    if (threadIdx.x == 0) smx = 0;
+    __syncthreads();
+    uint32_t mx = 0;
+    GRID_STRIDE(i, P) mx = max(mx, (uint32_t)(off[i + 1] - off[i]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(&smx, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(out, (unsigned long long)smx);
 }
 
 // node starts at depth D: pattern i is the first member of a depth-D node
@@ -239,12 +368,14 @@ __global__ void k_node_flags(const uint32_t* __restrict__ slen, const uint32_t* 
 }
 
 // nscan = exclusive scan of flags (P+1 entries); skey = the sorted patterns'
-// reversed-code chunk holding depth D (4 bits per symbol, most significant first)
+// reversed-code chunk holding depth D (BPS bits per symbol, most significant first)
+template <int BPS>
 __global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint64_t* __restrict__ skey, uint32_t sigma,
                              const uint32_t* __restrict__ flag, const uint32_t* __restrict__ nscan,
                              const uint32_t* __restrict__ nid_prev, uint32_t* __restrict__ nid_cur,
                              uint32_t* __restrict__ node_first, uint32_t* __restrict__ node_parent, uint8_t* __restrict__ node_char) {
-    const uint32_t sh = 4 * (15 - ((D - 1) & 15));
+    constexpr uint32_t SPC = 64 / BPS;
+    const uint32_t sh = BPS * (SPC - 1 - ((D - 1) % SPC));
     GRID_STRIDE(i, P) {
         if (slen[i] < D) { nid_cur[i] = 0xFFFFFFFFu; continue; }
         const uint32_t id = nscan[i] + flag[i] - 1;
@@ -252,7 +383,7 @@ __global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict_
         if (flag[i]) {
             node_first[id] = (uint32_t)i;
             node_parent[id] = nid_prev[i];
-            const uint32_t v = (uint32_t)(skey[i] >> sh) & 15u;
+            const uint32_t v = (uint32_t)(skey[i] >> sh) & ((1u << BPS) - 1u);
             node_char[id] = (uint8_t)((v >= 1 && v <= sigma) ? v - 1 : 0xFF);
         }
     }
@@ -282,8 +413,7 @@ __global__ void __launch_bounds__(256) k_expand(const uint32_t* __restrict__ ib,
                                                 uint32_t* __restrict__ ocb, uint32_t* __restrict__ oce) {
     GRID_STRIDE(j, n) {
         uint32_t rb[8], re[8];
-        rank_all(X.occ, ib[j], X.sigma, rb);
-        rank_all(X.occ, ie[j] + 1, X.sigma, re);
+        rank_all_pair(X.occ, ib[j], ie[j] + 1, X.sigma, rb, re);
         uint4* pb = reinterpret_cast<uint4*>(ocb + j * 8);
         uint4* pe = reinterpret_cast<uint4*>(oce + j * 8);
         pb[0] = make_uint4(rb[0], rb[1], rb[2], rb[3]);
@@ -456,7 +586,7 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, uint64_t* __restrict__ res_off,
                                               uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr) {
-    unsigned long long n_steps = 0, n_hash = 0;
+    unsigned long long n_steps = 0, n_hash = 0, n_blk = 0;  // n_blk: occ blocks read
     GRID_STRIDE(i, P) {
         const uint32_t L = slen[i];
         if (L <= D0) continue;
@@ -490,8 +620,7 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
             for (int j = 0; j < K; j++) {
                 if ((uint32_t)j < cn) {
                     uint32_t h0, h1;
-                    rank2(X.occ, cb[j], c, h0, sb[j]);
-                    rank2(X.occ, ce[j] + 1, c, h1, se[j]);
+                    n_blk += 2 - rank2_pair(X.occ, cb[j], ce[j] + 1, c, h0, sb[j], h1, se[j]);
                     n_hash += h1 - h0;
                     for (uint32_t k = h0; k < h1; k++) {  // dollars_in_interval (:607-625)
                         const uint32_t s = X.eof_seg[k];
@@ -542,8 +671,7 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
             auto close_run = [&]() {
                 const uint32_t r0 = X.seg_start[run_lo], r1 = X.seg_start[run_s] - 1;
                 uint32_t x0, x1, y0, y1;
-                rank2(X.occ, r0, c, x0, x1);
-                rank2(X.occ, r1 + 1, c, y0, y1);
+                n_blk += 2 - rank2_pair(X.occ, r0, r1 + 1, c, x0, x1, y0, y1);
                 if (y1 > x1) push(X.C[c] + x1, X.C[c] + y1 - 1);
                 n_steps++;
             };
@@ -591,8 +719,10 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
         res_cnt[o] = cn;
         res_occ[o] = occ;
     }
-    if (n_steps) atomicAdd(ctr + 2, n_steps);
-    if (n_hash) atomicAdd(ctr + 3, n_hash);
+    __shared__ unsigned long long sh[4];
+    stat_add(ctr, ST_DEEP_STEPS, n_steps, sh);
+    stat_add(ctr, ST_DEEP_HASH, n_hash, sh);
+    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, sh);
 }
 
 // Patterns k_deep<8> could not hold: the same walk with lists of up to KW intervals
@@ -627,8 +757,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
             uint32_t rn = 0;
             for (uint32_t q = 0; q < cn && !over; q++) {
                 uint32_t h0, h1;
-                rank2(X.occ, cb[q], c, h0, sb[q]);
-                rank2(X.occ, ce[q] + 1, c, h1, se[q]);
+                rank2_pair(X.occ, cb[q], ce[q] + 1, c, h0, sb[q], h1, se[q]);
                 for (uint32_t k = h0; k < h1; k++) {
                     const uint32_t s = X.eof_seg[k];
                     if (!s) continue;
@@ -655,8 +784,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
                 uint32_t t2 = t + 1;
                 while (t2 < rn && X.seg_lo[raw[t2]] <= hi) { hi = raw[t2]; t2++; }
                 uint32_t x0, x1, y0, y1;
-                rank2(X.occ, X.seg_start[lo], c, x0, x1);
-                rank2(X.occ, X.seg_start[hi], c, y0, y1);  // one past the last word of segment hi-1
+                rank2_pair(X.occ, X.seg_start[lo], X.seg_start[hi], c, x0, x1, y0, y1);  // hi: one past the last word of segment hi-1
                 if (y1 > x1) push(X.C[c] + x1, X.C[c] + y1 - 1);
                 t = t2;
             }
@@ -777,8 +905,9 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
                                                    uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
                                                    uint32_t cap_keys, uint32_t* __restrict__ ck_u, uint32_t* __restrict__ ck_k,
-                                                   uint32_t* __restrict__ ck_e, uint32_t cap_chunks) {
+                                                   uint32_t* __restrict__ ck_e, uint32_t cap_chunks, unsigned long long* __restrict__ stats) {
     const uint32_t sh = blockIdx.x % NSHARD;
+    unsigned long long n_blk = 0;  // occ blocks read
     uint32_t* cnt = cnt_all + sh * 32;
     nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
     keys += (size_t)sh * cap_keys;
@@ -793,8 +922,7 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
             cf = child_first[u];
             nch = child_end[u] - cf;
             if (nch) {
-                rank_all(X.occ, ib[i], X.sigma, rb);
-                rank_all(X.occ, ie[i] + 1, X.sigma, re);
+                n_blk += 2 - rank_all_pair(X.occ, ib[i], ie[i] + 1, X.sigma, rb, re);
             }
         }
         // backward step of every child symbol (updateSingleInterval, :424-510)
@@ -847,6 +975,8 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
                 }
         }
     }
+    __shared__ unsigned long long ssum[4];
+    stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
 }
 
 // long '#'-row ranges: one chunk (<= 256 rows, clipped to the item's end) per thread
@@ -881,8 +1011,9 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ de, const uint32_t* __restrict__ child_first,
                                                     const uint32_t* __restrict__ child_end, const uint8_t* __restrict__ node_char, KIdx X,
                                                     uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
-                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all) {
+                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, unsigned long long* __restrict__ stats) {
     const uint32_t n = *dn;  // link runs, counted on the device by k_run_build
+    unsigned long long n_blk = 0;  // occ blocks read
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
     nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
@@ -896,8 +1027,7 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
             cf = child_first[u];
             nch = child_end[u] - cf;
             if (nch) {
-                rank_all(X.occ, db[i], X.sigma, rb);
-                rank_all(X.occ, de[i] + 1, X.sigma, re);
+                n_blk += 2 - rank_all_pair(X.occ, db[i], de[i] + 1, X.sigma, rb, re);
             }
         }
         uint32_t nk = 0;
@@ -924,6 +1054,8 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
             }
         }
     }
+    __shared__ unsigned long long ssum[4];
+    stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
 }
 
 // finishing nodes (patterns of length D): (node << 32 | b, e) pairs, sorted later
@@ -1125,7 +1257,8 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
         r.offset = off;
         rec[o] = r;
     }
-    if (my_steps) atomicAdd(steps, my_steps);
+    __shared__ unsigned long long sh[4];
+    stat_add(steps, ST_LOC_STEPS, my_steps, sh);
 }
 
 // ------------------------------------------------- DA/OFF table (index open)
@@ -1153,39 +1286,13 @@ __global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, cons
     GRID_STRIDE(x, N) off[x] = wlen[da[x]] - off[x];
 }
 
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
-
-__global__ void k_count_found(const uint32_t* __restrict__ occ, uint64_t P, unsigned long long* __restrict__ found) {
+// launched with a small grid (kReduceBlocks): one atomic per block
+__global__ void __launch_bounds__(256) k_count_found(const uint32_t* __restrict__ occ, uint64_t P, unsigned long long* __restrict__ found) {
+    __shared__ unsigned long long sh[4];
     unsigned long long f = 0;
     GRID_STRIDE(i, P) f += occ[i] > 0;
-    f = wave_sum(f);
-    if ((threadIdx.x & 63) == 0 && f) atomicAdd(found, f);
-}
-
-// one launch: lengths, longest pattern, patterns holding the end-marker '#'
-__global__ void k_prep(const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes, uint64_t P, uint32_t* __restrict__ len,
-                       unsigned int* __restrict__ out /* [0] Lmax, [1] patterns with '#' */) {
-    uint32_t mx = 0;
-    unsigned long long nt = 0;
-    GRID_STRIDE(i, P) {
-        const uint64_t a = off[i], b = off[i + 1];
-        len[i] = (uint32_t)(b - a);
-        mx = max(mx, (uint32_t)(b - a));
-        uint32_t f = 0;
-        for (uint64_t t = a; t < b; t++) f |= bytes[t] == '#';
-        nt += f;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
-    nt = wave_sum(nt);
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(out + 0, mx);
-        if (nt) atomicAdd(out + 1, (unsigned int)nt);
-    }
+    f = block_sum(f, sh);
+    if (threadIdx.x == 0 && f) atomicAdd(found, f);
 }
 
 // per depth D: trie nodes M_D = #{i : lcp[i] < D <= slen[i]} (difference array over D)

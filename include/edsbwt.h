@@ -80,7 +80,9 @@ typedef struct {
     double ms_total;          /* device time of the call (hipEvent) */
     double ms_kernel[16];     /* EDSBWT_PROFILE: per kernel class, see edsbwt_kernel_name */
     uint64_t launches_kernel[16];
-    uint64_t bytes_kernel[16];/* algorithmic bytes per kernel class (DESIGN.md §Roofline) */
+    uint64_t bytes_kernel[16];/* algorithmic bytes per kernel class (SURVEY.md §8(d), DESIGN.md §Roofline) */
+    uint64_t lines_kernel[16];/* occ-block lines the kernels actually read (a narrow interval's two
+                                 ends share one line; the locate table reads none) */
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,

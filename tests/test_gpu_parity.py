@@ -98,6 +98,56 @@ def test_larger_eds_gpu(oracle, edsbwt, tmp_path):
     _compare(oracle, edsbwt, base, pats)
 
 
+@pytest.mark.parametrize("alphabet", ["ACGT", "ACGTNRY"])
+def test_long_patterns_gpu(oracle, edsbwt, tmp_path, alphabet):
+    """Patterns spanning several key chunks (3-bit codes for ACGT, 4-bit once the
+    alphabet has 7 symbols + '#'), and blocks of patterns too long to stage in LDS."""
+    rng = random.Random(len(alphabet))
+    segs = edsgen.random_eds(rng, 3000, alphabet=alphabet, lmax=9, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.choice([15, 16, 17, 21, 22, 33, 48, 64, 70])) or "ACGT" for _ in range(1500)]
+    pats += [edsgen.planted(rng, segs, rng.randint(100, 200)) or "A" * 150 for _ in range(300)]
+    pats += ["".join(rng.choice(alphabet) for _ in range(rng.randint(1, 90))) for _ in range(1500)]
+    _compare(oracle, edsbwt, base, pats, table_too=False)
+
+
+def test_c5_style_gpu(oracle, edsbwt, tmp_path):
+    """C5's shape at a size the oracle finishes in seconds: ~20% empty-word segments and
+    a mixed 8–64-mer batch (BASELINE.json configs[2] is 1 Gchar / 100M patterns)."""
+    rng = random.Random(55)
+    segs = edsgen.random_eds(rng, 20000, kmax=4, lmax=12, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(8, 64)) or "ACGT" for _ in range(3000)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(8, 64))) for _ in range(3000)]
+    _compare(oracle, edsbwt, base, pats, table_too=False)
+
+
+def test_unaligned_device_bytes(oracle, edsbwt, tmp_path):
+    """search_device with a pattern buffer that is not 4-B aligned (the LDS staging
+    of the key kernel needs alignment and must fall back)."""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(3)
+    segs = edsgen.random_eds(rng, 800, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(4, 30)) or "ACGT" for _ in range(500)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    with edsbwt.Index(base) as idx:
+        raw = torch.zeros(buf.size + 1, dtype=torch.uint8, device="cuda")
+        raw[1:] = torch.from_numpy(buf.copy()).cuda()
+        d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_counts = torch.zeros(len(pats), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        ptr, n = idx.search_device(raw.data_ptr() + 1, d_offs.data_ptr(), len(pats), d_counts.data_ptr())
+        assert np.array_equal(d_counts.cpu().numpy().astype(np.uint32), oc)
+        occ = np.zeros(n, dtype=edsbwt.OCC_DTYPE)
+        if n:
+            assert hip.hipMemcpy(ctypes.c_void_p(occ.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(occ.nbytes), 2) == 0
+        assert np.array_equal(occ, oo)
+
+
 def test_deep_overflow_rerun(oracle, edsbwt, tmp_path):
     """Lists longer than k_deep's registers (many '#' rows / many intervals) fall back
     to the level path: force it with an EDS whose segments repeat one motif."""

@@ -1,0 +1,116 @@
+// Calibration of the access shape the search kernels use: each lane gathers one random
+// 64-B rank block (the OccBlock of kernels.h) from a table of a given size.
+//
+//   calib_gather [table_MB ...]          prints one JSON line per (shape, table size)
+//
+// Shapes: "gather64"   — one random 64-B block per lane (4 × 16-B loads, the rank query);
+//         "gather128"  — one random 128-B line per lane (8 × 16-B loads);
+//         "stream16"   — coalesced 16-B-per-lane streaming read of the whole table (the
+//                        shape MI355X_MICROARCH.md calibrates FETCH_SIZE on);
+//         "stream4"    — coalesced 4-B-per-lane streaming read (the item arrays' shape).
+// Algorithmic bytes are known exactly, so running this under
+// `rocprofv3 --pmc FETCH_SIZE` gives the FETCH_SIZE → bytes factor for each shape, and the
+// timed rate is the practical ceiling of the rank-block gathers (vs HBM peak 8 TB/s).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <vector>
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));             \
+            std::exit(2);                                                            \
+        }                                                                            \
+    } while (0)
+
+__device__ __forceinline__ uint32_t mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+// each lane: `iters` random blocks of LINES16 × 16 B
+template <int LINES16>
+__global__ void __launch_bounds__(256) k_gather(const uint4* __restrict__ t, uint32_t nblk, uint32_t iters, uint32_t seed,
+                                                uint32_t* __restrict__ sink) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t h = mix(g ^ seed), acc = 0;
+    for (uint32_t i = 0; i < iters; i++) {
+        h = mix(h + i);
+        const uint4* p = t + (size_t)(h % nblk) * LINES16;
+        uint4 v[LINES16];
+#pragma unroll
+        for (int k = 0; k < LINES16; k++) v[k] = p[k];
+#pragma unroll
+        for (int k = 0; k < LINES16; k++) acc ^= v[k].x + v[k].y + v[k].z + v[k].w;
+    }
+    if (acc == 0x12345678u) sink[g] = acc;  // keeps the loads alive; never true in practice
+}
+
+__global__ void __launch_bounds__(256) k_stream4(const uint32_t* __restrict__ t, size_t n4, uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) acc ^= t[i];
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(256) k_stream(const uint4* __restrict__ t, size_t n16, uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 v = t[i];
+        acc ^= v.x + v.y + v.z + v.w;
+    }
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
+int main(int argc, char** argv) {
+    std::vector<size_t> mbs;
+    for (int i = 1; i < argc; i++) mbs.push_back(std::strtoull(argv[i], nullptr, 10));
+    if (mbs.empty()) mbs = {16, 100, 200, 1024, 4096};
+    uint32_t* sink;
+    const uint32_t grid = 256 * 32, block = 256, iters = 64;
+    CK(hipMalloc(&sink, (size_t)grid * block * 4));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (size_t mb : mbs) {
+        const size_t bytes = mb << 20;
+        uint4* t;
+        CK(hipMalloc(&t, bytes));
+        CK(hipMemset(t, 1, bytes));
+        for (int shape = 0; shape < 4; shape++) {
+            float best = 1e30f;
+            double alg = 0;
+            for (int rep = 0; rep < 5; rep++) {
+                CK(hipEventRecord(a));
+                if (shape == 0) {
+                    hipLaunchKernelGGL(k_gather<4>, dim3(grid), dim3(block), 0, 0, t, (uint32_t)(bytes / 64), iters, 17u + rep, sink);
+                    alg = (double)grid * block * iters * 64;
+                } else if (shape == 1) {
+                    hipLaunchKernelGGL(k_gather<8>, dim3(grid), dim3(block), 0, 0, t, (uint32_t)(bytes / 128), iters, 17u + rep, sink);
+                    alg = (double)grid * block * iters * 128;
+                } else if (shape == 2) {
+                    hipLaunchKernelGGL(k_stream, dim3(grid), dim3(block), 0, 0, t, bytes / 16, sink);
+                    alg = (double)bytes;
+                } else {
+                    hipLaunchKernelGGL(k_stream4, dim3(grid), dim3(block), 0, 0, reinterpret_cast<const uint32_t*>(t), bytes / 4, sink);
+                    alg = (double)bytes;
+                }
+                CK(hipGetLastError());
+                CK(hipEventRecord(b));
+                CK(hipEventSynchronize(b));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, a, b));
+                if (rep > 0 && ms < best) best = ms;
+            }
+            const char* nm = shape == 0 ? "gather64" : shape == 1 ? "gather128" : shape == 2 ? "stream16" : "stream4";
+            std::printf("{\"shape\": \"%s\", \"table_MB\": %zu, \"bytes_per_launch\": %.0f, \"best_ms\": %.4f, \"GBps\": %.1f}\n", nm, mb, alg,
+                        best, alg / best / 1e6);
+            std::fflush(stdout);
+        }
+        CK(hipFree(t));
+    }
+    return 0;
+}

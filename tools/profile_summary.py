@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of a bench.py run.
+
+    python tools/profile_summary.py <trace_dir> <pmc_fetch_dir> <pmc_write_dir> <bench.json> <out_summary.json> \
+        [--traffic profiles/traffic_<cfg>.json --source "<what was run>"]
+
+* kernel trace (--kernel-trace --stats): per kernel calls / total / average duration,
+  and per bench.py kernel class (the `roofline.kernel` the bench line names);
+* PMC (separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes, as MI355X_MICROARCH.md
+  §HBM prescribes): per kernel bytes fetched / written.  FETCH_SIZE is in KB and its
+  byte factor depends on the access shape; tools/calib_gather.hip measured it on
+  MI355X (profiles/r01_calib_fetch.csv): 1.00 for one random 64-B line per lane — the
+  shape of every rank query, which dominates the step / deep / locate classes — and
+  2.0 for 16-B-per-lane streaming reads (the guide's gfx950 correction).  The classes
+  below use the gather factor; WRITE_SIZE × 1024 as is.
+* --traffic writes the per-class HBM bytes per launch that bench.py reports as
+  `roofline.traffic`.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+
+# bench.py kernel class -> kernels (engine.hip KClass)
+CLASSES = {
+    "step": ("k_lvl_items", "k_lvl_dollar"),
+    "deep": ("k_deep", "k_deep_wide"),
+    "locate": ("k_locate",),
+}
+FETCH_FACTOR_GATHER64 = 1.0
+
+
+def short(name: str) -> str:
+    n = name.split("(")[0]
+    n = n.replace("void ", "").replace("edsbwt::", "")
+    return n.split("<")[0] if not n.startswith("rocprim") else "rocprim"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace_dir")
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("bench_json")
+    ap.add_argument("out")
+    ap.add_argument("--traffic")
+    ap.add_argument("--source", default="")
+    a = ap.parse_args()
+
+    def first_csv(d, suffix):
+        for f in sorted(os.listdir(d)):
+            if f.endswith(suffix):
+                return os.path.join(d, f)
+        raise FileNotFoundError(f"{d}/*{suffix}")
+
+    stats = list(csv.DictReader(open(first_csv(a.trace_dir, "kernel_stats.csv"))))
+    per = collections.defaultdict(lambda: {"calls": 0, "total_ms": 0.0})
+    for r in stats:
+        k = short(r["Name"])
+        per[k]["calls"] += int(r["Calls"])
+        per[k]["total_ms"] += float(r["TotalDurationNs"]) / 1e6
+    for v in per.values():
+        v["avg_us"] = 1e3 * v["total_ms"] / max(1, v["calls"])
+    pmc = collections.defaultdict(lambda: {"fetch_bytes": 0.0, "write_bytes": 0.0, "dispatches": 0})
+    for d, key in ((a.fetch_dir, "fetch_bytes"), (a.write_dir, "write_bytes")):
+        for r in csv.DictReader(open(first_csv(d, "counter_collection.csv"))):
+            k = short(r["Kernel_Name"])
+            v = float(r["Counter_Value"]) * 1024.0
+            pmc[k][key] += FETCH_FACTOR_GATHER64 * v if key == "fetch_bytes" else v
+            if key == "fetch_bytes":
+                pmc[k]["dispatches"] += 1
+    bench = json.load(open(a.bench_json))
+    classes = {}
+    for c, ks in CLASSES.items():
+        calls = sum(per[k]["calls"] for k in ks if k in per)
+        tot = sum(per[k]["total_ms"] for k in ks if k in per)
+        disp = sum(pmc[k]["dispatches"] for k in ks if k in pmc)
+        fb = sum(pmc[k]["fetch_bytes"] for k in ks if k in pmc)
+        wb = sum(pmc[k]["write_bytes"] for k in ks if k in pmc)
+        classes[c] = {"rocprof_calls": calls, "rocprof_avg_launch_ms": tot / max(1, calls),
+                      "pmc_hbm_bytes_per_launch": (fb + wb) / max(1, disp),
+                      "pmc_fetch_bytes_per_launch": fb / max(1, disp), "pmc_write_bytes_per_launch": wb / max(1, disp)}
+    out_d = {"bench": {k: bench.get(k) for k in ("value", "ms_per_step", "roofline", "kernel_ms_per_step")},
+             "fetch_factor": FETCH_FACTOR_GATHER64,
+             "classes": classes,
+             "kernels": {k: {**per[k], **pmc.get(k, {})} for k in sorted(per, key=lambda k: -per[k]["total_ms"])}}
+    json.dump(out_d, open(a.out, "w"), indent=1)
+    if a.traffic:
+        json.dump({"source": a.source, "fetch_factor": FETCH_FACTOR_GATHER64, "classes": classes}, open(a.traffic, "w"), indent=1)
+    print(json.dumps(classes, indent=1))
+
+
+if __name__ == "__main__":
+    main()
