@@ -152,6 +152,12 @@ struct Engine {
     struct Ev { int k; hipEvent_t a, b; };
     std::vector<Ev> evs, ev_pool;
 
+    // bits needed for values 0..v
+    static uint32_t bits_for(uint64_t v) {
+        uint32_t b = 1;
+        while (b < 64 && (v >> b)) b++;
+        return b;
+    }
     KIdx kidx() const {
         KIdx X;
         X.occ = occ.p;
@@ -163,6 +169,8 @@ struct Engine {
         X.da = da.p;
         X.offt = offt.p;
         X.N = N; X.W = W; X.S = S; X.sigma = sigma;
+        X.segbits = bits_for(S);
+        X.rowbits = bits_for(N);
         for (int c = 0; c < 8; c++) X.C[c] = C[c];
         return X;
     }
@@ -628,11 +636,11 @@ struct Engine {
                         tmp.ensure(tb);
                         timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream)); });
                         rflag.ensure(V);
-                        launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, rflag.p);
+                        launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, 32u, rflag.p);
                         R = scan_u32(rflag.p, rscan, V);
                         rb.ensure(R); re.ensure(R); ru.ensure(R);
                         launch(KC_LINK, k_run_build, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
-                               (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p, (uint32_t*)nullptr);
+                               (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, 32u, rb.p, re.p, ru.p, (uint32_t*)nullptr);
                         launch(KC_LINK, k_bounds, R, (const uint32_t*)ru.p, (uint64_t)R, doff.p, dend.p);
                         docb.ensure((size_t)R * 8);
                         doce.ensure((size_t)R * 8);
@@ -879,19 +887,18 @@ struct Engine {
                 lkeys.ensure(nkeys);
                 lkeys2.ensure(nkeys);
                 unshard1(1, cap_keys, ekeys.p, lkeys.p, nkeys);
-                int endbit = 33;
-                while (endbit < 64 && ((uint64_t)Mcur >> (endbit - 32))) endbit++;
+                const int endbit = (int)std::min<uint32_t>(64, X.segbits + bits_for(Mcur));
                 size_t tb = 0;
                 HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream));
                 tmp.ensure(tb);
                 timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream)); });
                 rflag.ensure(nkeys);
                 rscan.ensure(nkeys);
-                launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, rflag.p);
+                launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, X.segbits, rflag.p);
                 exclusive_scan(rflag.p, rscan.p, nkeys);
                 rb.ensure(nkeys); re.ensure(nkeys); ru.ensure(nkeys);
                 launch(KC_LINK, k_run_build, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
-                       (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, rb.p, re.p, ru.p, d_runs);
+                       (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, X.segbits, rb.p, re.p, ru.p, d_runs);
                 const std::vector<uint32_t> keep_items = shard_counts(0);
                 for (;;) {
                     launch(KC_STEP, k_lvl_dollar, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
@@ -927,23 +934,22 @@ struct Engine {
                 const size_t cap_fin = shard_bound(nnext, 1);
                 efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD);
                 launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
-                       (const uint8_t*)fin.p, lcnt.p, efk.p, efv.p, (uint32_t)cap_fin, node_occ.p);
+                       (const uint8_t*)fin.p, lcnt.p, efk.p, efv.p, (uint32_t)cap_fin, node_occ.p, X.rowbits);
                 fetch_shards();
                 const uint32_t F = shard_total(4);
                 fk.ensure(F); fv.ensure(F);
                 if (F) {
                     unshard2(4, cap_fin, efk.p, efv.p, fk.p, fv.p, F);
                     fk2.ensure(F); fv2.ensure(F);
-                    int endbit = 33;
-                    while (endbit < 64 && ((uint64_t)M >> (endbit - 32))) endbit++;
+                    const int endbit = (int)std::min<uint32_t>(64, X.rowbits + bits_for(M));
                     size_t tb = 0;
                     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream));
                     tmp.ensure(tb);
                     timed(KC_FINISH, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream)); });
-                    launch(KC_FINISH, k_fin_bounds, F, F, (const uint64_t*)fk2.p, foff.p, fend.p);
+                    launch(KC_FINISH, k_fin_bounds, F, F, (const uint64_t*)fk2.p, X.rowbits, foff.p, fend.p);
                     ab.grow_keep(abase + F, stream);
                     ae.grow_keep(abase + F, stream);
-                    launch(KC_FINISH, k_fin_archive, F, F, (const uint64_t*)fk2.p, (const uint32_t*)fv2.p, abase, ab.p, ae.p);
+                    launch(KC_FINISH, k_fin_archive, F, F, (const uint64_t*)fk2.p, (const uint32_t*)fv2.p, abase, X.rowbits, ab.p, ae.p);
                 }
                 launch(KC_FINISH, k_finish2, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
                        (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r_off, r_cnt, r_occ);

@@ -43,6 +43,8 @@ struct KIdx {
     const uint32_t* da;        // [N] optional DA per row
     const uint32_t* offt;      // [N] optional offset-in-word per row
     uint32_t N, W, S, sigma;
+    uint32_t segbits;          // bits of a segment id (1..S): link keys are node << segbits | segment
+    uint32_t rowbits;          // bits of a BWT row (< N): finisher keys are node << rowbits | row
     uint32_t C[8];             // first row of each pile
 };
 

@@ -454,30 +454,33 @@ __global__ void k_link_emit(uint64_t H, const uint32_t* __restrict__ hoff, uint6
 
 // LINK step 3: union of previous-segment ranges [seg_lo[s], s-1] per owner
 // (the deque walk of link(), :533-561, yields exactly these maximal runs, ascending)
-__global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ seg_lo, uint32_t* __restrict__ flag) {
+// keys: node << sb | segment
+__global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ seg_lo, uint32_t sb,
+                            uint32_t* __restrict__ flag) {
+    const uint64_t sm = (1ull << sb) - 1;
     GRID_STRIDE(t, V) {
         const uint64_t k = keys[t];
         uint32_t f = 1;
         if (t) {
             const uint64_t kp = keys[t - 1];
-            if ((kp >> 32) == (k >> 32) && seg_lo[(uint32_t)k] <= (uint32_t)kp) f = 0;
+            if ((kp >> sb) == (k >> sb) && seg_lo[(uint32_t)(k & sm)] <= (uint32_t)(kp & sm)) f = 0;
         }
         flag[t] = f;
     }
 }
 
 __global__ void k_run_build(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rscan,
-                            const uint32_t* __restrict__ seg_lo, const uint32_t* __restrict__ seg_start,
+                            const uint32_t* __restrict__ seg_lo, const uint32_t* __restrict__ seg_start, uint32_t sb,
                             uint32_t* __restrict__ rb, uint32_t* __restrict__ re, uint32_t* __restrict__ rown,
                             uint32_t* __restrict__ nruns) {
     GRID_STRIDE(t, V) {
         if (nruns && t + 1 == V) *nruns = rscan[t] + flag[t];
         const uint64_t k = keys[t];
-        const uint32_t s = (uint32_t)k;
+        const uint32_t s = (uint32_t)(k & ((1ull << sb) - 1));
         const uint32_t r = rscan[t] + flag[t] - 1;
         if (flag[t]) {
             rb[r] = seg_start[seg_lo[s]];
-            rown[r] = (uint32_t)(k >> 32);
+            rown[r] = (uint32_t)(k >> sb);
         }
         if (t + 1 == V || flag[t + 1]) re[r] = seg_start[s] - 1;
     }
@@ -885,6 +888,26 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* __restrict__ counter, 
     return base + x - n;
 }
 
+// two appends with one atomic round trip (both counters in the same shard line)
+__device__ __forceinline__ void wave_append2(uint32_t* __restrict__ c0, uint32_t n0, uint32_t* __restrict__ c1, uint32_t n1, uint32_t& a0,
+                                             uint32_t& a1) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = n0, y = n1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t px = __shfl_up(x, o, 64), py = __shfl_up(y, o, 64);
+        if (lane >= o) { x += px; y += py; }
+    }
+    const uint32_t t0 = __shfl(x, 63, 64), t1 = __shfl(y, 63, 64);
+    uint32_t b0 = 0, b1 = 0;
+    if (lane == 63) {
+        if (t0) b0 = atomicAdd(c0, t0);
+        if (t1) b1 = atomicAdd(c1, t1);
+    }
+    a0 = __shfl(b0, 63, 64) + x - n0;
+    a1 = __shfl(b1, 63, 64) + y - n1;
+}
+
 // Appends go to NSHARD independent regions (counter k of shard s at cnt[s*32+k],
 // one 128-B line per shard) so that no single address takes every wave's atomic;
 // k_unshard packs the regions afterwards.
@@ -936,7 +959,12 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
                 if (c < 8 && re[c] > rb[c]) { cc[t] = c; nk++; }
             }
         }
-        uint32_t at = wave_append(cnt + 0, nk);
+        // '#' rows of the item (dollars_in_interval, :607-625): short ranges inline,
+        // long ones as chunks of 256 rows for k_lvl_chunks
+        const uint32_t h = (LINK && nch) ? re[0] - rb[0] : 0u;
+        const uint32_t nc = h > 16 ? (h + 255) / 256 : 0u;
+        uint32_t at, cat;
+        wave_append2(cnt + 0, nk, cnt + 2, nc, at, cat);  // one round trip for both
 #pragma unroll
         for (int t = 0; t < 9; t++) {
             if (cc[t] != 0xFF) {
@@ -950,9 +978,6 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
             }
         }
         if (LINK) {
-            // '#' rows of the item (dollars_in_interval, :607-625): short ranges inline,
-            // long ones as chunks of 256 rows for k_lvl_chunks
-            const uint32_t h = nch ? re[0] - rb[0] : 0u;
             uint32_t nz = 0;
             if (h && h <= 16)
                 for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
@@ -961,18 +986,33 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
                 for (uint32_t k = rb[0]; k < re[0]; k++) {
                     const uint32_t s = X.eof_seg[k];
                     if (s) {
-                        if (kat < cap_keys) keys[kat] = ((uint64_t)u << 32) | s;
+                        if (kat < cap_keys) keys[kat] = ((uint64_t)u << X.segbits) | s;
                         kat++;
                     }
                 }
-            const uint32_t nc = h > 16 ? (h + 255) / 256 : 0u;
-            uint32_t cat = wave_append(cnt + 2, nc);
-            for (uint32_t q = 0; q < nc; q++, cat++)
-                if (cat < cap_chunks) {
-                    ck_u[cat] = u;
-                    ck_k[cat] = rb[0] + 256 * q;
-                    ck_e[cat] = min(rb[0] + 256 * (q + 1), re[0]);
-                }
+            // chunk records: a lane writes a few itself; the wave writes long runs together
+            // (the root's items hold every '#' row: thousands of chunks each)
+            if (nc && nc <= 8)
+                for (uint32_t q = 0; q < nc; q++)
+                    if (cat + q < cap_chunks) {
+                        ck_u[cat + q] = u;
+                        ck_k[cat + q] = rb[0] + 256 * q;
+                        ck_e[cat + q] = min(rb[0] + 256 * (q + 1), re[0]);
+                    }
+            uint64_t big = __ballot(nc > 8);
+            const uint32_t lane = threadIdx.x & 63;
+            while (big) {
+                const int l = __ffsll((unsigned long long)big) - 1;
+                big &= big - 1;
+                const uint32_t lu = __shfl(u, l, 64), lb = __shfl(rb[0], l, 64), le = __shfl(re[0], l, 64);
+                const uint32_t lc = __shfl(cat, l, 64), ln = __shfl(nc, l, 64);
+                for (uint32_t q = lane; q < ln; q += 64)
+                    if (lc + q < cap_chunks) {
+                        ck_u[lc + q] = lu;
+                        ck_k[lc + q] = lb + 256 * q;
+                        ck_e[lc + q] = min(lb + 256 * (q + 1), le);
+                    }
+            }
         }
     }
     __shared__ unsigned long long ssum[4];
@@ -999,7 +1039,7 @@ __global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* 
             for (uint32_t k = k0; k < k1; k++) {
                 const uint32_t s = X.eof_seg[k];
                 if (s) {
-                    if (kat < cap_keys) keys[kat] = ((uint64_t)u << 32) | s;
+                    if (kat < cap_keys) keys[kat] = ((uint64_t)u << X.segbits) | s;
                     kat++;
                 }
             }
@@ -1058,11 +1098,11 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
     stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
 }
 
-// finishing nodes (patterns of length D): (node << 32 | b, e) pairs, sorted later
+// finishing nodes (patterns of length D): (node << rowbits | b, e) pairs, sorted later
 __global__ void __launch_bounds__(256) k_fin_emit(uint32_t n, const uint32_t* __restrict__ nu, const uint32_t* __restrict__ nb,
                                                   const uint32_t* __restrict__ ne, const uint8_t* __restrict__ fin, uint32_t* __restrict__ cnt_all,
                                                   uint64_t* __restrict__ fk, uint32_t* __restrict__ fv, uint32_t cap,
-                                                  uint32_t* __restrict__ node_occ) {
+                                                  uint32_t* __restrict__ node_occ, uint32_t rowbits) {
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
     fk += (size_t)sh * cap; fv += (size_t)sh * cap;
@@ -1075,7 +1115,7 @@ __global__ void __launch_bounds__(256) k_fin_emit(uint32_t n, const uint32_t* __
         uint32_t at = wave_append(cnt + 4, f);
         if (f) {
             if (at < cap) {
-                fk[at] = ((uint64_t)u << 32) | nb[i];
+                fk[at] = ((uint64_t)u << rowbits) | nb[i];
                 fv[at] = ne[i];
             }
             atomicAdd(node_occ + u, ne[i] - nb[i] + 1);
@@ -1110,18 +1150,19 @@ __global__ void k_fin_flags(uint32_t M, uint32_t D, const uint32_t* __restrict__
 }
 
 // per node [off, end) in the sorted finisher keys
-__global__ void k_fin_bounds(uint32_t F, const uint64_t* __restrict__ fk, uint32_t* __restrict__ foff, uint32_t* __restrict__ fend) {
+__global__ void k_fin_bounds(uint32_t F, const uint64_t* __restrict__ fk, uint32_t rowbits, uint32_t* __restrict__ foff,
+                             uint32_t* __restrict__ fend) {
     GRID_STRIDE(t, F) {
-        const uint32_t u = (uint32_t)(fk[t] >> 32);
-        if (t == 0 || (uint32_t)(fk[t - 1] >> 32) != u) foff[u] = (uint32_t)t;
-        if (t + 1 == F || (uint32_t)(fk[t + 1] >> 32) != u) fend[u] = (uint32_t)t + 1;
+        const uint32_t u = (uint32_t)(fk[t] >> rowbits);
+        if (t == 0 || (uint32_t)(fk[t - 1] >> rowbits) != u) foff[u] = (uint32_t)t;
+        if (t + 1 == F || (uint32_t)(fk[t + 1] >> rowbits) != u) fend[u] = (uint32_t)t + 1;
     }
 }
 
-__global__ void k_fin_archive(uint32_t F, const uint64_t* __restrict__ fk, const uint32_t* __restrict__ fv, uint64_t abase,
+__global__ void k_fin_archive(uint32_t F, const uint64_t* __restrict__ fk, const uint32_t* __restrict__ fv, uint64_t abase, uint32_t rowbits,
                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae) {
     GRID_STRIDE(t, F) {
-        ab[abase + t] = (uint32_t)fk[t];
+        ab[abase + t] = (uint32_t)(fk[t] & ((1ull << rowbits) - 1));
         ae[abase + t] = fv[t];
     }
 }
