@@ -124,7 +124,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (default: the config's)")
-    ap.add_argument("--table", action="store_true", help="locate from the per-row (word, offset) table")
+    ap.add_argument("--locate", default="sampled", choices=("sampled", "walk", "table"),
+                    help="position recovery: LF walk to the first sampled row (default), the reference's full "
+                         "walk to '#', or the per-row (word, offset) table")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=0)
     ap.add_argument("--workdir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "edsbwt_bench"))
@@ -162,7 +164,7 @@ def main():
     t = time.time()
     idx = pkg.Index(base, device=local)
     t_open = time.time() - t
-    if args.table and locate:
+    if args.locate == "table" and locate:
         idx.search([b"A"], table=True)  # builds the table outside the timed region
     buf, offs = pkg.read_pattern_file(pats_path)
     dev = torch.device("cuda", local)
@@ -174,8 +176,8 @@ def main():
 
     def step(profile=False):
         return idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(),
-                                 first_pattern_id=first_id, locate=locate, table=args.table, profile=profile,
-                                 stream=stream)
+                                 first_pattern_id=first_id, locate=locate, table=args.locate == "table", profile=profile,
+                                 stream=stream, walk=args.locate == "walk")
 
     gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     gathered = torch.zeros(npat * world, dtype=torch.int32, device=gdev) if world > 1 else None
@@ -195,12 +197,14 @@ def main():
     kstats = {}
     total_occ = 0
     lf_steps = 0
+    ref_loc_steps = 0
     for i in range(args.steps):
         _, nocc = step(profile="light")
         exchange()
         st = idx.stats()
         total_occ += nocc
         lf_steps += 2 * st["intervals_stepped"] + st["locate_lf_steps"]
+        ref_loc_steps += st["locate_offsets"]
         for k, v in st["kernels"].items():
             a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
             a["ms"] += v["ms"]
@@ -214,9 +218,9 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        agg = torch.tensor([lf_steps, total_occ], dtype=torch.float64, device=gdev)
+        agg = torch.tensor([lf_steps, total_occ, ref_loc_steps], dtype=torch.float64, device=gdev)
         dist.all_reduce(agg)
-        lf_steps, total_occ = float(agg[0].item()), float(agg[1].item())
+        lf_steps, total_occ, ref_loc_steps = float(agg[0].item()), float(agg[1].item()), float(agg[2].item())
     last = idx.stats()
 
     if rank == 0:
@@ -244,9 +248,14 @@ def main():
             "data": "synthetic (edsbwt_gen, seeded)",
             "config": {"workload": WORKLOAD[cfg], "config": cfg, "patterns_per_gpu": npat,
                        "index_rows": idx.n_rows, "words": idx.n_words, "segments": idx.n_segments,
-                       "locate": ("table" if args.table else "lf-walk") if locate else "count-only",
+                       "locate": {"sampled": "lf-walk to the first sampled row (1 in 8 word offsets)",
+                                  "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
+                       if locate else "count-only",
                        "parallelism": f"pattern-shard x{world}"},
+            # LF steps the device executed (2 per interval step + locate walk moves)
             "lf_steps_per_sec": round(lf_steps / elapsed, 1),
+            # the reference's locate walk moves for the same records (sum of offsets, :348-353)
+            "reference_locate_lf_steps_per_sec": round(ref_loc_steps / elapsed, 1),
             "occurrences_per_step": int(total_occ / args.steps / max(1, world)) if world == 1 else int(total_occ / args.steps),
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": MI355X_HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / MI355X_HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -34,6 +34,7 @@ NO_DEEP = 0x10
 ORDERED = 0x20
 PROFILE_LIGHT = 0x40
 NO_WIDE = 0x80
+LOCATE_WALK = 0x100
 
 OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
 CSV_HEADER = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"  # MOVE_EDSBWTSearch.cpp:59 (note the trailing space)
@@ -59,7 +60,8 @@ class _Stats(ctypes.Structure):
                 ("deep_level_rerun", ctypes.c_uint64), ("ms_total", ctypes.c_double),
                 ("ms_kernel", ctypes.c_double * 16), ("launches_kernel", ctypes.c_uint64 * 16),
                 ("bytes_kernel", ctypes.c_uint64 * 16),
-                ("lines_kernel", ctypes.c_uint64 * 16)]
+                ("lines_kernel", ctypes.c_uint64 * 16),
+                ("locate_offsets", ctypes.c_uint64)]
 
 
 _LIB = None
@@ -168,15 +170,18 @@ class Index:
 
     def search(self, patterns: Sequence[bytes | str] | tuple[np.ndarray, np.ndarray], *, first_pattern_id: int = 1,
                locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
-               ordered: bool = False, wide: bool = True):
-        """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc])."""
+               ordered: bool = False, wide: bool = True, walk: bool = False):
+        """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc]).
+        ``table``: (word, offset) per row from the full table; ``walk``: the reference's
+        full LF walk to '#'; default: walk to the first sampled row."""
         buf, offs = patterns if isinstance(patterns, tuple) else pack_patterns(patterns)
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         npat = offs.size - 1
         counts = np.zeros(max(npat, 0), dtype=np.uint32)
         flags = ((LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
-                 | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0) | (0 if wide else NO_WIDE))
+                 | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0) | (0 if wide else NO_WIDE)
+                 | (LOCATE_WALK if walk else 0))
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         bp = buf.ctypes.data if buf.size else None
@@ -191,11 +196,12 @@ class Index:
 
     def search_device(self, d_bytes: int, d_offsets: int, npat: int, d_counts: int, *, first_pattern_id: int = 1,
                       locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
-                      stream: int = 0):
+                      stream: int = 0, walk: bool = False):
         """Device-resident batch (pointers are device addresses, e.g. torch data_ptr()).
         Returns (device pointer of the records, number of records)."""
         pflag = {False: 0, True: PROFILE, "light": PROFILE_LIGHT}[profile]
-        flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | pflag | (0 if deep else NO_DEEP)
+        flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | pflag | (0 if deep else NO_DEEP) \
+            | (LOCATE_WALK if walk else 0)
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,

@@ -89,6 +89,8 @@ constexpr int kDeepK = 8;
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
+// locate samples every 2^kSampleShift positions of a word (8 B per sampled row)
+[[maybe_unused]] constexpr uint32_t kSampleShift = 3;
 // patterns k_deep<kDeepK> cannot hold retry with lists of up to kDeepWide intervals
 constexpr int kDeepWide = 64;
 // levels2() result meaning "the batch needs the ordered path"
@@ -108,6 +110,8 @@ struct Engine {
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
     bool have_table = false;
+    DBuf<uint2> samples;     // locate samples (word, offset) of rows whose offset % 2^kSampleShift == 0
+    bool have_samples = false;
     // workspace
     DBuf<uint32_t> len, perm, perm2, slen, lcp, nid[2], flag, scan, node_first, node_parent, child_first, child_end;
     DBuf<uint8_t> node_char;
@@ -146,7 +150,15 @@ struct Engine {
     edsbwt_stats st{};
     // profiling
     bool prof = false;
-    bool no_wide = false;  // EDSBWT_NO_WIDE (tests): overflowed deep patterns go straight to the level path
+    bool no_wide = false;
+    // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
+    double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
+    double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
+    uint32_t deep_k = env_double("EDSBWT_DEEP_K", kDeepK) == 4 ? 4u : (uint32_t)kDeepK;  // register list length of k_deep
+    static double env_double(const char* name, double dflt) {
+        const char* v = std::getenv(name);
+        return v && *v ? std::atof(v) : dflt;
+    }  // EDSBWT_NO_WIDE (tests): overflowed deep patterns go straight to the level path
     uint32_t prof_mask = ~0u;  // kernel classes timed with events when profiling
     bool trace = std::getenv("EDSBWT_TRACE") != nullptr;
     struct Ev { int k; hipEvent_t a, b; };
@@ -168,6 +180,7 @@ struct Engine {
         X.seg_lo = seg_lo.p;
         X.da = da.p;
         X.offt = offt.p;
+        X.samples = samples.p;
         X.N = N; X.W = W; X.S = S; X.sigma = sigma;
         X.segbits = bits_for(S);
         X.rowbits = bits_for(N);
@@ -448,6 +461,37 @@ struct Engine {
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
         counters.ensure(16);
+        if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
+    }
+
+    // Locate samples: one (word, offset) per row whose offset in its word is a multiple
+    // of 2^kSampleShift, marked in the occ blocks' `samp` plane (sigma <= 7 frees cnt[7]
+    // for their running count).  Built from the per-row table, which is then dropped.
+    void build_samples() {
+#if EDSBWT_OCC_ROWS == 64
+        if (sigma > 7 || have_samples) return;
+        const bool keep_table = have_table;
+        build_table();
+        const uint64_t nblk = (uint64_t)N / kOccRows + 1;
+        DBuf<uint32_t> bcnt;
+        bcnt.ensure(nblk);
+        launch(KC_TABLE, k_samp_blocks, nblk, nblk, N, (const uint32_t*)offt.p, kSampleShift, occ.p, bcnt.p);
+        DBuf<uint32_t> bbase;
+        const uint32_t ns = scan_u32(bcnt.p, bbase, nblk);  // bbase[0..nblk], total read back
+        if (ns < W) throw Fail(EDSBWT_E_FORMAT, "locate samples: fewer sampled rows than words");
+        samples.ensure(ns);
+        device_bytes += (size_t)ns * sizeof(uint2);
+        launch(KC_TABLE, k_samp_fill, nblk, nblk, N, (const uint32_t*)da.p, (const uint32_t*)offt.p, (const uint32_t*)bbase.p, occ.p,
+               samples.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        if (!keep_table) {
+            da.release();
+            offt.release();
+            device_bytes -= (size_t)N * 8;
+            have_table = false;
+        }
+        have_samples = true;
+#endif
     }
 
     void build_table() {
@@ -586,7 +630,7 @@ struct Engine {
             const uint32_t M = scan_u32(flag.p, scan, P);
             if (M == 0) break;
             // the trie stopped sharing below depth d: finish every pattern alone (k_deep)
-            if (allow_deep && d >= 1 && (double)M >= kDeepShare * (double)ge[D]) {
+            if (allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D]) {
                 novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, ioff[cur].p, iend[cur].p, ib[cur].p, ie[cur].p, r_off, r_cnt,
                                 r_occ, abase, ovf_orig);
                 break;
@@ -717,11 +761,12 @@ struct Engine {
         DBuf<uint32_t>& ovf = tflag;  // per sorted pattern
         ovf.ensure(P);
         zero(ovf.p, P * 4);
-        ab.grow_keep(abase + (uint64_t)P * kDeepK, stream);
-        ae.grow_keep(abase + (uint64_t)P * kDeepK, stream);
-        launch(KC_DEEP, k_deep<kDeepK>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, (const uint32_t*)len.p, d_off, d_bytes,
-               (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
-        abase += (uint64_t)P * kDeepK;
+        const uint32_t K = deep_k;
+        ab.grow_keep(abase + (uint64_t)P * K, stream);
+        ae.grow_keep(abase + (uint64_t)P * K, stream);
+        launch(KC_DEEP, K == 4 ? k_deep<4> : k_deep<kDeepK>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, (const uint32_t*)len.p,
+               d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
+        abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace) std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu\n", D, M, (unsigned long long)active);
         st.bytes_kernel[KC_DEEP] += (uint64_t)P * 24;  // + interval steps and '#' rows, folded at the end of search()
@@ -789,7 +834,7 @@ struct Engine {
             const int nxt = cur ^ 1;
             const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
-            if (allow_deep && d >= 1 && (double)M >= kDeepShare * (double)ge[D] && (double)ncur <= kDeepItems * (double)Mcur) {
+            if (allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D] && (double)ncur <= deep_items * (double)Mcur) {
                 // group the unordered items by node, then finish patterns one per thread
                 gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur); goff.ensure(Mcur);
                 launch(KC_DEEP, k_zero4, 2 * (size_t)Mcur, gcnt.p, (uint64_t)Mcur, gfill.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0,
@@ -970,6 +1015,7 @@ struct Engine {
         prof_mask = (flags & EDSBWT_PROFILE) ? ~0u : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_LOCATE) | (1u << KC_LINKSORT));
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
         const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
+        const int loc_mode = use_table ? 1 : ((flags & EDSBWT_LOCATE_WALK) || !have_samples) ? 0 : 2;
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
         no_wide = (flags & EDSBWT_NO_WIDE) != 0;
         if (use_table) build_table();
@@ -1045,7 +1091,7 @@ struct Engine {
                        (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p);
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
-                       X, use_table ? 1 : 0, rec.p, stats.p);
+                       X, loc_mode, rec.p, stats.p);
             }
         }
         HIPCHK(hipMemcpyAsync(pinned_stats, stats.p, kStatSlots * 8, hipMemcpyDeviceToHost, stream));
@@ -1059,10 +1105,13 @@ struct Engine {
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];
-            if (locate && !use_table) st.lines_kernel[KC_LOCATE] += st.locate_lf_steps + OCC;  // one line per walk position
+            st.locate_offsets = sv[ST_LOC_OFFSETS];
+            // one line per walk position, plus the sample read
+            if (locate && !use_table) st.lines_kernel[KC_LOCATE] += st.locate_lf_steps + OCC + (loc_mode == 2 ? OCC : 0);
         }
         if (locate && OCC) {
-            st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * sizeof(OccBlock) + OCC * (sizeof(OccBlock) + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) + (use_table ? OCC * 8 : 0);
+            st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * sizeof(OccBlock) + OCC * (sizeof(OccBlock) + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) +
+                                          (loc_mode != 0 ? OCC * 8 : 0);
         }
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));

@@ -19,12 +19,15 @@ struct alignas(128) OccBlock {
 };
 static_assert(sizeof(OccBlock) == 128, "occ block must be one 128-B line");
 #elif EDSBWT_OCC_ROWS == 64
-// 64-B rank block over 64 BWT rows: 1 B/row, one half-line per rank query
+// 64-B rank block over 64 BWT rows: 1 B/row, one half-line per rank query.
+// When sigma <= 7 the block also carries the locate samples: `samp` marks the rows
+// whose offset in their word is a multiple of the sample rate, and cnt[7] (no symbol
+// has code 7) holds the number of sampled rows before the block.
 constexpr uint32_t kOccShift = 6;
 struct alignas(64) OccBlock {
     uint32_t cnt[8];
     uint64_t plane[3][1];
-    uint64_t pad;
+    uint64_t samp;
 };
 static_assert(sizeof(OccBlock) == 64, "occ block must be 64 B");
 #else
@@ -43,6 +46,7 @@ struct KIdx {
     const uint32_t* da;        // [N] optional DA per row
     const uint32_t* offt;      // [N] optional offset-in-word per row
     uint32_t N, W, S, sigma;
+    const uint2* samples;      // (word, offset) of the sampled rows, in row order (locate)
     uint32_t segbits;          // bits of a segment id (1..S): link keys are node << segbits | segment
     uint32_t rowbits;          // bits of a BWT row (< N): finisher keys are node << rowbits | row
     uint32_t C[8];             // first row of each pile

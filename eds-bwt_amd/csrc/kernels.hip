@@ -130,7 +130,7 @@ __device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ,
 #else  // 64 rows per 64-B block
 struct OccV {
     uint32_t cnt[8];
-    uint64_t p0, p1, p2;
+    uint64_t p0, p1, p2, samp;
 };
 __device__ __forceinline__ OccV load_block(const OccBlock* __restrict__ occ, uint32_t blk) {
     const uint4* p = reinterpret_cast<const uint4*>(occ + blk);
@@ -141,7 +141,7 @@ __device__ __forceinline__ OccV load_block(const OccBlock* __restrict__ occ, uin
     o.p0 = (uint64_t)c.y << 32 | c.x;
     o.p1 = (uint64_t)c.w << 32 | c.z;
     o.p2 = (uint64_t)d.y << 32 | d.x;
-    (void)d;
+    o.samp = (uint64_t)d.w << 32 | d.z;
     return o;
 }
 
@@ -237,7 +237,7 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long x, un
 // Every thread of the block must call it.
 constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards * kStatStride;
 // statistic slots (zeroed once per search, folded at its end)
-enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4 };
+enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5 };
 __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats, uint32_t k, unsigned long long v, unsigned long long* sh) {
     v = block_sum(v, sh);
     if (threadIdx.x == 0 && v) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + k, v);
@@ -1267,28 +1267,51 @@ __global__ void k_tasks(uint64_t P, const uint64_t* __restrict__ res_off, const 
 
 // locate (:328-369): walk LF until L = '#'; the walk length is the offset in the
 // word, the '#'-rank gives EOF_ID, the segment bitvector gives (D, S_j).
+// mode 0: the reference's full walk; 1: per-row (word, offset) table; 2: walk until
+// the first sampled row (offset a multiple of the sample rate) and add its stored
+// (word, offset) — '#' rows have offset 0 and are always sampled.
 __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
-                                                const uint32_t* __restrict__ tpat, uint32_t first_id, KIdx X, int use_table,
-                                                edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ steps) {
-    unsigned long long my_steps = 0;
+                                                const uint32_t* __restrict__ tpat, uint32_t first_id, KIdx X, int mode,
+                                                edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
+    unsigned long long my_steps = 0, my_off = 0;
     GRID_STRIDE(o, OCC) {
         const size_t t = upper_bound_dev<uint64_t>(tout, TT, (uint64_t)o) - 1;
         uint32_t x = trow[t] + (uint32_t)(o - tout[t]);
         uint32_t word, off;
-        if (use_table) {
+        if (mode == 1) {
             word = X.da[x];
             off = X.offt[x];
         } else {
             off = 0;
             for (;;) {
+#if EDSBWT_OCC_ROWS == 64
+                const OccV v = load_block(X.occ, x >> 6);
+                const uint32_t bit = x & 63u;
+                const uint64_t m = (1ull << bit) - 1ull;
+                if (mode == 2 && ((v.samp >> bit) & 1)) {
+                    const uint2 s = X.samples[v.cnt[7] + (uint32_t)__popcll(v.samp & m)];
+                    word = s.x;
+                    my_steps += off;
+                    off += s.y;
+                    break;
+                }
+                const uint32_t c = (uint32_t)((v.p0 >> bit) & 1) | (uint32_t)(((v.p1 >> bit) & 1) << 1) | (uint32_t)(((v.p2 >> bit) & 1) << 2);
+                uint32_t acc = 0;
+#pragma unroll
+                for (uint32_t cc = 0; cc < 8; cc++)
+                    if (cc == c) acc = v.cnt[cc];
+                const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
+                const uint32_t rk = acc + (uint32_t)__popcll(e & m);
+#else
                 uint32_t rk;
                 const uint32_t c = sym_rank(X.occ, x, &rk);
-                if (c == 0) { word = X.eof_word[rk]; break; }
+#endif
+                if (c == 0) { word = X.eof_word[rk]; my_steps += off; break; }
                 x = X.C[c] + rk;
                 off++;
             }
-            my_steps += off;
         }
+        my_off += off;
         const uint32_t seg = X.seg_of_word[word];
         edsbwt_occ r;
         r.pat = first_id + tpat[t];
@@ -1299,8 +1322,40 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
         rec[o] = r;
     }
     __shared__ unsigned long long sh[4];
-    stat_add(steps, ST_LOC_STEPS, my_steps, sh);
+    stat_add(stats, ST_LOC_STEPS, my_steps, sh);
+    stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
 }
+
+// ---------------------------------------------- locate samples (index open)
+#if EDSBWT_OCC_ROWS == 64
+// per 64-row block: the sampled-row plane (offset % 2^shift == 0) and its count
+__global__ void k_samp_blocks(uint64_t nblk, uint32_t N, const uint32_t* __restrict__ offt, uint32_t shift, OccBlock* __restrict__ occ,
+                              uint32_t* __restrict__ bcnt) {
+    GRID_STRIDE(b, nblk) {
+        uint64_t p = 0;
+        for (uint32_t r = 0; r < 64; r++) {
+            const uint64_t x = b * 64 + r;
+            if (x < N && (offt[x] & ((1u << shift) - 1)) == 0) p |= 1ull << r;
+        }
+        occ[b].samp = p;
+        bcnt[b] = (uint32_t)__popcll(p);
+    }
+}
+
+__global__ void k_samp_fill(uint64_t nblk, uint32_t N, const uint32_t* __restrict__ da, const uint32_t* __restrict__ offt,
+                            const uint32_t* __restrict__ bbase, OccBlock* __restrict__ occ, uint2* __restrict__ samples) {
+    GRID_STRIDE(b, nblk) {
+        uint32_t at = bbase[b];
+        occ[b].cnt[7] = at;
+        const uint64_t p = occ[b].samp;
+        for (uint32_t r = 0; r < 64; r++)
+            if ((p >> r) & 1) {
+                const uint64_t x = b * 64 + r;
+                samples[at++] = make_uint2(da[x], offt[x]);
+            }
+    }
+}
+#endif
 
 // ------------------------------------------------- DA/OFF table (index open)
 // For every word w, walk LF from row w (its '#'-suffix) to the row with L='#'

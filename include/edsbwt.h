@@ -44,6 +44,9 @@ enum {
 #define EDSBWT_PROFILE_LIGHT 0x40u/* events only around the few large launches (fused step, deep,
                                     locate, link sort): what bench.py uses inside its timed region */
 #define EDSBWT_NO_WIDE      0x80u/* tests: skip the wide-list retry of k_deep overflows */
+#define EDSBWT_LOCATE_WALK  0x100u/* with LOCATE: walk LF all the way to the '#' row as the
+                                    reference does (:348-353), ignoring the row samples;
+                                    identical records (default: stop at the first sampled row) */
 #define EDSBWT_ORDERED      0x20u/* keep every interval list in the reference's order at every
                                     depth (the path patterns holding '#' take); same results */
 
@@ -83,6 +86,8 @@ typedef struct {
     uint64_t bytes_kernel[16];/* algorithmic bytes per kernel class */
     uint64_t lines_kernel[16];/* occ-block lines the kernels actually read (a narrow interval's two
                                  ends share one line; the locate table reads none) */
+    uint64_t locate_offsets;  /* sum of the records' offsets = the LF moves of the reference's
+                                 locate walk (:348-353), whatever walk the device did */
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,

@@ -37,6 +37,7 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         gc, go = idx.search((buf, offs))
         assert np.array_equal(gc, oc)
         assert np.array_equal(go, oo), (go[:10], oo[:10])
+        assert idx.stats()["locate_offsets"] == int(oo["offset"].astype(np.uint64).sum())
         gc2, go2 = idx.search((buf, offs), locate=False)
         assert np.array_equal(gc2, oc) and go2.size == 0
         if table_too:
@@ -44,6 +45,9 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
             assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)
         st = idx.stats()
         assert st["found"] == int((oc > 0).sum())
+        gw, gow = idx.search((buf, offs), walk=True)      # the reference's full walk to '#'
+        assert np.array_equal(gw, oc) and np.array_equal(gow, oo)
+        assert idx.stats()["locate_lf_steps"] == int(oo["offset"].astype(np.uint64).sum())
         gc4, go4 = idx.search((buf, offs), deep=False)   # level-synchronous path only
         assert np.array_equal(gc4, oc) and np.array_equal(go4, oo)
         for deep in (True, False):                       # reference-ordered lists at every depth
