@@ -106,7 +106,7 @@ struct Engine {
     uint32_t C[8] = {0};
     uint64_t device_bytes = 0;
     DBuf<OccBlock> occ;
-    DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt;
+    DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt, segtab;
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
     bool have_table = false;
@@ -115,6 +115,7 @@ struct Engine {
     // workspace
     DBuf<uint32_t> len, perm, perm2, slen, lcp, nid[2], flag, scan, node_first, node_parent, child_first, child_end;
     DBuf<uint8_t> node_char;
+    DBuf<uint64_t> child_info;  // per parent node: first child | live-child symbol mask << 32
     DBuf<uint64_t> keys, kc, kc2, skey;
     DBuf<uint32_t> ib[2], ie[2], iu[2], ioff[2], iend[2], iocb, ioce;
     DBuf<uint32_t> hcnt, hoff, rflag, rscan, rb, re, ru, doff, dend, docb, doce;
@@ -181,6 +182,9 @@ struct Engine {
         X.da = da.p;
         X.offt = offt.p;
         X.samples = samples.p;
+        X.segtab = segtab.p;
+        X.seg_stride = sigma <= 7 ? 16u : 32u;
+        X.seg_hi = sigma <= 7 ? 8u : 9u;
         X.N = N; X.W = W; X.S = S; X.sigma = sigma;
         X.segbits = bits_for(S);
         X.rowbits = bits_for(N);
@@ -461,6 +465,13 @@ struct Engine {
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
         counters.ensure(16);
+        {  // segment link table (k_deep)
+            const KIdx X0 = kidx();
+            segtab.ensure((size_t)(S + 2) * X0.seg_stride);
+            device_bytes += (size_t)(S + 2) * X0.seg_stride * 4;
+            launch(KC_TABLE, k_segtab, (size_t)S + 2, S, kidx(), segtab.p);
+            HIPCHK(hipStreamSynchronize(stream));
+        }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
     }
 
@@ -852,11 +863,10 @@ struct Engine {
             st.trie_nodes += M;
             const bool finishing = hist[D] != 0;
             // one zeroing launch: shard counters, child links of the parents, finisher tables
-            child_first.ensure(Mcur);
-            child_end.ensure(Mcur);
+            child_info.ensure(Mcur);
             if (finishing) { node_occ.ensure(M); foff.ensure(M); fend.ensure(M); fin.ensure(M); }
-            launch(KC_NODES, k_zero4, (size_t)NSHARD * 32 + 32 + 2 * (size_t)Mcur, lcnt.p, (uint64_t)NSHARD * 32 + 32, child_first.p,
-                   (uint64_t)Mcur, child_end.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0);
+            launch(KC_NODES, k_zero4, (size_t)NSHARD * 32 + 32 + 2 * (size_t)Mcur, lcnt.p, (uint64_t)NSHARD * 32 + 32,
+                   (uint32_t*)child_info.p, 2 * (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0, (uint32_t*)nullptr, (uint64_t)0);
             if (finishing)
                 launch(KC_NODES, k_zero4, 3 * (size_t)M, node_occ.p, (uint64_t)M, foff.p, (uint64_t)M, fend.p, (uint64_t)M, (uint32_t*)nullptr,
                        (uint64_t)0);
@@ -865,7 +875,7 @@ struct Engine {
             exclusive_scan(flag.p, scan.p, P);
             launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
-            launch(KC_NODES, k_child_links, M, (const uint32_t*)node_parent.p, M, child_first.p, child_end.p);
+            launch(KC_NODES, k_child_info, M, M, (const uint32_t*)node_parent.p, (const uint8_t*)node_char.p, child_info.p);
             // fused step + '#'-row emission over the current items (sharded appends)
             size_t cap_next = std::max<size_t>(shard_bound(ncur, 2), 4096);
             size_t cap_keys = std::max<size_t>(shard_bound(ncur, 1), 4096);
@@ -881,13 +891,11 @@ struct Engine {
                 if (!first) zero(lcnt.p, NSHARD * 32 * 4);
                 if (d > 0)
                     launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
-                           (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
-                           X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
+                           (const uint32_t*)ie[cur].p, (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
                            (uint32_t)cap_chunks, stats.p);
                 else  // no link before the first step (:246-258)
                     launch(KC_STEP, k_lvl_items<false>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
-                           (const uint32_t*)ie[cur].p, (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p,
-                           X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
+                           (const uint32_t*)ie[cur].p, (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
                            (uint32_t)cap_chunks, stats.p);
                 fetch_shards();  // sync A
                 const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
@@ -947,7 +955,7 @@ struct Engine {
                 const std::vector<uint32_t> keep_items = shard_counts(0);
                 for (;;) {
                     launch(KC_STEP, k_lvl_dollar, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
-                           (const uint32_t*)child_first.p, (const uint32_t*)child_end.p, (const uint8_t*)node_char.p, X, eu.p, eb.p, ee.p,
+                           (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p,
                            (uint32_t)cap_next, lcnt.p, stats.p);
                     fetch_shards();  // sync B
                     const uint32_t m0 = shard_max(0);

@@ -47,6 +47,10 @@ struct KIdx {
     const uint32_t* offt;      // [N] optional offset-in-word per row
     uint32_t N, W, S, sigma;
     const uint2* samples;      // (word, offset) of the sampled rows, in row order (locate)
+    // per segment s (link of a word in s): [0] seg_lo[s]; [1 + c] rank_c at the first word of
+    // segment seg_lo[s]; [seg_hi + c] rank_c at the first word of s.  seg_stride u32 per entry.
+    const uint32_t* segtab;
+    uint32_t seg_stride, seg_hi;
     uint32_t segbits;          // bits of a segment id (1..S): link keys are node << segbits | segment
     uint32_t rowbits;          // bits of a BWT row (< N): finisher keys are node << rowbits | row
     uint32_t C[8];             // first row of each pile

@@ -669,22 +669,24 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
                 nn++;
                 last_e = e;
             };
-            uint32_t run_lo = 0, run_s = 0;
+            // a run [seg_lo[s_first], s_last - 1] of previous-segment words, stepped by c:
+            // its c-ranks come precomputed from the segment table (one line per segment)
+            uint32_t run_x = 0, run_y = 0, run_s = 0;
             bool have = false;
             auto close_run = [&]() {
-                const uint32_t r0 = X.seg_start[run_lo], r1 = X.seg_start[run_s] - 1;
-                uint32_t x0, x1, y0, y1;
-                n_blk += 2 - rank2_pair(X.occ, r0, r1 + 1, c, x0, x1, y0, y1);
-                if (y1 > x1) push(X.C[c] + x1, X.C[c] + y1 - 1);
+                if (run_y > run_x) push(X.C[c] + run_x, X.C[c] + run_y - 1);
                 n_steps++;
             };
 #pragma unroll
             for (int t = 0; t < K; t++) {
                 if ((uint32_t)t < rn) {
                     const uint32_t s = raw[t];
-                    const uint32_t lo = X.seg_lo[s];
+                    const uint32_t* e = X.segtab + (size_t)s * X.seg_stride;
+                    const uint32_t lo = e[0];
+                    n_blk++;
                     if (have && lo > run_s) { close_run(); have = false; }
-                    if (!have) { run_lo = lo; have = true; }
+                    if (!have) { run_x = e[1 + c]; have = true; }
+                    run_y = e[X.seg_hi + c];
                     run_s = s;
                 }
             }
@@ -888,24 +890,25 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* __restrict__ counter, 
     return base + x - n;
 }
 
-// two appends with one atomic round trip (both counters in the same shard line)
-__device__ __forceinline__ void wave_append2(uint32_t* __restrict__ c0, uint32_t n0, uint32_t* __restrict__ c1, uint32_t n1, uint32_t& a0,
-                                             uint32_t& a1) {
+// three appends (counters cnt[0..2] of one shard line) with one atomic round trip
+__device__ __forceinline__ void wave_append3(uint32_t* __restrict__ cnt, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t& a0, uint32_t& a1,
+                                             uint32_t& a2) {
     const int lane = threadIdx.x & 63;
-    uint32_t x = n0, y = n1;
+    uint32_t x = n0, y = n1, z = n2;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t px = __shfl_up(x, o, 64), py = __shfl_up(y, o, 64);
-        if (lane >= o) { x += px; y += py; }
+        const uint32_t px = __shfl_up(x, o, 64), py = __shfl_up(y, o, 64), pz = __shfl_up(z, o, 64);
+        if (lane >= o) { x += px; y += py; z += pz; }
     }
-    const uint32_t t0 = __shfl(x, 63, 64), t1 = __shfl(y, 63, 64);
-    uint32_t b0 = 0, b1 = 0;
+    uint32_t b0 = 0, b1 = 0, b2 = 0;
     if (lane == 63) {
-        if (t0) b0 = atomicAdd(c0, t0);
-        if (t1) b1 = atomicAdd(c1, t1);
+        if (x) b0 = atomicAdd(cnt + 0, x);
+        if (y) b1 = atomicAdd(cnt + 1, y);
+        if (z) b2 = atomicAdd(cnt + 2, z);
     }
     a0 = __shfl(b0, 63, 64) + x - n0;
     a1 = __shfl(b1, 63, 64) + y - n1;
+    a2 = __shfl(b2, 63, 64) + z - n2;
 }
 
 // Appends go to NSHARD independent regions (counter k of shard s at cnt[s*32+k],
@@ -920,11 +923,53 @@ constexpr uint32_t NSHARD = 64;
         if (const size_t i = i##_b + threadIdx.x; true)                                                                  \
             if (const bool valid = i < (size_t)(n); true)
 
-// children of node u: [child_first[u], child_end[u]) at the next depth, symbol node_char
+// Children of node u, packed by k_child_info: child_info[u] = first child | symbol
+// mask << 32.  Children are in trie order (ascending symbol code, a child for bytes
+// outside the alphabet last), so the child with symbol c is first + popcount of the
+// mask bits below c.
+__global__ void k_child_info(uint32_t M, const uint32_t* __restrict__ node_parent, const uint8_t* __restrict__ node_char,
+                             uint64_t* __restrict__ info) {
+    GRID_STRIDE(u, M) {
+        const uint32_t p = node_parent[u];
+        if (u == 0 || node_parent[u - 1] != p) {
+            uint32_t mask = 0;
+            for (size_t v = u; v < M && node_parent[v] == p; v++) {
+                const uint32_t c = node_char[v];
+                if (c < 8) mask |= 1u << c;
+            }
+            info[p] = ((uint64_t)mask << 32) | (uint32_t)u;
+        }
+    }
+}
+
+// one interval (node u, rows b..e1-1) stepped by every live child symbol: appends the
+// non-empty children.  The rank loads do not wait for the node's child word.
+#define LVL_STEP_LOAD(u, b, e1)                                                         \
+    {                                                                                   \
+        const uint64_t ci = child_info[u];                                              \
+        n_blk += 2 - rank_all_pair(X.occ, b, e1, X.sigma, rb, re);                     \
+        cf = (uint32_t)ci;                                                              \
+        mask = (uint32_t)(ci >> 32);                                                    \
+    }
+
+__device__ __forceinline__ void lvl_emit(uint32_t mask, uint32_t emit, uint32_t cf, const uint32_t* rb, const uint32_t* re, const KIdx& X,
+                                         uint32_t at, uint32_t cap, uint32_t* __restrict__ nu, uint32_t* __restrict__ nb,
+                                         uint32_t* __restrict__ ne) {
+#pragma unroll
+    for (uint32_t c = 0; c < 8; c++)
+        if ((emit >> c) & 1) {
+            if (at < cap) {
+                nu[at] = cf + (uint32_t)__popc(mask & ((1u << c) - 1u));
+                nb[at] = X.C[c] + rb[c];
+                ne[at] = X.C[c] + re[c] - 1;
+            }
+            at++;
+        }
+}
+
 template <bool LINK>
 __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* __restrict__ iu, const uint32_t* __restrict__ ib,
-                                                   const uint32_t* __restrict__ ie, const uint32_t* __restrict__ child_first,
-                                                   const uint32_t* __restrict__ child_end, const uint8_t* __restrict__ node_char, KIdx X,
+                                                   const uint32_t* __restrict__ ie, const uint64_t* __restrict__ child_info, KIdx X,
                                                    uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
                                                    uint32_t cap_keys, uint32_t* __restrict__ ck_u, uint32_t* __restrict__ ck_k,
@@ -936,52 +981,31 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
     keys += (size_t)sh * cap_keys;
     ck_u += (size_t)sh * cap_chunks; ck_k += (size_t)sh * cap_chunks; ck_e += (size_t)sh * cap_chunks;
     UNIFORM_STRIDE(i, valid, n) {
-        uint32_t u = 0, cf = 0, nch = 0;
+        uint32_t u = 0, cf = 0, mask = 0;
         uint32_t rb[8], re[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
         if (valid) {
             u = iu[i];
-            cf = child_first[u];
-            nch = child_end[u] - cf;
-            if (nch) {
-                n_blk += 2 - rank_all_pair(X.occ, ib[i], ie[i] + 1, X.sigma, rb, re);
-            }
+            LVL_STEP_LOAD(u, ib[i], ie[i] + 1)
         }
         // backward step of every child symbol (updateSingleInterval, :424-510)
-        uint32_t nk = 0;
-        uint32_t cc[9];
+        uint32_t emit = 0;
 #pragma unroll
-        for (int t = 0; t < 9; t++) {
-            cc[t] = 0xFF;
-            if ((uint32_t)t < nch) {
-                const uint32_t c = node_char[cf + t];
-                if (c < 8 && re[c] > rb[c]) { cc[t] = c; nk++; }
-            }
-        }
+        for (uint32_t c = 0; c < 8; c++)
+            if (((mask >> c) & 1) && re[c] > rb[c]) emit |= 1u << c;
+        const uint32_t nk = (uint32_t)__popc(emit);
         // '#' rows of the item (dollars_in_interval, :607-625): short ranges inline,
         // long ones as chunks of 256 rows for k_lvl_chunks
-        const uint32_t h = (LINK && nch) ? re[0] - rb[0] : 0u;
+        const uint32_t h = (LINK && mask) ? re[0] - rb[0] : 0u;
         const uint32_t nc = h > 16 ? (h + 255) / 256 : 0u;
-        uint32_t at, cat;
-        wave_append2(cnt + 0, nk, cnt + 2, nc, at, cat);  // one round trip for both
-#pragma unroll
-        for (int t = 0; t < 9; t++) {
-            if (cc[t] != 0xFF) {
-                if (at < cap_next) {
-                    const uint32_t c = cc[t];
-                    nu[at] = cf + t;
-                    nb[at] = X.C[c] + rb[c];
-                    ne[at] = X.C[c] + re[c] - 1;
-                }
-                at++;
-            }
-        }
+        uint32_t nz = 0;
+        if (LINK && h && h <= 16)
+            for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
+        uint32_t at, kat, cat;
+        wave_append3(cnt, nk, nz, nc, at, kat, cat);  // one atomic round trip for the three lists
+        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne);
         if (LINK) {
-            uint32_t nz = 0;
-            if (h && h <= 16)
-                for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
-            uint32_t kat = wave_append(cnt + 1, nz);
             if (nz)
                 for (uint32_t k = rb[0]; k < re[0]; k++) {
                     const uint32_t s = X.eof_seg[k];
@@ -1048,8 +1072,7 @@ __global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* 
 
 // dollar items (previous-segment word ranges of a node) stepped by each child
 __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__ dn, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
-                                                    const uint32_t* __restrict__ de, const uint32_t* __restrict__ child_first,
-                                                    const uint32_t* __restrict__ child_end, const uint8_t* __restrict__ node_char, KIdx X,
+                                                    const uint32_t* __restrict__ de, const uint64_t* __restrict__ child_info, KIdx X,
                                                     uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                     uint32_t cap_next, uint32_t* __restrict__ cnt_all, unsigned long long* __restrict__ stats) {
     const uint32_t n = *dn;  // link runs, counted on the device by k_run_build
@@ -1058,41 +1081,20 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
     uint32_t* cnt = cnt_all + sh * 32;
     nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
     UNIFORM_STRIDE(i, valid, n) {
-        uint32_t cf = 0, nch = 0;
+        uint32_t cf = 0, mask = 0;
         uint32_t rb[8], re[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
         if (valid) {
             const uint32_t u = du[i];
-            cf = child_first[u];
-            nch = child_end[u] - cf;
-            if (nch) {
-                n_blk += 2 - rank_all_pair(X.occ, db[i], de[i] + 1, X.sigma, rb, re);
-            }
+            LVL_STEP_LOAD(u, db[i], de[i] + 1)
         }
-        uint32_t nk = 0;
-        uint32_t cc[9];
+        uint32_t emit = 0;
 #pragma unroll
-        for (int t = 0; t < 9; t++) {
-            cc[t] = 0xFF;
-            if ((uint32_t)t < nch) {
-                const uint32_t c = node_char[cf + t];
-                if (c < 8 && re[c] > rb[c]) { cc[t] = c; nk++; }
-            }
-        }
-        uint32_t at = wave_append(cnt + 0, nk);
-#pragma unroll
-        for (int t = 0; t < 9; t++) {
-            if (cc[t] != 0xFF) {
-                if (at < cap_next) {
-                    const uint32_t c = cc[t];
-                    nu[at] = cf + t;
-                    nb[at] = X.C[c] + rb[c];
-                    ne[at] = X.C[c] + re[c] - 1;
-                }
-                at++;
-            }
-        }
+        for (uint32_t c = 0; c < 8; c++)
+            if (((mask >> c) & 1) && re[c] > rb[c]) emit |= 1u << c;
+        const uint32_t at = wave_append(cnt + 0, (uint32_t)__popc(emit));
+        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne);
     }
     __shared__ unsigned long long ssum[4];
     stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
@@ -1360,6 +1362,28 @@ __global__ void k_samp_fill(uint64_t nblk, uint32_t N, const uint32_t* __restric
 // ------------------------------------------------- DA/OFF table (index open)
 // For every word w, walk LF from row w (its '#'-suffix) to the row with L='#'
 // (position 0): rows visited get DA = w and their distance from the word end.
+// segment link table (index open): for s >= 2 the c-ranks at both ends of the words of
+// segments [seg_lo[s], s-1] (the range link() adds for a word of s, :533-561, :620)
+__global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
+    GRID_STRIDE(s, (size_t)S + 2) {
+        uint32_t* e = tab + s * X.seg_stride;
+        uint32_t r0[8], r1[8];
+        const uint32_t lo = X.seg_lo[s];
+        if (s >= 2) {
+            rank_all(X.occ, X.seg_start[lo], X.sigma, r0);
+            rank_all(X.occ, X.seg_start[s], X.sigma, r1);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; c++) r0[c] = r1[c] = 0;
+        }
+        e[0] = lo;
+        for (uint32_t c = 0; c < X.sigma; c++) {
+            e[1 + c] = r0[c];
+            e[X.seg_hi + c] = r1[c];
+        }
+    }
+}
+
 __global__ void k_table_walk(uint32_t W, KIdx X, uint32_t* __restrict__ da, uint32_t* __restrict__ dist, uint32_t* __restrict__ wlen) {
     GRID_STRIDE(w, W) {
         uint32_t x = (uint32_t)w, t = 0;
