@@ -163,9 +163,11 @@ __device__ __forceinline__ void rank_all(const OccBlock* __restrict__ occ, uint3
 // Returns 1 when one block served both.
 __device__ __forceinline__ uint32_t rank_all_pair(const OccBlock* __restrict__ occ, uint32_t x0, uint32_t x1, uint32_t sigma, uint32_t* o0,
                                                   uint32_t* o1) {
+    // only lanes whose ends lie in different blocks read a second line (measured: issuing
+    // both reads unconditionally costs the level step more than the serialisation saves)
+    const bool same = (x1 >> 6) == (x0 >> 6);
     OccV v = load_block(occ, x0 >> 6);
     rank_all_v(v, x0, sigma, o0);
-    const bool same = (x1 >> 6) == (x0 >> 6);
     if (!same) v = load_block(occ, x1 >> 6);
     rank_all_v(v, x1, sigma, o1);
     return same;
@@ -202,11 +204,13 @@ __device__ __forceinline__ void rank2(const OccBlock* __restrict__ occ, uint32_t
 
 __device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ, uint32_t x0, uint32_t x1, uint32_t c, uint32_t& h0, uint32_t& r0,
                                                uint32_t& h1, uint32_t& r1) {
-    OccV v = load_block(occ, x0 >> 6);
-    rank2_v(v, x0, c, h0, r0);
+    // both reads back to back, no branch between them (k_deep's intervals are narrow: the
+    // second read is nearly always the same line and k_deep is latency-bound)
     const bool same = (x1 >> 6) == (x0 >> 6);
-    if (!same) v = load_block(occ, x1 >> 6);
-    rank2_v(v, x1, c, h1, r1);
+    const OccV v0 = load_block(occ, x0 >> 6);
+    const OccV v1 = load_block(occ, x1 >> 6);
+    rank2_v(v0, x0, c, h0, r0);
+    rank2_v(v1, x1, c, h1, r1);
     return same;
 }
 #endif
@@ -590,6 +594,9 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
                                               uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr) {
     unsigned long long n_steps = 0, n_hash = 0, n_blk = 0;  // n_blk: occ blocks read
+    __shared__ uint8_t scode[256];
+    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) scode[t] = code_of[t];
+    __syncthreads();
     GRID_STRIDE(i, P) {
         const uint32_t L = slen[i];
         if (L <= D0) continue;
@@ -607,8 +614,11 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
         const uint32_t a = perm[i];
         const uint8_t* pat = bytes + off[a];
         bool over = false;
+        // the next character's byte is read one step ahead, so no step waits for it
+        uint32_t nbyte = pat[L - 1 - D0];
         for (uint32_t d = D0; d < L && cn; d++) {
-            const uint32_t code = code_of[pat[L - 1 - d]];
+            const uint32_t code = scode[nbyte];
+            if (d + 1 < L) nbyte = pat[L - 2 - d];
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
