@@ -1114,6 +1114,11 @@ struct Engine {
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];
             st.locate_offsets = sv[ST_LOC_OFFSETS];
+            if (trace && sv[ST_CLK_STEPS])
+                std::fprintf(stderr, "[edsbwt] k_deep lane-steps %llu (with '#' rows %llu): cycles/step rank+link %.0f, runs %.0f, rest %.0f\n",
+                             (unsigned long long)sv[ST_CLK_STEPS], (unsigned long long)sv[ST_CLK_HASH_STEPS],
+                             (double)sv[ST_CLK_RANK] / sv[ST_CLK_STEPS], (double)sv[ST_CLK_RUNS] / sv[ST_CLK_STEPS],
+                             (double)sv[ST_CLK_REST] / sv[ST_CLK_STEPS]);
             // one line per walk position, plus the sample read
             if (locate && !use_table) st.lines_kernel[KC_LOCATE] += st.locate_lf_steps + OCC + (loc_mode == 2 ? OCC : 0);
         }

@@ -241,7 +241,16 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long x, un
 // Every thread of the block must call it.
 constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards * kStatStride;
 // statistic slots (zeroed once per search, folded at its end)
-enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5 };
+enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5,
+                  ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10 };
+// k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
+#ifdef EDSBWT_DEEP_CLOCKS
+#define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
+#define DEEP_CLK_ADD(acc, x) acc += (x)
+#else
+#define DEEP_CLK(v)
+#define DEEP_CLK_ADD(acc, x)
+#endif
 __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats, uint32_t k, unsigned long long v, unsigned long long* sh) {
     v = block_sum(v, sh);
     if (threadIdx.x == 0 && v) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + k, v);
@@ -594,6 +603,9 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
                                               uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr) {
     unsigned long long n_steps = 0, n_hash = 0, n_blk = 0;  // n_blk: occ blocks read
+#ifdef EDSBWT_DEEP_CLOCKS
+    unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
+#endif
     __shared__ uint8_t scode[256];
     for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) scode[t] = code_of[t];
     __syncthreads();
@@ -617,6 +629,7 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
         // the next character's byte is read one step ahead, so no step waits for it
         uint32_t nbyte = pat[L - 1 - D0];
         for (uint32_t d = D0; d < L && cn; d++) {
+            DEEP_CLK(t0);
             const uint32_t code = scode[nbyte];
             if (d + 1 < L) nbyte = pat[L - 2 - d];
             if (code >= X.sigma) { cn = 0; break; }
@@ -659,6 +672,7 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
                 }
             }
             if (over) break;
+            DEEP_CLK(t1);
             // step: [dollar runs (ascending), own intervals] by c, adjacent merged (:275-324)
             uint32_t nb[K], ne[K];
             uint32_t nn = 0, last_e = 0;
@@ -701,6 +715,7 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
                 }
             }
             if (have) close_run();
+            DEEP_CLK(t2);
 #pragma unroll
             for (int j = 0; j < K; j++)
                 if ((uint32_t)j < cn && se[j] > sb[j]) push(X.C[c] + sb[j], X.C[c] + se[j] - 1);
@@ -709,6 +724,12 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
             cn = nn;
 #pragma unroll
             for (int t = 0; t < K; t++) { cb[t] = nb[t]; ce[t] = ne[t]; }
+            DEEP_CLK(t3);
+            DEEP_CLK_ADD(c_rank, t1 - t0);
+            DEEP_CLK_ADD(c_runs, t2 - t1);
+            DEEP_CLK_ADD(c_rest, t3 - t2);
+            DEEP_CLK_ADD(c_steps, 1);
+            DEEP_CLK_ADD(c_hsteps, rn ? 1 : 0);
         }
         if (over) { ovf[i] = 1; continue; }
         // ascending rows (the input lists may be unordered sets)
@@ -738,6 +759,13 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
     stat_add(ctr, ST_DEEP_STEPS, n_steps, sh);
     stat_add(ctr, ST_DEEP_HASH, n_hash, sh);
     stat_add(ctr, ST_DEEP_BLOCKS, n_blk, sh);
+#ifdef EDSBWT_DEEP_CLOCKS
+    stat_add(ctr, ST_CLK_RANK, c_rank, sh);
+    stat_add(ctr, ST_CLK_RUNS, c_runs, sh);
+    stat_add(ctr, ST_CLK_REST, c_rest, sh);
+    stat_add(ctr, ST_CLK_STEPS, c_steps, sh);
+    stat_add(ctr, ST_CLK_HASH_STEPS, c_hsteps, sh);
+#endif
 }
 
 // Patterns k_deep<8> could not hold: the same walk with lists of up to KW intervals
