@@ -135,6 +135,7 @@ struct Engine {
     DBuf<uint32_t> lcnt, ck_u, ck_k, ck_e, gcnt, gfill, goff, gend, gb, gee, fv, fv2, fend, hterm;
     DBuf<uint64_t> fk, fk2, ekeys, efk;
     DBuf<uint32_t> eu, eb, ee, eck_u, eck_k, eck_e, efv, shpre;
+    DBuf<uint32_t> fu, fb, fe, fpre;  // the previous depth's item shards, read in place by k_lvl_items
     uint32_t* pinned_big = nullptr;  // host shard counters + prefix
     DBuf<unsigned long long> stats;  // kStatSlots sharded statistics counters (stat_add)
     unsigned long long* pinned_stats = nullptr;
@@ -366,7 +367,7 @@ struct Engine {
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         HIPCHK(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc((void**)&pinned_big, (kCnt + NSHARD + 8) * 4, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&pinned_big, (kCnt + 2 * (NSHARD + 8)) * 4, hipHostMallocDefault));
         HIPCHK(hipHostMalloc((void**)&pinned_stats, kStatSlots * 8, hipHostMallocDefault));
         stats.ensure(kStatSlots);
         HostIndex H;
@@ -840,12 +841,22 @@ struct Engine {
             HIPCHK(hipMemcpyAsync(iu[0].p, &h[2], 4, hipMemcpyHostToDevice, stream));
         }
         uint32_t novf = 0;
+        bool in_sharded = false;  // current items in fu/fb/fe shards (prefix fpre, capacity fcap)
+        size_t fcap = 0;
+        auto pack_items = [&](int dst) {  // shards -> iu/ib/ie[dst]
+            iu[dst].ensure(ncur); ib[dst].ensure(ncur); ie[dst].ensure(ncur);
+            if (ncur)
+                launch(KC_MERGE, k_unshard<uint32_t, uint32_t, uint32_t>, ncur, ncur, (const uint32_t*)fpre.p, (uint32_t)fcap,
+                       (const uint32_t*)fu.p, (const uint32_t*)fb.p, (const uint32_t*)fe.p, iu[dst].p, ib[dst].p, ie[dst].p);
+            in_sharded = false;
+        };
         for (uint32_t d = 0; d < Lmax; d++) {
             const uint32_t D = d + 1;
             const int nxt = cur ^ 1;
             const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
             if (allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D] && (double)ncur <= deep_items * (double)Mcur) {
+                if (in_sharded) pack_items(cur);
                 // group the unordered items by node, then finish patterns one per thread
                 gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur); goff.ensure(Mcur);
                 launch(KC_DEEP, k_zero4, 2 * (size_t)Mcur, gcnt.p, (uint64_t)Mcur, gfill.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0,
@@ -890,13 +901,15 @@ struct Engine {
                 eck_u.ensure(cap_chunks * NSHARD); eck_k.ensure(cap_chunks * NSHARD); eck_e.ensure(cap_chunks * NSHARD);
                 if (!first) zero(lcnt.p, NSHARD * 32 * 4);
                 if (d > 0)
-                    launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
-                           (const uint32_t*)ie[cur].p, (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
-                           (uint32_t)cap_chunks, stats.p);
+                    launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
+                           (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
+                           (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
+                           eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap);
                 else  // no link before the first step (:246-258)
-                    launch(KC_STEP, k_lvl_items<false>, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p,
-                           (const uint32_t*)ie[cur].p, (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p, eck_k.p, eck_e.p,
-                           (uint32_t)cap_chunks, stats.p);
+                    launch(KC_STEP, k_lvl_items<false>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
+                           (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
+                           (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
+                           eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap);
                 fetch_shards();  // sync A
                 const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
                 if (m0 <= cap_next && m1 <= cap_keys && m2 <= cap_chunks) break;
@@ -911,7 +924,7 @@ struct Engine {
                 ck_u.ensure(nchunks); ck_k.ensure(nchunks); ck_e.ensure(nchunks);
                 unshard3(2, cap_chunks, eck_u.p, eck_k.p, eck_e.p, ck_u.p, ck_k.p, ck_e.p, nchunks);
                 for (;;) {
-                    launch(KC_LINK, k_lvl_chunks, nchunks, nchunks, (const uint32_t*)ck_u.p, (const uint32_t*)ck_k.p, (const uint32_t*)ck_e.p, X,
+                    launch(KC_LINK, k_lvl_chunks, (size_t)nchunks * 64, nchunks, (const uint32_t*)ck_u.p, (const uint32_t*)ck_k.p, (const uint32_t*)ck_e.p, X,
                            lcnt.p, ekeys.p, (uint32_t)cap_keys);
                     fetch_shards();
                     const uint32_t m1 = shard_max(1);
@@ -950,8 +963,8 @@ struct Engine {
                 launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, X.segbits, rflag.p);
                 exclusive_scan(rflag.p, rscan.p, nkeys);
                 rb.ensure(nkeys); re.ensure(nkeys); ru.ensure(nkeys);
-                launch(KC_LINK, k_run_build, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
-                       (const uint32_t*)seg_lo.p, (const uint32_t*)seg_start.p, X.segbits, rb.p, re.p, ru.p, d_runs);
+                launch(KC_LINK, k_run_build_seg, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p,
+                       (const uint32_t*)rscan.p, X.segbits, rb.p, re.p, ru.p, d_runs);
                 const std::vector<uint32_t> keep_items = shard_counts(0);
                 for (;;) {
                     launch(KC_STEP, k_lvl_dollar, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
@@ -979,10 +992,24 @@ struct Engine {
             st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * sizeof(OccBlock)) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
             if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
                                     ncur, nkeys, nkeys ? hsh[NSHARD * 32] : 0u, nnext);
-            ib[nxt].ensure(nnext); ie[nxt].ensure(nnext); iu[nxt].ensure(nnext);
-            if (nnext) unshard3(0, cap_next, eu.p, eb.p, ee.p, iu[nxt].p, ib[nxt].p, ie[nxt].p, nnext);
+            // hand the item shards to the next depth as they are (k_lvl_items reads them in
+            // place); they are packed only for the finishers below or the deep cutover
+            {
+                uint32_t* pre = pinned_big + kCnt + NSHARD + 8;  // own staging: upload_prefix uses pinned_big + kCnt
+                pre[0] = 0;
+                for (uint32_t sh = 0; sh < NSHARD; sh++) pre[sh + 1] = pre[sh] + hsh[sh * 32 + 0];
+                fpre.ensure(NSHARD + 1);
+                HIPCHK(hipMemcpyAsync(fpre.p, pre, (NSHARD + 1) * 4, hipMemcpyHostToDevice, stream));
+                std::swap(fu, eu); std::swap(fb, eb); std::swap(fe, ee);
+                fcap = cap_next;
+                in_sharded = true;
+            }
             // finish patterns of length D: their node's items, sorted by row
             if (finishing) {
+                const uint32_t ncur_saved = ncur;
+                ncur = nnext;
+                pack_items(nxt);
+                ncur = ncur_saved;
                 launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
                 const size_t cap_fin = shard_bound(nnext, 1);
                 efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD);

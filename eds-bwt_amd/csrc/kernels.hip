@@ -499,6 +499,25 @@ __global__ void k_run_build(const uint64_t* __restrict__ keys, uint64_t V, const
     }
 }
 
+// order-free path: a run is kept as its first and last segment (s_first, s_last): it
+// covers the words of segments [seg_lo[s_first], s_last - 1], whose c-ranks at both
+// ends the segment table holds — no row lookups here, no occ lines in k_lvl_dollar
+__global__ void k_run_build_seg(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ flag,
+                                const uint32_t* __restrict__ rscan, uint32_t sb, uint32_t* __restrict__ rs0, uint32_t* __restrict__ rs1,
+                                uint32_t* __restrict__ rown, uint32_t* __restrict__ nruns) {
+    GRID_STRIDE(t, V) {
+        if (nruns && t + 1 == V) *nruns = rscan[t] + flag[t];
+        const uint64_t k = keys[t];
+        const uint32_t s = (uint32_t)(k & ((1ull << sb) - 1));
+        const uint32_t r = rscan[t] + flag[t] - 1;
+        if (flag[t]) {
+            rs0[r] = s;
+            rown[r] = (uint32_t)(k >> sb);
+        }
+        if (t + 1 == V || flag[t + 1]) rs1[r] = s;
+    }
+}
+
 // STEP: per child node, its parent's list [dollar ranges..., own intervals...]
 // stepped by the child's symbol (backward_search_step + updateSingleInterval,
 // :376-510; concatenation order of :300).
@@ -1011,7 +1030,15 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
                                                    uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
                                                    uint32_t cap_keys, uint32_t* __restrict__ ck_u, uint32_t* __restrict__ ck_k,
-                                                   uint32_t* __restrict__ ck_e, uint32_t cap_chunks, unsigned long long* __restrict__ stats) {
+                                                   uint32_t* __restrict__ ck_e, uint32_t cap_chunks, unsigned long long* __restrict__ stats,
+                                                   const uint32_t* __restrict__ ipre, uint32_t icap) {
+    // ipre != nullptr: the input items are still in the previous depth's NSHARD regions
+    // (region s at s*icap, ipre = their prefix sums), read in place instead of packed
+    __shared__ uint32_t spre[NSHARD + 1];
+    if (ipre) {
+        for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) spre[t] = ipre[t];
+        __syncthreads();
+    }
     const uint32_t sh = blockIdx.x % NSHARD;
     unsigned long long n_blk = 0;  // occ blocks read
     uint32_t* cnt = cnt_all + sh * 32;
@@ -1024,8 +1051,17 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
 #pragma unroll
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
         if (valid) {
-            u = iu[i];
-            LVL_STEP_LOAD(u, ib[i], ie[i] + 1)
+            size_t src = i;
+            if (ipre) {
+                uint32_t lo = 0, hi = NSHARD;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (spre[mid] <= (uint32_t)i) lo = mid; else hi = mid;
+                }
+                src = (size_t)lo * icap + ((uint32_t)i - spre[lo]);
+            }
+            u = iu[src];
+            LVL_STEP_LOAD(u, ib[src], ie[src] + 1)
         }
         // backward step of every child symbol (updateSingleInterval, :424-510)
         uint32_t emit = 0;
@@ -1081,29 +1117,30 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
     stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
 }
 
-// long '#'-row ranges: one chunk (<= 256 rows, clipped to the item's end) per thread
+// long '#'-row ranges: one wave per chunk (<= 256 rows, clipped to the item's end);
+// lanes read 4 rows each (coalesced), one atomic per wave
 __global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* __restrict__ ck_u, const uint32_t* __restrict__ ck_k,
                                                     const uint32_t* __restrict__ ck_end, KIdx X, uint32_t* __restrict__ cnt_all,
                                                     uint64_t* __restrict__ keys, uint32_t cap_keys) {
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
     keys += (size_t)sh * cap_keys;
-    UNIFORM_STRIDE(i, valid, n) {
-        uint32_t k0 = 0, k1 = 0, u = 0, nz = 0;
-        if (valid) {
-            u = ck_u[i];
-            k0 = ck_k[i];
-            k1 = ck_end[i];
-            for (uint32_t k = k0; k < k1; k++) nz += X.eof_seg[k] != 0;
+    const uint32_t lane = threadIdx.x & 63, wib = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    for (size_t w = (size_t)blockIdx.x * wpb + wib; w < n; w += (size_t)gridDim.x * wpb) {  // wave-uniform
+        const uint32_t u = ck_u[w], k0 = ck_k[w], k1 = ck_end[w];
+        uint32_t s[4], nz = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t k = k0 + lane + 64 * q;
+            s[q] = k < k1 ? X.eof_seg[k] : 0u;
+            nz += s[q] != 0;
         }
-        uint32_t kat = wave_append(cnt + 1, nz);
-        if (nz)
-            for (uint32_t k = k0; k < k1; k++) {
-                const uint32_t s = X.eof_seg[k];
-                if (s) {
-                    if (kat < cap_keys) keys[kat] = ((uint64_t)u << X.segbits) | s;
-                    kat++;
-                }
+        uint32_t at = wave_append(cnt + 1, nz);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (s[q]) {
+                if (at < cap_keys) keys[at] = ((uint64_t)u << X.segbits) | s[q];
+                at++;
             }
     }
 }
@@ -1125,7 +1162,15 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
         if (valid) {
             const uint32_t u = du[i];
-            LVL_STEP_LOAD(u, db[i], de[i] + 1)
+            const uint64_t ci = child_info[u];
+            const uint32_t* e0 = X.segtab + (size_t)db[i] * X.seg_stride;  // s_first: ranks at the run's first word
+            const uint32_t* e1 = X.segtab + (size_t)de[i] * X.seg_stride;  // s_last: ranks one past its last word
+#pragma unroll
+            for (uint32_t c = 0; c < 8; c++)
+                if (c < X.sigma) { rb[c] = e0[1 + c]; re[c] = e1[X.seg_hi + c]; }
+            n_blk += 2;
+            cf = (uint32_t)ci;
+            mask = (uint32_t)(ci >> 32);
         }
         uint32_t emit = 0;
 #pragma unroll
