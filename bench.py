@@ -61,18 +61,21 @@ def ensure_built():
         run(["make", "-s", "-j", "16", "-C", os.path.join(ROOT, "eds-bwt_amd"), "all"])
 
 
-def prepare(cfg: str, workdir: str, rank: int, world: int, npat: int, barrier):
+def prepare(cfg: str, workdir: str, rank: int, world: int, npat: int, barrier, chars_override: int = 0):
     gcfg, chars, eseed, _, lens, mode, pseed, _ = CONFIGS[cfg]
+    tag = cfg
+    if chars_override:
+        chars, tag = chars_override, f"{cfg}_{chars_override}"
     os.makedirs(workdir, exist_ok=True)
-    eds = os.path.join(workdir, f"{cfg}.eds")
-    base = os.path.join(workdir, cfg)
+    eds = os.path.join(workdir, f"{tag}.eds")
+    base = os.path.join(workdir, tag)
     if rank == 0 and not os.path.exists(base + "_info.aux"):
         t = time.time()
         run([os.path.join(BUILD, "edsbwt_gen"), "eds", "--config", gcfg, "--chars", chars, "--seed", eseed, "--out", eds])
         run([os.path.join(BUILD, "eds_transform"), eds, base, "--no-runs"])
         log(f"[bench] index {base} built in {time.time() - t:.1f}s")
     barrier()
-    pats = os.path.join(workdir, f"{cfg}_pats_{npat}_r{rank}of{world}.txt")
+    pats = os.path.join(workdir, f"{tag}_pats_{npat}_r{rank}of{world}.txt")
     if not os.path.exists(pats):
         run([os.path.join(BUILD, "edsbwt_gen"), "patterns", "--eds", eds, "--count", npat, "--lens", lens, "--mode", mode,
              "--seed", pseed * 1000003 + rank, "--out", pats])
@@ -124,6 +127,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (default: the config's)")
+    ap.add_argument("--chars", type=int, default=0, help="EDS size override (scaled-down parity/diagnostic runs)")
     ap.add_argument("--locate", default="sampled", choices=("sampled", "walk", "table"),
                     help="position recovery: LF walk to the first sampled row (default), the reference's full "
                          "walk to '#', or the per-row (word, offset) table")
@@ -159,7 +163,7 @@ def main():
     cfg = args.config
     npat = args.patterns or CONFIGS[cfg][3]
     locate = CONFIGS[cfg][7]
-    base, pats_path = prepare(cfg, args.workdir, rank, world, npat, barrier)
+    base, pats_path = prepare(cfg, args.workdir, rank, world, npat, barrier, args.chars)
 
     t = time.time()
     idx = pkg.Index(base, device=local)

@@ -313,6 +313,17 @@ struct Engine {
         }
     }
 
+    // scan.p[0..P) = exclusive prefix sum of the depth-D node-start flags, computed on the fly
+    void node_scan(uint32_t D, uint64_t P) {
+        if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+        using It = hipcub::TransformInputIterator<uint32_t, NodeFlag, hipcub::CountingInputIterator<uint32_t>>;
+        It in(hipcub::CountingInputIterator<uint32_t>(0), NodeFlag{slen.p, lcp.p, D});
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, scan.p, (int)P, stream));
+        tmp.ensure(tb);
+        timed(KC_NODES, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, scan.p, (int)P, stream)); });
+    }
+
     // out[0..n) = exclusive prefix sum of in[0..n) (no read-back)
     void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n) {
         if (!n) return;
@@ -538,8 +549,8 @@ struct Engine {
         bps = sigma + 2 <= 8 ? 3u : 4u;
         const uint32_t spc = 64 / bps;
         const uint32_t nch = (Lmax + spc - 1) / spc;
-        lhist.ensure(2 * (size_t)(Lmax + 2) + 1);
-        zero(lhist.p, (2 * (size_t)(Lmax + 2) + 1) * 8);
+        lhist.ensure(2 * (size_t)(Lmax + 2) + 3);
+        zero(lhist.p, (2 * (size_t)(Lmax + 2) + 3) * 8);
         unsigned long long* d_nterm = lhist.p + 2 * (size_t)(Lmax + 2);
         len.ensure(P);
         keys.ensure((size_t)nch * P);
@@ -551,49 +562,58 @@ struct Engine {
         perm2.ensure(P);
         kc.ensure(P);
         kc2.ensure(P);
-        launch(KC_TRIE, k_iota, P, perm.p, P);
-        // LSD over the chunks, last (least significant) first; only the bits that hold
-        // symbols are sorted (the last chunk is partly empty)
-        for (int c = (int)nch - 1; c >= 0; c--) {
-            const uint32_t nsym = std::min(spc, Lmax - (uint32_t)c * spc);
-            const int begin_bit = (int)(bps * (spc - nsym)), end_bit = (int)(bps * spc);
-            const uint64_t* kin = keys.p + (size_t)c * P;
-            if (c != (int)nch - 1) {  // the first pass sorts the chunk in place order (perm = identity)
-                launch(KC_TRIE, k_gather_key, P, kin, (const uint32_t*)perm.p, P, kc.p);
-                kin = kc.p;
-            }
-            size_t tb = 0;
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
-            tmp.ensure(tb);
-            timed(KC_TRIE, [&] {
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
-            });
-            std::swap(perm.p, perm2.p);
-            std::swap(perm.cap, perm2.cap);
-        }
-        // sorted chunks 1.. (chunk 0 is the last pass's output, kc2)
-        if (nch > 1) {
-            skey.ensure((size_t)(nch - 1) * P);
-            for (uint32_t c = 1; c < nch; c++)
-                launch(KC_TRIE, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, skey.p + (size_t)(c - 1) * P);
-        }
         slen.ensure(P);
         lcp.ensure(P);
-        if (bps == 3)
-            launch(KC_TRIE, k_slen_lcp<3>, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)kc2.p, (const uint64_t*)skey.p,
-                   nch, P, slen.p, lcp.p);
-        else
-            launch(KC_TRIE, k_slen_lcp<4>, P, (const uint32_t*)perm.p, (const uint32_t*)len.p, (const uint64_t*)kc2.p, (const uint64_t*)skey.p,
-                   nch, P, slen.p, lcp.p);
-        // ---- C. nodes per depth and patterns per length, read once
-        if (Lmax + 2 <= 1024)
-            launch_reduce(KC_TRIE, k_trie_counts, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, Lmax, lhist.p, lhist.p + (Lmax + 2));
-        else
-            launch(KC_TRIE, k_trie_counts_global, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, lhist.p, lhist.p + (Lmax + 2));
-        std::vector<unsigned long long> hv(2 * (size_t)(Lmax + 2) + 1);
-        HIPCHK(hipMemcpyAsync(hv.data(), lhist.p, hv.size() * 8, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipStreamSynchronize(stream));
-        if (n_term) *n_term = (uint32_t)hv.back();
+        if (nch > 1) skey.ensure((size_t)(nch - 1) * P);
+        unsigned long long* d_ties = d_nterm + 1;  // neighbours equal in chunk 0 only (statistic)
+        unsigned long long* d_big = d_nterm + 2;   // tie groups too large for k_fix_ties
+        std::vector<unsigned long long> hv(2 * (size_t)(Lmax + 2) + 3);
+        // Trie order.  Sort by chunk 0 (the first SPC reversed symbols) only, then order each
+        // group of equal chunk 0 by the later chunks in place (k_fix_ties: groups are small —
+        // patterns ending at the same place through different variant words, or duplicates).
+        // Only when a group is too large does the full LSD sort over every chunk run.
+        // Only the bits that hold symbols are sorted.
+        auto order = [&](bool full) {
+            launch(KC_TRIE, k_iota, P, perm.p, P);
+            for (int c = full ? (int)nch - 1 : 0; c >= 0; c--) {
+                const uint32_t nsym = std::min(spc, Lmax - (uint32_t)c * spc);
+                const int begin_bit = (int)(bps * (spc - nsym)), end_bit = (int)(bps * spc);
+                const uint64_t* kin = keys.p + (size_t)c * P;
+                if (full && c != (int)nch - 1) {  // later passes sort the chunk in the current order
+                    launch(KC_TRIE, k_gather_key, P, kin, (const uint32_t*)perm.p, P, kc.p);
+                    kin = kc.p;
+                }
+                size_t tb = 0;
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
+                tmp.ensure(tb);
+                timed(KC_TRIE, [&] {
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
+                });
+                std::swap(perm.p, perm2.p);
+                std::swap(perm.cap, perm2.cap);
+            }
+            // sorted chunks 1.. (chunk 0 is the last pass's output, kc2)
+            for (uint32_t c = 1; c < nch; c++)
+                launch(KC_TRIE, k_gather_key, P, (const uint64_t*)(keys.p + (size_t)c * P), (const uint32_t*)perm.p, P, skey.p + (size_t)(c - 1) * P);
+            if (!full && nch > 1) launch(KC_TRIE, k_fix_ties, P, (const uint64_t*)kc2.p, skey.p, nch, P, perm.p, d_big);
+            if (bps == 3)
+                launch(KC_TRIE, k_slen_lcp<3>, P, (const uint64_t*)kc2.p, (const uint64_t*)skey.p, nch, P, slen.p, lcp.p, d_ties);
+            else
+                launch(KC_TRIE, k_slen_lcp<4>, P, (const uint64_t*)kc2.p, (const uint64_t*)skey.p, nch, P, slen.p, lcp.p, d_ties);
+            // ---- C. nodes per depth and patterns per length, read once (with the '#' count and ties)
+            if (Lmax + 2 <= 1024)
+                launch_reduce(KC_TRIE, k_trie_counts, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, Lmax, lhist.p, lhist.p + (Lmax + 2));
+            else
+                launch(KC_TRIE, k_trie_counts_global, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, lhist.p, lhist.p + (Lmax + 2));
+            HIPCHK(hipMemcpyAsync(hv.data(), lhist.p, hv.size() * 8, hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+        };
+        order(false);
+        if (hv[2 * (size_t)(Lmax + 2) + 2]) {  // a tie group too large to fix in place: sort every chunk
+            zero(lhist.p, 2 * (size_t)(Lmax + 2) * 8);
+            order(true);
+        }
+        if (n_term) *n_term = (uint32_t)hv[2 * (size_t)(Lmax + 2)];
         hist.assign(hv.begin() + (Lmax + 2), hv.begin() + (Lmax + 2) + (Lmax + 1));
         nodes_at.assign(Lmax + 2, 0);
         int64_t run = 0;
@@ -653,7 +673,7 @@ struct Engine {
             node_first.ensure(M);
             node_parent.ensure(M);
             node_char.ensure(M);
-            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
+            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)lcp.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             child_first.ensure(Mcur);
             child_end.ensure(Mcur);
@@ -882,9 +902,8 @@ struct Engine {
                 launch(KC_NODES, k_zero4, 3 * (size_t)M, node_occ.p, (uint64_t)M, foff.p, (uint64_t)M, fend.p, (uint64_t)M, (uint32_t*)nullptr,
                        (uint64_t)0);
             // children nodes at depth D (node count known from build_trie: no read-back)
-            launch(KC_NODES, k_node_flags, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, D, flag.p);
-            exclusive_scan(flag.p, scan.p, P);
-            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)flag.p,
+            node_scan(D, P);
+            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)lcp.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
             launch(KC_NODES, k_child_info, M, M, (const uint32_t*)node_parent.p, (const uint8_t*)node_char.p, child_info.p);
             // fused step + '#'-row emission over the current items (sharded appends)

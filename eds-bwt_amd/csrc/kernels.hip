@@ -338,26 +338,79 @@ __global__ void k_gather_key(const uint64_t* __restrict__ keys_c, const uint32_t
     GRID_STRIDE(i, P) out[i] = keys_c[perm[i]];
 }
 
-// sorted order: slen[i] = len[perm[i]]; lcp[i] = common reversed prefix (= common
-// suffix) of sorted neighbours i-1, i, from the sorted key chunks (chunk 0 in k0,
-// chunks 1.. in krest[(c-1)*P + i]) — neighbours are adjacent, so reads coalesce
+// Sorted order, from the sorted key chunks alone (chunk 0 in k0, chunks 1.. in
+// krest[(c-1)*P + i]; neighbours are adjacent, so every read coalesces):
+//   slen[i] = pattern length (its codes are nonzero up to the end of the pattern);
+//   lcp[i]  = common reversed prefix (= common suffix) of neighbours i-1, i;
+//   *ties  += neighbours equal in chunk 0 but not later (the order is then not a trie order)
 template <int BPS>
-__global__ void k_slen_lcp(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len, const uint64_t* __restrict__ k0,
-                           const uint64_t* __restrict__ krest, uint32_t nch, uint64_t P, uint32_t* __restrict__ slen, uint32_t* __restrict__ lcp) {
+__device__ __forceinline__ uint32_t key_len(const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t nch, uint64_t P,
+                                            size_t i) {
+    constexpr uint32_t SPC = 64 / BPS;
+    for (int c = (int)nch - 1; c >= 0; c--) {
+        const uint64_t k = c == 0 ? k0[i] : krest[(size_t)(c - 1) * P + i];
+        if (k) return (uint32_t)c * SPC + SPC - (uint32_t)__builtin_ctzll(k) / BPS;
+    }
+    return 0;
+}
+
+template <int BPS>
+__global__ void __launch_bounds__(256) k_slen_lcp(const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t nch, uint64_t P,
+                                                  uint32_t* __restrict__ slen, uint32_t* __restrict__ lcp, unsigned long long* __restrict__ ties) {
     constexpr uint32_t SPC = 64 / BPS, LEAD = 64 - SPC * BPS;
+    __shared__ unsigned long long sh[4];
+    unsigned long long nt = 0;
     GRID_STRIDE(i, P) {
-        const uint32_t la = len[perm[i]];
+        const uint32_t la = key_len<BPS>(k0, krest, nch, P, i);
         slen[i] = la;
         if (i == 0) { lcp[0] = 0; continue; }
-        const uint32_t lb = len[perm[i - 1]];
+        const uint32_t lb = key_len<BPS>(k0, krest, nch, P, i - 1);
         uint32_t l = SPC * nch;
         for (uint32_t c = 0; c < nch; c++) {
             const uint64_t x = c == 0 ? (k0[i] ^ k0[i - 1]) : (krest[(size_t)(c - 1) * P + i] ^ krest[(size_t)(c - 1) * P + i - 1]);
-            if (x) { l = c * SPC + ((uint32_t)__clzll(x) - LEAD) / BPS; break; }
+            if (x) {
+                l = c * SPC + ((uint32_t)__clzll(x) - LEAD) / BPS;
+                nt += c > 0;
+                break;
+            }
         }
         l = l < la ? l : la;
         l = l < lb ? l : lb;
         lcp[i] = l;
+    }
+    nt = block_sum(nt, sh);
+    if (threadIdx.x == 0 && nt) atomicAdd(ties, nt);
+}
+
+// After the chunk-0 sort: order each tie group (run of equal chunk 0) by the later chunks,
+// one thread per group, insertion sort (linear on groups of identical patterns).  Groups
+// over kTieMax members are left alone and counted: the caller then runs the full sort.
+constexpr uint32_t kTieMax = 256;
+__global__ void __launch_bounds__(256) k_fix_ties(const uint64_t* __restrict__ k0, uint64_t* __restrict__ krest, uint32_t nch, uint64_t P,
+                                                  uint32_t* __restrict__ perm, unsigned long long* __restrict__ big) {
+    GRID_STRIDE(i, P) {
+        if (i + 1 >= P || k0[i] != k0[i + 1] || (i > 0 && k0[i - 1] == k0[i])) continue;
+        size_t j = i + 1;
+        while (j < P && k0[j] == k0[i] && j - i <= kTieMax) j++;
+        if (j - i > kTieMax) { atomicAdd(big, 1ull); continue; }
+        auto less = [&](size_t a, size_t b) {  // chunk-wise (later chunks) a < b
+            for (uint32_t c = 1; c < nch; c++) {
+                const uint64_t x = krest[(size_t)(c - 1) * P + a], y = krest[(size_t)(c - 1) * P + b];
+                if (x != y) return x < y;
+            }
+            return false;
+        };
+        for (size_t a = i + 1; a < j; a++) {
+            size_t b = a;
+            while (b > i && less(b, b - 1)) {  // bubble a down to its place
+                const uint32_t tp = perm[b]; perm[b] = perm[b - 1]; perm[b - 1] = tp;
+                for (uint32_t c = 1; c < nch; c++) {
+                    uint64_t* r = krest + (size_t)(c - 1) * P;
+                    const uint64_t t = r[b]; r[b] = r[b - 1]; r[b - 1] = t;
+                }
+                b--;
+            }
+        }
     }
 }
 
@@ -382,18 +435,27 @@ __global__ void k_node_flags(const uint32_t* __restrict__ slen, const uint32_t* 
 
 // nscan = exclusive scan of flags (P+1 entries); skey = the sorted patterns'
 // reversed-code chunk holding depth D (BPS bits per symbol, most significant first)
+// node-start flag of pattern i at depth D (scanned on the fly by the host's transform scan)
+struct NodeFlag {
+    const uint32_t* slen;
+    const uint32_t* lcp;
+    uint32_t D;
+    __host__ __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return (slen[i] >= D && lcp[i] < D) ? 1u : 0u; }
+};
+
 template <int BPS>
 __global__ void k_node_build(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint64_t* __restrict__ skey, uint32_t sigma,
-                             const uint32_t* __restrict__ flag, const uint32_t* __restrict__ nscan,
+                             const uint32_t* __restrict__ lcp, const uint32_t* __restrict__ nscan,
                              const uint32_t* __restrict__ nid_prev, uint32_t* __restrict__ nid_cur,
                              uint32_t* __restrict__ node_first, uint32_t* __restrict__ node_parent, uint8_t* __restrict__ node_char) {
     constexpr uint32_t SPC = 64 / BPS;
     const uint32_t sh = BPS * (SPC - 1 - ((D - 1) % SPC));
     GRID_STRIDE(i, P) {
         if (slen[i] < D) { nid_cur[i] = 0xFFFFFFFFu; continue; }
-        const uint32_t id = nscan[i] + flag[i] - 1;
+        const uint32_t f = lcp[i] < D;
+        const uint32_t id = nscan[i] + f - 1;
         nid_cur[i] = id;
-        if (flag[i]) {
+        if (f) {
             node_first[id] = (uint32_t)i;
             node_parent[id] = nid_prev[i];
             const uint32_t v = (uint32_t)(skey[i] >> sh) & ((1u << BPS) - 1u);

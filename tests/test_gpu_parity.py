@@ -112,7 +112,16 @@ def test_long_patterns_gpu(oracle, edsbwt, tmp_path, alphabet):
     pats = [edsgen.planted(rng, segs, rng.choice([15, 16, 17, 21, 22, 33, 48, 64, 70])) or "ACGT" for _ in range(1500)]
     pats += [edsgen.planted(rng, segs, rng.randint(100, 200)) or "A" * 150 for _ in range(300)]
     pats += ["".join(rng.choice(alphabet) for _ in range(rng.randint(1, 90))) for _ in range(1500)]
+    # suffixes shared beyond one key chunk (21 / 16 symbols) with different heads: the
+    # chunk-0 sort sees ties and the full multi-chunk sort must run
+    for _ in range(30):
+        tail = edsgen.planted(rng, segs, 26) or "ACGT" * 7
+        pats += ["".join(rng.choice(alphabet) for _ in range(rng.randint(1, 12))) + tail for _ in range(5)]
     _compare(oracle, edsbwt, base, pats, table_too=False)
+    # one tie group larger than k_fix_ties takes (kTieMax = 256): the full sort runs
+    tail = edsgen.planted(rng, segs, 26) or "ACGT" * 7
+    big = ["".join(rng.choice(alphabet) for _ in range(rng.randint(3, 10))) + tail for _ in range(400)]
+    _compare(oracle, edsbwt, base, pats[:500] + big, table_too=False)
 
 
 def test_c5_style_gpu(oracle, edsbwt, tmp_path):
