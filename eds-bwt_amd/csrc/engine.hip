@@ -324,6 +324,13 @@ struct Engine {
         timed(KC_NODES, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, scan.p, (int)P, stream)); });
     }
 
+    void sort_link_keys(const uint64_t* in, uint64_t* out, size_t n, int end_bit) {
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, in, out, (int)n, 0, end_bit, stream));
+        tmp.ensure(tb);
+        timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, in, out, (int)n, 0, end_bit, stream)); });
+    }
+
     // out[0..n) = exclusive prefix sum of in[0..n) (no read-back)
     void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n) {
         if (!n) return;
@@ -973,10 +980,7 @@ struct Engine {
                 lkeys2.ensure(nkeys);
                 unshard1(1, cap_keys, ekeys.p, lkeys.p, nkeys);
                 const int endbit = (int)std::min<uint32_t>(64, X.segbits + bits_for(Mcur));
-                size_t tb = 0;
-                HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream));
-                tmp.ensure(tb);
-                timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)nkeys, 0, endbit, stream)); });
+                sort_link_keys(lkeys.p, lkeys2.p, nkeys, endbit);
                 rflag.ensure(nkeys);
                 rscan.ensure(nkeys);
                 launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, X.segbits, rflag.p);
