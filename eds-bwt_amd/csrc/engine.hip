@@ -136,6 +136,8 @@ struct Engine {
     DBuf<uint64_t> fk, fk2, ekeys, efk;
     DBuf<uint32_t> eu, eb, ee, eck_u, eck_k, eck_e, efv, shpre;
     DBuf<uint32_t> fu, fb, fe, fpre;  // the previous depth's item shards, read in place by k_lvl_items
+    DBuf<uint4> dq;                   // k_deep_fast -> k_deep queue (pattern, depth, b, e), sharded
+    DBuf<uint32_t> dqpre;
     uint32_t* pinned_big = nullptr;  // host shard counters + prefix
     DBuf<unsigned long long> stats;  // kStatSlots sharded statistics counters (stat_add)
     unsigned long long* pinned_stats = nullptr;
@@ -803,8 +805,19 @@ struct Engine {
         const uint32_t K = deep_k;
         ab.grow_keep(abase + (uint64_t)P * K, stream);
         ae.grow_keep(abase + (uint64_t)P * K, stream);
-        launch(KC_DEEP, K == 4 ? k_deep<4> : k_deep<kDeepK>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, (const uint32_t*)len.p,
-               d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
+        // single-interval walks first; patterns needing lists or links are queued for k_deep
+        const size_t qcap = std::max<size_t>(shard_bound(P, 1), 1024);
+        dq.ensure(qcap * NSHARD);
+        dqpre.ensure(NSHARD + 1);
+        lcnt.ensure(NSHARD * 32 + 32);
+        zero(lcnt.p, NSHARD * 32 * 4);
+        launch(KC_DEEP, k_deep_fast, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, d_off, d_bytes, (const uint8_t*)code_of.p, nid_d,
+               goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p);
+        hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
+        HIPCHK(hipGetLastError());
+        launch(KC_DEEP, K == 4 ? k_deep<4> : k_deep<kDeepK>, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d,
+               (const uint32_t*)slen.p, (const uint32_t*)perm.p, d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase,
+               ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace) std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu\n", D, M, (unsigned long long)active);

@@ -256,6 +256,57 @@ __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats,
     if (threadIdx.x == 0 && v) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + k, v);
 }
 
+// ------------------------------------------------------ sharded appends
+// Appends are wave-aggregated: one atomic per wave per buffer.  Call with every
+// lane of the wave active.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* __restrict__ counter, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(counter, total);
+    base = __shfl(base, 63, 64);
+    return base + x - n;
+}
+
+// three appends (counters cnt[0..2] of one shard line) with one atomic round trip
+__device__ __forceinline__ void wave_append3(uint32_t* __restrict__ cnt, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t& a0, uint32_t& a1,
+                                             uint32_t& a2) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = n0, y = n1, z = n2;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t px = __shfl_up(x, o, 64), py = __shfl_up(y, o, 64), pz = __shfl_up(z, o, 64);
+        if (lane >= o) { x += px; y += py; z += pz; }
+    }
+    uint32_t b0 = 0, b1 = 0, b2 = 0;
+    if (lane == 63) {
+        if (x) b0 = atomicAdd(cnt + 0, x);
+        if (y) b1 = atomicAdd(cnt + 1, y);
+        if (z) b2 = atomicAdd(cnt + 2, z);
+    }
+    a0 = __shfl(b0, 63, 64) + x - n0;
+    a1 = __shfl(b1, 63, 64) + y - n1;
+    a2 = __shfl(b2, 63, 64) + z - n2;
+}
+
+// Appends go to NSHARD independent regions (counter k of shard s at cnt[s*32+k],
+// one 128-B line per shard) so that no single address takes every wave's atomic;
+// k_unshard packs the regions afterwards.
+constexpr uint32_t NSHARD = 64;
+
+// grid-stride loop whose trip count is uniform across each block (so wave-wide
+// shuffles inside it see every lane); `valid` marks the lanes past the end
+#define UNIFORM_STRIDE(i, valid, n)                                                                                     \
+    for (size_t i##_b = (size_t)blockIdx.x * blockDim.x; i##_b < (size_t)(n); i##_b += (size_t)gridDim.x * blockDim.x) \
+        if (const size_t i = i##_b + threadIdx.x; true)                                                                  \
+            if (const bool valid = i < (size_t)(n); true)
+
 template <typename T>
 __device__ __forceinline__ size_t upper_bound_dev(const T* __restrict__ a, size_t n, T key) {
     size_t lo = 0, hi = n;
@@ -673,9 +724,88 @@ __global__ void k_merge_build(uint64_t n, const uint32_t* __restrict__ flag, con
 // runs with the interval lists in registers (at most K each).  A pattern whose
 // lists outgrow K, or whose link reads more than K '#' rows at once, is flagged and
 // re-run by the level-synchronous path, which has no size limit.
+// Deep stage, two kernels.  k_deep_fast walks every pattern whose list is one interval
+// with two registers, as long as no step meets '#' rows (no link); a pattern that needs
+// a list or a link is queued as (pattern, depth, b, e) — b = ~0u: "from its node's
+// items" — and k_deep finishes the queued ones with register lists.  The queue is
+// sharded like the item appends (region s at s*qcap, counter s at qcnt[s*32]).
+__global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
+                                                   const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                                                   const uint8_t* __restrict__ code_of, const uint32_t* __restrict__ nid,
+                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
+                                                   const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
+                                                   uint32_t K, uint32_t* __restrict__ ab, uint32_t* __restrict__ ae,
+                                                   uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
+                                                   uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
+                                                   unsigned long long* __restrict__ ctr) {
+    unsigned long long n_steps = 0, n_blk = 0;
+    __shared__ uint8_t scode[256];
+    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) scode[t] = code_of[t];
+    __syncthreads();
+    const uint32_t sh = blockIdx.x % NSHARD;
+    q += (size_t)sh * qcap;
+    UNIFORM_STRIDE(i, valid, P) {
+        uint32_t want = 0;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        const uint32_t L = valid ? slen[i] : 0u;
+        const uint32_t u = L > D0 ? nid[i] : 0u;
+        const uint32_t n0 = L > D0 ? iend[u] - ioff[u] : 0u;
+        if (n0 > 1) {
+            want = 1;
+            w = make_uint4((uint32_t)i, D0, ~0u, 0u);
+        } else if (n0 == 1) {
+            uint32_t b = ib[ioff[u]], e = ie[ioff[u]];
+            const uint8_t* pat = bytes + off[perm[i]];
+            uint32_t nbyte = pat[L - 1 - D0];
+            bool alive = true;
+            uint32_t d = D0;
+            for (; d < L; d++) {
+                const uint32_t c = scode[nbyte];
+                if (d + 1 < L) nbyte = pat[L - 2 - d];
+                if (c >= X.sigma) { alive = false; break; }
+                uint32_t h0, h1, sb, se;
+                n_blk += 2 - rank2_pair(X.occ, b, e + 1, c, h0, sb, h1, se);
+                if (h1 > h0) { want = 1; break; }  // '#' rows: the link needs k_deep
+                n_steps++;
+                if (se <= sb) { alive = false; break; }
+                b = X.C[c] + sb;
+                e = X.C[c] + se - 1;
+            }
+            if (want) {
+                w = make_uint4((uint32_t)i, d, b, e);
+            } else {
+                const uint32_t o = perm[i];
+                const uint64_t at = abase + (uint64_t)i * K;
+                if (alive) {
+                    ab[at] = b;
+                    ae[at] = e;
+                }
+                res_off[o] = at;
+                res_cnt[o] = alive ? 1u : 0u;
+                res_occ[o] = alive ? e - b + 1 : 0u;
+            }
+        }
+        const uint32_t at = wave_append(qcnt + sh * 32, want);
+        if (want && at < qcap) q[at] = w;
+    }
+    __shared__ unsigned long long ssum[4];
+    stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
+    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
+}
+
+// shard prefix sums of k_deep_fast's queue counters (one block)
+__global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __restrict__ qpre) {
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (uint32_t t = 0; t < NSHARD; t++) { qpre[t] = s; s += qcnt[t * 32]; }
+        qpre[NSHARD] = s;
+    }
+}
+
 template <int K>
-__global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
-                                              const uint32_t* __restrict__ len, const uint64_t* __restrict__ off,
+__global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
+                                              const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
+                                              const uint64_t* __restrict__ off,
                                               const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of,
                                               const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
                                               const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
@@ -688,28 +818,44 @@ __global__ void __launch_bounds__(256) k_deep(uint64_t P, uint32_t D0, const uin
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
     __shared__ uint8_t scode[256];
+    __shared__ uint32_t spre[NSHARD + 1];
     for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) scode[t] = code_of[t];
+    for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) spre[t] = qpre[t];
     __syncthreads();
-    GRID_STRIDE(i, P) {
+    const uint32_t total = spre[NSHARD];
+    GRID_STRIDE(j, total) {
+        uint32_t lo = 0, hi = NSHARD;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (spre[mid] <= (uint32_t)j) lo = mid; else hi = mid;
+        }
+        const uint4 w = q[(size_t)lo * qcap + ((uint32_t)j - spre[lo])];
+        const uint32_t i = w.x, d0 = w.y;
         const uint32_t L = slen[i];
-        if (L <= D0) continue;
-        const uint32_t u = nid[i];
-        const uint32_t n0 = iend[u] - ioff[u];
-        if (n0 == 0) continue;  // dead suffix: count 0
-        if (n0 > K) { ovf[i] = 1; continue; }
         uint32_t cb[K], ce[K];
-        uint32_t cn = n0;
+        uint32_t cn;
+        if (w.z == ~0u) {  // from the node's items at the cutover depth
+            const uint32_t u = nid[i];
+            cn = iend[u] - ioff[u];
+            if (cn > K) { ovf[i] = 1; continue; }
 #pragma unroll
-        for (int t = 0; t < K; t++) {
-            cb[t] = (uint32_t)t < cn ? ib[ioff[u] + t] : 0u;
-            ce[t] = (uint32_t)t < cn ? ie[ioff[u] + t] : 0u;
+            for (int t = 0; t < K; t++) {
+                cb[t] = (uint32_t)t < cn ? ib[ioff[u] + t] : 0u;
+                ce[t] = (uint32_t)t < cn ? ie[ioff[u] + t] : 0u;
+            }
+        } else {
+            cn = 1;
+#pragma unroll
+            for (int t = 0; t < K; t++) cb[t] = ce[t] = 0;
+            cb[0] = w.z;
+            ce[0] = w.w;
         }
         const uint32_t a = perm[i];
         const uint8_t* pat = bytes + off[a];
         bool over = false;
         // the next character's byte is read one step ahead, so no step waits for it
-        uint32_t nbyte = pat[L - 1 - D0];
-        for (uint32_t d = D0; d < L && cn; d++) {
+        uint32_t nbyte = pat[L - 1 - d0];
+        for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
             const uint32_t code = scode[nbyte];
             if (d + 1 < L) nbyte = pat[L - 2 - d];
@@ -992,55 +1138,6 @@ __global__ void k_sub_scatter(uint64_t n, const uint32_t* __restrict__ map, cons
 // (LF_c is monotone on each pile and the reference's lists are ascending and
 // disjoint for patterns without '#'), so every level is one fused pass that reads
 // each item's two occ-block lines and appends only the non-empty children.
-// Appends are wave-aggregated: one atomic per wave per buffer.  Call with every
-// lane of the wave active.
-__device__ __forceinline__ uint32_t wave_append(uint32_t* __restrict__ counter, uint32_t n) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    const uint32_t total = __shfl(x, 63, 64);
-    uint32_t base = 0;
-    if (lane == 63 && total) base = atomicAdd(counter, total);
-    base = __shfl(base, 63, 64);
-    return base + x - n;
-}
-
-// three appends (counters cnt[0..2] of one shard line) with one atomic round trip
-__device__ __forceinline__ void wave_append3(uint32_t* __restrict__ cnt, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t& a0, uint32_t& a1,
-                                             uint32_t& a2) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = n0, y = n1, z = n2;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t px = __shfl_up(x, o, 64), py = __shfl_up(y, o, 64), pz = __shfl_up(z, o, 64);
-        if (lane >= o) { x += px; y += py; z += pz; }
-    }
-    uint32_t b0 = 0, b1 = 0, b2 = 0;
-    if (lane == 63) {
-        if (x) b0 = atomicAdd(cnt + 0, x);
-        if (y) b1 = atomicAdd(cnt + 1, y);
-        if (z) b2 = atomicAdd(cnt + 2, z);
-    }
-    a0 = __shfl(b0, 63, 64) + x - n0;
-    a1 = __shfl(b1, 63, 64) + y - n1;
-    a2 = __shfl(b2, 63, 64) + z - n2;
-}
-
-// Appends go to NSHARD independent regions (counter k of shard s at cnt[s*32+k],
-// one 128-B line per shard) so that no single address takes every wave's atomic;
-// k_unshard packs the regions afterwards.
-constexpr uint32_t NSHARD = 64;
-
-// grid-stride loop whose trip count is uniform across each block (so wave-wide
-// shuffles inside it see every lane); `valid` marks the lanes past the end
-#define UNIFORM_STRIDE(i, valid, n)                                                                                     \
-    for (size_t i##_b = (size_t)blockIdx.x * blockDim.x; i##_b < (size_t)(n); i##_b += (size_t)gridDim.x * blockDim.x) \
-        if (const size_t i = i##_b + threadIdx.x; true)                                                                  \
-            if (const bool valid = i < (size_t)(n); true)
 
 // Children of node u, packed by k_child_info: child_info[u] = first child | symbol
 // mask << 32.  Children are in trie order (ascending symbol code, a child for bytes
