@@ -61,7 +61,8 @@ class _Stats(ctypes.Structure):
                 ("ms_kernel", ctypes.c_double * 16), ("launches_kernel", ctypes.c_uint64 * 16),
                 ("bytes_kernel", ctypes.c_uint64 * 16),
                 ("lines_kernel", ctypes.c_uint64 * 16),
-                ("locate_offsets", ctypes.c_uint64)]
+                ("locate_offsets", ctypes.c_uint64),
+                ("search_groups", ctypes.c_uint64)]
 
 
 _LIB = None

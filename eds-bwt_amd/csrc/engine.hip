@@ -36,6 +36,10 @@ struct Fail : std::runtime_error {
     int code;
     Fail(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
+// a depth of the batch outgrew 32-bit counts: search() retries it in trie-subtree groups
+struct TooBig : Fail {
+    explicit TooBig(const std::string& m) : Fail(EDSBWT_E_UNSUPPORTED, m) {}
+};
 
 #define HIPCHK(x)                                                                                 \
     do {                                                                                          \
@@ -136,6 +140,10 @@ struct Engine {
     DBuf<uint64_t> fk, fk2, ekeys, efk;
     DBuf<uint32_t> eu, eb, ee, eck_u, eck_k, eck_e, efv, shpre;
     DBuf<uint32_t> fu, fb, fe, fpre;  // the previous depth's item shards, read in place by k_lvl_items
+    // run_grouped: group of each pattern, its members as a sub-batch
+    DBuf<uint32_t> glen, gid, gflag, gscan, g_map, g_rcnt, g_rocc;
+    DBuf<uint64_t> g_len, g_off, g_roff;
+    DBuf<uint8_t> g_bytes;
     DBuf<uint4> dq;                   // k_deep_fast -> k_deep queue (pattern, depth, b, e), sharded
     DBuf<uint32_t> dqpre;
     uint32_t* pinned_big = nullptr;  // host shard counters + prefix
@@ -159,6 +167,7 @@ struct Engine {
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
     uint32_t deep_k = env_double("EDSBWT_DEEP_K", kDeepK) == 4 ? 4u : (uint32_t)kDeepK;  // register list length of k_deep
+    uint32_t force_groups = (uint32_t)env_double("EDSBWT_FORCE_GROUPS", 0);  // tests: always search in trie-subtree groups
     static double env_double(const char* name, double dflt) {
         const char* v = std::getenv(name);
         return v && *v ? std::atof(v) : dflt;
@@ -278,7 +287,7 @@ struct Engine {
     uint32_t shard_total(int k) const {
         uint64_t t = 0;
         for (uint32_t sh = 0; sh < NSHARD; sh++) t += hsh[sh * 32 + k];
-        if (t > 0xffffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^32 items at one depth");
+        if (t > 0xffffffffull) throw TooBig("more than 2^32 items at one depth");
         return (uint32_t)t;
     }
     void upload_prefix(int k) {
@@ -317,7 +326,7 @@ struct Engine {
 
     // scan.p[0..P) = exclusive prefix sum of the depth-D node-start flags, computed on the fly
     void node_scan(uint32_t D, uint64_t P) {
-        if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+        if (P > 0x7fffffffull) throw TooBig("scan over >2^31 items");
         using It = hipcub::TransformInputIterator<uint32_t, NodeFlag, hipcub::CountingInputIterator<uint32_t>>;
         It in(hipcub::CountingInputIterator<uint32_t>(0), NodeFlag{slen.p, lcp.p, D});
         size_t tb = 0;
@@ -336,7 +345,7 @@ struct Engine {
     // out[0..n) = exclusive prefix sum of in[0..n) (no read-back)
     void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n) {
         if (!n) return;
-        if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+        if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
         size_t tb = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, stream));
         tmp.ensure(tb);
@@ -348,7 +357,7 @@ struct Engine {
         out.ensure(n + 1);
         zero(out.p, 8);
         if (!n) return;
-        if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+        if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
         size_t tb = 0;
         HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
         tmp.ensure(tb);
@@ -360,7 +369,7 @@ struct Engine {
         out.ensure(n + 1);
         zero(out.p, 4);
         if (n) {
-            if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+            if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
             size_t tb = 0;
             HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
             tmp.ensure(tb);
@@ -372,7 +381,7 @@ struct Engine {
         out.ensure(n + 1);
         zero(out.p, 8);
         if (n) {
-            if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "scan over >2^31 items");
+            if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
             size_t tb = 0;
             HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
             tmp.ensure(tb);
@@ -1079,6 +1088,72 @@ struct Engine {
         return novf;
     }
 
+    // One batch: the trie walk (order-free unless patterns hold '#'), then the patterns
+    // k_deep could not hold re-run through the unbounded level path.
+    void run_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, uint64_t* r_off,
+                   uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase) {
+        uint32_t novf = 0;
+        if (!ordered) {
+            novf = levels2(d_bytes, d_off, P, allow_deep, r_off, r_cnt, r_occ, abase, ovf_orig.p);
+            if (novf == kNeedOrdered) ordered = true;
+        }
+        if (ordered) novf = levels(d_bytes, d_off, P, allow_deep, r_off, r_cnt, r_occ, abase, ovf_orig.p);
+        if (!novf) return;
+        // patterns k_deep could not hold: gather them and run the unbounded level path
+        const uint32_t n = scan_u32(ovf_orig.p, ovf_scan, P);
+        sub_map.ensure(n);
+        sub_len.ensure(n + 1);
+        launch(KC_DEEP, k_sub_build, P, P, (const uint32_t*)ovf_orig.p, (const uint32_t*)ovf_scan.p, (const uint32_t*)len.p, sub_map.p, sub_len.p);
+        const uint64_t nbytes = scan_u64(sub_len.p, sub_off, n);
+        sub_bytes.ensure(nbytes + 1);
+        launch(KC_DEEP, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)sub_map.p, d_off, (const uint64_t*)sub_off.p, d_bytes, sub_bytes.p);
+        sub_roff.ensure(n);
+        sub_rcnt.ensure(n);
+        sub_rocc.ensure(n);
+        zero(sub_rcnt.p, (size_t)n * 4);
+        zero(sub_rocc.p, (size_t)n * 4);
+        if (ordered) levels(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
+        else levels2(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
+        launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const uint64_t*)sub_roff.p, (const uint32_t*)sub_rcnt.p,
+               (const uint32_t*)sub_rocc.p, r_off, r_cnt, r_occ);
+    }
+
+    // The batch as separate trie subtrees: patterns grouped by their last k characters
+    // (the first k levels of the reversed-pattern trie), each group one run_batch, so a
+    // depth's items split over the groups.  Results land in res_* as for one batch.
+    void run_grouped(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, uint32_t k, uint64_t& abase) {
+        abase = 0;
+        zero(res_cnt.p, P * 4);
+        zero(res_occ.p, P * 4);
+        glen.ensure(P);
+        gid.ensure(P);
+        gflag.ensure(P);
+        launch(KC_TRIE, k_lens, P, d_off, P, glen.p);
+        launch(KC_TRIE, k_pattern_group, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, k, gid.p);
+        uint32_t G = 1;
+        for (uint32_t t = 0; t < k; t++) G *= sigma + 2;
+        for (uint32_t g = 0; g < G; g++) {
+            launch(KC_TRIE, k_eq_flag, P, (const uint32_t*)gid.p, P, g, gflag.p);
+            const uint32_t n = scan_u32(gflag.p, gscan, P);
+            if (!n) continue;
+            g_map.ensure(n);
+            g_len.ensure(n + 1);
+            launch(KC_TRIE, k_sub_build, P, P, (const uint32_t*)gflag.p, (const uint32_t*)gscan.p, (const uint32_t*)glen.p, g_map.p, g_len.p);
+            const uint64_t nbytes = scan_u64(g_len.p, g_off, n);
+            g_bytes.ensure(nbytes + 1);
+            launch(KC_TRIE, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)g_map.p, d_off, (const uint64_t*)g_off.p, d_bytes, g_bytes.p);
+            g_roff.ensure(n);
+            g_rcnt.ensure(n);
+            g_rocc.ensure(n);
+            zero(g_rcnt.p, (size_t)n * 4);
+            zero(g_rocc.p, (size_t)n * 4);
+            run_batch(g_bytes.p, g_off.p, n, allow_deep, ordered, g_roff.p, g_rcnt.p, g_rocc.p, abase);
+            launch(KC_TRIE, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)g_map.p, (const uint64_t*)g_roff.p, (const uint32_t*)g_rcnt.p,
+                   (const uint32_t*)g_rocc.p, res_off.p, res_cnt.p, res_occ.p);
+        }
+        st.search_groups = G;
+    }
+
     // d_bytes/d_off/d_counts are device pointers; returns number of records
     uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
         st = edsbwt_stats{};
@@ -1106,31 +1181,21 @@ struct Engine {
         ovf_orig.ensure(P);
         uint64_t abase = 0;
         // patterns holding '#' make the reference's lists overlap: they take the ordered path
-        bool ordered = (flags & EDSBWT_ORDERED) != 0;
-        uint32_t novf = 0;
-        if (!ordered) {
-            novf = levels2(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
-            if (novf == kNeedOrdered) ordered = true;
-        }
-        if (ordered) novf = levels(d_bytes, d_off, P, allow_deep, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
-        if (novf) {
-            // patterns k_deep could not hold: gather them and run the unbounded level path
-            const uint32_t n = scan_u32(ovf_orig.p, ovf_scan, P);
-            sub_map.ensure(n);
-            sub_len.ensure(n + 1);
-            launch(KC_DEEP, k_sub_build, P, P, (const uint32_t*)ovf_orig.p, (const uint32_t*)ovf_scan.p, (const uint32_t*)len.p, sub_map.p, sub_len.p);
-            const uint64_t nbytes = scan_u64(sub_len.p, sub_off, n);
-            sub_bytes.ensure(nbytes + 1);
-            launch(KC_DEEP, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)sub_map.p, d_off, (const uint64_t*)sub_off.p, d_bytes, sub_bytes.p);
-            sub_roff.ensure(n);
-            sub_rcnt.ensure(n);
-            sub_rocc.ensure(n);
-            zero(sub_rcnt.p, (size_t)n * 4);
-            zero(sub_rocc.p, (size_t)n * 4);
-            if (ordered) levels(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
-            else levels2(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
-            launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const uint64_t*)sub_roff.p, (const uint32_t*)sub_rcnt.p,
-                   (const uint32_t*)sub_rocc.p, res_off.p, res_cnt.p, res_occ.p);
+        const bool ordered = (flags & EDSBWT_ORDERED) != 0;
+        try {
+            if (force_groups) run_grouped(d_bytes, d_off, P, allow_deep, ordered, force_groups, abase);
+            else run_batch(d_bytes, d_off, P, allow_deep, ordered, res_off.p, res_cnt.p, res_occ.p, abase);
+        } catch (const TooBig&) {
+            // a depth outgrew 32-bit counts (e.g. a 1 Gchar EDS with many empty words):
+            // search the batch as separate trie subtrees, grouped by the last k characters
+            for (uint32_t k = 2;; k++) {
+                try {
+                    run_grouped(d_bytes, d_off, P, allow_deep, ordered, k, abase);
+                    break;
+                } catch (const TooBig&) {
+                    if (k >= 4) throw;
+                }
+            }
         }
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
         HIPCHK(hipMemcpyAsync(d_counts, res_occ.p, P * 4, hipMemcpyDeviceToDevice, stream));

@@ -385,6 +385,29 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
 
 __global__ void k_iota(uint32_t* __restrict__ a, uint64_t n) { GRID_STRIDE(i, n) a[i] = (uint32_t)i; }
 
+// group of a pattern = its last k characters' sort codes (0 past the pattern's start),
+// i.e. its depth-k node of the reversed-pattern trie, in base sigma+2
+__global__ void k_pattern_group(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
+                                const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t k, uint32_t* __restrict__ gid) {
+    GRID_STRIDE(i, P) {
+        const uint64_t a = off[i], L = off[i + 1] - a;
+        uint32_t g = 0;
+        for (uint32_t t = 0; t < k; t++) {
+            uint32_t v = 0;
+            if (t < L) {
+                const uint32_t c = code_of[bytes[a + L - 1 - t]];
+                v = c < sigma ? c + 1 : sigma + 1;
+            }
+            g = g * (sigma + 2) + v;
+        }
+        gid[i] = g;
+    }
+}
+
+__global__ void k_eq_flag(const uint32_t* __restrict__ v, uint64_t n, uint32_t x, uint32_t* __restrict__ flag) {
+    GRID_STRIDE(i, n) flag[i] = v[i] == x;
+}
+
 __global__ void k_gather_key(const uint64_t* __restrict__ keys_c, const uint32_t* __restrict__ perm, uint64_t P, uint64_t* __restrict__ out) {
     GRID_STRIDE(i, P) out[i] = keys_c[perm[i]];
 }

@@ -88,6 +88,8 @@ typedef struct {
                                  ends share one line; the locate table reads none) */
     uint64_t locate_offsets;  /* sum of the records' offsets = the LF moves of the reference's
                                  locate walk (:348-353), whatever walk the device did */
+    uint64_t search_groups;   /* 0, or the number of trie-subtree groups the batch was split into
+                                 because a depth outgrew 32-bit counts */
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,

@@ -135,6 +135,24 @@ def test_c5_style_gpu(oracle, edsbwt, tmp_path):
     _compare(oracle, edsbwt, base, pats, table_too=False)
 
 
+@pytest.mark.parametrize("k", [1, 2])
+def test_grouped_search(oracle, edsbwt, tmp_path, monkeypatch, k):
+    """The trie-subtree split a batch falls back to when a depth outgrows 32-bit counts
+    (forced here): same counts and records, in the same order."""
+    monkeypatch.setenv("EDSBWT_FORCE_GROUPS", str(k))
+    rng = random.Random(41 + k)
+    segs = edsgen.random_eds(rng, 2000, lmax=6, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 30)) or "ACGT" for _ in range(1500)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(1, 20))) for _ in range(500)] + ["", "N", "#A"]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert idx.stats()["search_groups"] > 1
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+
+
 def test_unaligned_device_bytes(oracle, edsbwt, tmp_path):
     """search_device with a pattern buffer that is not 4-B aligned (the LDS staging
     of the key kernel needs alignment and must fall back)."""
