@@ -163,11 +163,13 @@ struct Engine {
     // profiling
     bool prof = false;
     bool no_wide = false;
+    bool count_only = false;  // current search returns counts only (no interval archive at finishing depths)
     // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
     uint32_t deep_k = env_double("EDSBWT_DEEP_K", kDeepK) == 4 ? 4u : (uint32_t)kDeepK;  // register list length of k_deep
     uint32_t force_groups = (uint32_t)env_double("EDSBWT_FORCE_GROUPS", 0);  // tests: always search in trie-subtree groups
+    uint32_t sticky_groups = 0;  // grouping depth a previous batch on this index needed
     static double env_double(const char* name, double dflt) {
         const char* v = std::getenv(name);
         return v && *v ? std::atof(v) : dflt;
@@ -1056,12 +1058,18 @@ struct Engine {
                 pack_items(nxt);
                 ncur = ncur_saved;
                 launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
-                const size_t cap_fin = shard_bound(nnext, 1);
-                efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD);
+                const size_t cap_fin = count_only ? 0 : shard_bound(nnext, 1);
+                if (!count_only) { efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD); }
+                // count only: per-node occurrence sums, no interval archive (C5-scale batches
+                // finish billions of intervals)
                 launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
-                       (const uint8_t*)fin.p, lcnt.p, efk.p, efv.p, (uint32_t)cap_fin, node_occ.p, X.rowbits);
-                fetch_shards();
-                const uint32_t F = shard_total(4);
+                       (const uint8_t*)fin.p, lcnt.p, count_only ? (uint64_t*)nullptr : efk.p, count_only ? (uint32_t*)nullptr : efv.p,
+                       (uint32_t)cap_fin, node_occ.p, X.rowbits);
+                uint32_t F = 0;
+                if (!count_only) {
+                    fetch_shards();
+                    F = shard_total(4);
+                }
                 fk.ensure(F); fv.ensure(F);
                 if (F) {
                     unshard2(4, cap_fin, efk.p, efv.p, fk.p, fv.p, F);
@@ -1161,6 +1169,7 @@ struct Engine {
         prof_mask = (flags & EDSBWT_PROFILE) ? ~0u : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_LOCATE) | (1u << KC_LINKSORT));
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
         const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
+        count_only = !locate;
         const int loc_mode = use_table ? 1 : ((flags & EDSBWT_LOCATE_WALK) || !have_samples) ? 0 : 2;
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
         no_wide = (flags & EDSBWT_NO_WIDE) != 0;
@@ -1183,14 +1192,17 @@ struct Engine {
         // patterns holding '#' make the reference's lists overlap: they take the ordered path
         const bool ordered = (flags & EDSBWT_ORDERED) != 0;
         try {
-            if (force_groups) run_grouped(d_bytes, d_off, P, allow_deep, ordered, force_groups, abase);
+            const uint32_t g0 = force_groups ? force_groups : sticky_groups;
+            if (g0) run_grouped(d_bytes, d_off, P, allow_deep, ordered, g0, abase);
             else run_batch(d_bytes, d_off, P, allow_deep, ordered, res_off.p, res_cnt.p, res_occ.p, abase);
         } catch (const TooBig&) {
             // a depth outgrew 32-bit counts (e.g. a 1 Gchar EDS with many empty words):
-            // search the batch as separate trie subtrees, grouped by the last k characters
-            for (uint32_t k = 2;; k++) {
+            // search the batch as separate trie subtrees, grouped by the last k characters;
+            // later batches on this index start grouped (sticky_groups)
+            for (uint32_t k = std::max(2u, sticky_groups + 1);; k++) {
                 try {
                     run_grouped(d_bytes, d_off, P, allow_deep, ordered, k, abase);
+                    sticky_groups = k;
                     break;
                 } catch (const TooBig&) {
                     if (k >= 4) throw;

@@ -1372,16 +1372,17 @@ __global__ void __launch_bounds__(256) k_fin_emit(uint32_t n, const uint32_t* __
                                                   uint32_t* __restrict__ node_occ, uint32_t rowbits) {
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
-    fk += (size_t)sh * cap; fv += (size_t)sh * cap;
+    if (fk) { fk += (size_t)sh * cap; fv += (size_t)sh * cap; }
     UNIFORM_STRIDE(i, valid, n) {
         uint32_t f = 0, u = 0;
         if (valid) {
             u = nu[i];
             f = fin[u];
         }
-        uint32_t at = wave_append(cnt + 4, f);
+        // fk == nullptr (count only): the occurrence sums are all that is kept
+        uint32_t at = wave_append(cnt + 4, fk ? f : 0u);
         if (f) {
-            if (at < cap) {
+            if (fk && at < cap) {
                 fk[at] = ((uint64_t)u << rowbits) | nb[i];
                 fv[at] = ne[i];
             }
