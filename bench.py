@@ -33,7 +33,7 @@ CONFIGS = {
     # name: (generator config, EDS chars, EDS seed, patterns per GPU, lengths, mode, pattern seed, locate)
     "c2": ("c2", 10_000_000, 1, 1_000_000, "20", "random", 2, False),
     "c3": ("c3", 100_000_000, 3, 10_000_000, "31", "planted", 4, True),
-    "c5": ("c5", 1_000_000_000, 6, 10_000_000, "8,16,32,64", "mixed", 7, False),
+    "c5": ("c5", 1_000_000_000, 6, 200_000, "8,16,32,64", "mixed", 7, False),
 }
 WORKLOAD = {
     "c2": "C2: 10 Mchar synthetic EDS (sigma=4, ~3 strings/segment), 1M random 20-mers per GPU, count-only",
