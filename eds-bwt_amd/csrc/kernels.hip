@@ -1347,9 +1347,16 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
             const uint64_t ci = child_info[u];
             const uint32_t* e0 = X.segtab + (size_t)db[i] * X.seg_stride;  // s_first: ranks at the run's first word
             const uint32_t* e1 = X.segtab + (size_t)de[i] * X.seg_stride;  // s_last: ranks one past its last word
+            if (X.seg_stride == 16) {  // sigma <= 7: [lo, lo-ranks 1..7 | hi-ranks 8..14, pad] as 16-B vectors
+                const uint4 a0 = reinterpret_cast<const uint4*>(e0)[0], a1 = reinterpret_cast<const uint4*>(e0)[1];
+                const uint4 b0 = reinterpret_cast<const uint4*>(e1)[2], b1 = reinterpret_cast<const uint4*>(e1)[3];
+                rb[0] = a0.y; rb[1] = a0.z; rb[2] = a0.w; rb[3] = a1.x; rb[4] = a1.y; rb[5] = a1.z; rb[6] = a1.w;
+                re[0] = b0.x; re[1] = b0.y; re[2] = b0.z; re[3] = b0.w; re[4] = b1.x; re[5] = b1.y; re[6] = b1.z;
+            } else {
 #pragma unroll
-            for (uint32_t c = 0; c < 8; c++)
-                if (c < X.sigma) { rb[c] = e0[1 + c]; re[c] = e1[X.seg_hi + c]; }
+                for (uint32_t c = 0; c < 8; c++)
+                    if (c < X.sigma) { rb[c] = e0[1 + c]; re[c] = e1[X.seg_hi + c]; }
+            }
             n_blk += 2;
             cf = (uint32_t)ci;
             mask = (uint32_t)(ci >> 32);
