@@ -35,6 +35,7 @@ ORDERED = 0x20
 PROFILE_LIGHT = 0x40
 NO_WIDE = 0x80
 LOCATE_WALK = 0x100
+LEGACY_ORDER = 0x200
 
 OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
 CSV_HEADER = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"  # MOVE_EDSBWTSearch.cpp:59 (note the trailing space)
@@ -171,10 +172,11 @@ class Index:
 
     def search(self, patterns: Sequence[bytes | str] | tuple[np.ndarray, np.ndarray], *, first_pattern_id: int = 1,
                locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
-               ordered: bool = False, wide: bool = True, walk: bool = False):
+               ordered: bool = False, wide: bool = True, walk: bool = False, legacy: bool = False):
         """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc]).
         ``table``: (word, offset) per row from the full table; ``walk``: the reference's
-        full LF walk to '#'; default: walk to the first sampled row."""
+        full LF walk to '#'; default: walk to the first sampled row.  ``legacy``: records in
+        the legacy EDSBWTsearch engine's order (``<patterns>output.csv``) instead of MOVE's."""
         buf, offs = patterns if isinstance(patterns, tuple) else pack_patterns(patterns)
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
@@ -182,7 +184,7 @@ class Index:
         counts = np.zeros(max(npat, 0), dtype=np.uint32)
         flags = ((LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
                  | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0) | (0 if wide else NO_WIDE)
-                 | (LOCATE_WALK if walk else 0))
+                 | (LOCATE_WALK if walk else 0) | (LEGACY_ORDER if legacy else 0))
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         bp = buf.ctypes.data if buf.size else None

@@ -111,6 +111,7 @@ struct Engine {
     uint64_t device_bytes = 0;
     DBuf<OccBlock> occ;
     DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt, segtab;
+    DBuf<uint32_t> kpos;  // '#'-row rank of each word (inverse of eof_word): legacy output order
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
     bool have_table = false;
@@ -129,7 +130,9 @@ struct Engine {
     DBuf<uint32_t> ab, ae, res_cnt, res_occ;
     DBuf<uint64_t> res_off, occ64, oscan, tc64, tscan64, tout;
     DBuf<uint32_t> trow, tpat;
-    DBuf<edsbwt_occ> rec;
+    DBuf<edsbwt_occ> rec, rec2;
+    DBuf<uint64_t> lk, lk2;                 // legacy_order keys
+    DBuf<uint32_t> lp, lp2, li, li2;
     DBuf<unsigned long long> counters;
     DBuf<uint8_t> tmp;      // hipcub temp storage
     DBuf<unsigned long long> lhist;
@@ -491,6 +494,11 @@ struct Engine {
         up(occ, hb);
         up(eof_seg, eseg);
         up(eof_word, H.eof_id);
+        {
+            std::vector<uint32_t> kp(W);
+            for (uint32_t t = 0; t < W; t++) kp[H.eof_id[t]] = t;
+            up(kpos, kp);
+        }
         up(seg_of_word, sow);
         up(seg_start, sst);
         up(seg_lo, slo);
@@ -1162,6 +1170,30 @@ struct Engine {
         st.search_groups = G;
     }
 
+    // reorder rec[0..n) into the legacy engine's order (k_legacy_keys)
+    void legacy_order(uint64_t n, uint64_t P, uint32_t first_id) {
+        if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "legacy order over >2^31 records");
+        const uint32_t kbits = bits_for(W), obits = bits_for(N);
+        if (kbits + obits > 64) throw Fail(EDSBWT_E_UNSUPPORTED, "legacy order key wider than 64 bits");
+        lk.ensure(n); lk2.ensure(n); lp.ensure(n); lp2.ensure(n); li.ensure(n); li2.ensure(n);
+        launch(KC_LOCATE, k_legacy_keys, n, (uint64_t)n, (const edsbwt_occ*)rec.p, (const uint32_t*)kpos.p, kbits, lk.p, lp.p, li.p);
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lk.p, lk2.p, li.p, li2.p, (int)n, 0, (int)(kbits + obits), stream));
+        tmp.ensure(tb);
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lk.p, lk2.p, li.p, li2.p, (int)n, 0, (int)(kbits + obits), stream));
+        // stable by pattern: gather the pattern ids in key order, then sort them carrying the indices
+        launch(KC_LOCATE, k_gather_u32, n, (const uint32_t*)lp.p, (const uint32_t*)li2.p, (uint64_t)n, lp2.p);
+        const int pbits = (int)bits_for((uint64_t)first_id + P);
+        tb = 0;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lp2.p, lp.p, li2.p, li.p, (int)n, 0, pbits, stream));
+        tmp.ensure(tb);
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lp2.p, lp.p, li2.p, li.p, (int)n, 0, pbits, stream));
+        rec2.ensure(n);
+        launch(KC_LOCATE, k_gather_rec, n, (uint64_t)n, (const uint32_t*)li.p, (const edsbwt_occ*)rec.p, rec2.p);
+        std::swap(rec.p, rec2.p);
+        std::swap(rec.cap, rec2.cap);
+    }
+
     // d_bytes/d_off/d_counts are device pointers; returns number of records
     uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
         st = edsbwt_stats{};
@@ -1240,6 +1272,7 @@ struct Engine {
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
                        X, loc_mode, rec.p, stats.p);
+                if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);
             }
         }
         HIPCHK(hipMemcpyAsync(pinned_stats, stats.p, kStatSlots * 8, hipMemcpyDeviceToHost, stream));

@@ -1632,6 +1632,29 @@ __global__ void k_samp_fill(uint64_t nblk, uint32_t N, const uint32_t* __restric
 }
 #endif
 
+// Legacy output order (findMultipleDollarsBackward, EDSBWTsearch.cpp:300-610): for one
+// pattern, round r outputs the '#' rows reached after r LF steps, rounds ascending, and
+// inside a round the intervals are sorted by row, so a record's position is (offset,
+// '#'-row rank of its word).  Records arrive pattern-major: a stable sort by that key
+// then a stable sort by pattern gives the order.
+__global__ void k_legacy_keys(uint64_t n, const edsbwt_occ* __restrict__ rec, const uint32_t* __restrict__ kpos, uint32_t kbits,
+                              uint64_t* __restrict__ key, uint32_t* __restrict__ pat, uint32_t* __restrict__ idx) {
+    GRID_STRIDE(i, n) {
+        const edsbwt_occ r = rec[i];
+        key[i] = ((uint64_t)r.offset << kbits) | kpos[r.word];
+        pat[i] = r.pat;
+        idx[i] = (uint32_t)i;
+    }
+}
+
+__global__ void k_gather_u32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx, uint64_t n, uint32_t* __restrict__ out) {
+    GRID_STRIDE(i, n) out[i] = src[idx[i]];
+}
+
+__global__ void k_gather_rec(uint64_t n, const uint32_t* __restrict__ idx, const edsbwt_occ* __restrict__ in, edsbwt_occ* __restrict__ out) {
+    GRID_STRIDE(i, n) out[i] = in[idx[i]];
+}
+
 // ------------------------------------------------- DA/OFF table (index open)
 // For every word w, walk LF from row w (its '#'-suffix) to the row with L='#'
 // (position 0): rows visited get DA = w and their distance from the word end.

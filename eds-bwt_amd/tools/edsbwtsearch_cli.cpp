@@ -1,6 +1,6 @@
 // eds-bwt_amd/tools/edsbwtsearch_cli.cpp — the EDSBWTsearch / MOVE_EDSBWTSearch CLI.
 //
-//   EDSBWTsearch <index_base> <pattern_file> [--device D] [--quiet] [--count-only] [--table]
+//   EDSBWTsearch <index_base> <pattern_file> [--device D] [--quiet] [--count-only] [--table] [--legacy]
 //
 // Same argv, files and console contract as mainMove_EDSBWT.cpp:17-62 driving
 // MOVE_EDSBWT::MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:23-176):
@@ -12,6 +12,8 @@
 //     "count_found = N" / "count_not_found = M" (:154-155) — the lines the
 //     reference's scripts grep (launch_COVID.sh:106-108).
 // --quiet drops the per-pattern lines (they dominate console time at 10^7 patterns).
+// --legacy writes <pattern_file>output.csv in the legacy EDSBWTsearch engine's record order
+// and header (EDSBWTsearch.cpp:180-186, findMultipleDollarsBackward :300-610) instead.
 // The search itself runs on the GPU through libedsbwt.so (include/edsbwt.h).
 #include <chrono>
 #include <cstdio>
@@ -25,11 +27,12 @@
 int main(int argc, char** argv) {
     std::vector<std::string> pos;
     int device = 0;
-    bool quiet = false, count_only = false, table = false;
+    bool quiet = false, count_only = false, table = false, legacy = false;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "--quiet")) quiet = true;
         else if (!std::strcmp(argv[i], "--count-only")) count_only = true;
         else if (!std::strcmp(argv[i], "--table")) table = true;
+        else if (!std::strcmp(argv[i], "--legacy")) legacy = true;
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else pos.push_back(argv[i]);
     }
@@ -79,18 +82,19 @@ int main(int argc, char** argv) {
         s = e + 1;
     }
     const uint64_t npat = offs.size() - 1;
-    const std::string out = pfile + "output_M_LF.csv";
+    const std::string out = pfile + (legacy ? "output.csv" : "output_M_LF.csv");
     FILE* fo = std::fopen(out.c_str(), "wb");
     if (!fo) {
         std::fprintf(stderr, "ERROR opening file %s to write output\n", out.c_str());
         return 1;
     }
-    std::fputs("#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n", fo);
+    std::fputs(legacy ? "#Pat\t$_i\tD[i]\tS_j\tS_j[r]\n" : "#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n", fo);
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint32_t> counts(npat + 1, 0);
     edsbwt_occ* occ = nullptr;
     uint64_t nocc = 0;
-    uint32_t flags = count_only ? EDSBWT_COUNT_ONLY : (EDSBWT_LOCATE | (table ? EDSBWT_LOCATE_TABLE : 0));
+    uint32_t flags = count_only ? EDSBWT_COUNT_ONLY
+                                : (EDSBWT_LOCATE | (table ? EDSBWT_LOCATE_TABLE : 0) | (legacy ? EDSBWT_LEGACY_ORDER : 0));
     rc = edsbwt_search(idx, bytes.data(), offs.data(), npat, 1, flags, counts.data(), &occ, &nocc);
     if (rc) {
         std::fprintf(stderr, "%s\n", edsbwt_last_error());

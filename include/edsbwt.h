@@ -44,6 +44,10 @@ enum {
 #define EDSBWT_PROFILE_LIGHT 0x40u/* events only around the few large launches (fused step, deep,
                                     locate, link sort): what bench.py uses inside its timed region */
 #define EDSBWT_NO_WIDE      0x80u/* tests: skip the wide-list retry of k_deep overflows */
+#define EDSBWT_LEGACY_ORDER 0x200u/* with LOCATE: records in the legacy EDSBWTsearch engine's order
+                                    (findMultipleDollarsBackward, EDSBWTsearch.cpp:300-610): per
+                                    pattern by offset, then by the word's '#' row — the order of
+                                    <patterns>output.csv and of the README example */
 #define EDSBWT_LOCATE_WALK  0x100u/* with LOCATE: walk LF all the way to the '#' row as the
                                     reference does (:348-353), ignoring the row samples;
                                     identical records (default: stop at the first sampled row) */

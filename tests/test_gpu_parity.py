@@ -203,6 +203,47 @@ def test_deep_overflow_rerun(oracle, edsbwt, tmp_path):
         assert st2["deep_level_rerun"] > 0, st2
 
 
+def _kpos(base):
+    """'#'-row rank of every word, from <base>_info.aux (EOF_ID_Copy, Appendix A)."""
+    raw = open(base + "_info.aux", "rb").read()
+    N, W = np.frombuffer(raw, np.uint32, 2)
+    sigma = raw[8]
+    eof = np.frombuffer(raw, np.uint32, count=int(W), offset=9 + sigma)
+    kp = np.empty(int(W), np.int64)
+    kp[eof] = np.arange(int(W))
+    return kp
+
+
+def test_legacy_order_readme(oracle, tmp_path):
+    """README.md:144-167 example, produced by the legacy EDSBWTsearch engine: with
+    --legacy the CLI's output.csv equals it byte for byte (rows in the legacy order)."""
+    import subprocess
+    from conftest import ROOT
+    base = _build(oracle, tmp_path, open(os.path.join(GOLDEN, "test.eds")).read(), "test")
+    shutil.copy(os.path.join(GOLDEN, "readme_kat_patterns.txt"), tmp_path / "p.txt")
+    cli = os.path.join(ROOT, "eds-bwt_amd", "_build", "EDSBWTsearch")
+    r = subprocess.run([cli, base, str(tmp_path / "p.txt"), "--quiet", "--legacy"], capture_output=True, text=True)
+    assert r.returncode == 1, r.stderr
+    assert (tmp_path / "p.txtoutput.csv").read_bytes() == open(os.path.join(GOLDEN, "readme_kat_expected.tsv"), "rb").read()
+
+
+def test_legacy_order_random(oracle, edsbwt, tmp_path):
+    """Legacy order = per pattern, by offset, then by the '#'-row rank of the word
+    (findMultipleDollarsBackward's rounds, EDSBWTsearch.cpp:300-610)."""
+    rng = random.Random(12)
+    segs = edsgen.random_eds(rng, 1500, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 12)) or "ACGT" for _ in range(800)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    kp = _kpos(base)
+    order = np.lexsort((kp[oo["word"]], oo["offset"], oo["pat"]))
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs), legacy=True)
+        assert np.array_equal(gc, oc)
+        assert np.array_equal(go, oo[order])
+
+
 def test_cli_matches_oracle_csv(oracle, tmp_path):
     """EDSBWTsearch (C++ CLI over the C ABI) vs the oracle's MOVE_EDSBWTSearch restatement:
     identical <patterns>output_M_LF.csv bytes, count lines on stderr, exit code 1."""
