@@ -298,7 +298,10 @@ __device__ __forceinline__ void wave_append3(uint32_t* __restrict__ cnt, uint32_
 // Appends go to NSHARD independent regions (counter k of shard s at cnt[s*32+k],
 // one 128-B line per shard) so that no single address takes every wave's atomic;
 // k_unshard packs the regions afterwards.
-constexpr uint32_t NSHARD = 64;
+#ifndef EDSBWT_NSHARD
+#define EDSBWT_NSHARD 64
+#endif
+constexpr uint32_t NSHARD = EDSBWT_NSHARD;
 
 // grid-stride loop whose trip count is uniform across each block (so wave-wide
 // shuffles inside it see every lane); `valid` marks the lanes past the end
