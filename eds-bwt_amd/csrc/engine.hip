@@ -13,6 +13,8 @@
 // DESIGN.md §Search walks through the phases and why each equals the reference.
 #include <hipcub/hipcub.hpp>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -52,6 +54,15 @@ template <class T>
 struct DBuf {
     T* p = nullptr;
     size_t cap = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    DBuf(DBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+    DBuf& operator=(DBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; cap = o.cap; o.p = nullptr; o.cap = 0; }
+        return *this;
+    }
+    ~DBuf() { release(); }  // index_close frees the HBM the index and its workspace hold
     void ensure(size_t n) {
         if (n <= cap && p) return;
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
@@ -61,6 +72,21 @@ struct DBuf {
             throw Fail(EDSBWT_E_NOMEM, "hipMalloc of " + std::to_string(c * sizeof(T)) + " bytes failed");
         }
         cap = c;
+        if (poison()) { (void)hipMemsetD32((hipDeviceptr_t)p, poison_value(), c * sizeof(T) / 4); (void)hipDeviceSynchronize(); }
+    }
+    // EDSBWT_POISON=<u32> (debugging): fresh allocations are filled with that 32-bit word
+    // (0 or empty: 0xA5A5A5A5) so a read of memory no kernel wrote shows up as a parity
+    // failure instead of depending on what the allocator hands back
+    static bool poison() {
+        static const bool on = std::getenv("EDSBWT_POISON") != nullptr;
+        return on;
+    }
+    static uint32_t poison_value() {
+        static const uint32_t v = [] {
+            const uint32_t x = (uint32_t)std::strtoul(std::getenv("EDSBWT_POISON"), nullptr, 0);
+            return x ? x : 0xA5A5A5A5u;
+        }();
+        return v;
     }
     // grow keeping contents (archive)
     void grow_keep(size_t n, hipStream_t s) {
@@ -68,6 +94,7 @@ struct DBuf {
         size_t c = std::max<size_t>({n, cap + cap / 2, 1024});
         T* q = nullptr;
         if (hipMalloc(&q, c * sizeof(T)) != hipSuccess) throw Fail(EDSBWT_E_NOMEM, "hipMalloc (grow) failed");
+        if (poison()) { (void)hipMemsetD32((hipDeviceptr_t)q, poison_value(), c * sizeof(T) / 4); (void)hipDeviceSynchronize(); }
         if (p) {
             HIPCHK(hipMemcpyAsync(q, p, cap * sizeof(T), hipMemcpyDeviceToDevice, s));
             HIPCHK(hipStreamSynchronize(s));
@@ -97,6 +124,12 @@ constexpr double kDeepItems = 2.0;
 [[maybe_unused]] constexpr uint32_t kSampleShift = 3;
 // patterns k_deep<kDeepK> cannot hold retry with lists of up to kDeepWide intervals
 constexpr int kDeepWide = 64;
+// k-mer start table: deepest depth tried, most D-mers (offsets) and intervals kept, and the
+// shallowest depth worth a table
+constexpr double kKtabK = 12;
+constexpr uint64_t kKtabMaxEntries = 1ull << 25;
+constexpr double kKtabItems = 268435456.0;  // 2^28 intervals (2 GiB)
+constexpr uint32_t kKtabMinDepth = 2;
 // levels2() result meaning "the batch needs the ordered path"
 constexpr uint32_t kNeedOrdered = 0xFFFFFFFFu;
 
@@ -117,6 +150,24 @@ struct Engine {
     bool have_table = false;
     DBuf<uint2> samples;     // locate samples (word, offset) of rows whose offset % 2^kSampleShift == 0
     bool have_samples = false;
+    // k-mer start table (build_ktab): for every D-mer x over the non-'#' symbols, the
+    // order-free walk's intervals after its D characters, [ktab_off[x], ktab_off[x+1]) of
+    // ktab_b / ktab_e; searches whose patterns are all longer than D start at depth D
+    uint32_t ktab_depth = 0;
+    uint64_t ktab_items = 0;
+    DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
+    bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
+    // levels2() capture mode (table build): the items of the deepest depth <= K whose
+    // count fits the budget, as (D-mer index, b, e)
+    struct Capture {
+        uint32_t K = 0, B = 0;
+        uint64_t budget = 0;
+        uint32_t depth = 0;
+        uint64_t n = 0;
+        DBuf<uint32_t> k, b, e;
+    };
+    Capture* cap = nullptr;
+    DBuf<uint32_t> kt_kid, kt_cnt, kt_pos;
     // workspace
     DBuf<uint32_t> len, perm, perm2, slen, lcp, nid[2], flag, scan, node_first, node_parent, child_first, child_end;
     DBuf<uint8_t> node_char;
@@ -234,6 +285,7 @@ struct Engine {
     void launch_reduce(int k, K kern, A... a) {
         timed(k, [&] { hipLaunchKernelGGL(kern, dim3(kReduceBlocks), dim3(256), 0, stream, a...); });
         HIPCHK(hipGetLastError());
+        sync_check((const void*)kern);
         st.launches_kernel[k]++;
     }
     template <typename K, typename... A>
@@ -241,7 +293,19 @@ struct Engine {
         if (!n) return;
         timed(k, [&] { hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(256), 0, stream, a...); });
         HIPCHK(hipGetLastError());
+        sync_check((const void*)kern);
         st.launches_kernel[k]++;
+    }
+    // EDSBWT_SYNC_CHECK=1 (debugging): wait for every launch and name the kernel that failed
+    const bool sync_checks = std::getenv("EDSBWT_SYNC_CHECK") != nullptr;
+    void sync_check(const void* kern, const char* label = nullptr) {
+        if (!sync_checks) return;
+        const hipError_t e = hipStreamSynchronize(stream);
+        if (e == hipSuccess) return;
+        Dl_info di{};
+        const char* name = label ? label : (kern && dladdr(kern, &di) && di.dli_sname ? di.dli_sname : "?");
+        std::fprintf(stderr, "[edsbwt] kernel %s failed: %s\n", name, hipGetErrorString(e));
+        throw Fail(EDSBWT_E_DEVICE, std::string("kernel ") + name + ": " + hipGetErrorString(e));
     }
     uint32_t read_u32(const uint32_t* d) {
         HIPCHK(hipMemcpyAsync(pinned, d, 4, hipMemcpyDeviceToHost, stream));
@@ -338,6 +402,7 @@ struct Engine {
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, scan.p, (int)P, stream));
         tmp.ensure(tb);
         timed(KC_NODES, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, scan.p, (int)P, stream)); });
+        sync_check(nullptr, "hipcub call at engine.hip:396");
     }
 
     void sort_link_keys(const uint64_t* in, uint64_t* out, size_t n, int end_bit) {
@@ -345,6 +410,7 @@ struct Engine {
         HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, in, out, (int)n, 0, end_bit, stream));
         tmp.ensure(tb);
         timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, in, out, (int)n, 0, end_bit, stream)); });
+        sync_check(nullptr, "link key sort");
     }
 
     // out[0..n) = exclusive prefix sum of in[0..n) (no read-back)
@@ -355,6 +421,7 @@ struct Engine {
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, stream));
         tmp.ensure(tb);
         timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, out, (int)n, stream)); });
+        sync_check(nullptr, "hipcub call at engine.hip:414");
     }
 
     // out[0..n] = exclusive prefix sum (out[0] = 0, out[n] = total), no read-back
@@ -367,6 +434,7 @@ struct Engine {
         HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
         tmp.ensure(tb);
         timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+        sync_check(nullptr, "hipcub call at engine.hip:426");
     }
 
     // out[0..n] = exclusive prefix sum of in[0..n); returns out[n]
@@ -379,6 +447,7 @@ struct Engine {
             HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
             tmp.ensure(tb);
             timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+            sync_check(nullptr, "hipcub call at engine.hip:438");
         }
         return read_u32(out.p + n);
     }
@@ -391,6 +460,7 @@ struct Engine {
             HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
             tmp.ensure(tb);
             timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+            sync_check(nullptr, "hipcub call at engine.hip:450");
         }
         return read_u64(out.p + n);
     }
@@ -513,6 +583,71 @@ struct Engine {
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
+        build_ktab();
+    }
+
+    // k-mer start table: the order-free walk run once over every K-mer of the non-'#'
+    // symbols (B = sigma-1 of them), capturing the items of the deepest depth D <= K whose
+    // count stays within the budget; kept as per-D-mer interval lists sorted by row.
+    // EDSBWT_KTAB_K (default kKtabK, 0 = no table) and EDSBWT_KTAB_ITEMS bound it.
+    void build_ktab() {
+        const uint32_t B = sigma - 1;
+        uint32_t K = (uint32_t)env_double("EDSBWT_KTAB_K", kKtabK);
+        const uint64_t budget = (uint64_t)env_double("EDSBWT_KTAB_ITEMS", kKtabItems);
+        if (B < 1 || K < 2) return;
+        auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
+        // no deeper than B^K <= B*N: most longer D-mers do not occur at all
+        while (K > 2 && (pw(K) > kKtabMaxEntries || pw(K - 1) > (uint64_t)N)) K--;
+        if (pw(K) > kKtabMaxEntries) return;
+        const uint64_t P = pw(K);
+        DBuf<uint8_t> kb;
+        DBuf<uint64_t> ko;
+        kb.ensure(P * K);
+        ko.ensure(P + 1);
+        uint64_t sym = 0;
+        for (uint32_t v = 0; v < B; v++) sym |= (uint64_t)alpha[v + 1] << (8 * v);
+        launch(KC_TABLE, k_kmer_batch, P, P, K, B, sym, kb.p, ko.p);
+        res_off.ensure(P); res_cnt.ensure(P); res_occ.ensure(P); ovf_orig.ensure(P);
+        zero(stats.p, kStatSlots * 8);
+        Capture c;
+        c.K = K; c.B = B; c.budget = budget;
+        cap = &c;
+        const bool was_count_only = count_only;
+        count_only = true;
+        uint64_t abase = 0;
+        try {
+            levels2(kb.p, ko.p, P, false, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
+        } catch (const TooBig&) {
+            // a depth past the budget outgrew 32-bit counts: keep what was captured
+        }
+        cap = nullptr;
+        count_only = was_count_only;
+        st = edsbwt_stats{};
+        HIPCHK(hipStreamSynchronize(stream));
+        if (c.depth < kKtabMinDepth || c.n == 0) return;
+        const uint64_t E = pw(c.depth), n = c.n;
+        DBuf<uint64_t> k1, k2;
+        DBuf<uint32_t> e2;
+        k1.ensure(n); k2.ensure(n); e2.ensure(n);
+        launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
+        size_t tb = 0;
+        const int endbit = 32 + (int)bits_for(E);
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, (int)n, 0, endbit, stream));
+        tmp.ensure(tb);
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, (int)n, 0, endbit, stream));
+        sync_check(nullptr, "hipcub call at engine.hip:624");
+        ktab_off.ensure(E + 1);
+        ktab_b.ensure(n);
+        ktab_e.ensure(n);
+        launch(KC_TABLE, k_ktab_bounds, E + 1, E, (const uint64_t*)k2.p, n, ktab_off.p);
+        launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, ktab_b.p);
+        HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        ktab_depth = c.depth;
+        ktab_items = n;
+        device_bytes += (E + 1) * 4 + n * 8;
+        if (trace) std::fprintf(stderr, "[edsbwt] k-mer start table: depth %u, %llu D-mers, %llu intervals\n", ktab_depth,
+                                (unsigned long long)E, (unsigned long long)n);
     }
 
     // Locate samples: one (word, offset) per row whose offset in its word is a multiple
@@ -605,7 +740,11 @@ struct Engine {
             launch(KC_TRIE, k_iota, P, perm.p, P);
             for (int c = full ? (int)nch - 1 : 0; c >= 0; c--) {
                 const uint32_t nsym = std::min(spc, Lmax - (uint32_t)c * spc);
-                const int begin_bit = (int)(bps * (spc - nsym)), end_bit = (int)(bps * spc);
+                // rocPRIM (ROCm 7.2) mis-sorts u64 keys over [begin_bit, 64) when begin_bit > 0
+                // (measured: tools/diag/sort_check.hip): 4-bit codes fill all 64 bits, so their
+                // partial chunks are sorted over the whole word
+                const int end_bit = (int)(bps * spc);
+                const int begin_bit = end_bit == 64 ? 0 : (int)(bps * (spc - nsym));
                 const uint64_t* kin = keys.p + (size_t)c * P;
                 if (full && c != (int)nch - 1) {  // later passes sort the chunk in the current order
                     launch(KC_TRIE, k_gather_key, P, kin, (const uint32_t*)perm.p, P, kc.p);
@@ -616,6 +755,7 @@ struct Engine {
                 tmp.ensure(tb);
                 timed(KC_TRIE, [&] {
                     HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
+                    sync_check(nullptr, "hipcub call at engine.hip:739");
                 });
                 std::swap(perm.p, perm2.p);
                 std::swap(perm.cap, perm2.cap);
@@ -739,6 +879,7 @@ struct Engine {
                         HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream));
                         tmp.ensure(tb);
                         timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream)); });
+                        sync_check(nullptr, "hipcub call at engine.hip:862");
                         rflag.ensure(V);
                         launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, 32u, rflag.p);
                         R = scan_u32(rflag.p, rscan, V);
@@ -909,12 +1050,41 @@ struct Engine {
                        (const uint32_t*)fu.p, (const uint32_t*)fb.p, (const uint32_t*)fe.p, iu[dst].p, ib[dst].p, ie[dst].p);
             in_sharded = false;
         };
-        for (uint32_t d = 0; d < Lmax; d++) {
+        // k-mer start table: when every pattern is longer than its depth d0, the items of
+        // depth d0 are the table's lists of the depth-d0 nodes' d0-mers (no steps 1..d0)
+        uint32_t d0 = 0;
+        if (!cap && use_ktab && ktab_depth) {
+            uint32_t lmin = 0;
+            while (lmin <= Lmax && hist[lmin] == 0) lmin++;
+            if (lmin > ktab_depth) d0 = ktab_depth;
+        }
+        if (d0) {
+            const uint32_t M0 = (uint32_t)nodes_at[d0];
+            node_scan(d0, P);
+            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, d0, (const uint32_t*)slen.p, sorted_chunk(d0, P), sigma,
+                   (const uint32_t*)lcp.p, (const uint32_t*)scan.p, (const uint32_t*)nid[0].p, nid[1].p, node_first.p, node_parent.p, node_char.p);
+            kt_kid.ensure(M0);
+            kt_cnt.ensure(M0);
+            launch(KC_NODES, k_ktab_count, M0, M0, d0, sigma - 1, (const uint32_t*)node_first.p, (const uint32_t*)perm.p, d_off, d_bytes,
+                   (const uint8_t*)code_of.p, (const uint32_t*)ktab_off.p, kt_kid.p, kt_cnt.p);
+            const uint32_t n0 = scan_u32(kt_cnt.p, kt_pos, M0);
+            iu[1].ensure(n0); ib[1].ensure(n0); ie[1].ensure(n0);
+            launch(KC_NODES, k_ktab_emit, M0, M0, (const uint32_t*)kt_kid.p, (const uint32_t*)kt_pos.p, (const uint32_t*)ktab_off.p,
+                   (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p, iu[1].p, ib[1].p, ie[1].p);
+            cur = 1;
+            Mcur = M0;
+            ncur = n0;
+            st.start_depth = d0;
+            st.trie_nodes += M0;
+            if (trace) std::fprintf(stderr, "[edsbwt] start at depth %u from the k-mer table: nodes %u, items %u\n", d0, M0, n0);
+            if (ncur == 0) return 0;  // no pattern's last d0 characters occur
+        }
+        for (uint32_t d = d0; d < Lmax; d++) {
             const uint32_t D = d + 1;
             const int nxt = cur ^ 1;
             const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
-            if (allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D] && (double)ncur <= deep_items * (double)Mcur) {
+            if (!cap && allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D] && (double)ncur <= deep_items * (double)Mcur) {
                 if (in_sharded) pack_items(cur);
                 // group the unordered items by node, then finish patterns one per thread
                 gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur); goff.ensure(Mcur);
@@ -1059,6 +1229,24 @@ struct Engine {
                 fcap = cap_next;
                 in_sharded = true;
             }
+            if (cap) {  // table build: keep this depth's items as (D-mer, b, e) while they fit
+                if (nnext > cap->budget) break;
+                cap->k.ensure(nnext); cap->b.ensure(nnext); cap->e.ensure(nnext);
+                if (nnext) {
+                    launch(KC_TABLE, k_unshard<uint32_t, uint32_t, uint32_t>, nnext, nnext, (const uint32_t*)fpre.p, (uint32_t)fcap,
+                           (const uint32_t*)fu.p, (const uint32_t*)fb.p, (const uint32_t*)fe.p, cap->k.p, cap->b.p, cap->e.p);
+                    uint64_t BD = 1;
+                    for (uint32_t t = 0; t < D; t++) BD *= cap->B;
+                    launch(KC_TABLE, k_ktab_capture_map, nnext, (uint64_t)nnext, cap->k.p, (const uint32_t*)node_first.p, (const uint32_t*)perm.p, BD);
+                }
+                cap->depth = D;
+                cap->n = nnext;
+                if (D >= cap->K || nnext == 0) break;
+                cur = nxt;
+                Mcur = M;
+                ncur = nnext;
+                continue;
+            }
             // finish patterns of length D: their node's items, sorted by row
             if (finishing) {
                 const uint32_t ncur_saved = ncur;
@@ -1087,6 +1275,7 @@ struct Engine {
                     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream));
                     tmp.ensure(tb);
                     timed(KC_FINISH, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream)); });
+                    sync_check(nullptr, "hipcub call at engine.hip:1257");
                     launch(KC_FINISH, k_fin_bounds, F, F, (const uint64_t*)fk2.p, X.rowbits, foff.p, fend.p);
                     ab.grow_keep(abase + F, stream);
                     ae.grow_keep(abase + F, stream);
@@ -1181,6 +1370,7 @@ struct Engine {
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lk.p, lk2.p, li.p, li2.p, (int)n, 0, (int)(kbits + obits), stream));
         tmp.ensure(tb);
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lk.p, lk2.p, li.p, li2.p, (int)n, 0, (int)(kbits + obits), stream));
+        sync_check(nullptr, "hipcub call at engine.hip:1351");
         // stable by pattern: gather the pattern ids in key order, then sort them carrying the indices
         launch(KC_LOCATE, k_gather_u32, n, (const uint32_t*)lp.p, (const uint32_t*)li2.p, (uint64_t)n, lp2.p);
         const int pbits = (int)bits_for((uint64_t)first_id + P);
@@ -1188,6 +1378,7 @@ struct Engine {
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lp2.p, lp.p, li2.p, li.p, (int)n, 0, pbits, stream));
         tmp.ensure(tb);
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lp2.p, lp.p, li2.p, li.p, (int)n, 0, pbits, stream));
+        sync_check(nullptr, "hipcub call at engine.hip:1358");
         rec2.ensure(n);
         launch(KC_LOCATE, k_gather_rec, n, (uint64_t)n, (const uint32_t*)li.p, (const edsbwt_occ*)rec.p, rec2.p);
         std::swap(rec.p, rec2.p);
@@ -1205,6 +1396,7 @@ struct Engine {
         const int loc_mode = use_table ? 1 : ((flags & EDSBWT_LOCATE_WALK) || !have_samples) ? 0 : 2;
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
         no_wide = (flags & EDSBWT_NO_WIDE) != 0;
+        use_ktab = (flags & EDSBWT_NO_KTAB) == 0;
         if (use_table) build_table();
         st.patterns = P;
         if (P == 0) return 0;
@@ -1386,6 +1578,8 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
     info->sigma = E.sigma;
     std::memcpy(info->alphabet, E.alpha, sizeof info->alphabet);
     info->device_bytes = E.device_bytes;
+    info->ktab_depth = E.ktab_depth;
+    info->ktab_items = E.ktab_items;
     return 0;
 }
 

@@ -1763,4 +1763,90 @@ __global__ void k_zero4(uint32_t* __restrict__ a, uint64_t na, uint32_t* __restr
 
 __global__ void k_fill_u32(uint32_t* __restrict__ a, uint64_t n, uint32_t v) { GRID_STRIDE(i, n) a[i] = v; }
 
+// ------------------------------------------------------- k-mer start table
+// The order-free walk's state after D characters is a function of those D characters
+// alone, so the index keeps it for every D-mer over the B = sigma-1
+// non-'#' symbols and a search starts at depth D.  A D-mer's index has its LAST
+// character as the least significant base-B digit (digit = code - 1).
+
+// every K-mer as a pattern: pattern i spells i's base-B digits, last character = digit 0
+// (so i mod B^D is the index of its last D characters); sym[v] = byte of code v + 1
+__global__ void k_kmer_batch(uint64_t P, uint32_t K, uint32_t B, uint64_t sym, uint8_t* __restrict__ bytes, uint64_t* __restrict__ off) {
+    GRID_STRIDE(i, P) {
+        uint64_t x = i;
+        for (uint32_t t = 0; t < K; t++) {
+            bytes[i * K + (K - 1 - t)] = (uint8_t)(sym >> (8 * (x % B)));
+            x /= B;
+        }
+        off[i] = i * K;
+        if (i + 1 == P) off[P] = P * K;
+    }
+}
+
+// captured items: node id at depth D -> index of the node's D-mer (from its first pattern's id)
+__global__ void k_ktab_capture_map(uint64_t n, uint32_t* __restrict__ u, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ perm,
+                                   uint64_t BD) {
+    GRID_STRIDE(t, n) u[t] = (uint32_t)(perm[node_first[u[t]]] % BD);
+}
+
+__global__ void k_ktab_keys(uint64_t n, const uint32_t* __restrict__ km, const uint32_t* __restrict__ b, uint64_t* __restrict__ key) {
+    GRID_STRIDE(t, n) key[t] = (uint64_t)km[t] << 32 | b[t];
+}
+
+// off[x] = first item of D-mer x in the sorted keys (off[E] = n)
+__global__ void k_ktab_bounds(uint64_t E, const uint64_t* __restrict__ key, uint64_t n, uint32_t* __restrict__ off) {
+    GRID_STRIDE(x, E + 1) {
+        if (x == E) { off[E] = (uint32_t)n; continue; }
+        uint64_t lo = 0, hi = n;
+        const uint64_t want = (uint64_t)x << 32;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (key[mid] < want) lo = mid + 1; else hi = mid;
+        }
+        off[x] = (uint32_t)lo;
+    }
+}
+
+__global__ void k_ktab_split(uint64_t n, const uint64_t* __restrict__ key, uint32_t* __restrict__ b) {
+    GRID_STRIDE(t, n) b[t] = (uint32_t)key[t];
+}
+
+// search side: per depth-D node, its D-mer (read from its first pattern's last D bytes)
+// and the length of that D-mer's list; bytes outside the non-'#' alphabet -> empty list
+__global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ perm,
+                             const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of,
+                             const uint32_t* __restrict__ toff, uint32_t* __restrict__ kid, uint32_t* __restrict__ cnt) {
+    GRID_STRIDE(u, M) {
+        const uint32_t p = perm[node_first[u]];
+        const uint64_t end = off[p + 1];
+        uint32_t x = 0, mul = 1;
+        bool ok = true;
+        for (uint32_t t = 0; t < D; t++) {
+            const uint32_t c = code_of[bytes[end - 1 - t]];
+            ok &= c >= 1 && c <= B;
+            x += (c - 1) * mul;
+            mul *= B;
+        }
+        kid[u] = ok ? x : 0xFFFFFFFFu;
+        cnt[u] = ok ? toff[x + 1] - toff[x] : 0u;
+    }
+}
+
+// items of depth D: node u's list copied from the table at pos[u] (exclusive scan of cnt)
+__global__ void __launch_bounds__(256) k_ktab_emit(uint32_t M, const uint32_t* __restrict__ kid, const uint32_t* __restrict__ pos,
+                                                   const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tb,
+                                                   const uint32_t* __restrict__ te, uint32_t* __restrict__ iu, uint32_t* __restrict__ ib,
+                                                   uint32_t* __restrict__ ie) {
+    GRID_STRIDE(u, M) {
+        const uint32_t x = kid[u];
+        if (x == 0xFFFFFFFFu) continue;
+        uint32_t o = pos[u];
+        for (uint32_t j = toff[x], j1 = toff[x + 1]; j < j1; j++, o++) {
+            iu[o] = (uint32_t)u;
+            ib[o] = tb[j];
+            ie[o] = te[j];
+        }
+    }
+}
+
 }  // namespace edsbwt

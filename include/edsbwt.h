@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EDSBWT_ABI_VERSION 1
+#define EDSBWT_ABI_VERSION 2
 
 enum {
     EDSBWT_OK = 0,
@@ -53,6 +53,8 @@ enum {
                                     identical records (default: stop at the first sampled row) */
 #define EDSBWT_ORDERED      0x20u/* keep every interval list in the reference's order at every
                                     depth (the path patterns holding '#' take); same results */
+#define EDSBWT_NO_KTAB      0x400u/* start the trie walk at depth 0 instead of at the k-mer start
+                                    table's depth (tests: same results either way) */
 
 typedef struct edsbwt_index edsbwt_index;
 
@@ -70,6 +72,10 @@ typedef struct {
     uint32_t sigma;       /* sizeAlpha */
     uint8_t alphabet[16]; /* alphaInverse[0..sigma) */
     uint64_t device_bytes;/* HBM held by the index */
+    uint32_t ktab_depth;  /* k-mer start table: depth D (0 = none) — the interval lists of
+                             every D-mer over the non-'#' symbols, built at open */
+    uint32_t pad;
+    uint64_t ktab_items;  /* intervals held by that table */
 } edsbwt_index_info;
 
 /* Per-call counters and timings (filled by every edsbwt_search*). */
@@ -94,6 +100,8 @@ typedef struct {
                                  locate walk (:348-353), whatever walk the device did */
     uint64_t search_groups;   /* 0, or the number of trie-subtree groups the batch was split into
                                  because a depth outgrew 32-bit counts */
+    uint64_t start_depth;     /* depth the trie walk started from (the k-mer start table's
+                                 depth when it served the batch, else 0) */
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,

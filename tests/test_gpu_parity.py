@@ -50,6 +50,9 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         assert idx.stats()["locate_lf_steps"] == int(oo["offset"].astype(np.uint64).sum())
         gc4, go4 = idx.search((buf, offs), deep=False)   # level-synchronous path only
         assert np.array_equal(gc4, oc) and np.array_equal(go4, oo)
+        gk, gok = idx.search((buf, offs), ktab=False)     # walk from depth 0, no k-mer start table
+        assert np.array_equal(gk, oc) and np.array_equal(gok, oo)
+        assert idx.stats()["start_depth"] == 0
         for deep in (True, False):                       # reference-ordered lists at every depth
             gc5, go5 = idx.search((buf, offs), ordered=True, deep=deep)
             assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
@@ -266,3 +269,37 @@ def test_cli_matches_oracle_csv(oracle, tmp_path):
     assert (tmp_path / "p1.txtoutput_M_LF.csv").read_bytes() == (tmp_path / "p2.txtoutput_M_LF.csv").read_bytes()
     r = subprocess.run([cli, base], capture_output=True, text=True)
     assert r.returncode == 1 and "usage" in r.stderr
+
+
+def test_short_patterns_4bit_codes_gpu(oracle, edsbwt, tmp_path):
+    """7 symbols + '#' (4-bit sort codes) and patterns shorter than one key chunk: the
+    chunk's significant bits end at bit 64, the range rocPRIM mis-sorts unless it starts at 0."""
+    rng = random.Random(77)
+    segs = edsgen.random_eds(rng, 2000, alphabet="ACGTNRY", lmax=6, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(3, 15)) or "ACG" for _ in range(3000)]
+    pats += ["".join(rng.choice("ACGTNRY") for _ in range(rng.randint(1, 15))) for _ in range(3000)]
+    _compare(oracle, edsbwt, base, pats, table_too=False)
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_kmer_start_table_gpu(oracle, edsbwt, tmp_path, seed):
+    """Batches whose patterns are all longer than the k-mer start table's depth start the
+    trie walk there; results equal the oracle's and the walk from depth 0."""
+    rng = random.Random(900 + seed)
+    alphabet = ("ACGTN", "ACGT", "ACGTN", "ACGT", "ACGTNRY")[seed]  # 3-bit codes; 4-bit codes for 7 symbols
+    segs = edsgen.random_eds(rng, 1500 + 500 * seed, alphabet=alphabet, lmax=4 + 2 * (seed % 4), p_empty=0.25 if seed % 2 else 0.1)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D = idx.ktab_depth
+        assert D >= 2 and idx.ktab_items > 0
+    pats = [edsgen.planted(rng, segs, rng.randint(D + 1, D + 20)) or "ACGT" * 8 for _ in range(800)]
+    pats += ["".join(rng.choice(alphabet + "N") for _ in range(rng.randint(D + 1, 40))) for _ in range(400)]
+    pats += ["N" * (D + 1), "ACGT" * 10 + "X"]  # a byte outside the alphabet inside / before the last D
+    _compare(oracle, edsbwt, base, pats, table_too=seed == 0)
+    buf, offs = _pack(pats)
+    with edsbwt.Index(base) as idx:
+        idx.search((buf, offs))
+        assert idx.stats()["start_depth"] == D
+        idx.search((buf, offs), ordered=True)  # the ordered path never uses the table
+        assert idx.stats()["start_depth"] == 0
