@@ -594,6 +594,7 @@ struct Engine {
         const uint32_t B = sigma - 1;
         uint32_t K = (uint32_t)env_double("EDSBWT_KTAB_K", kKtabK);
         const uint64_t budget = (uint64_t)env_double("EDSBWT_KTAB_ITEMS", kKtabItems);
+        K = std::min(K, 16u);  // a search reads a node's D-mer from its sorted key chunk 0 (>= 16 symbols)
         if (B < 1 || K < 2) return;
         auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
         // no deeper than B^K <= B*N: most longer D-mers do not occur at all
@@ -1065,11 +1066,11 @@ struct Engine {
                    (const uint32_t*)lcp.p, (const uint32_t*)scan.p, (const uint32_t*)nid[0].p, nid[1].p, node_first.p, node_parent.p, node_char.p);
             kt_kid.ensure(M0);
             kt_cnt.ensure(M0);
-            launch(KC_NODES, k_ktab_count, M0, M0, d0, sigma - 1, (const uint32_t*)node_first.p, (const uint32_t*)perm.p, d_off, d_bytes,
-                   (const uint8_t*)code_of.p, (const uint32_t*)ktab_off.p, kt_kid.p, kt_cnt.p);
+            launch(KC_NODES, bps == 3 ? k_ktab_count<3> : k_ktab_count<4>, M0, M0, d0, sigma - 1, (const uint32_t*)node_first.p,
+                   sorted_chunk(1, P), (const uint32_t*)ktab_off.p, kt_kid.p, kt_cnt.p);
             const uint32_t n0 = scan_u32(kt_cnt.p, kt_pos, M0);
             iu[1].ensure(n0); ib[1].ensure(n0); ie[1].ensure(n0);
-            launch(KC_NODES, k_ktab_emit, M0, M0, (const uint32_t*)kt_kid.p, (const uint32_t*)kt_pos.p, (const uint32_t*)ktab_off.p,
+            launch(KC_NODES, k_ktab_emit, ((size_t)M0 + 63) / 64 * 64, M0, (const uint32_t*)kt_kid.p, (const uint32_t*)kt_pos.p, (const uint32_t*)ktab_off.p,
                    (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p, iu[1].p, ib[1].p, ie[1].p);
             cur = 1;
             Mcur = M0;

@@ -1811,20 +1811,23 @@ __global__ void k_ktab_split(uint64_t n, const uint64_t* __restrict__ key, uint3
     GRID_STRIDE(t, n) b[t] = (uint32_t)key[t];
 }
 
-// search side: per depth-D node, its D-mer (read from its first pattern's last D bytes)
-// and the length of that D-mer's list; bytes outside the non-'#' alphabet -> empty list
-__global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ perm,
-                             const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of,
+// search side: per depth-D node, its D-mer and the length of that D-mer's list.  The
+// D-mer comes from the node's first pattern's sorted key chunk 0 (reversed sort codes,
+// BPS bits each, most significant first; D <= SPC): sort code v = 1 + symbol code, so a
+// non-'#' alphabet symbol has v in [2, B+1] and digit v-2; '#' or a byte outside the
+// alphabet -> empty list.
+template <int BPS>
+__global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t* __restrict__ node_first, const uint64_t* __restrict__ k0,
                              const uint32_t* __restrict__ toff, uint32_t* __restrict__ kid, uint32_t* __restrict__ cnt) {
+    constexpr uint32_t SPC = 64 / BPS;
     GRID_STRIDE(u, M) {
-        const uint32_t p = perm[node_first[u]];
-        const uint64_t end = off[p + 1];
+        const uint64_t key = k0[node_first[u]];
         uint32_t x = 0, mul = 1;
         bool ok = true;
         for (uint32_t t = 0; t < D; t++) {
-            const uint32_t c = code_of[bytes[end - 1 - t]];
-            ok &= c >= 1 && c <= B;
-            x += (c - 1) * mul;
+            const uint32_t v = (uint32_t)(key >> (BPS * (SPC - 1 - t))) & ((1u << BPS) - 1u);
+            ok &= v >= 2 && v <= B + 1;
+            x += (v - 2) * mul;
             mul *= B;
         }
         kid[u] = ok ? x : 0xFFFFFFFFu;
@@ -1832,19 +1835,43 @@ __global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t*
     }
 }
 
-// items of depth D: node u's list copied from the table at pos[u] (exclusive scan of cnt)
+// items of depth D: node u's list copied from the table to pos[u] (exclusive scan of cnt).
+// One wave per 64 consecutive nodes, whose outputs are contiguous: the wave walks its
+// items 64 at a time, each lane finding its item's node by a binary search over the
+// lanes' running counts (balanced and coalesced however long single lists are).
 __global__ void __launch_bounds__(256) k_ktab_emit(uint32_t M, const uint32_t* __restrict__ kid, const uint32_t* __restrict__ pos,
                                                    const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tb,
                                                    const uint32_t* __restrict__ te, uint32_t* __restrict__ iu, uint32_t* __restrict__ ib,
                                                    uint32_t* __restrict__ ie) {
-    GRID_STRIDE(u, M) {
-        const uint32_t x = kid[u];
-        if (x == 0xFFFFFFFFu) continue;
-        uint32_t o = pos[u];
-        for (uint32_t j = toff[x], j1 = toff[x + 1]; j < j1; j++, o++) {
-            iu[o] = (uint32_t)u;
-            ib[o] = tb[j];
-            ie[o] = te[j];
+    const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+    for (size_t base = ((size_t)blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; base < M; base += (size_t)gridDim.x * wpb * 64) {
+        const size_t u = base + lane;
+        uint32_t n = 0, start = 0;
+        if (u < M) {
+            const uint32_t x = kid[u];
+            if (x != 0xFFFFFFFFu) { start = toff[x]; n = toff[x + 1] - start; }
+        }
+        uint32_t incl = n;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if ((int)lane >= o) incl += y;
+        }
+        const uint32_t excl = incl - n;
+        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t out0 = pos[base];
+        for (uint32_t q0 = 0; q0 < total; q0 += 64) {  // wave-uniform trip count: every lane joins the shuffles
+            const uint32_t q = q0 + lane;
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t step = 32; step; step >>= 1)
+                if ((uint32_t)__shfl(excl, (int)(lo + step), 64) <= q) lo += step;
+            const uint32_t src = (uint32_t)__shfl(start, (int)lo, 64) + (q - (uint32_t)__shfl(excl, (int)lo, 64));
+            if (q < total) {
+                iu[out0 + q] = (uint32_t)base + lo;
+                ib[out0 + q] = tb[src];
+                ie[out0 + q] = te[src];
+            }
         }
     }
 }
