@@ -120,7 +120,7 @@ constexpr int kDeepK = 8;
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
-// locate samples every 2^kSampleShift positions of a word (8 B per sampled row)
+// locate samples every 2^kSampleShift positions of a word (16 B per sampled row)
 [[maybe_unused]] constexpr uint32_t kSampleShift = 3;
 // patterns k_deep<kDeepK> cannot hold retry with lists of up to kDeepWide intervals
 constexpr int kDeepWide = 64;
@@ -148,7 +148,7 @@ struct Engine {
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
     bool have_table = false;
-    DBuf<uint2> samples;     // locate samples (word, offset) of rows whose offset % 2^kSampleShift == 0
+    DBuf<uint4> samples;     // locate samples (word, offset, segment, word in segment) of rows whose offset % 2^kSampleShift == 0
     bool have_samples = false;
     // k-mer start table (build_ktab): for every D-mer x over the non-'#' symbols, the
     // order-free walk's intervals after its D characters, [ktab_off[x], ktab_off[x+1]) of
@@ -181,6 +181,7 @@ struct Engine {
     DBuf<uint32_t> ab, ae, res_cnt, res_occ;
     DBuf<uint64_t> res_off, occ64, oscan, tc64, tscan64, tout;
     DBuf<uint32_t> trow, tpat;
+    DBuf<uint64_t> blk_first;  // per kLocRun records: the task holding the first (k_tasks -> k_locate)
     DBuf<edsbwt_occ> rec, rec2;
     DBuf<uint64_t> lk, lk2;                 // legacy_order keys
     DBuf<uint32_t> lp, lp2, li, li2;
@@ -667,9 +668,9 @@ struct Engine {
         const uint32_t ns = scan_u32(bcnt.p, bbase, nblk);  // bbase[0..nblk], total read back
         if (ns < W) throw Fail(EDSBWT_E_FORMAT, "locate samples: fewer sampled rows than words");
         samples.ensure(ns);
-        device_bytes += (size_t)ns * sizeof(uint2);
-        launch(KC_TABLE, k_samp_fill, nblk, nblk, N, (const uint32_t*)da.p, (const uint32_t*)offt.p, (const uint32_t*)bbase.p, occ.p,
-               samples.p);
+        device_bytes += (size_t)ns * sizeof(uint4);
+        launch(KC_TABLE, k_samp_fill, nblk, nblk, N, (const uint32_t*)da.p, (const uint32_t*)offt.p, (const uint32_t*)bbase.p,
+               (const uint32_t*)seg_of_word.p, (const uint32_t*)seg_start.p, occ.p, samples.p);
         HIPCHK(hipStreamSynchronize(stream));
         if (!keep_table) {
             da.release();
@@ -1460,11 +1461,12 @@ struct Engine {
             const uint64_t TT = rb3[2];
             if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
+                blk_first.ensure(OCC / kLocRun + 1);
                 launch(KC_LOCPREP, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
-                       (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p);
+                       (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p);
                 rec.ensure(OCC);
-                launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p, first_id,
-                       X, loc_mode, rec.p, stats.p);
+                launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
+                       (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p);
                 if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);
             }
         }

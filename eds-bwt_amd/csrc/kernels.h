@@ -46,7 +46,7 @@ struct KIdx {
     const uint32_t* da;        // [N] optional DA per row
     const uint32_t* offt;      // [N] optional offset-in-word per row
     uint32_t N, W, S, sigma;
-    const uint2* samples;      // (word, offset) of the sampled rows, in row order (locate)
+    const uint4* samples;      // (word, offset, segment, word in segment) of the sampled rows, in row order (locate)
     // per segment s (link of a word in s): [0] seg_lo[s]; [1 + c] rank_c at the first word of
     // segment seg_lo[s]; [seg_hi + c] rank_c at the first word of s.  seg_stride u32 per entry.
     const uint32_t* segtab;

@@ -1525,20 +1525,27 @@ __global__ void k_finish(uint64_t P, uint32_t D, const uint32_t* __restrict__ sl
 // --------------------------------------------------------------- locate
 __global__ void k_u32_to_u64(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ b) { GRID_STRIDE(i, n) b[i] = a[i]; }
 
+// one task per finished interval: its first row, first output record and pattern; and,
+// per run of kLocRun records, the task holding the run's first record (blk_first), so
+// k_locate finds a record's task in LDS instead of searching all tasks
+constexpr uint32_t kLocRun = 256;
 __global__ void k_tasks(uint64_t P, const uint64_t* __restrict__ res_off, const uint32_t* __restrict__ res_cnt,
                         const uint64_t* __restrict__ tscan, const uint64_t* __restrict__ oscan,
                         const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
-                        uint32_t* __restrict__ trow, uint64_t* __restrict__ tout, uint32_t* __restrict__ tpat) {
+                        uint32_t* __restrict__ trow, uint64_t* __restrict__ tout, uint32_t* __restrict__ tpat,
+                        uint64_t* __restrict__ blk_first) {
     GRID_STRIDE(i, P) {
         uint64_t base = oscan[i];
         const uint64_t t0 = tscan[i];
         const uint32_t n = res_cnt[i];
         for (uint32_t q = 0; q < n; q++) {
             const uint64_t a = res_off[i] + q;
+            const uint64_t len = (uint64_t)(ae[a] - ab[a]) + 1;
             trow[t0 + q] = ab[a];
             tout[t0 + q] = base;
             tpat[t0 + q] = (uint32_t)i;
-            base += (uint64_t)(ae[a] - ab[a]) + 1;
+            for (uint64_t k = (base + kLocRun - 1) / kLocRun; k * kLocRun < base + len; k++) blk_first[k] = t0 + q;
+            base += len;
         }
     }
 }
@@ -1548,13 +1555,33 @@ __global__ void k_tasks(uint64_t P, const uint64_t* __restrict__ res_off, const 
 // mode 0: the reference's full walk; 1: per-row (word, offset) table; 2: walk until
 // the first sampled row (offset a multiple of the sample rate) and add its stored
 // (word, offset) — '#' rows have offset 0 and are always sampled.
+// launched with 256-thread blocks: a block's pass covers records [o0, o0 + kLocRun), whose
+// tasks (at most kLocRun + 1, from blk_first) are staged in LDS
 __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
-                                                const uint32_t* __restrict__ tpat, uint32_t first_id, KIdx X, int mode,
-                                                edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
+                                                const uint32_t* __restrict__ tpat, const uint64_t* __restrict__ blk_first, uint32_t first_id,
+                                                KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
     unsigned long long my_steps = 0, my_off = 0;
-    GRID_STRIDE(o, OCC) {
-        const size_t t = upper_bound_dev<uint64_t>(tout, TT, (uint64_t)o) - 1;
-        uint32_t x = trow[t] + (uint32_t)(o - tout[t]);
+    __shared__ uint64_t s_out[kLocRun + 1];
+    __shared__ uint32_t s_row[kLocRun + 1], s_pat[kLocRun + 1];
+    for (uint64_t o0 = (uint64_t)blockIdx.x * kLocRun; o0 < OCC; o0 += (uint64_t)gridDim.x * kLocRun) {  // block-uniform
+        const uint64_t t0 = blk_first[o0 / kLocRun];
+        const uint32_t nt = (uint32_t)min((uint64_t)kLocRun + 1, TT - t0);
+        __syncthreads();  // the previous pass is done with the staged tasks
+        for (uint32_t j = threadIdx.x; j < nt; j += blockDim.x) {
+            s_out[j] = tout[t0 + j];
+            s_row[j] = trow[t0 + j];
+            s_pat[j] = tpat[t0 + j];
+        }
+        __syncthreads();
+        const uint64_t o = o0 + threadIdx.x;
+        if (o >= OCC) continue;
+        uint32_t lo = 0, hi = nt;  // last staged task with s_out <= o
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_out[mid] <= o) lo = mid; else hi = mid;
+        }
+        const uint32_t pat = s_pat[lo];
+        uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
         uint32_t word, off;
         if (mode == 1) {
             word = X.da[x];
@@ -1566,11 +1593,18 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
                 const OccV v = load_block(X.occ, x >> 6);
                 const uint32_t bit = x & 63u;
                 const uint64_t m = (1ull << bit) - 1ull;
-                if (mode == 2 && ((v.samp >> bit) & 1)) {
-                    const uint2 s = X.samples[v.cnt[7] + (uint32_t)__popcll(v.samp & m)];
-                    word = s.x;
+                if (mode == 2 && ((v.samp >> bit) & 1)) {  // (word, offset, segment, word in segment)
+                    const uint4 s = X.samples[v.cnt[7] + (uint32_t)__popcll(v.samp & m)];
                     my_steps += off;
-                    off += s.y;
+                    my_off += off + s.y;
+                    edsbwt_occ r;
+                    r.pat = first_id + pat;
+                    r.word = s.x;
+                    r.seg = s.z;
+                    r.word_in_seg = s.w;
+                    r.offset = off + s.y;
+                    rec[o] = r;
+                    word = ~0u;
                     break;
                 }
                 const uint32_t c = (uint32_t)((v.p0 >> bit) & 1) | (uint32_t)(((v.p1 >> bit) & 1) << 1) | (uint32_t)(((v.p2 >> bit) & 1) << 2);
@@ -1589,10 +1623,11 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
                 off++;
             }
         }
+        if (word == ~0u) continue;  // written from its sample
         my_off += off;
         const uint32_t seg = X.seg_of_word[word];
         edsbwt_occ r;
-        r.pat = first_id + tpat[t];
+        r.pat = first_id + pat;
         r.word = word;
         r.seg = seg;
         r.word_in_seg = word - X.seg_start[seg];
@@ -1621,7 +1656,8 @@ __global__ void k_samp_blocks(uint64_t nblk, uint32_t N, const uint32_t* __restr
 }
 
 __global__ void k_samp_fill(uint64_t nblk, uint32_t N, const uint32_t* __restrict__ da, const uint32_t* __restrict__ offt,
-                            const uint32_t* __restrict__ bbase, OccBlock* __restrict__ occ, uint2* __restrict__ samples) {
+                            const uint32_t* __restrict__ bbase, const uint32_t* __restrict__ seg_of_word,
+                            const uint32_t* __restrict__ seg_start, OccBlock* __restrict__ occ, uint4* __restrict__ samples) {
     GRID_STRIDE(b, nblk) {
         uint32_t at = bbase[b];
         occ[b].cnt[7] = at;
@@ -1629,7 +1665,8 @@ __global__ void k_samp_fill(uint64_t nblk, uint32_t N, const uint32_t* __restric
         for (uint32_t r = 0; r < 64; r++)
             if ((p >> r) & 1) {
                 const uint64_t x = b * 64 + r;
-                samples[at++] = make_uint2(da[x], offt[x]);
+                const uint32_t w = da[x], sg = seg_of_word[w];
+                samples[at++] = make_uint4(w, offt[x], sg, w - seg_start[sg]);
             }
     }
 }
