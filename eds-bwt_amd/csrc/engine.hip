@@ -973,13 +973,16 @@ struct Engine {
         dqpre.ensure(NSHARD + 1);
         lcnt.ensure(NSHARD * 32 + 32);
         zero(lcnt.p, NSHARD * 32 * 4);
-        launch(KC_DEEP, k_deep_fast, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, d_off, d_bytes, (const uint8_t*)code_of.p, nid_d,
-               goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p);
+        // the patterns' remaining symbols come from the sorted key chunks (chunk 0, then skey)
+        const uint64_t* k0 = sorted_chunk(1, P);
+        const uint64_t* krest = skey.p;
+        launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, k0, krest,
+               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
-        launch(KC_DEEP, K == 4 ? k_deep<4> : k_deep<kDeepK>, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d,
-               (const uint32_t*)slen.p, (const uint32_t*)perm.p, d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase,
-               ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
+        auto kd = K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>) : (bps == 3 ? k_deep<kDeepK, 3> : k_deep<kDeepK, 4>);
+        launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, (const uint32_t*)slen.p,
+               (const uint32_t*)perm.p, k0, krest, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace) std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu\n", D, M, (unsigned long long)active);

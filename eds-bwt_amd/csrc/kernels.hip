@@ -750,14 +750,39 @@ __global__ void k_merge_build(uint64_t n, const uint32_t* __restrict__ flag, con
 // runs with the interval lists in registers (at most K each).  A pattern whose
 // lists outgrow K, or whose link reads more than K '#' rows at once, is flagged and
 // re-run by the level-synchronous path, which has no size limit.
+// Symbol codes of sorted pattern i from its reversed sort-code chunks (chunk 0 in k0,
+// chunk c >= 1 at krest[(c-1)*P + i]; BPS bits per symbol, most significant first): the
+// deep kernels read a pattern's remaining symbols one coalesced chunk at a time instead of
+// byte by byte.  code(d) = symbol code of the d-th character from the pattern's end (d < its
+// length); >= sigma for a byte outside the alphabet.
+template <int BPS>
+struct SymReader {
+    const uint64_t* k0;
+    const uint64_t* krest;
+    uint64_t P;
+    size_t i;
+    uint64_t cur = 0;
+    uint32_t chunk = ~0u;
+    __device__ __forceinline__ uint32_t code(uint32_t d) {
+        constexpr uint32_t SPC = 64 / BPS;
+        const uint32_t c = d / SPC, t = d - c * SPC;
+        if (c != chunk) {
+            cur = c == 0 ? k0[i] : krest[(size_t)(c - 1) * P + i];
+            chunk = c;
+        }
+        return (uint32_t)((cur >> (BPS * (SPC - 1 - t))) & ((1u << BPS) - 1u)) - 1u;
+    }
+};
+
 // Deep stage, two kernels.  k_deep_fast walks every pattern whose list is one interval
 // with two registers, as long as no step meets '#' rows (no link); a pattern that needs
 // a list or a link is queued as (pattern, depth, b, e) — b = ~0u: "from its node's
 // items" — and k_deep finishes the queued ones with register lists.  The queue is
 // sharded like the item appends (region s at s*qcap, counter s at qcnt[s*32]).
+template <int BPS>
 __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
-                                                   const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                                                   const uint8_t* __restrict__ code_of, const uint32_t* __restrict__ nid,
+                                                   const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest,
+                                                   const uint32_t* __restrict__ nid,
                                                    const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
                                                    const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                                    uint32_t K, uint32_t* __restrict__ ab, uint32_t* __restrict__ ae,
@@ -765,9 +790,6 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
                                                    unsigned long long* __restrict__ ctr) {
     unsigned long long n_steps = 0, n_blk = 0;
-    __shared__ uint8_t scode[256];
-    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) scode[t] = code_of[t];
-    __syncthreads();
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     UNIFORM_STRIDE(i, valid, P) {
@@ -781,13 +803,11 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             w = make_uint4((uint32_t)i, D0, ~0u, 0u);
         } else if (n0 == 1) {
             uint32_t b = ib[ioff[u]], e = ie[ioff[u]];
-            const uint8_t* pat = bytes + off[perm[i]];
-            uint32_t nbyte = pat[L - 1 - D0];
+            SymReader<BPS> sym{k0, krest, P, i};
             bool alive = true;
             uint32_t d = D0;
             for (; d < L; d++) {
-                const uint32_t c = scode[nbyte];
-                if (d + 1 < L) nbyte = pat[L - 2 - d];
+                const uint32_t c = sym.code(d);
                 if (c >= X.sigma) { alive = false; break; }
                 uint32_t h0, h1, sb, se;
                 n_blk += 2 - rank2_pair(X.occ, b, e + 1, c, h0, sb, h1, se);
@@ -828,11 +848,10 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
     }
 }
 
-template <int K>
+template <int K, int BPS>
 __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
-                                              const uint64_t* __restrict__ off,
-                                              const uint8_t* __restrict__ bytes, const uint8_t* __restrict__ code_of,
+                                              const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint64_t P,
                                               const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
                                               const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
@@ -843,9 +862,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
-    __shared__ uint8_t scode[256];
     __shared__ uint32_t spre[NSHARD + 1];
-    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) scode[t] = code_of[t];
     for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) spre[t] = qpre[t];
     __syncthreads();
     const uint32_t total = spre[NSHARD];
@@ -876,15 +893,11 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             cb[0] = w.z;
             ce[0] = w.w;
         }
-        const uint32_t a = perm[i];
-        const uint8_t* pat = bytes + off[a];
+        SymReader<BPS> sym{k0, krest, P, i};
         bool over = false;
-        // the next character's byte is read one step ahead, so no step waits for it
-        uint32_t nbyte = pat[L - 1 - d0];
         for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
-            const uint32_t code = scode[nbyte];
-            if (d + 1 < L) nbyte = pat[L - 2 - d];
+            const uint32_t code = sym.code(d);
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
