@@ -126,8 +126,8 @@ constexpr double kDeepItems = 2.0;
 constexpr int kDeepWide = 64;
 // k-mer start table: deepest depth tried, most D-mers (offsets) and intervals kept, and the
 // shallowest depth worth a table
-constexpr double kKtabK = 12;
-constexpr uint64_t kKtabMaxEntries = 1ull << 25;
+constexpr double kKtabK = 13;
+constexpr uint64_t kKtabMaxEntries = 1ull << 27;
 constexpr double kKtabItems = 268435456.0;  // 2^28 intervals (2 GiB)
 constexpr uint32_t kKtabMinDepth = 2;
 // levels2() result meaning "the batch needs the ordered path"
@@ -599,8 +599,9 @@ struct Engine {
         if (B < 1 || K < 2) return;
         auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
         // no deeper than B^K <= B*N: most longer D-mers do not occur at all
-        while (K > 2 && (pw(K) > kKtabMaxEntries || pw(K - 1) > (uint64_t)N)) K--;
-        if (pw(K) > kKtabMaxEntries) return;
+        const uint64_t max_entries = (uint64_t)env_double("EDSBWT_KTAB_ENTRIES", (double)kKtabMaxEntries);
+        while (K > 2 && (pw(K) > max_entries || pw(K - 1) > (uint64_t)N)) K--;
+        if (pw(K) > max_entries) return;
         const uint64_t P = pw(K);
         DBuf<uint8_t> kb;
         DBuf<uint64_t> ko;
@@ -985,7 +986,9 @@ struct Engine {
                (const uint32_t*)perm.p, k0, krest, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
-        if (trace) std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu\n", D, M, (unsigned long long)active);
+        if (trace)
+            std::fprintf(stderr, "[edsbwt] deep from depth %u: nodes %u, patterns %llu, queued for k_deep %u\n", D, M, (unsigned long long)active,
+                         read_u32(dqpre.p + NSHARD));
         st.bytes_kernel[KC_DEEP] += (uint64_t)P * 24;  // + interval steps and '#' rows, folded at the end of search()
         // lists that outgrew k_deep's registers: retry those patterns with wide lists
         uint32_t nw = scan_u32(ovf.p, tscan, P);
@@ -1090,9 +1093,17 @@ struct Engine {
             const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
             if (!cap && allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D] && (double)ncur <= deep_items * (double)Mcur) {
+                gend.ensure(Mcur);
+                if (d0 && d == d0) {
+                    // the table's items are already grouped by node: [kt_pos[u], + kt_cnt[u])
+                    launch(KC_DEEP, k_group_end, Mcur, Mcur, (const uint32_t*)kt_pos.p, (const uint32_t*)kt_cnt.p, gend.p);
+                    novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, kt_pos.p, gend.p, ib[cur].p, ie[cur].p, r_off, r_cnt, r_occ, abase,
+                                    ovf_orig);
+                    break;
+                }
                 if (in_sharded) pack_items(cur);
                 // group the unordered items by node, then finish patterns one per thread
-                gcnt.ensure(Mcur); gfill.ensure(Mcur); gend.ensure(Mcur); goff.ensure(Mcur);
+                gcnt.ensure(Mcur); gfill.ensure(Mcur); goff.ensure(Mcur);
                 launch(KC_DEEP, k_zero4, 2 * (size_t)Mcur, gcnt.p, (uint64_t)Mcur, gfill.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0,
                        (uint32_t*)nullptr, (uint64_t)0);
                 launch(KC_DEEP, k_group_count, ncur, ncur, (const uint32_t*)iu[cur].p, gcnt.p);
