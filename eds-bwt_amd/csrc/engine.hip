@@ -114,8 +114,9 @@ enum KClass { KC_TRIE = 0, KC_NODES, KC_EXPAND, KC_LINK, KC_LINKSORT, KC_STEP, K
               KC_TABLE, KC_COUNT };
 static const char* kKNames[KC_COUNT] = {"trie_sort", "trie_nodes", "expand", "link", "link_sort", "step", "merge", "finish",
                                         "deep", "locate_prep", "locate", "scan", "table"};
-// k_deep keeps at most kDeepK intervals per list in registers
-constexpr int kDeepK = 8;
+// k_deep keeps at most kDeepK intervals per list in registers (C3 sweep, 1x MI355X: K=2 1.08e9,
+// K=3 1.20e9, K=4 1.21e9, K=8 1.15e9 patterns/s; longer lists retry in k_deep_wide)
+constexpr int kDeepK = 4;
 // switch to k_deep once depth-D nodes >= kDeepShare x patterns of length >= D
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
@@ -155,6 +156,8 @@ struct Engine {
     // ktab_b / ktab_e; searches whose patterns are all longer than D start at depth D
     uint32_t ktab_depth = 0;
     uint64_t ktab_items = 0;
+    uint64_t ktab_entries = 0;  // B^ktab_depth
+    bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // levels2() capture mode (table build): the items of the deepest depth <= K whose
@@ -222,7 +225,12 @@ struct Engine {
     // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
-    uint32_t deep_k = env_double("EDSBWT_DEEP_K", kDeepK) == 4 ? 4u : (uint32_t)kDeepK;  // register list length of k_deep
+    // direct start only from tables whose lists average at most this many intervals per D-mer
+    double direct_items = env_double("EDSBWT_DIRECT_ITEMS", kDeepItems);
+    uint32_t deep_k = [] {  // register list length of k_deep: 2, 3, 4 or 8
+        const uint32_t k = (uint32_t)env_double("EDSBWT_DEEP_K", kDeepK);
+        return k == 2 || k == 3 || k == 4 || k == 8 ? k : (uint32_t)kDeepK;
+    }();
     uint32_t force_groups = (uint32_t)env_double("EDSBWT_FORCE_GROUPS", 0);  // tests: always search in trie-subtree groups
     uint32_t sticky_groups = 0;  // grouping depth a previous batch on this index needed
     static double env_double(const char* name, double dflt) {
@@ -648,6 +656,7 @@ struct Engine {
         HIPCHK(hipStreamSynchronize(stream));
         ktab_depth = c.depth;
         ktab_items = n;
+        ktab_entries = E;
         device_bytes += (E + 1) * 4 + n * 8;
         if (trace) std::fprintf(stderr, "[edsbwt] k-mer start table: depth %u, %llu D-mers, %llu intervals\n", ktab_depth,
                                 (unsigned long long)E, (unsigned long long)n);
@@ -959,7 +968,8 @@ struct Engine {
     // depth-d node ([goff[u], gend[u]) in gb/ge).  Returns the overflow count.
     uint32_t run_deep(uint32_t d, uint32_t M, uint64_t P, uint64_t active, const uint8_t* d_bytes, const uint64_t* d_off,
                       const uint32_t* nid_d, const uint32_t* goff, const uint32_t* gend, const uint32_t* gb, const uint32_t* gee,
-                      uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
+                      uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig,
+                      const uint64_t* k0 = nullptr, const uint64_t* krest = nullptr) {
         const KIdx X = kidx();
         const uint32_t D = d + 1;
         DBuf<uint32_t>& ovf = tflag;  // per sorted pattern
@@ -975,13 +985,18 @@ struct Engine {
         lcnt.ensure(NSHARD * 32 + 32);
         zero(lcnt.p, NSHARD * 32 * 4);
         // the patterns' remaining symbols come from the sorted key chunks (chunk 0, then skey)
-        const uint64_t* k0 = sorted_chunk(1, P);
-        const uint64_t* krest = skey.p;
+        if (!k0) {
+            k0 = sorted_chunk(1, P);
+            krest = skey.p;
+        }
         launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, k0, krest,
                nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
-        auto kd = K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>) : (bps == 3 ? k_deep<kDeepK, 3> : k_deep<kDeepK, 4>);
+        auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
+                  : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
+                  : K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>)
+                           : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, (const uint32_t*)slen.p,
                (const uint32_t*)perm.p, k0, krest, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
         abase += (uint64_t)P * K;
@@ -1013,6 +1028,50 @@ struct Engine {
         if (no_wide) st.deep_overflow += nw;
         st.deep_level_rerun += novf;
         return novf;
+    }
+
+    // Direct start: when every pattern is longer than the k-mer table's depth D0 and the
+    // table's lists are short on average, no trie is built.  Each pattern (in input order)
+    // takes its D0-mer's list straight from the table and k_deep walks it from there: the
+    // sharing a trie would add past depth D0 is small (nodes ~ patterns), and the sort,
+    // node build and list copy it needs cost more than the deep walk saves.  Returns
+    // kNotDirect when the batch does not qualify (nothing was written), kNeedOrdered for
+    // patterns holding '#', else k_deep's overflow count as run_deep.
+    static constexpr uint32_t kNotDirect = 0xFFFFFFFEu;
+    uint32_t direct(const uint64_t* d_off, const uint8_t* d_bytes, uint64_t P, uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ,
+                    uint64_t& abase, uint32_t* ovf_orig) {
+        if (cap || !use_ktab || !use_direct || !ktab_depth || (double)ktab_items > direct_items * (double)ktab_entries) return kNotDirect;
+        if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
+        const uint32_t D0 = ktab_depth;
+        zero(counters.p + 8, 24);
+        launch_reduce(KC_TRIE, k_lminmax, d_off, P, counters.p + 8);
+        HIPCHK(hipMemcpyAsync(pinned, counters.p + 8, 16, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        uint64_t mm[2];
+        std::memcpy(mm, pinned, 16);
+        const uint32_t Lmax = (uint32_t)mm[0], Lmin = ~(uint32_t)mm[1];
+        if (Lmin <= D0) return kNotDirect;
+        bps = sigma + 2 <= 8 ? 3u : 4u;
+        const uint32_t nch = (Lmax + 64 / bps - 1) / (64 / bps);
+        len.ensure(P);
+        keys.ensure((size_t)nch * P);
+        unsigned long long* d_nterm = counters.p + 10;
+        if (bps == 3)
+            launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
+        else
+            launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
+        if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
+        nid[0].ensure(P);
+        slen.ensure(P);
+        perm.ensure(P);
+        launch(KC_NODES, bps == 3 ? k_ktab_direct<3> : k_ktab_direct<4>, P, P, D0, sigma - 1, (const uint64_t*)keys.p, (const uint32_t*)len.p,
+               nid[0].p, slen.p);
+        launch(KC_NODES, k_iota, P, perm.p, P);
+        st.start_depth = D0;
+        if (trace) std::fprintf(stderr, "[edsbwt] direct start at depth %u from the k-mer table: %llu patterns\n", D0, (unsigned long long)P);
+        // chunk c of pattern i is keys[c*P + i]: chunk 0 and then chunks 1.. as k_deep reads them
+        return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
+                        ktab_b.p, ktab_e.p, r_off, r_cnt, r_occ, abase, ovf_orig, keys.p, keys.p + P);
     }
 
     // Order-free level walk (default): a depth's lists are unordered (node, b, e)
@@ -1313,8 +1372,10 @@ struct Engine {
     // k_deep could not hold re-run through the unbounded level path.
     void run_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, uint64_t* r_off,
                    uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase) {
-        uint32_t novf = 0;
-        if (!ordered) {
+        uint32_t novf = kNotDirect;
+        if (!ordered && allow_deep) novf = direct(d_off, d_bytes, P, r_off, r_cnt, r_occ, abase, ovf_orig.p);
+        if (novf == kNeedOrdered) ordered = true;
+        if (!ordered && novf == kNotDirect) {
             novf = levels2(d_bytes, d_off, P, allow_deep, r_off, r_cnt, r_occ, abase, ovf_orig.p);
             if (novf == kNeedOrdered) ordered = true;
         }
@@ -1413,6 +1474,7 @@ struct Engine {
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
         no_wide = (flags & EDSBWT_NO_WIDE) != 0;
         use_ktab = (flags & EDSBWT_NO_KTAB) == 0;
+        use_direct = (flags & EDSBWT_NO_DIRECT) == 0 && env_double("EDSBWT_NO_DIRECT", 0) == 0;
         if (use_table) build_table();
         st.patterns = P;
         if (P == 0) return 0;

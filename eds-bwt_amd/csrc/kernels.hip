@@ -505,6 +505,27 @@ __global__ void __launch_bounds__(256) k_lmax(const uint64_t* __restrict__ off, 
     if (threadIdx.x == 0) atomicMax(out, (unsigned long long)smx);
 }
 
+// longest and shortest pattern: out[0] = max length, out[1] = ~min length (both by atomicMax)
+__global__ void __launch_bounds__(256) k_lminmax(const uint64_t* __restrict__ off, uint64_t P, unsigned long long* __restrict__ out) {
+    __shared__ unsigned int smx, smn;
+    if (threadIdx.x == 0) smx = smn = 0;
+    __syncthreads();
+    uint32_t mx = 0, nmn = 0;
+    GRID_STRIDE(i, P) {
+        const uint32_t L = (uint32_t)(off[i + 1] - off[i]);
+        mx = max(mx, L);
+        nmn = max(nmn, ~L);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+        nmn = max(nmn, (uint32_t)__shfl_xor(nmn, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) { atomicMax(&smx, mx); atomicMax(&smn, nmn); }
+    __syncthreads();
+    if (threadIdx.x == 0) { atomicMax(out, (unsigned long long)smx); atomicMax(out + 1, (unsigned long long)smn); }
+}
+
 // node starts at depth D: pattern i is the first member of a depth-D node
 __global__ void k_node_flags(const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp, uint64_t P, uint32_t D, uint32_t* __restrict__ flag) {
     GRID_STRIDE(i, P) flag[i] = (slen[i] >= D && lcp[i] < D) ? 1u : 0u;
@@ -1882,6 +1903,30 @@ __global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t*
         }
         kid[u] = ok ? x : 0xFFFFFFFFu;
         cnt[u] = ok ? toff[x + 1] - toff[x] : 0u;
+    }
+}
+
+// direct start (every pattern longer than D): pattern i's D-mer straight from its own
+// (unsorted) key chunk 0, as k_ktab_count reads a node's; k_deep then takes the table's
+// list [toff[kid[i]], toff[kid[i]+1]) as the pattern's items of depth D.  A D-mer holding
+// '#' or a byte outside the alphabet has no list: slen = 0 keeps k_deep off the pattern
+// (its count stays 0).
+template <int BPS>
+__global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, const uint64_t* __restrict__ k0, const uint32_t* __restrict__ len,
+                              uint32_t* __restrict__ kid, uint32_t* __restrict__ slen) {
+    constexpr uint32_t SPC = 64 / BPS;
+    GRID_STRIDE(i, P) {
+        const uint64_t key = k0[i];
+        uint32_t x = 0, mul = 1;
+        bool ok = true;
+        for (uint32_t t = 0; t < D; t++) {
+            const uint32_t v = (uint32_t)(key >> (BPS * (SPC - 1 - t))) & ((1u << BPS) - 1u);
+            ok &= v >= 2 && v <= B + 1;
+            x += (v - 2) * mul;
+            mul *= B;
+        }
+        kid[i] = ok ? x : 0u;
+        slen[i] = ok ? len[i] : 0u;
     }
 }
 

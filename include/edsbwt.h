@@ -55,6 +55,8 @@ enum {
                                     depth (the path patterns holding '#' take); same results */
 #define EDSBWT_NO_KTAB      0x400u/* start the trie walk at depth 0 instead of at the k-mer start
                                     table's depth (tests: same results either way) */
+#define EDSBWT_NO_DIRECT    0x800u/* build the reversed-pattern trie even when every pattern could
+                                    start straight from its k-mer table list (tests: same results) */
 
 typedef struct edsbwt_index edsbwt_index;
 

@@ -53,6 +53,8 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         gk, gok = idx.search((buf, offs), ktab=False)     # walk from depth 0, no k-mer start table
         assert np.array_equal(gk, oc) and np.array_equal(gok, oo)
         assert idx.stats()["start_depth"] == 0
+        gt, got = idx.search((buf, offs), direct=False)   # trie seeded from the table, never the direct start
+        assert np.array_equal(gt, oc) and np.array_equal(got, oo)
         for deep in (True, False):                       # reference-ordered lists at every depth
             gc5, go5 = idx.search((buf, offs), ordered=True, deep=deep)
             assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
@@ -283,9 +285,12 @@ def test_short_patterns_4bit_codes_gpu(oracle, edsbwt, tmp_path):
 
 
 @pytest.mark.parametrize("seed", range(5))
-def test_kmer_start_table_gpu(oracle, edsbwt, tmp_path, seed):
-    """Batches whose patterns are all longer than the k-mer start table's depth start the
-    trie walk there; results equal the oracle's and the walk from depth 0."""
+def test_kmer_start_table_gpu(oracle, edsbwt, tmp_path, monkeypatch, seed):
+    """Batches whose patterns are all longer than the k-mer start table's depth start
+    straight from their D-mers' lists (direct start; forced here, since these small tables
+    hold long lists) or from the trie seeded by the table (direct=False); results equal the
+    oracle's and the walk from depth 0."""
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
     rng = random.Random(900 + seed)
     alphabet = ("ACGTN", "ACGT", "ACGTN", "ACGT", "ACGTNRY")[seed]  # 3-bit codes; 4-bit codes for 7 symbols
     segs = edsgen.random_eds(rng, 1500 + 500 * seed, alphabet=alphabet, lmax=4 + 2 * (seed % 4), p_empty=0.25 if seed % 2 else 0.1)
@@ -301,5 +306,8 @@ def test_kmer_start_table_gpu(oracle, edsbwt, tmp_path, seed):
     with edsbwt.Index(base) as idx:
         idx.search((buf, offs))
         assert idx.stats()["start_depth"] == D
+        assert idx.stats()["trie_nodes"] == 0  # direct start: no trie built
+        idx.search((buf, offs), direct=False)
+        assert idx.stats()["start_depth"] == D and idx.stats()["trie_nodes"] > 0
         idx.search((buf, offs), ordered=True)  # the ordered path never uses the table
         assert idx.stats()["start_depth"] == 0
