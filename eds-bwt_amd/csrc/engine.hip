@@ -121,16 +121,19 @@ constexpr int kDeepK = 4;
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
-// locate samples every 2^kSampleShift positions of a word (16 B per sampled row)
-[[maybe_unused]] constexpr uint32_t kSampleShift = 3;
+// locate samples every 2^kSampleShift positions of a word (16 B per sampled row; C3: 1 in 4
+// offsets 1.477e9 vs 1 in 8 1.424e9 patterns/s)
+constexpr uint32_t kSampleShift = 2;
 // patterns k_deep<kDeepK> cannot hold retry with lists of up to kDeepWide intervals
 constexpr int kDeepWide = 64;
 // k-mer start table: deepest depth tried, most D-mers (offsets) and intervals kept, and the
 // shallowest depth worth a table
-constexpr double kKtabK = 13;
-constexpr uint64_t kKtabMaxEntries = 1ull << 27;
+constexpr double kKtabK = 15;  // D-mer ids stay below 2^32 (B^15 = 2^30 for B = 4)
+constexpr uint64_t kKtabMaxEntries = 1ull << 31;  // 8 GiB of offsets at most
 constexpr double kKtabItems = 268435456.0;  // 2^28 intervals (2 GiB)
 constexpr uint32_t kKtabMinDepth = 2;
+// ... and no deeper than B^(K-1) <= kKtabOver * N: most longer D-mers do not occur
+constexpr double kKtabOver = 4.0;
 // levels2() result meaning "the batch needs the ordered path"
 constexpr uint32_t kNeedOrdered = 0xFFFFFFFFu;
 
@@ -158,6 +161,7 @@ struct Engine {
     uint64_t ktab_items = 0;
     uint64_t ktab_entries = 0;  // B^ktab_depth
     bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
+    bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // levels2() capture mode (table build): the items of the deepest depth <= K whose
@@ -606,9 +610,10 @@ struct Engine {
         K = std::min(K, 16u);  // a search reads a node's D-mer from its sorted key chunk 0 (>= 16 symbols)
         if (B < 1 || K < 2) return;
         auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
-        // no deeper than B^K <= B*N: most longer D-mers do not occur at all
+        // no deeper than B^(K-1) <= kKtabOver*N: most longer D-mers do not occur at all
         const uint64_t max_entries = (uint64_t)env_double("EDSBWT_KTAB_ENTRIES", (double)kKtabMaxEntries);
-        while (K > 2 && (pw(K) > max_entries || pw(K - 1) > (uint64_t)N)) K--;
+        const double over = env_double("EDSBWT_KTAB_OVER", kKtabOver);
+        while (K > 2 && (pw(K) > max_entries || (double)pw(K - 1) > over * (double)N)) K--;
         if (pw(K) > max_entries) return;
         const uint64_t P = pw(K);
         DBuf<uint8_t> kb;
@@ -647,10 +652,11 @@ struct Engine {
         tmp.ensure(tb);
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, (int)n, 0, endbit, stream));
         sync_check(nullptr, "hipcub call at engine.hip:624");
-        ktab_off.ensure(E + 1);
+        ktab_off.ensure(E + 2);  // [E, E+1): the empty list of D-mers outside the alphabet (direct start)
         ktab_b.ensure(n);
         ktab_e.ensure(n);
         launch(KC_TABLE, k_ktab_bounds, E + 1, E, (const uint64_t*)k2.p, n, ktab_off.p);
+        HIPCHK(hipMemcpyAsync(ktab_off.p + E + 1, ktab_off.p + E, 4, hipMemcpyDeviceToDevice, stream));
         launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, ktab_b.p);
         HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
@@ -673,7 +679,8 @@ struct Engine {
         const uint64_t nblk = (uint64_t)N / kOccRows + 1;
         DBuf<uint32_t> bcnt;
         bcnt.ensure(nblk);
-        launch(KC_TABLE, k_samp_blocks, nblk, nblk, N, (const uint32_t*)offt.p, kSampleShift, occ.p, bcnt.p);
+        const uint32_t shift = std::min(8u, (uint32_t)env_double("EDSBWT_SAMPLE_SHIFT", kSampleShift));  // tuning knob
+        launch(KC_TABLE, k_samp_blocks, nblk, nblk, N, (const uint32_t*)offt.p, shift, occ.p, bcnt.p);
         DBuf<uint32_t> bbase;
         const uint32_t ns = scan_u32(bcnt.p, bbase, nblk);  // bbase[0..nblk], total read back
         if (ns < W) throw Fail(EDSBWT_E_FORMAT, "locate samples: fewer sampled rows than words");
@@ -969,7 +976,9 @@ struct Engine {
     uint32_t run_deep(uint32_t d, uint32_t M, uint64_t P, uint64_t active, const uint8_t* d_bytes, const uint64_t* d_off,
                       const uint32_t* nid_d, const uint32_t* goff, const uint32_t* gend, const uint32_t* gb, const uint32_t* gee,
                       uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig,
-                      const uint64_t* k0 = nullptr, const uint64_t* krest = nullptr) {
+                      const uint64_t* k0 = nullptr, const uint64_t* krest = nullptr, const uint32_t* lens = nullptr, uint32_t ind = 0) {
+        // k0/krest/lens/ind: the direct start's input-order key chunks and lengths (ind: read
+        // through perm); by default the trie's sorted chunks and slen
         const KIdx X = kidx();
         const uint32_t D = d + 1;
         DBuf<uint32_t>& ovf = tflag;  // per sorted pattern
@@ -988,8 +997,9 @@ struct Engine {
         if (!k0) {
             k0 = sorted_chunk(1, P);
             krest = skey.p;
+            lens = slen.p;
         }
-        launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, (const uint32_t*)slen.p, (const uint32_t*)perm.p, k0, krest,
+        launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
                nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
@@ -997,8 +1007,8 @@ struct Engine {
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
-        launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, (const uint32_t*)slen.p,
-               (const uint32_t*)perm.p, k0, krest, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
+        launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
+               (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace)
@@ -1016,7 +1026,7 @@ struct Engine {
             zero(ovf2.p, P * 4);
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
-            launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, (const uint32_t*)todo.p, nw, (const uint32_t*)slen.p, (const uint32_t*)perm.p,
+            launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, (const uint32_t*)todo.p, nw, lens, (const uint32_t*)perm.p, ind,
                    d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf2.p);
             abase += (uint64_t)nw * kDeepWide;
             st.deep_overflow += nw;
@@ -1062,16 +1072,32 @@ struct Engine {
             launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
         if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
         nid[0].ensure(P);
-        slen.ensure(P);
         perm.ensure(P);
-        launch(KC_NODES, bps == 3 ? k_ktab_direct<3> : k_ktab_direct<4>, P, P, D0, sigma - 1, (const uint64_t*)keys.p, (const uint32_t*)len.p,
-               nid[0].p, slen.p);
-        launch(KC_NODES, k_iota, P, perm.p, P);
+        const uint32_t E = (uint32_t)ktab_entries;
+        if (direct_sort) {
+            nid[1].ensure(P);
+            perm2.ensure(P);
+        }
+        uint32_t* kid = direct_sort ? nid[1].p : nid[0].p;
+        launch(KC_NODES, bps == 3 ? k_ktab_direct<3> : k_ktab_direct<4>, P, P, D0, sigma - 1, E, (const uint64_t*)keys.p, kid);
+        launch(KC_NODES, k_iota, P, direct_sort ? perm2.p : perm.p, P);
+        if (direct_sort) {
+            // patterns ordered by D-mer: a wave's lanes share their table lists and the rows of
+            // their first steps (their lengths and key chunks stay in input order, read via perm)
+            size_t tb = 0;
+            const int endbit = (int)bits_for(E);
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, perm2.p, perm.p, (int)P, 0, endbit, stream));
+            tmp.ensure(tb);
+            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, perm2.p, perm.p, (int)P, 0, endbit, stream)); });
+            sync_check(nullptr, "hipcub call in direct()");
+        }
         st.start_depth = D0;
-        if (trace) std::fprintf(stderr, "[edsbwt] direct start at depth %u from the k-mer table: %llu patterns\n", D0, (unsigned long long)P);
-        // chunk c of pattern i is keys[c*P + i]: chunk 0 and then chunks 1.. as k_deep reads them
+        if (trace)
+            std::fprintf(stderr, "[edsbwt] direct start at depth %u from the k-mer table: %llu patterns%s\n", D0, (unsigned long long)P,
+                         direct_sort ? ", sorted by D-mer" : "");
+        // chunk c of input pattern j is keys[c*P + j]: chunk 0 and then chunks 1.. as k_deep reads them
         return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
-                        ktab_b.p, ktab_e.p, r_off, r_cnt, r_occ, abase, ovf_orig, keys.p, keys.p + P);
+                        ktab_b.p, ktab_e.p, r_off, r_cnt, r_occ, abase, ovf_orig, keys.p, keys.p + P, len.p, direct_sort ? 1u : 0u);
     }
 
     // Order-free level walk (default): a depth's lists are unordered (node, b, e)

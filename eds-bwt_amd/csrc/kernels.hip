@@ -802,7 +802,7 @@ struct SymReader {
 // sharded like the item appends (region s at s*qcap, counter s at qcnt[s*32]).
 template <int BPS>
 __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
-                                                   const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest,
+                                                   const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind,
                                                    const uint32_t* __restrict__ nid,
                                                    const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
                                                    const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
@@ -816,7 +816,9 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
     UNIFORM_STRIDE(i, valid, P) {
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
-        const uint32_t L = valid ? slen[i] : 0u;
+        // ind: slen and the key chunks are in input order, pattern i (sorted) is input perm[i]
+        const uint32_t pi = valid && ind ? perm[i] : (uint32_t)i;
+        const uint32_t L = valid ? slen[pi] : 0u;
         const uint32_t u = L > D0 ? nid[i] : 0u;
         const uint32_t n0 = L > D0 ? iend[u] - ioff[u] : 0u;
         if (n0 > 1) {
@@ -824,7 +826,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             w = make_uint4((uint32_t)i, D0, ~0u, 0u);
         } else if (n0 == 1) {
             uint32_t b = ib[ioff[u]], e = ie[ioff[u]];
-            SymReader<BPS> sym{k0, krest, P, i};
+            SymReader<BPS> sym{k0, krest, P, pi};
             bool alive = true;
             uint32_t d = D0;
             for (; d < L; d++) {
@@ -872,7 +874,7 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
 template <int K, int BPS>
 __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
-                                              const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint64_t P,
+                                              const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind, uint64_t P,
                                               const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
                                               const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
@@ -895,7 +897,8 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
         }
         const uint4 w = q[(size_t)lo * qcap + ((uint32_t)j - spre[lo])];
         const uint32_t i = w.x, d0 = w.y;
-        const uint32_t L = slen[i];
+        const uint32_t pi = ind ? perm[i] : i;  // slen and key chunks in input order (k_deep_fast)
+        const uint32_t L = slen[pi];
         uint32_t cb[K], ce[K];
         uint32_t cn;
         if (w.z == ~0u) {  // from the node's items at the cutover depth
@@ -914,7 +917,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             cb[0] = w.z;
             ce[0] = w.w;
         }
-        SymReader<BPS> sym{k0, krest, P, i};
+        SymReader<BPS> sym{k0, krest, P, pi};
         bool over = false;
         for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
@@ -1059,7 +1062,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
 // in private (scratch) arrays, one thread per flagged pattern.  Rare, so plain loops.
 template <int KW>
 __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, const uint32_t* __restrict__ todo, uint32_t ntodo,
-                                                  const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
+                                                  const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm, uint32_t ind,
                                                   const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
                                                   const uint8_t* __restrict__ code_of, const uint32_t* __restrict__ nid,
                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
@@ -1070,7 +1073,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
     (void)P;
     GRID_STRIDE(j, ntodo) {
         const uint32_t i = todo[j];
-        const uint32_t L = slen[i];
+        const uint32_t L = slen[ind ? perm[i] : i];
         const uint32_t u = nid[i];
         const uint32_t n0 = iend[u] - ioff[u];
         if (n0 > KW) { ovf2[i] = 1; continue; }
@@ -1907,13 +1910,12 @@ __global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t*
 }
 
 // direct start (every pattern longer than D): pattern i's D-mer straight from its own
-// (unsorted) key chunk 0, as k_ktab_count reads a node's; k_deep then takes the table's
+// key chunk 0 (input order), as k_ktab_count reads a node's; k_deep then takes the table's
 // list [toff[kid[i]], toff[kid[i]+1]) as the pattern's items of depth D.  A D-mer holding
-// '#' or a byte outside the alphabet has no list: slen = 0 keeps k_deep off the pattern
-// (its count stays 0).
+// '#' or a byte outside the alphabet has no list: kid = E (= B^D), whose list
+// [toff[E], toff[E+1]) is empty, so the pattern's count stays 0.
 template <int BPS>
-__global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, const uint64_t* __restrict__ k0, const uint32_t* __restrict__ len,
-                              uint32_t* __restrict__ kid, uint32_t* __restrict__ slen) {
+__global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, uint32_t E, const uint64_t* __restrict__ k0, uint32_t* __restrict__ kid) {
     constexpr uint32_t SPC = 64 / BPS;
     GRID_STRIDE(i, P) {
         const uint64_t key = k0[i];
@@ -1925,8 +1927,7 @@ __global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, const uint64_t
             x += (v - 2) * mul;
             mul *= B;
         }
-        kid[i] = ok ? x : 0u;
-        slen[i] = ok ? len[i] : 0u;
+        kid[i] = ok ? x : E;
     }
 }
 

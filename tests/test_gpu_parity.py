@@ -301,8 +301,14 @@ def test_kmer_start_table_gpu(oracle, edsbwt, tmp_path, monkeypatch, seed):
     pats = [edsgen.planted(rng, segs, rng.randint(D + 1, D + 20)) or "ACGT" * 8 for _ in range(800)]
     pats += ["".join(rng.choice(alphabet + "N") for _ in range(rng.randint(D + 1, 40))) for _ in range(400)]
     pats += ["N" * (D + 1), "ACGT" * 10 + "X"]  # a byte outside the alphabet inside / before the last D
-    _compare(oracle, edsbwt, base, pats, table_too=seed == 0)
+    oc, oo = _compare(oracle, edsbwt, base, pats, table_too=seed == 0)
     buf, offs = _pack(pats)
+    monkeypatch.setenv("EDSBWT_DIRECT_SORT", "0")  # direct start in input order
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert idx.stats()["trie_nodes"] == 0
+    monkeypatch.delenv("EDSBWT_DIRECT_SORT")
     with edsbwt.Index(base) as idx:
         idx.search((buf, offs))
         assert idx.stats()["start_depth"] == D
