@@ -25,7 +25,10 @@ import os
 # bench.py kernel class -> kernels (engine.hip KClass)
 CLASSES = {
     "step": ("k_lvl_items", "k_lvl_dollar"),
-    "deep": ("k_deep", "k_deep_wide"),
+    # every kernel the engine launches under KC_DEEP (engine.hip), so the rocprof
+    # average per launch is comparable with bench.py's event-timed class average
+    "deep": ("k_deep_fast", "k_deep", "k_deep_wide", "k_list_flagged", "k_ovf_lens",
+             "k_group_end", "k_group_count", "k_group_scatter", "k_sub_build", "k_sub_bytes", "k_sub_scatter"),
     "locate": ("k_locate",),
 }
 FETCH_FACTOR_GATHER64 = 1.0
