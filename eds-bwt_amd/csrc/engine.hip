@@ -164,6 +164,10 @@ struct Engine {
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
+    // pair blocks (build_pairs): two backward steps per rank line in k_deep_fast (sigma <= 5)
+    DBuf<PairBlock> pocc;
+    uint32_t PC[kPairCodes + 3] = {0};
+    bool use_pairs = true;  // per search (EDSBWT_NO_PAIRS clears it)
     // levels2() capture mode (table build): the items of the deepest depth <= K whose
     // count fits the budget, as (D-mer index, b, e)
     struct Capture {
@@ -270,6 +274,8 @@ struct Engine {
         X.segbits = bits_for(S);
         X.rowbits = bits_for(N);
         for (int c = 0; c < 8; c++) X.C[c] = C[c];
+        X.pocc = use_pairs && pocc.p ? pocc.p : nullptr;
+        for (uint32_t k = 0; k < kPairCodes + 3; k++) X.PC[k] = PC[k];
         return X;
     }
 
@@ -596,7 +602,41 @@ struct Engine {
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
+        if (env_double("EDSBWT_PAIRS", 1.0) != 0.0) build_pairs();
         build_ktab();
+    }
+
+    // Pair blocks (kernels.h PairBlock): the code of (L[x], L[LF(x)]) of every row, bit-sliced
+    // per 64 rows with block-start counts, and PC[p], the first row of the suffixes c2 c1 ...
+    // (C[c2] + rank_c2(L, C[c1])).  2 B per row; only for sigma <= 5 (codes fit 5 bits and the
+    // counts one 128-B line).
+    void build_pairs() {
+        if (sigma > 5 || sigma < 2 || kOccRows != 64) return;
+        const uint32_t nc = 1 + (sigma - 1) * sigma;
+        const uint64_t nblk = (uint64_t)N / 64 + 1, nrows = nblk * 64;
+        if ((uint64_t)nc * nblk > 0x7fffffffull) return;  // scan_u32 bound
+        const KIdx X = kidx();
+        DBuf<uint8_t> code;
+        DBuf<uint32_t> cnt, cscan;
+        code.ensure(nrows);
+        cnt.ensure((size_t)nc * nblk);
+        launch(KC_TABLE, k_pair_codes, nrows, nrows, X, code.p);
+        launch(KC_TABLE, k_pair_counts, nrows, nblk, (const uint8_t*)code.p, nc, cnt.p);
+        scan_u32(cnt.p, cscan, (size_t)nc * nblk);
+        cnt.release();
+        pocc.ensure(nblk);
+        launch(KC_TABLE, k_pair_fill, nrows, nblk, (const uint8_t*)code.p, nc, (const uint32_t*)cscan.p, pocc.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        device_bytes += nblk * sizeof(PairBlock);
+        // PC from the ranks at the pile starts
+        std::vector<uint32_t> rk((size_t)sigma * sigma);
+        DBuf<uint32_t> d_rk;
+        d_rk.ensure(rk.size());
+        launch(KC_TABLE, k_pile_ranks, 1, X, d_rk.p);
+        HIPCHK(hipMemcpyAsync(rk.data(), d_rk.p, rk.size() * 4, hipMemcpyDeviceToHost, stream));  // the stream is non-blocking
+        HIPCHK(hipStreamSynchronize(stream));
+        for (uint32_t c1 = 1; c1 < sigma; c1++)
+            for (uint32_t c2 = 0; c2 < sigma; c2++) PC[1 + (c1 - 1) * sigma + c2] = C[c2] + rk[(size_t)c1 * sigma + c2];
     }
 
     // k-mer start table: the order-free walk run once over every K-mer of the non-'#'
@@ -1500,6 +1540,7 @@ struct Engine {
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
         no_wide = (flags & EDSBWT_NO_WIDE) != 0;
         use_ktab = (flags & EDSBWT_NO_KTAB) == 0;
+        use_pairs = (flags & EDSBWT_NO_PAIRS) == 0 && env_double("EDSBWT_NO_PAIRS", 0) == 0;
         use_direct = (flags & EDSBWT_NO_DIRECT) == 0 && env_double("EDSBWT_NO_DIRECT", 0) == 0;
         if (use_table) build_table();
         st.patterns = P;
@@ -1685,6 +1726,7 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
     info->device_bytes = E.device_bytes;
     info->ktab_depth = E.ktab_depth;
     info->ktab_items = E.ktab_items;
+    info->pair_blocks = E.pocc.p != nullptr;
     return 0;
 }
 

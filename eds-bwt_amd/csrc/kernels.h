@@ -35,6 +35,19 @@ static_assert(sizeof(OccBlock) == 64, "occ block must be 64 B");
 #endif
 constexpr uint32_t kOccRows = 1u << kOccShift;
 
+// Two-step rank block ("pair block", 128 B per 64 rows, sigma <= 5): each row x carries the
+// pair code of (L[x], L[LF(x)]) — 0 when L[x] = '#', else 1 + (L[x]-1)*sigma + L[LF(x)] —
+// bit-sliced in 5 planes, and cnt[k] = rows before the block with code k.  Rows of the
+// suffixes c2 c1 Q are [PC[p] + rank_p(b), PC[p] + rank_p(e+1)) for p = (c1, c2) and Q's
+// rows [b, e], so one line answers two backward steps; rank of (c1, '#') tells whether
+// the intermediate interval holds '#' rows (a link), rank of code 0 whether [b, e] does.
+constexpr uint32_t kPairCodes = 21;  // sigma = 5: 1 + 4 * 5
+struct alignas(128) PairBlock {
+    uint64_t plane[5];
+    uint32_t cnt[22];
+};
+static_assert(sizeof(PairBlock) == 128, "pair block must be one 128-B line");
+
 // kernel-side view of the device index (passed by value)
 struct KIdx {
     const OccBlock* occ;       // ceil((N+1)/256) blocks
@@ -54,6 +67,8 @@ struct KIdx {
     uint32_t segbits;          // bits of a segment id (1..S): link keys are node << segbits | segment
     uint32_t rowbits;          // bits of a BWT row (< N): finisher keys are node << rowbits | row
     uint32_t C[8];             // first row of each pile
+    const PairBlock* pocc;     // two-step rank blocks (nullptr: not built)
+    uint32_t PC[kPairCodes + 3];  // first row of the suffixes c2 c1 ... for pair code p = (c1, c2)
 };
 
 }  // namespace edsbwt

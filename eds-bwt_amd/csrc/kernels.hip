@@ -215,6 +215,41 @@ __device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ,
 }
 #endif
 
+// pair block at one interval end: the planes and the counts of codes 0 ('#' rows), p and q
+struct PairV {
+    uint64_t pl[5];
+    uint32_t c0, cp, cq;
+};
+__device__ __forceinline__ PairV pair_load(const PairBlock* __restrict__ pb, uint32_t blk, uint32_t p, uint32_t q) {
+    const PairBlock* B = pb + blk;
+    const uint4* v = reinterpret_cast<const uint4*>(B);
+    const uint4 a = v[0], b = v[1];
+    const uint2 c = reinterpret_cast<const uint2*>(B)[4];
+    PairV o;
+    o.pl[0] = (uint64_t)a.y << 32 | a.x;
+    o.pl[1] = (uint64_t)a.w << 32 | a.z;
+    o.pl[2] = (uint64_t)b.y << 32 | b.x;
+    o.pl[3] = (uint64_t)b.w << 32 | b.z;
+    o.pl[4] = (uint64_t)c.y << 32 | c.x;
+    o.c0 = B->cnt[0];
+    o.cp = B->cnt[p];
+    o.cq = B->cnt[q];
+    return o;
+}
+__device__ __forceinline__ uint64_t pair_match(const PairV& v, uint32_t k) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < 5; j++) m &= ((k >> j) & 1u) ? v.pl[j] : ~v.pl[j];
+    return m;
+}
+// ranks of codes 0, p, q at row x (rows [0, x) counted)
+__device__ __forceinline__ void pair_rank_v(const PairV& v, uint32_t x, uint32_t p, uint32_t q, uint32_t& h, uint32_t& rp, uint32_t& rq) {
+    const uint64_t m = (1ull << (x & 63u)) - 1ull;
+    h = v.c0 + (uint32_t)__popcll(pair_match(v, 0) & m);
+    rp = v.cp + (uint32_t)__popcll(pair_match(v, p) & m);
+    rq = v.cq + (uint32_t)__popcll(pair_match(v, q) & m);
+}
+
 #define GRID_STRIDE(i, n) for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(n); i += (size_t)gridDim.x * blockDim.x)
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -829,9 +864,36 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             SymReader<BPS> sym{k0, krest, P, pi};
             bool alive = true;
             uint32_t d = D0;
+            bool pair_skip = false;  // the pair step just found '#' rows after its first step
             for (; d < L; d++) {
                 const uint32_t c = sym.code(d);
                 if (c >= X.sigma) { alive = false; break; }
+                // two characters from one pair-block line per interval end, when neither
+                // [b, e] nor the interval between the two steps holds '#' rows and the
+                // pattern survives both; otherwise the single step below decides
+                if (X.pocc && !pair_skip && d + 1 < L && c != 0) {
+                    const uint32_t c2 = sym.code(d + 1);
+                    if (c2 != 0 && c2 < X.sigma) {
+                        const uint32_t q = 1 + (c - 1) * X.sigma, p = q + c2;
+                        const bool same = (b >> 6) == ((e + 1) >> 6);
+                        const PairV v0 = pair_load(X.pocc, b >> 6, p, q);
+                        const PairV v1 = pair_load(X.pocc, (e + 1) >> 6, p, q);
+                        uint32_t h0, p0, q0, h1, p1, q1;
+                        pair_rank_v(v0, b, p, q, h0, p0, q0);
+                        pair_rank_v(v1, e + 1, p, q, h1, p1, q1);
+                        n_blk += same ? 1 : 2;
+                        if (h1 == h0 && q1 == q0 && p1 > p0) {
+                            n_steps += 2;
+                            b = X.PC[p] + p0;
+                            e = X.PC[p] + p1 - 1;
+                            d++;
+                            continue;
+                        }
+                        pair_skip = h1 == h0 && q1 > q0;
+                    }
+                } else {
+                    pair_skip = false;
+                }
                 uint32_t h0, h1, sb, se;
                 n_blk += 2 - rank2_pair(X.occ, b, e + 1, c, h0, sb, h1, se);
                 if (h1 > h0) { want = 1; break; }  // '#' rows: the link needs k_deep
@@ -1733,6 +1795,66 @@ __global__ void k_gather_rec(uint64_t n, const uint32_t* __restrict__ idx, const
 }
 
 // ------------------------------------------------- DA/OFF table (index open)
+// ------------------------------------------------------------ pair blocks (index open)
+// pair code of every row (kernels.h PairBlock); 31 for the padding rows past N
+__global__ void k_pair_codes(uint64_t nrows, KIdx X, uint8_t* __restrict__ code) {
+    GRID_STRIDE(x, nrows) {
+        uint32_t k = 31;
+        if (x < X.N) {
+            uint32_t r;
+            const uint32_t c1 = sym_rank(X.occ, (uint32_t)x, &r);
+            if (c1 == 0) {
+                k = 0;
+            } else {
+                uint32_t r2;
+                const uint32_t c2 = sym_rank(X.occ, X.C[c1] + r, &r2);  // L[LF(x)]
+                k = 1 + (c1 - 1) * X.sigma + c2;
+            }
+        }
+        code[x] = (uint8_t)k;
+    }
+}
+
+// rank of every symbol at every pile start: out[c1 * sigma + c2] = rank_c2(L, C[c1])
+__global__ void k_pile_ranks(KIdx X, uint32_t* __restrict__ out) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (uint32_t c1 = 0; c1 < X.sigma; c1++) {
+            uint32_t r[8];
+            rank_all(X.occ, X.C[c1], X.sigma, r);
+            for (uint32_t c2 = 0; c2 < X.sigma; c2++) out[c1 * X.sigma + c2] = r[c2];
+        }
+}
+
+// one wave per 64-row block: rows of each code, code-major ([k * nblk + blk])
+__global__ void k_pair_counts(uint64_t nblk, const uint8_t* __restrict__ code, uint32_t nc, uint32_t* __restrict__ cnt) {
+    GRID_STRIDE(t, nblk * 64) {  // wave-uniform: nblk * 64 and the stride are multiples of 64
+        const uint64_t blk = t >> 6;
+        const uint32_t lane = (uint32_t)(t & 63), k = code[t];
+        for (uint32_t j = 0; j < nc; j++) {
+            const uint32_t n = (uint32_t)__popcll(__ballot(k == j));
+            if (lane == j) cnt[(size_t)j * nblk + blk] = n;
+        }
+    }
+}
+
+// planes and block-start counts; scan = scan_u32 of the code-major counts (scan[0] = 0)
+__global__ void k_pair_fill(uint64_t nblk, const uint8_t* __restrict__ code, uint32_t nc, const uint32_t* __restrict__ scan,
+                            PairBlock* __restrict__ pb) {
+    GRID_STRIDE(t, nblk * 64) {
+        const uint64_t blk = t >> 6;
+        const uint32_t lane = (uint32_t)(t & 63), k = code[t];
+        uint64_t pl = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++) {
+            const uint64_t v = __ballot((k >> j) & 1u);
+            if (lane == j) pl = v;
+        }
+        PairBlock* B = pb + blk;
+        if (lane < 5) B->plane[lane] = pl;
+        if (lane < 22) B->cnt[lane] = lane < nc ? scan[(size_t)lane * nblk + blk] - scan[(size_t)lane * nblk] : 0u;
+    }
+}
+
 // For every word w, walk LF from row w (its '#'-suffix) to the row with L='#'
 // (position 0): rows visited get DA = w and their distance from the word end.
 // segment link table (index open): for s >= 2 the c-ranks at both ends of the words of

@@ -57,6 +57,8 @@ enum {
                                     table's depth (tests: same results either way) */
 #define EDSBWT_NO_DIRECT    0x800u/* build the reversed-pattern trie even when every pattern could
                                     start straight from its k-mer table list (tests: same results) */
+#define EDSBWT_NO_PAIRS     0x1000u/* deep walk one character per rank line instead of two from the
+                                    pair blocks (sigma <= 5; tests: same results) */
 
 typedef struct edsbwt_index edsbwt_index;
 
@@ -76,7 +78,7 @@ typedef struct {
     uint64_t device_bytes;/* HBM held by the index */
     uint32_t ktab_depth;  /* k-mer start table: depth D (0 = none) — the interval lists of
                              every D-mer over the non-'#' symbols, built at open */
-    uint32_t pad;
+    uint32_t pair_blocks; /* 1 when the two-step rank blocks are built (sigma <= 5) */
     uint64_t ktab_items;  /* intervals held by that table */
 } edsbwt_index_info;
 

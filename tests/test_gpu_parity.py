@@ -55,6 +55,8 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         assert idx.stats()["start_depth"] == 0
         gt, got = idx.search((buf, offs), direct=False)   # trie seeded from the table, never the direct start
         assert np.array_equal(gt, oc) and np.array_equal(got, oo)
+        gp, gop = idx.search((buf, offs), pairs=False)   # one character per rank line in k_deep_fast
+        assert np.array_equal(gp, oc) and np.array_equal(gop, oo)
         for deep in (True, False):                       # reference-ordered lists at every depth
             gc5, go5 = idx.search((buf, offs), ordered=True, deep=deep)
             assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
@@ -317,3 +319,43 @@ def test_kmer_start_table_gpu(oracle, edsbwt, tmp_path, monkeypatch, seed):
         assert idx.stats()["start_depth"] == D and idx.stats()["trie_nodes"] > 0
         idx.search((buf, offs), ordered=True)  # the ordered path never uses the table
         assert idx.stats()["start_depth"] == 0
+
+
+def _covid_like(rng, nseg):
+    """Solid segments (one long string) alternating with short variant segments, some
+    holding the empty word: the shape of BASELINE config C3 at test size."""
+    segs = []
+    for t in range(nseg):
+        if t % 2 == 0:
+            segs.append(["".join(rng.choice("ACGT") for _ in range(rng.randint(40, 120)))])
+        else:
+            segs.append(["" if rng.random() < 0.1 else "".join(rng.choice("ACGT") for _ in range(rng.randint(1, 3)))
+                         for _ in range(rng.randint(2, 4))])
+    return segs
+
+
+def test_pair_blocks_gpu(oracle, edsbwt, tmp_path):
+    """Two backward steps per pair-block line (k_deep_fast): planted and random 31-mers,
+    odd and even remaining lengths, patterns that die between the two steps and ones
+    that meet '#' rows after the first — identical counts, records and step counts with
+    the pair blocks on and off, and equal to the oracle."""
+    rng = random.Random(355)
+    segs = _covid_like(rng, 800)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.choice([20, 21, 31, 32, 40, 47])) or "ACGT" * 8 for _ in range(3000)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.choice([18, 19, 31]))) for _ in range(1000)]
+    buf, offs = _pack(pats)
+    eng = oracle.Engine(base, 8)
+    oc, oo, _ = eng.search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        assert idx.pair_blocks
+        for direct in (True, False):
+            gc, go = idx.search((buf, offs), direct=direct)
+            assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+            st_on = idx.stats()
+            gc2, go2 = idx.search((buf, offs), direct=direct, pairs=False)
+            assert np.array_equal(gc2, oc) and np.array_equal(go2, oo)
+            st_off = idx.stats()
+            assert st_on["intervals_stepped"] == st_off["intervals_stepped"]
