@@ -162,6 +162,8 @@ struct Engine {
     uint64_t ktab_entries = 0;  // B^ktab_depth
     bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
+    bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
+    DBuf<uint64_t> pv_in, pv_out;
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // pair blocks (build_pairs): two backward steps per rank line in k_deep_fast (sigma <= 5)
@@ -1016,9 +1018,11 @@ struct Engine {
     uint32_t run_deep(uint32_t d, uint32_t M, uint64_t P, uint64_t active, const uint8_t* d_bytes, const uint64_t* d_off,
                       const uint32_t* nid_d, const uint32_t* goff, const uint32_t* gend, const uint32_t* gb, const uint32_t* gee,
                       uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig,
-                      const uint64_t* k0 = nullptr, const uint64_t* krest = nullptr, const uint32_t* lens = nullptr, uint32_t ind = 0) {
+                      const uint64_t* k0 = nullptr, const uint64_t* krest = nullptr, const uint32_t* lens = nullptr, uint32_t ind = 0,
+                      const uint64_t* pv = nullptr) {
         // k0/krest/lens/ind: the direct start's input-order key chunks and lengths (ind: read
-        // through perm); by default the trie's sorted chunks and slen
+        // through perm); by default the trie's sorted chunks and slen.  pv: the packed direct
+        // start (k_ktab_direct), from which k_deep_fast also writes perm
         const KIdx X = kidx();
         const uint32_t D = d + 1;
         DBuf<uint32_t>& ovf = tflag;  // per sorted pattern
@@ -1040,7 +1044,7 @@ struct Engine {
             lens = slen.p;
         }
         launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
-               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p);
+               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
@@ -1119,7 +1123,26 @@ struct Engine {
             perm2.ensure(P);
         }
         uint32_t* kid = direct_sort ? nid[1].p : nid[0].p;
-        launch(KC_NODES, bps == 3 ? k_ktab_direct<3> : k_ktab_direct<4>, P, P, D0, sigma - 1, E, (const uint64_t*)keys.p, kid);
+        // packed start: each pattern's input index and remaining symbols travel through the
+        // D-mer sort as its value, so k_deep_fast reads no key chunks or lengths at random
+        const bool packed = direct_sort && use_packed && sigma - 1 <= 4 && Lmax - D0 <= 16 && bps == 3;
+        if (packed) {
+            pv_in.ensure(P);
+            pv_out.ensure(P);
+        }
+        launch(KC_NODES, bps == 3 ? k_ktab_direct<3> : k_ktab_direct<4>, P, P, D0, sigma - 1, E, (const uint64_t*)keys.p,
+               (const uint64_t*)(keys.p + P), kid, packed ? pv_in.p : (uint64_t*)nullptr);
+        if (packed) {
+            size_t tb = 0;
+            const int endbit = (int)bits_for(E);
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, 0, endbit, stream));
+            tmp.ensure(tb);
+            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, 0, endbit, stream)); });
+            sync_check(nullptr, "hipcub call in direct() (packed)");
+            st.start_depth = D0;
+            return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
+                            ktab_b.p, ktab_e.p, r_off, r_cnt, r_occ, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_out.p);
+        }
         launch(KC_NODES, k_iota, P, direct_sort ? perm2.p : perm.p, P);
         if (direct_sort) {
             // patterns ordered by D-mer: a wave's lanes share their table lists and the rows of

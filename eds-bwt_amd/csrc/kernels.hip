@@ -844,16 +844,29 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    uint32_t K, uint32_t* __restrict__ ab, uint32_t* __restrict__ ae,
                                                    uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
-                                                   unsigned long long* __restrict__ ctr) {
+                                                   unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
+                                                   uint32_t* __restrict__ perm_out) {
     unsigned long long n_steps = 0, n_blk = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     UNIFORM_STRIDE(i, valid, P) {
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
-        // ind: slen and the key chunks are in input order, pattern i (sorted) is input perm[i]
-        const uint32_t pi = valid && ind ? perm[i] : (uint32_t)i;
-        const uint32_t L = valid ? slen[pi] : 0u;
+        // ind: slen and the key chunks are in input order, pattern i (sorted) is input perm[i].
+        // pv (packed direct start): input index and remaining symbols sorted along with the
+        // D-mers, so neither slen nor the key chunks are read; perm is written for k_deep
+        uint32_t pi, L;
+        uint64_t rem = 0;
+        if (pv) {
+            const uint64_t v = valid ? pv[i] : 0ull;
+            pi = (uint32_t)(v & 0x7fffffffu);
+            rem = v >> 31;
+            L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
+            if (valid) perm_out[i] = pi;
+        } else {
+            pi = valid && ind ? perm[i] : (uint32_t)i;
+            L = valid ? slen[pi] : 0u;
+        }
         const uint32_t u = L > D0 ? nid[i] : 0u;
         const uint32_t n0 = L > D0 ? iend[u] - ioff[u] : 0u;
         if (n0 > 1) {
@@ -862,17 +875,20 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
         } else if (n0 == 1) {
             uint32_t b = ib[ioff[u]], e = ie[ioff[u]];
             SymReader<BPS> sym{k0, krest, P, pi};
+            auto code_at = [&](uint32_t dd) -> uint32_t {
+                return pv ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd);
+            };
             bool alive = true;
             uint32_t d = D0;
             bool pair_skip = false;  // the pair step just found '#' rows after its first step
             for (; d < L; d++) {
-                const uint32_t c = sym.code(d);
+                const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
                 // two characters from one pair-block line per interval end, when neither
                 // [b, e] nor the interval between the two steps holds '#' rows and the
                 // pattern survives both; otherwise the single step below decides
                 if (X.pocc && !pair_skip && d + 1 < L && c != 0) {
-                    const uint32_t c2 = sym.code(d + 1);
+                    const uint32_t c2 = code_at(d + 1);
                     if (c2 != 0 && c2 < X.sigma) {
                         const uint32_t q = 1 + (c - 1) * X.sigma, p = q + c2;
                         const bool same = (b >> 6) == ((e + 1) >> 6);
@@ -905,7 +921,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             if (want) {
                 w = make_uint4((uint32_t)i, d, b, e);
             } else {
-                const uint32_t o = perm[i];
+                const uint32_t o = pv ? pi : perm[i];
                 const uint64_t at = abase + (uint64_t)i * K;
                 if (alive) {
                     ab[at] = b;
@@ -2037,7 +2053,8 @@ __global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t*
 // '#' or a byte outside the alphabet has no list: kid = E (= B^D), whose list
 // [toff[E], toff[E+1]) is empty, so the pattern's count stays 0.
 template <int BPS>
-__global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, uint32_t E, const uint64_t* __restrict__ k0, uint32_t* __restrict__ kid) {
+__global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, uint32_t E, const uint64_t* __restrict__ k0,
+                              const uint64_t* __restrict__ krest, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
     constexpr uint32_t SPC = 64 / BPS;
     GRID_STRIDE(i, P) {
         const uint64_t key = k0[i];
@@ -2048,6 +2065,29 @@ __global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, uint32_t E, co
             ok &= v >= 2 && v <= B + 1;
             x += (v - 2) * mul;
             mul *= B;
+        }
+        if (pv) {
+            // packed start (B <= 4, at most 16 symbols after depth D): input index in bits
+            // [0, 31), the remaining symbols' 2-bit digits from bit 31 up, closed by a 1 bit.
+            // A symbol outside the alphabet makes the pattern unmatchable: the empty list.
+            uint64_t rem = 0;
+            uint32_t n = 0;
+            uint64_t cur = key;
+            uint32_t chunk = 0;
+            for (uint32_t t = D;; t++) {
+                const uint32_t c = t / SPC;
+                if (c != chunk) {
+                    cur = krest[(size_t)(c - 1) * P + i];
+                    chunk = c;
+                }
+                const uint32_t v = (uint32_t)(cur >> (BPS * (SPC - 1 - (t - c * SPC)))) & ((1u << BPS) - 1u);
+                if (v == 0) break;  // end of the pattern
+                ok &= v >= 2 && v <= B + 1;
+                rem |= (uint64_t)((v - 2) & 3u) << (2 * n);
+                n++;
+            }
+            rem |= 1ull << (2 * n);
+            pv[i] = rem << 31 | (uint64_t)i;
         }
         kid[i] = ok ? x : E;
     }

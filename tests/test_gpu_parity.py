@@ -359,3 +359,38 @@ def test_pair_blocks_gpu(oracle, edsbwt, tmp_path):
             assert np.array_equal(gc2, oc) and np.array_equal(go2, oo)
             st_off = idx.stats()
             assert st_on["intervals_stepped"] == st_off["intervals_stepped"]
+
+
+def test_packed_direct_start_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """Packed direct start: when every pattern is longer than the k-mer table's depth D0 by at
+    most 16 symbols, each pattern's input index and remaining symbols are sorted along with
+    its D-mer (k_ktab_direct) and k_deep_fast reads neither lengths nor key chunks.  Patterns
+    with a symbol outside the alphabet after D0 take the empty list.  Same results as the
+    unpacked direct start and the oracle."""
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")  # small tables hold long lists
+    rng = random.Random(4096)
+    segs = _covid_like(rng, 600)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    assert D0 >= 2
+    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(3000)]
+    pats = [p[: D0 + 16] if len(p) > D0 + 16 else p for p in pats]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(D0 + 1, D0 + 16))) for _ in range(500)]
+    pats += [p[:-1] + "N" for p in pats[:50]]  # outside the alphabet: in the D-mer (read first) ...
+    pats += ["N" + p[1:] for p in pats[50:100]]  # ... and in the remaining symbols
+    buf, offs = _pack(pats)
+    eng = oracle.Engine(base, 8)
+    oc, oo, _ = eng.search(buf, offs)
+    got = {}
+    for packed in ("1", "0"):
+        monkeypatch.setenv("EDSBWT_DIRECT_PACKED", packed)
+        with edsbwt.Index(base) as idx:
+            gc, go = idx.search((buf, offs))
+            assert idx.stats()["start_depth"] == D0 and idx.stats()["trie_nodes"] == 0  # direct start
+            assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+            got[packed] = (gc, go)
+            gp, gop = idx.search((buf, offs), pairs=False)
+            assert np.array_equal(gp, oc) and np.array_equal(gop, oo)
