@@ -191,8 +191,9 @@ struct Engine {
     DBuf<uint64_t> lkeys, lkeys2;
     DBuf<uint32_t> tcnt, toff, tb, te, tu, tflag, tscan, cb, ce, cu, mflag, mscan;
     DBuf<uint32_t> fcnt, foff, node_occ;
-    DBuf<uint32_t> ab, ae, res_cnt, res_occ;
-    DBuf<uint64_t> res_off, occ64, oscan, tc64, tscan64, tout;
+    DBuf<uint32_t> ab, ae;
+    DBuf<Res> res, sub_res, g_res;  // per-pattern results (kernels.h Res)
+    DBuf<uint64_t> occ64, oscan, tc64, tscan64, tout;
     DBuf<uint32_t> trow, tpat;
     DBuf<uint64_t> blk_first;  // per kLocRun records: the task holding the first (k_tasks -> k_locate)
     DBuf<edsbwt_occ> rec, rec2;
@@ -201,16 +202,16 @@ struct Engine {
     DBuf<unsigned long long> counters;
     DBuf<uint8_t> tmp;      // hipcub temp storage
     DBuf<unsigned long long> lhist;
-    DBuf<uint32_t> ovf_orig, ovf_scan, sub_map, sub_rcnt, sub_rocc;
-    DBuf<uint64_t> sub_len, sub_off, sub_roff;
+    DBuf<uint32_t> ovf_orig, ovf_scan, sub_map;
+    DBuf<uint64_t> sub_len, sub_off;
     DBuf<uint8_t> sub_bytes, fin;
     DBuf<uint32_t> lcnt, ck_u, ck_k, ck_e, gcnt, gfill, goff, gend, gb, gee, fv, fv2, fend, hterm;
     DBuf<uint64_t> fk, fk2, ekeys, efk;
     DBuf<uint32_t> eu, eb, ee, eck_u, eck_k, eck_e, efv, shpre;
     DBuf<uint32_t> fu, fb, fe, fpre;  // the previous depth's item shards, read in place by k_lvl_items
     // run_grouped: group of each pattern, its members as a sub-batch
-    DBuf<uint32_t> glen, gid, gflag, gscan, g_map, g_rcnt, g_rocc;
-    DBuf<uint64_t> g_len, g_off, g_roff;
+    DBuf<uint32_t> glen, gid, gflag, gscan, g_map;
+    DBuf<uint64_t> g_len, g_off;
     DBuf<uint8_t> g_bytes;
     DBuf<uint4> dq;                   // k_deep_fast -> k_deep queue (pattern, depth, b, e), sharded
     DBuf<uint32_t> dqpre;
@@ -665,7 +666,7 @@ struct Engine {
         uint64_t sym = 0;
         for (uint32_t v = 0; v < B; v++) sym |= (uint64_t)alpha[v + 1] << (8 * v);
         launch(KC_TABLE, k_kmer_batch, P, P, K, B, sym, kb.p, ko.p);
-        res_off.ensure(P); res_cnt.ensure(P); res_occ.ensure(P); ovf_orig.ensure(P);
+        res.ensure(P); ovf_orig.ensure(P);
         zero(stats.p, kStatSlots * 8);
         Capture c;
         c.K = K; c.B = B; c.budget = budget;
@@ -674,7 +675,7 @@ struct Engine {
         count_only = true;
         uint64_t abase = 0;
         try {
-            levels2(kb.p, ko.p, P, false, res_off.p, res_cnt.p, res_occ.p, abase, ovf_orig.p);
+            levels2(kb.p, ko.p, P, false, res.p, abase, ovf_orig.p);
         } catch (const TooBig&) {
             // a depth past the budget outgrew 32-bit counts: keep what was captured
         }
@@ -855,8 +856,7 @@ struct Engine {
         return true;
     }
 
-    uint32_t levels(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, uint64_t* r_off, uint32_t* r_cnt,
-                    uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
+    uint32_t levels(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, Res* r, uint64_t& abase, uint32_t* ovf_orig) {
         const KIdx X = kidx();
         uint32_t Lmax = 0;
         std::vector<unsigned long long> hist;
@@ -892,8 +892,7 @@ struct Engine {
             if (M == 0) break;
             // the trie stopped sharing below depth d: finish every pattern alone (k_deep)
             if (allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D]) {
-                novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, ioff[cur].p, iend[cur].p, ib[cur].p, ie[cur].p, r_off, r_cnt,
-                                r_occ, abase, ovf_orig);
+                novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, ioff[cur].p, iend[cur].p, ib[cur].p, ie[cur].p, r, abase, ovf_orig);
                 break;
             }
             st.depths++;
@@ -1003,7 +1002,7 @@ struct Engine {
             }
             if (hist[D])
                 launch(KC_FINISH, k_finish, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
-                       (const uint32_t*)foff.p, (const uint32_t*)fcnt.p, (const uint32_t*)node_occ.p, abase, r_off, r_cnt, r_occ);
+                       (const uint32_t*)foff.p, (const uint32_t*)fcnt.p, (const uint32_t*)node_occ.p, abase, r);
             abase += F;
             cur = nxt;
             Mcur = M;
@@ -1017,7 +1016,7 @@ struct Engine {
     // depth-d node ([goff[u], gend[u]) in gb/ge).  Returns the overflow count.
     uint32_t run_deep(uint32_t d, uint32_t M, uint64_t P, uint64_t active, const uint8_t* d_bytes, const uint64_t* d_off,
                       const uint32_t* nid_d, const uint32_t* goff, const uint32_t* gend, const uint32_t* gb, const uint32_t* gee,
-                      uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig,
+                      Res* r, uint64_t& abase, uint32_t* ovf_orig,
                       const uint64_t* k0 = nullptr, const uint64_t* krest = nullptr, const uint32_t* lens = nullptr, uint32_t ind = 0,
                       const uint64_t* pv = nullptr) {
         // k0/krest/lens/ind: the direct start's input-order key chunks and lengths (ind: read
@@ -1044,7 +1043,7 @@ struct Engine {
             lens = slen.p;
         }
         launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
-               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r_off, r_cnt, r_occ, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p);
+               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
@@ -1052,7 +1051,7 @@ struct Engine {
                   : K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
-               (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf.p, stats.p);
+               (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace)
@@ -1071,7 +1070,7 @@ struct Engine {
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, (const uint32_t*)todo.p, nw, lens, (const uint32_t*)perm.p, ind,
-                   d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r_off, r_cnt, r_occ, ovf2.p);
+                   d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p);
             abase += (uint64_t)nw * kDeepWide;
             st.deep_overflow += nw;
             HIPCHK(hipMemcpyAsync(ovf.p, ovf2.p, P * 4, hipMemcpyDeviceToDevice, stream));
@@ -1092,7 +1091,7 @@ struct Engine {
     // kNotDirect when the batch does not qualify (nothing was written), kNeedOrdered for
     // patterns holding '#', else k_deep's overflow count as run_deep.
     static constexpr uint32_t kNotDirect = 0xFFFFFFFEu;
-    uint32_t direct(const uint64_t* d_off, const uint8_t* d_bytes, uint64_t P, uint64_t* r_off, uint32_t* r_cnt, uint32_t* r_occ,
+    uint32_t direct(const uint64_t* d_off, const uint8_t* d_bytes, uint64_t P, Res* r,
                     uint64_t& abase, uint32_t* ovf_orig) {
         if (cap || !use_ktab || !use_direct || !ktab_depth || (double)ktab_items > direct_items * (double)ktab_entries) return kNotDirect;
         if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
@@ -1141,7 +1140,7 @@ struct Engine {
             sync_check(nullptr, "hipcub call in direct() (packed)");
             st.start_depth = D0;
             return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
-                            ktab_b.p, ktab_e.p, r_off, r_cnt, r_occ, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_out.p);
+                            ktab_b.p, ktab_e.p, r, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_out.p);
         }
         launch(KC_NODES, k_iota, P, direct_sort ? perm2.p : perm.p, P);
         if (direct_sort) {
@@ -1160,7 +1159,7 @@ struct Engine {
                          direct_sort ? ", sorted by D-mer" : "");
         // chunk c of input pattern j is keys[c*P + j]: chunk 0 and then chunks 1.. as k_deep reads them
         return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
-                        ktab_b.p, ktab_e.p, r_off, r_cnt, r_occ, abase, ovf_orig, keys.p, keys.p + P, len.p, direct_sort ? 1u : 0u);
+                        ktab_b.p, ktab_e.p, r, abase, ovf_orig, keys.p, keys.p + P, len.p, direct_sort ? 1u : 0u);
     }
 
     // Order-free level walk (default): a depth's lists are unordered (node, b, e)
@@ -1168,8 +1167,7 @@ struct Engine {
     // '#' rows in the same pass; link keys are sorted per node into previous-segment
     // runs (k_run_*), which k_lvl_dollar steps.  Same outputs as levels() for
     // patterns without '#' (finished lists are sorted by row before archiving).
-    uint32_t levels2(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, uint64_t* r_off, uint32_t* r_cnt,
-                     uint32_t* r_occ, uint64_t& abase, uint32_t* ovf_orig) {
+    uint32_t levels2(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, Res* r, uint64_t& abase, uint32_t* ovf_orig) {
         const KIdx X = kidx();
         uint32_t Lmax = 0, n_term = 0;
         std::vector<unsigned long long> hist;
@@ -1245,7 +1243,7 @@ struct Engine {
                 if (d0 && d == d0) {
                     // the table's items are already grouped by node: [kt_pos[u], + kt_cnt[u])
                     launch(KC_DEEP, k_group_end, Mcur, Mcur, (const uint32_t*)kt_pos.p, (const uint32_t*)kt_cnt.p, gend.p);
-                    novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, kt_pos.p, gend.p, ib[cur].p, ie[cur].p, r_off, r_cnt, r_occ, abase,
+                    novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, kt_pos.p, gend.p, ib[cur].p, ie[cur].p, r, abase,
                                     ovf_orig);
                     break;
                 }
@@ -1260,7 +1258,7 @@ struct Engine {
                 launch(KC_DEEP, k_group_scatter, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p,
                        (const uint32_t*)goff.p, gfill.p, gb.p, gee.p);
                 launch(KC_DEEP, k_group_end, Mcur, Mcur, (const uint32_t*)goff.p, (const uint32_t*)gcnt.p, gend.p);
-                novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, goff.p, gend.p, gb.p, gee.p, r_off, r_cnt, r_occ, abase, ovf_orig);
+                novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, goff.p, gend.p, gb.p, gee.p, r, abase, ovf_orig);
                 break;
             }
             st.depths++;
@@ -1446,7 +1444,7 @@ struct Engine {
                     launch(KC_FINISH, k_fin_archive, F, F, (const uint64_t*)fk2.p, (const uint32_t*)fv2.p, abase, X.rowbits, ab.p, ae.p);
                 }
                 launch(KC_FINISH, k_finish2, P, P, D, (const uint32_t*)slen.p, (const uint32_t*)nid[nxt].p, (const uint32_t*)perm.p,
-                       (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r_off, r_cnt, r_occ);
+                       (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r);
                 abase += F;
             }
             cur = nxt;
@@ -1459,16 +1457,15 @@ struct Engine {
 
     // One batch: the trie walk (order-free unless patterns hold '#'), then the patterns
     // k_deep could not hold re-run through the unbounded level path.
-    void run_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, uint64_t* r_off,
-                   uint32_t* r_cnt, uint32_t* r_occ, uint64_t& abase) {
+    void run_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, Res* r, uint64_t& abase) {
         uint32_t novf = kNotDirect;
-        if (!ordered && allow_deep) novf = direct(d_off, d_bytes, P, r_off, r_cnt, r_occ, abase, ovf_orig.p);
+        if (!ordered && allow_deep) novf = direct(d_off, d_bytes, P, r, abase, ovf_orig.p);
         if (novf == kNeedOrdered) ordered = true;
         if (!ordered && novf == kNotDirect) {
-            novf = levels2(d_bytes, d_off, P, allow_deep, r_off, r_cnt, r_occ, abase, ovf_orig.p);
+            novf = levels2(d_bytes, d_off, P, allow_deep, r, abase, ovf_orig.p);
             if (novf == kNeedOrdered) ordered = true;
         }
-        if (ordered) novf = levels(d_bytes, d_off, P, allow_deep, r_off, r_cnt, r_occ, abase, ovf_orig.p);
+        if (ordered) novf = levels(d_bytes, d_off, P, allow_deep, r, abase, ovf_orig.p);
         if (!novf) return;
         // patterns k_deep could not hold: gather them and run the unbounded level path
         const uint32_t n = scan_u32(ovf_orig.p, ovf_scan, P);
@@ -1478,15 +1475,11 @@ struct Engine {
         const uint64_t nbytes = scan_u64(sub_len.p, sub_off, n);
         sub_bytes.ensure(nbytes + 1);
         launch(KC_DEEP, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)sub_map.p, d_off, (const uint64_t*)sub_off.p, d_bytes, sub_bytes.p);
-        sub_roff.ensure(n);
-        sub_rcnt.ensure(n);
-        sub_rocc.ensure(n);
-        zero(sub_rcnt.p, (size_t)n * 4);
-        zero(sub_rocc.p, (size_t)n * 4);
-        if (ordered) levels(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
-        else levels2(sub_bytes.p, sub_off.p, n, false, sub_roff.p, sub_rcnt.p, sub_rocc.p, abase, ovf_orig.p);
-        launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const uint64_t*)sub_roff.p, (const uint32_t*)sub_rcnt.p,
-               (const uint32_t*)sub_rocc.p, r_off, r_cnt, r_occ);
+        sub_res.ensure(n);
+        zero(sub_res.p, (size_t)n * sizeof(Res));
+        if (ordered) levels(sub_bytes.p, sub_off.p, n, false, sub_res.p, abase, ovf_orig.p);
+        else levels2(sub_bytes.p, sub_off.p, n, false, sub_res.p, abase, ovf_orig.p);
+        launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const Res*)sub_res.p, r);
     }
 
     // The batch as separate trie subtrees: patterns grouped by their last k characters
@@ -1494,8 +1487,7 @@ struct Engine {
     // depth's items split over the groups.  Results land in res_* as for one batch.
     void run_grouped(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, uint32_t k, uint64_t& abase) {
         abase = 0;
-        zero(res_cnt.p, P * 4);
-        zero(res_occ.p, P * 4);
+        zero(res.p, P * sizeof(Res));
         glen.ensure(P);
         gid.ensure(P);
         gflag.ensure(P);
@@ -1513,14 +1505,10 @@ struct Engine {
             const uint64_t nbytes = scan_u64(g_len.p, g_off, n);
             g_bytes.ensure(nbytes + 1);
             launch(KC_TRIE, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)g_map.p, d_off, (const uint64_t*)g_off.p, d_bytes, g_bytes.p);
-            g_roff.ensure(n);
-            g_rcnt.ensure(n);
-            g_rocc.ensure(n);
-            zero(g_rcnt.p, (size_t)n * 4);
-            zero(g_rocc.p, (size_t)n * 4);
-            run_batch(g_bytes.p, g_off.p, n, allow_deep, ordered, g_roff.p, g_rcnt.p, g_rocc.p, abase);
-            launch(KC_TRIE, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)g_map.p, (const uint64_t*)g_roff.p, (const uint32_t*)g_rcnt.p,
-                   (const uint32_t*)g_rocc.p, res_off.p, res_cnt.p, res_occ.p);
+            g_res.ensure(n);
+            zero(g_res.p, (size_t)n * sizeof(Res));
+            run_batch(g_bytes.p, g_off.p, n, allow_deep, ordered, g_res.p, abase);
+            launch(KC_TRIE, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)g_map.p, (const Res*)g_res.p, res.p);
         }
         st.search_groups = G;
     }
@@ -1573,11 +1561,8 @@ struct Engine {
         HIPCHK(hipEventCreate(&e1));
         HIPCHK(hipEventRecord(e0, stream));
         const KIdx X = kidx();
-        res_off.ensure(P);
-        res_cnt.ensure(P);
-        res_occ.ensure(P);
-        zero(res_cnt.p, P * 4);
-        zero(res_occ.p, P * 4);
+        res.ensure(P);
+        zero(res.p, P * sizeof(Res));
         zero(stats.p, kStatSlots * 8);
         ovf_orig.ensure(P);
         uint64_t abase = 0;
@@ -1586,7 +1571,7 @@ struct Engine {
         try {
             const uint32_t g0 = force_groups ? force_groups : sticky_groups;
             if (g0) run_grouped(d_bytes, d_off, P, allow_deep, ordered, g0, abase);
-            else run_batch(d_bytes, d_off, P, allow_deep, ordered, res_off.p, res_cnt.p, res_occ.p, abase);
+            else run_batch(d_bytes, d_off, P, allow_deep, ordered, res.p, abase);
         } catch (const TooBig&) {
             // a depth outgrew 32-bit counts (e.g. a 1 Gchar EDS with many empty words):
             // search the batch as separate trie subtrees, grouped by the last k characters;
@@ -1602,14 +1587,12 @@ struct Engine {
             }
         }
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
-        HIPCHK(hipMemcpyAsync(d_counts, res_occ.p, P * 4, hipMemcpyDeviceToDevice, stream));
         zero(counters.p + 1, 8);
-        launch_reduce(KC_FINISH, k_count_found, (const uint32_t*)res_occ.p, P, counters.p + 1);
+        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1);
         if (locate) {
             occ64.ensure(P);
             tc64.ensure(P);
-            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_occ.p, P, occ64.p);
-            launch(KC_LOCPREP, k_u32_to_u64, P, (const uint32_t*)res_cnt.p, P, tc64.p);
+            launch(KC_LOCPREP, k_res_scan_in, P, (const Res*)res.p, P, occ64.p, tc64.p);
             inclusive_scan_u64(occ64.p, oscan, P);
             inclusive_scan_u64(tc64.p, tscan64, P);
             HIPCHK(hipMemcpyAsync(pinned + 2, oscan.p + P, 8, hipMemcpyDeviceToHost, stream));
@@ -1628,7 +1611,7 @@ struct Engine {
             if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
                 blk_first.ensure(OCC / kLocRun + 1);
-                launch(KC_LOCPREP, k_tasks, P, P, (const uint64_t*)res_off.p, (const uint32_t*)res_cnt.p, (const uint64_t*)tscan64.p,
+                launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, (const uint64_t*)tscan64.p,
                        (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p);
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,

@@ -48,6 +48,13 @@ struct alignas(128) PairBlock {
 };
 static_assert(sizeof(PairBlock) == 128, "pair block must be one 128-B line");
 
+// per-pattern result (backwardSearch's final list): archive offset of its intervals, their
+// number and the occurrence count; one 16-B record, written with one store
+struct alignas(16) Res {
+    uint64_t off;
+    uint32_t cnt, occ;
+};
+
 // kernel-side view of the device index (passed by value)
 struct KIdx {
     const OccBlock* occ;       // ceil((N+1)/256) blocks

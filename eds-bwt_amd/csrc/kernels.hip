@@ -250,6 +250,10 @@ __device__ __forceinline__ void pair_rank_v(const PairV& v, uint32_t x, uint32_t
     rq = v.cq + (uint32_t)__popcll(pair_match(v, q) & m);
 }
 
+__device__ __forceinline__ void put_res(Res* __restrict__ r, size_t o, uint64_t off, uint32_t cnt, uint32_t occ) {
+    reinterpret_cast<uint4*>(r)[o] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), cnt, occ);
+}
+
 #define GRID_STRIDE(i, n) for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < (size_t)(n); i += (size_t)gridDim.x * blockDim.x)
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -842,7 +846,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
                                                    const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                                    uint32_t K, uint32_t* __restrict__ ab, uint32_t* __restrict__ ae,
-                                                   uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
+                                                   Res* __restrict__ res,
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
                                                    uint32_t* __restrict__ perm_out) {
@@ -927,9 +931,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                     ab[at] = b;
                     ae[at] = e;
                 }
-                res_off[o] = at;
-                res_cnt[o] = alive ? 1u : 0u;
-                res_occ[o] = alive ? e - b + 1 : 0u;
+                put_res(res, o, at, alive ? 1u : 0u, alive ? e - b + 1 : 0u);
             }
         }
         const uint32_t at = wave_append(qcnt + sh * 32, want);
@@ -956,8 +958,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
                                               const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
                                               const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
-                                              uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, uint64_t* __restrict__ res_off,
-                                              uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
+                                              uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr) {
     unsigned long long n_steps = 0, n_hash = 0, n_blk = 0;  // n_blk: occ blocks read
 #ifdef EDSBWT_DEEP_CLOCKS
@@ -1119,9 +1120,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
                 ae[at + t] = ce[t];
                 occ += ce[t] - cb[t] + 1;
             }
-        res_off[o] = at;
-        res_cnt[o] = cn;
-        res_occ[o] = occ;
+        put_res(res, o, at, cn, occ);
     }
     __shared__ unsigned long long sh[4];
     stat_add(ctr, ST_DEEP_STEPS, n_steps, sh);
@@ -1145,8 +1144,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
                                                   const uint8_t* __restrict__ code_of, const uint32_t* __restrict__ nid,
                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
                                                   const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
-                                                  uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, uint64_t* __restrict__ res_off,
-                                                  uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ,
+                                                  uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                                   uint32_t* __restrict__ ovf2) {
     (void)P;
     GRID_STRIDE(j, ntodo) {
@@ -1216,9 +1214,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
         uint32_t occ = 0;
         const uint64_t at = abase + (uint64_t)j * KW;
         for (uint32_t t = 0; t < cn; t++) { ab[at + t] = cb[t]; ae[at + t] = ce[t]; occ += ce[t] - cb[t] + 1; }
-        res_off[o] = at;
-        res_cnt[o] = cn;
-        res_occ[o] = occ;
+        put_res(res, o, at, cn, occ);
     }
 }
 
@@ -1262,15 +1258,8 @@ __global__ void k_sub_bytes(uint64_t n, const uint32_t* __restrict__ map, const 
     }
 }
 
-__global__ void k_sub_scatter(uint64_t n, const uint32_t* __restrict__ map, const uint64_t* __restrict__ so, const uint32_t* __restrict__ sc,
-                              const uint32_t* __restrict__ socc, uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt,
-                              uint32_t* __restrict__ res_occ) {
-    GRID_STRIDE(j, n) {
-        const uint32_t o = map[j];
-        res_off[o] = so[j];
-        res_cnt[o] = sc[j];
-        res_occ[o] = socc[j];
-    }
+__global__ void k_sub_scatter(uint64_t n, const uint32_t* __restrict__ map, const Res* __restrict__ sr, Res* __restrict__ res) {
+    GRID_STRIDE(j, n) res[map[j]] = sr[j];
 }
 
 // ------------------------------------------- order-free level step (default path)
@@ -1562,15 +1551,12 @@ __global__ void k_fin_archive(uint32_t F, const uint64_t* __restrict__ fk, const
 
 __global__ void k_finish2(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ nid,
                           const uint32_t* __restrict__ perm, const uint32_t* __restrict__ foff, const uint32_t* __restrict__ fend,
-                          const uint32_t* __restrict__ node_occ, uint64_t abase, uint64_t* __restrict__ res_off,
-                          uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ) {
+                          const uint32_t* __restrict__ node_occ, uint64_t abase, Res* __restrict__ res) {
     GRID_STRIDE(i, P) {
         if (slen[i] != D) continue;
         const uint32_t u = nid[i];
         const uint32_t o = perm[i];
-        res_off[o] = abase + foff[u];
-        res_cnt[o] = fend[u] - foff[u];
-        res_occ[o] = node_occ[u];
+        put_res(res, o, abase + foff[u], fend[u] - foff[u], node_occ[u]);
     }
 }
 
@@ -1626,25 +1612,31 @@ __global__ void k_archive(uint64_t n, const uint32_t* __restrict__ nu, const uin
 __global__ void k_finish(uint64_t P, uint32_t D, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ nid,
                          const uint32_t* __restrict__ perm, const uint32_t* __restrict__ foff, const uint32_t* __restrict__ fcnt,
                          const uint32_t* __restrict__ node_occ, uint64_t abase,
-                         uint64_t* __restrict__ res_off, uint32_t* __restrict__ res_cnt, uint32_t* __restrict__ res_occ) {
+                         Res* __restrict__ res) {
     GRID_STRIDE(i, P) {
         if (slen[i] != D) continue;
         const uint32_t u = nid[i];
         const uint32_t o = perm[i];
-        res_off[o] = abase + foff[u];
-        res_cnt[o] = fcnt[u];
-        res_occ[o] = node_occ[u];
+        put_res(res, o, abase + foff[u], fcnt[u], node_occ[u]);
     }
 }
 
 // --------------------------------------------------------------- locate
 __global__ void k_u32_to_u64(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ b) { GRID_STRIDE(i, n) b[i] = a[i]; }
+// scan inputs of locate: occurrences and intervals per pattern
+__global__ void k_res_scan_in(const Res* __restrict__ res, uint64_t n, uint64_t* __restrict__ occ, uint64_t* __restrict__ cnt) {
+    GRID_STRIDE(i, n) {
+        const Res r = res[i];
+        occ[i] = r.occ;
+        cnt[i] = r.cnt;
+    }
+}
 
 // one task per finished interval: its first row, first output record and pattern; and,
 // per run of kLocRun records, the task holding the run's first record (blk_first), so
 // k_locate finds a record's task in LDS instead of searching all tasks
 constexpr uint32_t kLocRun = 256;
-__global__ void k_tasks(uint64_t P, const uint64_t* __restrict__ res_off, const uint32_t* __restrict__ res_cnt,
+__global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
                         const uint64_t* __restrict__ tscan, const uint64_t* __restrict__ oscan,
                         const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                         uint32_t* __restrict__ trow, uint64_t* __restrict__ tout, uint32_t* __restrict__ tpat,
@@ -1652,9 +1644,10 @@ __global__ void k_tasks(uint64_t P, const uint64_t* __restrict__ res_off, const 
     GRID_STRIDE(i, P) {
         uint64_t base = oscan[i];
         const uint64_t t0 = tscan[i];
-        const uint32_t n = res_cnt[i];
+        const Res r = res[i];
+        const uint32_t n = r.cnt;
         for (uint32_t q = 0; q < n; q++) {
-            const uint64_t a = res_off[i] + q;
+            const uint64_t a = r.off + q;
             const uint64_t len = (uint64_t)(ae[a] - ab[a]) + 1;
             trow[t0 + q] = ab[a];
             tout[t0 + q] = base;
@@ -1918,10 +1911,15 @@ __global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, cons
 }
 
 // launched with a small grid (kReduceBlocks): one atomic per block
-__global__ void __launch_bounds__(256) k_count_found(const uint32_t* __restrict__ occ, uint64_t P, unsigned long long* __restrict__ found) {
+__global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
+                                                     unsigned long long* __restrict__ found) {
     __shared__ unsigned long long sh[4];
     unsigned long long f = 0;
-    GRID_STRIDE(i, P) f += occ[i] > 0;
+    GRID_STRIDE(i, P) {
+        const uint32_t occ = res[i].occ;
+        counts[i] = occ;  // backwardSearch's return value per pattern
+        f += occ > 0;
+    }
     f = block_sum(f, sh);
     if (threadIdx.x == 0 && f) atomicAdd(found, f);
 }
