@@ -250,6 +250,9 @@ __device__ __forceinline__ void pair_rank_v(const PairV& v, uint32_t x, uint32_t
     rq = v.cq + (uint32_t)__popcll(pair_match(v, q) & m);
 }
 
+// cnt | kResRow: the pattern's one interval is [off, off + occ) itself, not in the archive
+// (the deep kernels' single-interval results: no archive write, no archive read in k_tasks)
+constexpr uint32_t kResRow = 0x80000000u;
 __device__ __forceinline__ void put_res(Res* __restrict__ r, size_t o, uint64_t off, uint32_t cnt, uint32_t occ) {
     reinterpret_cast<uint4*>(r)[o] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), cnt, occ);
 }
@@ -927,11 +930,8 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             } else {
                 const uint32_t o = pv ? pi : perm[i];
                 const uint64_t at = abase + (uint64_t)i * K;
-                if (alive) {
-                    ab[at] = b;
-                    ae[at] = e;
-                }
-                put_res(res, o, at, alive ? 1u : 0u, alive ? e - b + 1 : 0u);
+                if (alive) put_res(res, o, b, 1u | kResRow, e - b + 1);
+                else put_res(res, o, at, 0u, 0u);
             }
         }
         const uint32_t at = wave_append(qcnt + sh * 32, want);
@@ -1113,6 +1113,10 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
         const uint32_t o = perm[i];
         uint32_t occ = 0;
         const uint64_t at = abase + (uint64_t)i * K;
+        if (cn == 1) {
+            put_res(res, o, cb[0], 1u | kResRow, ce[0] - cb[0] + 1);
+            continue;
+        }
 #pragma unroll
         for (int t = 0; t < K; t++)
             if ((uint32_t)t < cn) {
@@ -1213,6 +1217,10 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
         const uint32_t o = perm[i];
         uint32_t occ = 0;
         const uint64_t at = abase + (uint64_t)j * KW;
+        if (cn == 1) {
+            put_res(res, o, cb[0], 1u | kResRow, ce[0] - cb[0] + 1);
+            continue;
+        }
         for (uint32_t t = 0; t < cn; t++) { ab[at + t] = cb[t]; ae[at + t] = ce[t]; occ += ce[t] - cb[t] + 1; }
         put_res(res, o, at, cn, occ);
     }
@@ -1628,7 +1636,7 @@ __global__ void k_res_scan_in(const Res* __restrict__ res, uint64_t n, uint64_t*
     GRID_STRIDE(i, n) {
         const Res r = res[i];
         occ[i] = r.occ;
-        cnt[i] = r.cnt;
+        cnt[i] = r.cnt & ~kResRow;
     }
 }
 
@@ -1645,11 +1653,13 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
         uint64_t base = oscan[i];
         const uint64_t t0 = tscan[i];
         const Res r = res[i];
-        const uint32_t n = r.cnt;
+        const bool direct_row = (r.cnt & kResRow) != 0;
+        const uint32_t n = r.cnt & ~kResRow;
         for (uint32_t q = 0; q < n; q++) {
             const uint64_t a = r.off + q;
-            const uint64_t len = (uint64_t)(ae[a] - ab[a]) + 1;
-            trow[t0 + q] = ab[a];
+            const uint32_t row = direct_row ? (uint32_t)r.off : ab[a];
+            const uint64_t len = direct_row ? (uint64_t)r.occ : (uint64_t)(ae[a] - row) + 1;
+            trow[t0 + q] = row;
             tout[t0 + q] = base;
             tpat[t0 + q] = (uint32_t)i;
             for (uint64_t k = (base + kLocRun - 1) / kLocRun; k * kLocRun < base + len; k++) blk_first[k] = t0 + q;
