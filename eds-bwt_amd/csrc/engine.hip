@@ -164,6 +164,7 @@ struct Engine {
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
     DBuf<uint64_t> pv_in, pv_out;
+    bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // pair blocks (build_pairs): two backward steps per rank line in k_deep_fast (sigma <= 5)
@@ -1024,9 +1025,9 @@ struct Engine {
         // start (k_ktab_direct), from which k_deep_fast also writes perm
         const KIdx X = kidx();
         const uint32_t D = d + 1;
-        DBuf<uint32_t>& ovf = tflag;  // per sorted pattern
-        ovf.ensure(P);
-        zero(ovf.p, P * 4);
+        DBuf<uint32_t>& ovf = tflag;  // flag_push list of sorted patterns k_deep could not hold
+        ovf.ensure(P + 1);
+        zero(ovf.p, 4);
         const uint32_t K = deep_k;
         ab.grow_keep(abase + (uint64_t)P * K, stream);
         ae.grow_keep(abase + (uint64_t)P * K, stream);
@@ -1059,25 +1060,26 @@ struct Engine {
                          read_u32(dqpre.p + NSHARD));
         st.bytes_kernel[KC_DEEP] += (uint64_t)P * 24;  // + interval steps and '#' rows, folded at the end of search()
         // lists that outgrew k_deep's registers: retry those patterns with wide lists
-        uint32_t nw = scan_u32(ovf.p, tscan, P);
+        const uint32_t nw = read_u32(ovf.p);
+        uint32_t novf = nw;
+        const uint32_t* list = ovf.p + 1;
         if (nw && !no_wide) {
-            DBuf<uint32_t>& todo = sub_map;
-            todo.ensure(nw);
-            launch(KC_DEEP, k_list_flagged, P, P, (const uint32_t*)ovf.p, (const uint32_t*)tscan.p, todo.p);
-            DBuf<uint32_t>& ovf2 = hcnt;
-            ovf2.ensure(P);
-            zero(ovf2.p, P * 4);
+            DBuf<uint32_t>& ovf2 = hcnt;  // ... and those the wide lists could not hold either
+            ovf2.ensure((size_t)nw + 1);
+            zero(ovf2.p, 4);
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
-            launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, (const uint32_t*)todo.p, nw, lens, (const uint32_t*)perm.p, ind,
+            launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                    d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p);
             abase += (uint64_t)nw * kDeepWide;
             st.deep_overflow += nw;
-            HIPCHK(hipMemcpyAsync(ovf.p, ovf2.p, P * 4, hipMemcpyDeviceToDevice, stream));
+            novf = read_u32(ovf2.p);
+            list = ovf2.p + 1;
         }
-        zero(ovf_orig, P * 4);
-        launch(KC_DEEP, k_ovf_lens, P, P, (const uint32_t*)ovf.p, (const uint32_t*)perm.p, (const uint32_t*)len.p, ovf_orig);
-        const uint32_t novf = nw ? (no_wide ? nw : scan_u32(ovf.p, tscan, P)) : 0u;
+        if (novf) {
+            zero(ovf_orig, P * 4);
+            launch(KC_DEEP, k_ovf_mark, novf, novf, list, (const uint32_t*)perm.p, ovf_orig);
+        }
         if (no_wide) st.deep_overflow += nw;
         st.deep_level_rerun += novf;
         return novf;
@@ -1588,17 +1590,15 @@ struct Engine {
         }
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
         zero(counters.p + 1, 8);
-        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1);
-        if (locate) {
+        zero(counters.p + 12, 16);
+        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12);
+        if (locate) {  // occurrence and task offsets: one scan of both, packed
             occ64.ensure(P);
-            tc64.ensure(P);
-            launch(KC_LOCPREP, k_res_scan_in, P, (const Res*)res.p, P, occ64.p, tc64.p);
+            launch(KC_LOCPREP, k_res_scan_in, P, (const Res*)res.p, P, occ64.p, (uint64_t*)nullptr);
             inclusive_scan_u64(occ64.p, oscan, P);
-            inclusive_scan_u64(tc64.p, tscan64, P);
-            HIPCHK(hipMemcpyAsync(pinned + 2, oscan.p + P, 8, hipMemcpyDeviceToHost, stream));
-            HIPCHK(hipMemcpyAsync(pinned + 4, tscan64.p + P, 8, hipMemcpyDeviceToHost, stream));
         }
         HIPCHK(hipMemcpyAsync(pinned, counters.p + 1, 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(pinned + 2, counters.p + 12, 16, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         uint64_t rb3[3];
         std::memcpy(rb3, pinned, 24);
@@ -1608,10 +1608,18 @@ struct Engine {
         if (locate) {
             OCC = rb3[1];
             const uint64_t TT = rb3[2];
+            const uint64_t* tsc = nullptr;
+            if (OCC >> 32 || TT >> 32 || split_scans) {  // totals past 32 bits: the two scans apart
+                tc64.ensure(P);
+                launch(KC_LOCPREP, k_res_scan_in, P, (const Res*)res.p, P, occ64.p, tc64.p);
+                inclusive_scan_u64(occ64.p, oscan, P);
+                inclusive_scan_u64(tc64.p, tscan64, P);
+                tsc = tscan64.p;
+            }
             if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
                 blk_first.ensure(OCC / kLocRun + 1);
-                launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, (const uint64_t*)tscan64.p,
+                launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, tsc,
                        (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p);
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,

@@ -253,6 +253,8 @@ __device__ __forceinline__ void pair_rank_v(const PairV& v, uint32_t x, uint32_t
 // cnt | kResRow: the pattern's one interval is [off, off + occ) itself, not in the archive
 // (the deep kernels' single-interval results: no archive write, no archive read in k_tasks)
 constexpr uint32_t kResRow = 0x80000000u;
+// rare per-pattern events (deep-kernel overflows): lst[0] counts, the pattern ids follow
+__device__ __forceinline__ void flag_push(uint32_t* __restrict__ lst, uint32_t i) { lst[1 + atomicAdd(lst, 1u)] = i; }
 __device__ __forceinline__ void put_res(Res* __restrict__ r, size_t o, uint64_t off, uint32_t cnt, uint32_t occ) {
     reinterpret_cast<uint4*>(r)[o] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), cnt, occ);
 }
@@ -983,7 +985,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
         if (w.z == ~0u) {  // from the node's items at the cutover depth
             const uint32_t u = nid[i];
             cn = iend[u] - ioff[u];
-            if (cn > K) { ovf[i] = 1; continue; }
+            if (cn > K) { flag_push(ovf, (uint32_t)i); continue; }
 #pragma unroll
             for (int t = 0; t < K; t++) {
                 cb[t] = (uint32_t)t < cn ? ib[ioff[u] + t] : 0u;
@@ -1100,7 +1102,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             DEEP_CLK_ADD(c_steps, 1);
             DEEP_CLK_ADD(c_hsteps, rn ? 1 : 0);
         }
-        if (over) { ovf[i] = 1; continue; }
+        if (over) { flag_push(ovf, (uint32_t)i); continue; }
         // ascending rows (the input lists may be unordered sets)
 #pragma unroll
         for (int a = 0; a < K; a++)
@@ -1156,7 +1158,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
         const uint32_t L = slen[ind ? perm[i] : i];
         const uint32_t u = nid[i];
         const uint32_t n0 = iend[u] - ioff[u];
-        if (n0 > KW) { ovf2[i] = 1; continue; }
+        if (n0 > KW) { flag_push(ovf2, i); continue; }
         uint32_t cb[KW], ce[KW], nb[KW], ne[KW], sb[KW], se[KW], raw[KW];
         uint32_t cn = n0;
         for (uint32_t t = 0; t < cn; t++) { cb[t] = ib[ioff[u] + t]; ce[t] = ie[ioff[u] + t]; }
@@ -1207,7 +1209,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
             cn = nn;
             for (uint32_t t = 0; t < cn; t++) { cb[t] = nb[t]; ce[t] = ne[t]; }
         }
-        if (over) { ovf2[i] = 1; continue; }
+        if (over) { flag_push(ovf2, i); continue; }
         for (uint32_t t = 1; t < cn; t++) {  // ascending rows
             const uint32_t xb = cb[t], xe = ce[t];
             uint32_t q = t;
@@ -1248,9 +1250,9 @@ __global__ void __launch_bounds__(256) k_len_hist(const uint32_t* __restrict__ l
 }
 
 // overflowed patterns → a compact sub-batch (original ids kept in `map`)
-__global__ void k_ovf_lens(uint64_t P, const uint32_t* __restrict__ ovf, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ len,
-                           uint32_t* __restrict__ flag_orig) {
-    GRID_STRIDE(i, P) if (ovf[i]) flag_orig[perm[i]] = 1;
+// patterns the deep kernels could not hold (a flag_push list), flagged by input index
+__global__ void k_ovf_mark(uint32_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ perm, uint32_t* __restrict__ flag_orig) {
+    GRID_STRIDE(j, n) flag_orig[perm[list[j]]] = 1;
 }
 
 __global__ void k_sub_build(uint64_t P, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ fscan, const uint32_t* __restrict__ len,
@@ -1635,8 +1637,12 @@ __global__ void k_u32_to_u64(const uint32_t* __restrict__ a, uint64_t n, uint64_
 __global__ void k_res_scan_in(const Res* __restrict__ res, uint64_t n, uint64_t* __restrict__ occ, uint64_t* __restrict__ cnt) {
     GRID_STRIDE(i, n) {
         const Res r = res[i];
-        occ[i] = r.occ;
-        cnt[i] = r.cnt & ~kResRow;
+        if (cnt) {
+            occ[i] = r.occ;
+            cnt[i] = r.cnt & ~kResRow;
+        } else {  // one scan of both (the batch's totals stay below 2^32)
+            occ[i] = (uint64_t)r.occ << 32 | (r.cnt & ~kResRow);
+        }
     }
 }
 
@@ -1650,8 +1656,10 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
                         uint32_t* __restrict__ trow, uint64_t* __restrict__ tout, uint32_t* __restrict__ tpat,
                         uint64_t* __restrict__ blk_first) {
     GRID_STRIDE(i, P) {
-        uint64_t base = oscan[i];
-        const uint64_t t0 = tscan[i];
+        // tscan null: oscan holds the packed scan (occurrences << 32 | tasks)
+        const uint64_t ps = oscan[i];
+        uint64_t base = tscan ? ps : ps >> 32;
+        const uint64_t t0 = tscan ? tscan[i] : (ps & 0xffffffffull);
         const Res r = res[i];
         const bool direct_row = (r.cnt & kResRow) != 0;
         const uint32_t n = r.cnt & ~kResRow;
@@ -1922,16 +1930,24 @@ __global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, cons
 
 // launched with a small grid (kReduceBlocks): one atomic per block
 __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
-                                                     unsigned long long* __restrict__ found) {
+                                                     unsigned long long* __restrict__ found, unsigned long long* __restrict__ sums) {
     __shared__ unsigned long long sh[4];
-    unsigned long long f = 0;
+    unsigned long long f = 0, so = 0, st = 0;
     GRID_STRIDE(i, P) {
-        const uint32_t occ = res[i].occ;
-        counts[i] = occ;  // backwardSearch's return value per pattern
-        f += occ > 0;
+        const Res r = res[i];
+        counts[i] = r.occ;  // backwardSearch's return value per pattern
+        f += r.occ > 0;
+        so += r.occ;
+        st += r.cnt & ~kResRow;
     }
     f = block_sum(f, sh);
-    if (threadIdx.x == 0 && f) atomicAdd(found, f);
+    so = block_sum(so, sh);
+    st = block_sum(st, sh);
+    if (threadIdx.x == 0) {
+        if (f) atomicAdd(found, f);
+        if (so) atomicAdd(sums, so);
+        if (st) atomicAdd(sums + 1, st);
+    }
 }
 
 // per depth D: trie nodes M_D = #{i : lcp[i] < D <= slen[i]} (difference array over D)

@@ -394,3 +394,18 @@ def test_packed_direct_start_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             got[packed] = (gc, go)
             gp, gop = idx.search((buf, offs), pairs=False)
             assert np.array_equal(gp, oc) and np.array_equal(gop, oo)
+
+
+def test_split_locate_scans_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """Locate offsets from the two separate scans (the path batches whose totals pass 2^32
+    take) give the same records as the packed single scan."""
+    rng = random.Random(77)
+    segs = edsgen.random_eds(rng, 1500, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(2, 25)) or "ACGT" for _ in range(1500)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    monkeypatch.setenv("EDSBWT_SPLIT_SCANS", "1")
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
