@@ -252,7 +252,7 @@ def main():
             "data": "synthetic (edsbwt_gen, seeded)",
             "config": {"workload": WORKLOAD[cfg], "config": cfg, "patterns_per_gpu": npat,
                        "index_rows": idx.n_rows, "words": idx.n_words, "segments": idx.n_segments,
-                       "locate": {"sampled": "lf-walk to the first sampled row (1 in 4 word offsets)",
+                       "locate": {"sampled": "per-row samples (word, offset, segment, word-in-segment), one read per occurrence",
                                   "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
                        if locate else "count-only",
                        "parallelism": f"pattern-shard x{world}"},

@@ -121,9 +121,10 @@ constexpr int kDeepK = 4;
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
-// locate samples every 2^kSampleShift positions of a word (16 B per sampled row; C3: 1 in 4
-// offsets 1.477e9 vs 1 in 8 1.424e9 patterns/s)
-constexpr uint32_t kSampleShift = 2;
+// locate samples every 2^kSampleShift positions of a word (16 B per sampled row).  0: every
+// row, 16 B/row (C3: 1.66 GB of the 288 GB), and locate reads one sample per occurrence with
+// no LF walk and no occ-block read; EDSBWT_SAMPLE_SHIFT=2 keeps 1 in 4 (0.43 GB at C3)
+constexpr uint32_t kSampleShift = 0;
 // patterns k_deep<kDeepK> cannot hold retry with lists of up to kDeepWide intervals
 constexpr int kDeepWide = 64;
 // k-mer start table: deepest depth tried, most D-mers (offsets) and intervals kept, and the
@@ -154,6 +155,7 @@ struct Engine {
     bool have_table = false;
     DBuf<uint4> samples;     // locate samples (word, offset, segment, word in segment) of rows whose offset % 2^kSampleShift == 0
     bool have_samples = false;
+    uint32_t samp_shift = 0;  // rows sampled: offset % 2^samp_shift == 0 (0: every row)
     // k-mer start table (build_ktab): for every D-mer x over the non-'#' symbols, the
     // order-free walk's intervals after its D characters, [ktab_off[x], ktab_off[x+1]) of
     // ktab_b / ktab_e; searches whose patterns are all longer than D start at depth D
@@ -271,6 +273,7 @@ struct Engine {
         X.da = da.p;
         X.offt = offt.p;
         X.samples = samples.p;
+        X.samp_dense = have_samples && samp_shift == 0 ? 1u : 0u;
         X.segtab = segtab.p;
         X.seg_stride = sigma <= 7 ? 16u : 32u;
         X.seg_hi = sigma <= 7 ? 8u : 9u;
@@ -724,6 +727,7 @@ struct Engine {
         DBuf<uint32_t> bcnt;
         bcnt.ensure(nblk);
         const uint32_t shift = std::min(8u, (uint32_t)env_double("EDSBWT_SAMPLE_SHIFT", kSampleShift));  // tuning knob
+        samp_shift = shift;
         launch(KC_TABLE, k_samp_blocks, nblk, nblk, N, (const uint32_t*)offt.p, shift, occ.p, bcnt.p);
         DBuf<uint32_t> bbase;
         const uint32_t ns = scan_u32(bcnt.p, bbase, nblk);  // bbase[0..nblk], total read back
@@ -781,9 +785,11 @@ struct Engine {
         len.ensure(P);
         keys.ensure((size_t)nch * P);
         if (bps == 3)
-            launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
+            launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, 0u, 0u,
+                   (uint32_t*)nullptr, (uint64_t*)nullptr);
         else
-            launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
+            launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, 0u, 0u,
+                   (uint32_t*)nullptr, (uint64_t*)nullptr);
         perm.ensure(P);
         perm2.ensure(P);
         kc.ensure(P);
@@ -1022,7 +1028,7 @@ struct Engine {
                       const uint64_t* pv = nullptr) {
         // k0/krest/lens/ind: the direct start's input-order key chunks and lengths (ind: read
         // through perm); by default the trie's sorted chunks and slen.  pv: the packed direct
-        // start (k_ktab_direct), from which k_deep_fast also writes perm
+        // start (k_keys), from which k_deep_fast also writes perm
         const KIdx X = kidx();
         const uint32_t D = d + 1;
         DBuf<uint32_t>& ovf = tflag;  // flag_push list of sorted patterns k_deep could not hold
@@ -1111,11 +1117,6 @@ struct Engine {
         len.ensure(P);
         keys.ensure((size_t)nch * P);
         unsigned long long* d_nterm = counters.p + 10;
-        if (bps == 3)
-            launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
-        else
-            launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm);
-        if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
         nid[0].ensure(P);
         perm.ensure(P);
         const uint32_t E = (uint32_t)ktab_entries;
@@ -1131,8 +1132,14 @@ struct Engine {
             pv_in.ensure(P);
             pv_out.ensure(P);
         }
-        launch(KC_NODES, bps == 3 ? k_ktab_direct<3> : k_ktab_direct<4>, P, P, D0, sigma - 1, E, (const uint64_t*)keys.p,
-               (const uint64_t*)(keys.p + P), kid, packed ? pv_in.p : (uint64_t*)nullptr);
+        // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass
+        if (bps == 3)
+            launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
+                   packed ? pv_in.p : (uint64_t*)nullptr);
+        else
+            launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
+                   (uint64_t*)nullptr);
+        if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
         if (packed) {
             size_t tb = 0;
             const int endbit = (int)bits_for(E);
@@ -1634,7 +1641,10 @@ struct Engine {
             const std::vector<uint64_t> sv = fold_pinned_stats();
             st.intervals_stepped += sv[ST_DEEP_STEPS];
             st.link_hash_rows += sv[ST_DEEP_HASH];
-            st.bytes_kernel[KC_DEEP] += sv[ST_DEEP_STEPS] * (2 * sizeof(OccBlock)) + sv[ST_DEEP_HASH] * 4;
+            // the lines the deep kernels gather (a narrow interval's two ends in one line count
+            // once; pair-block lines are 128 B) and the '#'-row reads; + P * 24 record bytes above
+            st.bytes_kernel[KC_DEEP] += (sv[ST_DEEP_BLOCKS] - sv[ST_DEEP_PAIR_LINES]) * sizeof(OccBlock) +
+                                        sv[ST_DEEP_PAIR_LINES] * sizeof(PairBlock) + sv[ST_DEEP_HASH] * 4;
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];

@@ -67,6 +67,7 @@ struct KIdx {
     const uint32_t* offt;      // [N] optional offset-in-word per row
     uint32_t N, W, S, sigma;
     const uint4* samples;      // (word, offset, segment, word in segment) of the sampled rows, in row order (locate)
+    uint32_t samp_dense;       // every row sampled: samples[x] is row x's (no occ-block rank needed)
     // per segment s (link of a word in s): [0] seg_lo[s]; [1 + c] rank_c at the first word of
     // segment seg_lo[s]; [seg_hi + c] rank_c at the first word of s.  seg_stride u32 per entry.
     const uint32_t* segtab;

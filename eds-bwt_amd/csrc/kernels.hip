@@ -286,7 +286,8 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long x, un
 constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards * kStatStride;
 // statistic slots (zeroed once per search, folded at its end)
 enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5,
-                  ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10 };
+                  ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10,
+                  ST_DEEP_PAIR_LINES = 11 };  // of ST_DEEP_BLOCKS, the 128-B pair-block lines
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -379,7 +380,14 @@ constexpr uint32_t kKeySpan = 24576;
 template <int BPS>
 __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
                                               const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t nch, uint64_t* __restrict__ keys,
-                                              uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term) {
+                                              uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term,
+                                              uint32_t D, uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
+    // kid / pv (direct start), from the chunks still in registers: kid = the D-mer id of the
+    // pattern's last D symbols (last character least significant digit, as k_ktab_count reads
+    // a node's); a D-mer holding '#' or a byte outside the alphabet has no list: kid = E
+    // (= B^D), whose list is empty.  pv = the packed start (B <= 4, at most 16 symbols after
+    // depth D): input index in bits [0, 31), the remaining symbols' 2-bit digits from bit 31
+    // up, closed by a 1 bit; a symbol outside the alphabet there also gives kid = E.
     constexpr uint32_t SPC = 64 / BPS;
     __shared__ uint32_t sbuf[kKeySpan / 4 + 2];
     __shared__ uint8_t scode[256];
@@ -409,6 +417,7 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
             const uint8_t* sg = bytes + a;
             const uint8_t* sl = reinterpret_cast<const uint8_t*>(sbuf) + (a - w0);
             uint32_t term = 0;
+            uint64_t kc0 = 0, kc1 = 0;
             for (uint32_t c = 0; c < nch; c++) {
                 uint64_t key = 0;
                 for (uint32_t t = 0; t < SPC; t++) {
@@ -422,8 +431,35 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
                     key = (key << BPS) | v;
                 }
                 keys[(size_t)c * P + i] = key;
+                if (c == 0) kc0 = key;
+                if (c == 1) kc1 = key;
             }
             nt += term;
+            if (kid) {
+                const uint32_t B = sigma - 1;
+                uint32_t x = 0, mul = 1;
+                bool ok = true;
+                for (uint32_t t = 0; t < D; t++) {
+                    const uint32_t v = (uint32_t)(kc0 >> (BPS * (SPC - 1 - t))) & ((1u << BPS) - 1u);
+                    ok &= v >= 2 && v <= B + 1;
+                    x += (v - 2) * mul;
+                    mul *= B;
+                }
+                if (pv) {  // L <= D + 16 <= 2 * SPC: the remaining symbols lie in chunks 0 and 1
+                    uint64_t rem = 0;
+                    uint32_t n = 0;
+                    for (uint32_t t = D; t < L; t++) {
+                        const uint64_t k = t < SPC ? kc0 : kc1;
+                        const uint32_t v = (uint32_t)(k >> (BPS * (SPC - 1 - (t < SPC ? t : t - SPC)))) & ((1u << BPS) - 1u);
+                        ok &= v >= 2 && v <= B + 1;
+                        rem |= (uint64_t)((v - 2) & 3u) << (2 * n);
+                        n++;
+                    }
+                    rem |= 1ull << (2 * n);
+                    pv[i] = rem << 31 | (uint64_t)i;
+                }
+                kid[i] = ok ? x : E;
+            }
         }
     }
     nt = block_sum(nt, sh);
@@ -855,7 +891,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
                                                    uint32_t* __restrict__ perm_out) {
-    unsigned long long n_steps = 0, n_blk = 0;
+    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     UNIFORM_STRIDE(i, valid, P) {
@@ -907,6 +943,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                         pair_rank_v(v0, b, p, q, h0, p0, q0);
                         pair_rank_v(v1, e + 1, p, q, h1, p1, q1);
                         n_blk += same ? 1 : 2;
+                        n_pl += same ? 1 : 2;
                         if (h1 == h0 && q1 == q0 && p1 > p0) {
                             n_steps += 2;
                             b = X.PC[p] + p0;
@@ -942,6 +979,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
     __shared__ unsigned long long ssum[4];
     stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
     stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
+    stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
 }
 
 // shard prefix sums of k_deep_fast's queue counters (one block)
@@ -1709,6 +1747,18 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
         const uint32_t pat = s_pat[lo];
         uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
         uint32_t word, off;
+        if (mode == 2 && X.samp_dense) {  // every row sampled: the record straight from row x's sample
+            const uint4 s = X.samples[x];
+            my_off += s.y;
+            edsbwt_occ r;
+            r.pat = first_id + pat;
+            r.word = s.x;
+            r.seg = s.z;
+            r.word_in_seg = s.w;
+            r.offset = s.y;
+            rec[o] = r;
+            continue;
+        }
         if (mode == 1) {
             word = X.da[x];
             off = X.offt[x];
@@ -2068,52 +2118,6 @@ __global__ void k_ktab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t*
         }
         kid[u] = ok ? x : 0xFFFFFFFFu;
         cnt[u] = ok ? toff[x + 1] - toff[x] : 0u;
-    }
-}
-
-// direct start (every pattern longer than D): pattern i's D-mer straight from its own
-// key chunk 0 (input order), as k_ktab_count reads a node's; k_deep then takes the table's
-// list [toff[kid[i]], toff[kid[i]+1]) as the pattern's items of depth D.  A D-mer holding
-// '#' or a byte outside the alphabet has no list: kid = E (= B^D), whose list
-// [toff[E], toff[E+1]) is empty, so the pattern's count stays 0.
-template <int BPS>
-__global__ void k_ktab_direct(uint64_t P, uint32_t D, uint32_t B, uint32_t E, const uint64_t* __restrict__ k0,
-                              const uint64_t* __restrict__ krest, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
-    constexpr uint32_t SPC = 64 / BPS;
-    GRID_STRIDE(i, P) {
-        const uint64_t key = k0[i];
-        uint32_t x = 0, mul = 1;
-        bool ok = true;
-        for (uint32_t t = 0; t < D; t++) {
-            const uint32_t v = (uint32_t)(key >> (BPS * (SPC - 1 - t))) & ((1u << BPS) - 1u);
-            ok &= v >= 2 && v <= B + 1;
-            x += (v - 2) * mul;
-            mul *= B;
-        }
-        if (pv) {
-            // packed start (B <= 4, at most 16 symbols after depth D): input index in bits
-            // [0, 31), the remaining symbols' 2-bit digits from bit 31 up, closed by a 1 bit.
-            // A symbol outside the alphabet makes the pattern unmatchable: the empty list.
-            uint64_t rem = 0;
-            uint32_t n = 0;
-            uint64_t cur = key;
-            uint32_t chunk = 0;
-            for (uint32_t t = D;; t++) {
-                const uint32_t c = t / SPC;
-                if (c != chunk) {
-                    cur = krest[(size_t)(c - 1) * P + i];
-                    chunk = c;
-                }
-                const uint32_t v = (uint32_t)(cur >> (BPS * (SPC - 1 - (t - c * SPC)))) & ((1u << BPS) - 1u);
-                if (v == 0) break;  // end of the pattern
-                ok &= v >= 2 && v <= B + 1;
-                rem |= (uint64_t)((v - 2) & 3u) << (2 * n);
-                n++;
-            }
-            rem |= 1ull << (2 * n);
-            pv[i] = rem << 31 | (uint64_t)i;
-        }
-        kid[i] = ok ? x : E;
     }
 }
 

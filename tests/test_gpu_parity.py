@@ -409,3 +409,23 @@ def test_split_locate_scans_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     with edsbwt.Index(base) as idx:
         gc, go = idx.search((buf, offs))
         assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+
+
+@pytest.mark.parametrize("shift", [0, 2, 3])
+def test_locate_sample_rates_gpu(oracle, edsbwt, tmp_path, monkeypatch, shift):
+    """Locate from samples of every row (default: one read per occurrence) or of 1 in 2^shift
+    word offsets (LF walk to the first sampled row): identical records and Σ offsets."""
+    monkeypatch.setenv("EDSBWT_SAMPLE_SHIFT", str(shift))
+    rng = random.Random(1200 + shift)
+    segs = _covid_like(rng, 300)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(3, 40)) or "ACGT" for _ in range(1500)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        st = idx.stats()
+        assert st["locate_offsets"] == int(oo["offset"].astype(np.uint64).sum())
+        if shift == 0:
+            assert st["locate_lf_steps"] == 0  # no walk: the sample of the row itself
