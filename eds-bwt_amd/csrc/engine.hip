@@ -169,8 +169,11 @@ struct Engine {
     bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
-    // pair blocks (build_pairs): two backward steps per rank line in k_deep_fast (sigma <= 5)
-    DBuf<PairBlock> pocc;
+    // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
+    // rent2 (sigma <= 5) answers two steps
+    DBuf<uint4> rent1, rent2;
+    uint32_t r2stride = 0;
+    bool use_rent = env_double("EDSBWT_NO_RANK_ENTRIES", 0) == 0;
     uint32_t PC[kPairCodes + 3] = {0};
     bool use_pairs = true;  // per search (EDSBWT_NO_PAIRS clears it)
     // levels2() capture mode (table build): the items of the deepest depth <= K whose
@@ -281,7 +284,9 @@ struct Engine {
         X.segbits = bits_for(S);
         X.rowbits = bits_for(N);
         for (int c = 0; c < 8; c++) X.C[c] = C[c];
-        X.pocc = use_pairs && pocc.p ? pocc.p : nullptr;
+        X.rent1 = use_rent ? rent1.p : nullptr;
+        X.rent2 = use_rent && use_pairs ? rent2.p : nullptr;
+        X.r2stride = r2stride;
         for (uint32_t k = 0; k < kPairCodes + 3; k++) X.PC[k] = PC[k];
         return X;
     }
@@ -609,20 +614,27 @@ struct Engine {
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
-        if (env_double("EDSBWT_PAIRS", 1.0) != 0.0) build_pairs();
+        build_rank_entries();
         build_ktab();
     }
 
-    // Pair blocks (kernels.h PairBlock): the code of (L[x], L[LF(x)]) of every row, bit-sliced
-    // per 64 rows with block-start counts, and PC[p], the first row of the suffixes c2 c1 ...
-    // (C[c2] + rank_c2(L, C[c1])).  2 B per row; only for sigma <= 5 (codes fit 5 bits and the
-    // counts one 128-B line).
-    void build_pairs() {
-        if (sigma > 5 || sigma < 2 || kOccRows != 64) return;
+    // Rank entries (kernels.h): rent1 for every alphabet, rent2 (the pair codes of every row,
+    // their 64-row counts scanned, then one entry per 32-row block and pair code) for
+    // sigma <= 5, and PC[p], the first row of the suffixes c2 c1 ... (C[c2] + rank_c2(L, C[c1])).
+    void build_rank_entries() {
+#if EDSBWT_OCC_ROWS == 64
+        const uint64_t nb32 = (uint64_t)N / 32 + 1;
+        const KIdx X = kidx();
+        rent1.ensure(nb32 * sigma);
+        launch(KC_TABLE, k_rent1, nb32, nb32, X, rent1.p);
+        device_bytes += nb32 * sigma * 16;
+        if (sigma > 5 || sigma < 2) {
+            HIPCHK(hipStreamSynchronize(stream));
+            return;
+        }
         const uint32_t nc = 1 + (sigma - 1) * sigma;
         const uint64_t nblk = (uint64_t)N / 64 + 1, nrows = nblk * 64;
         if ((uint64_t)nc * nblk > 0x7fffffffull) return;  // scan_u32 bound
-        const KIdx X = kidx();
         DBuf<uint8_t> code;
         DBuf<uint32_t> cnt, cscan;
         code.ensure(nrows);
@@ -631,11 +643,10 @@ struct Engine {
         launch(KC_TABLE, k_pair_counts, nrows, nblk, (const uint8_t*)code.p, nc, cnt.p);
         scan_u32(cnt.p, cscan, (size_t)nc * nblk);
         cnt.release();
-        pocc.ensure(nblk);
-        launch(KC_TABLE, k_pair_fill, nrows, nblk, (const uint8_t*)code.p, nc, (const uint32_t*)cscan.p, pocc.p);
-        HIPCHK(hipStreamSynchronize(stream));
-        device_bytes += nblk * sizeof(PairBlock);
-        // PC from the ranks at the pile starts
+        r2stride = nc - 1;
+        rent2.ensure(nb32 * r2stride);
+        launch(KC_TABLE, k_rent2, nb32, nb32, nblk, (const uint8_t*)code.p, nc, sigma, (const uint32_t*)cscan.p, rent2.p);
+        device_bytes += nb32 * r2stride * 16;
         std::vector<uint32_t> rk((size_t)sigma * sigma);
         DBuf<uint32_t> d_rk;
         d_rk.ensure(rk.size());
@@ -644,6 +655,7 @@ struct Engine {
         HIPCHK(hipStreamSynchronize(stream));
         for (uint32_t c1 = 1; c1 < sigma; c1++)
             for (uint32_t c2 = 0; c2 < sigma; c2++) PC[1 + (c1 - 1) * sigma + c2] = C[c2] + rk[(size_t)c1 * sigma + c2];
+#endif
     }
 
     // k-mer start table: the order-free walk run once over every K-mer of the non-'#'
@@ -1641,10 +1653,10 @@ struct Engine {
             const std::vector<uint64_t> sv = fold_pinned_stats();
             st.intervals_stepped += sv[ST_DEEP_STEPS];
             st.link_hash_rows += sv[ST_DEEP_HASH];
-            // the lines the deep kernels gather (a narrow interval's two ends in one line count
-            // once; pair-block lines are 128 B) and the '#'-row reads; + P * 24 record bytes above
-            st.bytes_kernel[KC_DEEP] += (sv[ST_DEEP_BLOCKS] - sv[ST_DEEP_PAIR_LINES]) * sizeof(OccBlock) +
-                                        sv[ST_DEEP_PAIR_LINES] * sizeof(PairBlock) + sv[ST_DEEP_HASH] * 4;
+            // the 64-B lines the deep kernels gather (occ blocks or the 16-B rank entries' lines; a
+            // narrow interval's two ends in one block count once) and the '#'-row reads; + P * 24
+            // record bytes above
+            st.bytes_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS] * 64 + sv[ST_DEEP_HASH] * 4;
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];
@@ -1750,7 +1762,7 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
     info->device_bytes = E.device_bytes;
     info->ktab_depth = E.ktab_depth;
     info->ktab_items = E.ktab_items;
-    info->pair_blocks = E.pocc.p != nullptr;
+    info->pair_blocks = E.rent2.p != nullptr;
     return 0;
 }
 

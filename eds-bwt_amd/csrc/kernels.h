@@ -35,18 +35,18 @@ static_assert(sizeof(OccBlock) == 64, "occ block must be 64 B");
 #endif
 constexpr uint32_t kOccRows = 1u << kOccShift;
 
-// Two-step rank block ("pair block", 128 B per 64 rows, sigma <= 5): each row x carries the
-// pair code of (L[x], L[LF(x)]) — 0 when L[x] = '#', else 1 + (L[x]-1)*sigma + L[LF(x)] —
-// bit-sliced in 5 planes, and cnt[k] = rows before the block with code k.  Rows of the
-// suffixes c2 c1 Q are [PC[p] + rank_p(b), PC[p] + rank_p(e+1)) for p = (c1, c2) and Q's
-// rows [b, e], so one line answers two backward steps; rank of (c1, '#') tells whether
-// the intermediate interval holds '#' rows (a link), rank of code 0 whether [b, e] does.
+// Rank entries (sigma <= 5): 32 BWT rows per block and one 16-B entry per query, so an
+// interval end costs ONE 16-B load per step (the gathers are bound by load instructions
+// per random line, not by bytes: DESIGN.md §5).
+//   rent1[k * sigma + c] = {rank_c(32k), mask of the block's rows with L = c,
+//                           rank_'#'(32k), mask of its '#' rows}
+// answers a backward step by c and the '#' rows (link) of the interval at once.  Pair codes
+// code(x) = 0 when L[x] = '#', else 1 + (L[x]-1)*sigma + L[LF(x)]: rows of the suffixes c2 c1 Q
+// are [PC[p] + rank_p(b), PC[p] + rank_p(e+1)) for p = (c1, c2) and Q's rows [b, e], and
+//   rent2[k * (nc-1) + p-1] = {rank_p(32k), mask_p, rank_{0|q}(32k), mask_{0|q}}, q = (c1, '#'),
+// answers two steps at once when no row of [b, e] holds '#' or (c1, '#') — no link at
+// either step.
 constexpr uint32_t kPairCodes = 21;  // sigma = 5: 1 + 4 * 5
-struct alignas(128) PairBlock {
-    uint64_t plane[5];
-    uint32_t cnt[22];
-};
-static_assert(sizeof(PairBlock) == 128, "pair block must be one 128-B line");
 
 // per-pattern result (backwardSearch's final list): archive offset of its intervals, their
 // number and the occurrence count; one 16-B record, written with one store
@@ -75,7 +75,9 @@ struct KIdx {
     uint32_t segbits;          // bits of a segment id (1..S): link keys are node << segbits | segment
     uint32_t rowbits;          // bits of a BWT row (< N): finisher keys are node << rowbits | row
     uint32_t C[8];             // first row of each pile
-    const PairBlock* pocc;     // two-step rank blocks (nullptr: not built)
+    const uint4* rent1;        // single-step rank entries (nullptr: not built)
+    const uint4* rent2;        // two-step rank entries (nullptr: not built or not used)
+    uint32_t r2stride;         // rent2 entries per block (pair codes - 1)
     uint32_t PC[kPairCodes + 3];  // first row of the suffixes c2 c1 ... for pair code p = (c1, c2)
 };
 

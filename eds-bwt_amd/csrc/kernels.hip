@@ -215,39 +215,24 @@ __device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ,
 }
 #endif
 
-// pair block at one interval end: the planes and the counts of codes 0 ('#' rows), p and q
-struct PairV {
-    uint64_t pl[5];
-    uint32_t c0, cp, cq;
-};
-__device__ __forceinline__ PairV pair_load(const PairBlock* __restrict__ pb, uint32_t blk, uint32_t p, uint32_t q) {
-    const PairBlock* B = pb + blk;
-    const uint4* v = reinterpret_cast<const uint4*>(B);
-    const uint4 a = v[0], b = v[1];
-    const uint2 c = reinterpret_cast<const uint2*>(B)[4];
-    PairV o;
-    o.pl[0] = (uint64_t)a.y << 32 | a.x;
-    o.pl[1] = (uint64_t)a.w << 32 | a.z;
-    o.pl[2] = (uint64_t)b.y << 32 | b.x;
-    o.pl[3] = (uint64_t)b.w << 32 | b.z;
-    o.pl[4] = (uint64_t)c.y << 32 | c.x;
-    o.c0 = B->cnt[0];
-    o.cp = B->cnt[p];
-    o.cq = B->cnt[q];
-    return o;
+// one 16-B rank entry (kernels.h): rank of its code and of its '#' (or '#'-or-(c1,'#')) rows at x
+__device__ __forceinline__ void rent_rank(uint4 v, uint32_t x, uint32_t& r, uint32_t& h) {
+    const uint32_t m = (1u << (x & 31u)) - 1u;
+    r = v.x + (uint32_t)__popc(v.y & m);
+    h = v.z + (uint32_t)__popc(v.w & m);
 }
-__device__ __forceinline__ uint64_t pair_match(const PairV& v, uint32_t k) {
-    uint64_t m = ~0ull;
-#pragma unroll
-    for (uint32_t j = 0; j < 5; j++) m &= ((k >> j) & 1u) ? v.pl[j] : ~v.pl[j];
-    return m;
-}
-// ranks of codes 0, p, q at row x (rows [0, x) counted)
-__device__ __forceinline__ void pair_rank_v(const PairV& v, uint32_t x, uint32_t p, uint32_t q, uint32_t& h, uint32_t& rp, uint32_t& rq) {
-    const uint64_t m = (1ull << (x & 63u)) - 1ull;
-    h = v.c0 + (uint32_t)__popcll(pair_match(v, 0) & m);
-    rp = v.cp + (uint32_t)__popcll(pair_match(v, p) & m);
-    rq = v.cq + (uint32_t)__popcll(pair_match(v, q) & m);
+// '#'-rank and c-rank at both interval ends (x0 = b, x1 = e + 1): one 16-B rank entry per
+// end when built, else the occ blocks.  Returns 1 when one block served both ends.
+__device__ __forceinline__ uint32_t rank2_any(const KIdx& X, uint32_t x0, uint32_t x1, uint32_t c, uint32_t& h0, uint32_t& r0, uint32_t& h1,
+                                              uint32_t& r1) {
+    if (X.rent1) {
+        const uint4 v0 = X.rent1[(size_t)(x0 >> 5) * X.sigma + c];
+        const uint4 v1 = X.rent1[(size_t)(x1 >> 5) * X.sigma + c];
+        rent_rank(v0, x0, r0, h0);
+        rent_rank(v1, x1, r1, h1);
+        return (x0 >> 5) == (x1 >> 5);
+    }
+    return rank2_pair(X.occ, x0, x1, c, h0, r0, h1, r1);
 }
 
 // cnt | kResRow: the pattern's one interval is [off, off + occ) itself, not in the archive
@@ -287,7 +272,7 @@ constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards 
 // statistic slots (zeroed once per search, folded at its end)
 enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5,
                   ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10,
-                  ST_DEEP_PAIR_LINES = 11 };  // of ST_DEEP_BLOCKS, the 128-B pair-block lines
+                  ST_DEEP_PAIR_LINES = 11 };  // of ST_DEEP_BLOCKS, the rank-entry lines
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -925,39 +910,40 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             };
             bool alive = true;
             uint32_t d = D0;
-            bool pair_skip = false;  // the pair step just found '#' rows after its first step
+            bool pair_skip = false;  // the pair entry just found '#' rows: take one step
             for (; d < L; d++) {
                 const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
-                // two characters from one pair-block line per interval end, when neither
-                // [b, e] nor the interval between the two steps holds '#' rows and the
-                // pattern survives both; otherwise the single step below decides
-                if (X.pocc && !pair_skip && d + 1 < L && c != 0) {
+                // two characters from one rank entry per interval end, when no row of [b, e]
+                // holds '#' or (c, '#') and the pattern survives both; else one step
+                if (X.rent2 && !pair_skip && d + 1 < L && c != 0) {
                     const uint32_t c2 = code_at(d + 1);
                     if (c2 != 0 && c2 < X.sigma) {
-                        const uint32_t q = 1 + (c - 1) * X.sigma, p = q + c2;
-                        const bool same = (b >> 6) == ((e + 1) >> 6);
-                        const PairV v0 = pair_load(X.pocc, b >> 6, p, q);
-                        const PairV v1 = pair_load(X.pocc, (e + 1) >> 6, p, q);
-                        uint32_t h0, p0, q0, h1, p1, q1;
-                        pair_rank_v(v0, b, p, q, h0, p0, q0);
-                        pair_rank_v(v1, e + 1, p, q, h1, p1, q1);
-                        n_blk += same ? 1 : 2;
-                        n_pl += same ? 1 : 2;
-                        if (h1 == h0 && q1 == q0 && p1 > p0) {
+                        const uint32_t p = 1 + (c - 1) * X.sigma + c2;
+                        const uint4 v0 = X.rent2[(size_t)(b >> 5) * X.r2stride + p - 1];
+                        const uint4 v1 = X.rent2[(size_t)((e + 1) >> 5) * X.r2stride + p - 1];
+                        uint32_t p0, x0, p1, x1;
+                        rent_rank(v0, b, p0, x0);
+                        rent_rank(v1, e + 1, p1, x1);
+                        const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
+                        n_blk += nl;
+                        n_pl += nl;
+                        if (x1 == x0 && p1 > p0) {
                             n_steps += 2;
                             b = X.PC[p] + p0;
                             e = X.PC[p] + p1 - 1;
                             d++;
                             continue;
                         }
-                        pair_skip = h1 == h0 && q1 > q0;
+                        pair_skip = true;
                     }
                 } else {
                     pair_skip = false;
                 }
                 uint32_t h0, h1, sb, se;
-                n_blk += 2 - rank2_pair(X.occ, b, e + 1, c, h0, sb, h1, se);
+                const uint32_t nl = 2 - rank2_any(X, b, e + 1, c, h0, sb, h1, se);
+                n_blk += nl;
+                if (X.rent1) n_pl += nl;
                 if (h1 > h0) { want = 1; break; }  // '#' rows: the link needs k_deep
                 n_steps++;
                 if (se <= sb) { alive = false; break; }
@@ -1055,7 +1041,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             for (int j = 0; j < K; j++) {
                 if ((uint32_t)j < cn) {
                     uint32_t h0, h1;
-                    n_blk += 2 - rank2_pair(X.occ, cb[j], ce[j] + 1, c, h0, sb[j], h1, se[j]);
+                    n_blk += 2 - rank2_any(X, cb[j], ce[j] + 1, c, h0, sb[j], h1, se[j]);
                     n_hash += h1 - h0;
                     for (uint32_t k = h0; k < h1; k++) {  // dollars_in_interval (:607-625)
                         const uint32_t s = X.eof_seg[k];
@@ -1210,7 +1196,7 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
             uint32_t rn = 0;
             for (uint32_t q = 0; q < cn && !over; q++) {
                 uint32_t h0, h1;
-                rank2_pair(X.occ, cb[q], ce[q] + 1, c, h0, sb[q], h1, se[q]);
+                rank2_any(X, cb[q], ce[q] + 1, c, h0, sb[q], h1, se[q]);
                 for (uint32_t k = h0; k < h1; k++) {
                     const uint32_t s = X.eof_seg[k];
                     if (!s) continue;
@@ -1873,7 +1859,7 @@ __global__ void k_gather_rec(uint64_t n, const uint32_t* __restrict__ idx, const
 
 // ------------------------------------------------- DA/OFF table (index open)
 // ------------------------------------------------------------ pair blocks (index open)
-// pair code of every row (kernels.h PairBlock); 31 for the padding rows past N
+// pair code of every row (kernels.h rank entries); 31 for the padding rows past N
 __global__ void k_pair_codes(uint64_t nrows, KIdx X, uint8_t* __restrict__ code) {
     GRID_STRIDE(x, nrows) {
         uint32_t k = 31;
@@ -1914,21 +1900,60 @@ __global__ void k_pair_counts(uint64_t nblk, const uint8_t* __restrict__ code, u
     }
 }
 
-// planes and block-start counts; scan = scan_u32 of the code-major counts (scan[0] = 0)
-__global__ void k_pair_fill(uint64_t nblk, const uint8_t* __restrict__ code, uint32_t nc, const uint32_t* __restrict__ scan,
-                            PairBlock* __restrict__ pb) {
-    GRID_STRIDE(t, nblk * 64) {
-        const uint64_t blk = t >> 6;
-        const uint32_t lane = (uint32_t)(t & 63), k = code[t];
-        uint64_t pl = 0;
+// rank entries over 32-row blocks (kernels.h): one thread per block
+__global__ void k_rent1(uint64_t nb32, KIdx X, uint4* __restrict__ rent1) {
+    GRID_STRIDE(k, nb32) {
+        const uint32_t x0 = (uint32_t)(k * 32);
+        uint32_t r[8];
+        rank_all(X.occ, x0, X.sigma, r);
+        const OccV v = load_block(X.occ, x0 >> 6);
+        const uint32_t sh = (uint32_t)(k & 1) * 32;
+        uint32_t m[8];
 #pragma unroll
-        for (uint32_t j = 0; j < 5; j++) {
-            const uint64_t v = __ballot((k >> j) & 1u);
-            if (lane == j) pl = v;
+        for (uint32_t c = 0; c < 8; c++)
+            m[c] = (uint32_t)((((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2)) >> sh);
+        for (uint32_t c = 0; c < X.sigma; c++) {
+            uint32_t rc = 0, mc = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 8; t++)
+                if (t == c) { rc = r[t]; mc = m[t]; }
+            rent1[k * X.sigma + c] = make_uint4(rc, mc, r[0], m[0]);
         }
-        PairBlock* B = pb + blk;
-        if (lane < 5) B->plane[lane] = pl;
-        if (lane < 22) B->cnt[lane] = lane < nc ? scan[(size_t)lane * nblk + blk] - scan[(size_t)lane * nblk] : 0u;
+    }
+}
+
+// rows of pair code j in the 32 codes w[0..3] (8 per word) as a bit mask
+__device__ __forceinline__ uint32_t code_mask32(const uint64_t* w, uint32_t j) {
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 32; t++) m |= (uint32_t)(((w[t >> 3] >> (8 * (t & 7))) & 0xffu) == j) << t;
+    return m;
+}
+// scan = scan_u32 of k_pair_counts' code-major 64-row counts (scan[0] = 0)
+__global__ void k_rent2(uint64_t nb32, uint64_t nblk, const uint8_t* __restrict__ code, uint32_t nc, uint32_t sigma,
+                        const uint32_t* __restrict__ scan, uint4* __restrict__ rent2) {
+    GRID_STRIDE(k, nb32) {
+        const uint64_t blk = k >> 1;
+        const bool odd = (k & 1) != 0;
+        const uint64_t* cw = reinterpret_cast<const uint64_t*>(code + blk * 64);
+        uint64_t lo[4], hi[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) { lo[t] = cw[t]; hi[t] = cw[4 + t]; }
+        const uint64_t* w = odd ? hi : lo;
+        auto rank_at = [&](uint32_t j) -> uint32_t {
+            uint32_t r = scan[(size_t)j * nblk + blk] - scan[(size_t)j * nblk];
+            if (odd) r += (uint32_t)__popc(code_mask32(lo, j));
+            return r;
+        };
+        const uint32_t r0 = rank_at(0), m0 = code_mask32(w, 0);
+        for (uint32_t c1 = 1; c1 < sigma; c1++) {
+            const uint32_t q = 1 + (c1 - 1) * sigma;
+            const uint32_t rh = r0 + rank_at(q), mh = m0 | code_mask32(w, q);
+            for (uint32_t c2 = 0; c2 < sigma; c2++) {
+                const uint32_t p = q + c2;
+                rent2[k * (nc - 1) + p - 1] = make_uint4(rank_at(p), code_mask32(w, p), rh, mh);
+            }
+        }
     }
 }
 

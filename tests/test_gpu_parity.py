@@ -334,8 +334,8 @@ def _covid_like(rng, nseg):
     return segs
 
 
-def test_pair_blocks_gpu(oracle, edsbwt, tmp_path):
-    """Two backward steps per pair-block line (k_deep_fast): planted and random 31-mers,
+def test_pair_blocks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """Two backward steps per rank entry (k_deep_fast, rent2): planted and random 31-mers,
     odd and even remaining lengths, patterns that die between the two steps and ones
     that meet '#' rows after the first — identical counts, records and step counts with
     the pair blocks on and off, and equal to the oracle."""
@@ -359,6 +359,11 @@ def test_pair_blocks_gpu(oracle, edsbwt, tmp_path):
             assert np.array_equal(gc2, oc) and np.array_equal(go2, oo)
             st_off = idx.stats()
             assert st_on["intervals_stepped"] == st_off["intervals_stepped"]
+    monkeypatch.setenv("EDSBWT_NO_RANK_ENTRIES", "1")  # the 64-row occ blocks only
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert idx.stats()["intervals_stepped"] == st_on["intervals_stepped"]
 
 
 def test_packed_direct_start_gpu(oracle, edsbwt, tmp_path, monkeypatch):
