@@ -168,6 +168,7 @@ struct Engine {
     DBuf<uint64_t> pv_in, pv_out;
     bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
+    DBuf<uint64_t> ktab_one;  // per D-mer: its one interval inline, else list length and offset (k_ktab_one)
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
@@ -718,6 +719,12 @@ struct Engine {
         HIPCHK(hipMemcpyAsync(ktab_off.p + E + 1, ktab_off.p + E, 4, hipMemcpyDeviceToDevice, stream));
         launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, ktab_b.p);
         HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+        if (N < 0x80000000u) {  // inline single intervals need bit 63 free
+            ktab_one.ensure(E + 1);
+            launch(KC_TABLE, k_ktab_one, E + 1, E, (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p,
+                   ktab_one.p);
+            device_bytes += (E + 1) * 8;
+        }
         HIPCHK(hipStreamSynchronize(stream));
         ktab_depth = c.depth;
         ktab_items = n;
@@ -1062,7 +1069,8 @@ struct Engine {
             lens = slen.p;
         }
         launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
-               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p);
+               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p,
+               goff == ktab_off.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)

@@ -875,7 +875,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    Res* __restrict__ res,
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
-                                                   uint32_t* __restrict__ perm_out) {
+                                                   uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1) {
     unsigned long long n_steps = 0, n_blk = 0, n_pl = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
@@ -898,12 +898,21 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             L = valid ? slen[pi] : 0u;
         }
         const uint32_t u = L > D0 ? nid[i] : 0u;
-        const uint32_t n0 = L > D0 ? iend[u] - ioff[u] : 0u;
+        // kt1 (direct start): the D-mer's one interval inline, or its list's length
+        const uint64_t ent = kt1 && L > D0 ? kt1[u] : 0ull;
+        const uint32_t n0 = L <= D0 ? 0u : kt1 ? ((ent >> 63) ? 1u : (uint32_t)(ent >> 32)) : iend[u] - ioff[u];
         if (n0 > 1) {
             want = 1;
             w = make_uint4((uint32_t)i, D0, ~0u, 0u);
         } else if (n0 == 1) {
-            uint32_t b = ib[ioff[u]], e = ie[ioff[u]];
+            uint32_t b, e;
+            if (kt1) {
+                b = (uint32_t)ent;
+                e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+            } else {
+                b = ib[ioff[u]];
+                e = ie[ioff[u]];
+            }
             SymReader<BPS> sym{k0, krest, P, pi};
             auto code_at = [&](uint32_t dd) -> uint32_t {
                 return pv ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd);
@@ -2115,6 +2124,16 @@ __global__ void k_ktab_bounds(uint64_t E, const uint64_t* __restrict__ key, uint
             if (key[mid] < want) lo = mid + 1; else hi = mid;
         }
         off[x] = (uint32_t)lo;
+    }
+}
+
+// per D-mer: its one interval inline (bit 63 | e << 32 | b; rows < 2^31) or its list's
+// length << 32 | offset — one 8-B read per pattern at the direct start
+__global__ void k_ktab_one(uint64_t E, const uint32_t* __restrict__ off, const uint32_t* __restrict__ b, const uint32_t* __restrict__ e,
+                           uint64_t* __restrict__ one) {
+    GRID_STRIDE(u, E + 1) {
+        const uint32_t o = off[u], n = off[u + 1] - o;
+        one[u] = n == 1 ? (1ull << 63 | (uint64_t)e[o] << 32 | b[o]) : ((uint64_t)n << 32 | o);
     }
 }
 
