@@ -221,6 +221,7 @@ struct Engine {
     DBuf<uint64_t> g_len, g_off;
     DBuf<uint8_t> g_bytes;
     DBuf<uint4> dq;                   // k_deep_fast -> k_deep queue (pattern, depth, b, e), sharded
+    DBuf<uint64_t> dq2;               // ... and, for the packed direct start, each entry's packed start
     DBuf<uint32_t> dqpre;
     uint32_t* pinned_big = nullptr;  // host shard counters + prefix
     DBuf<unsigned long long> stats;  // kStatSlots sharded statistics counters (stat_add)
@@ -1059,6 +1060,7 @@ struct Engine {
         // single-interval walks first; patterns needing lists or links are queued for k_deep
         const size_t qcap = std::max<size_t>(shard_bound(P, 1), 1024);
         dq.ensure(qcap * NSHARD);
+        if (pv) dq2.ensure(qcap * NSHARD);
         dqpre.ensure(NSHARD + 1);
         lcnt.ensure(NSHARD * 32 + 32);
         zero(lcnt.p, NSHARD * 32 * 4);
@@ -1070,7 +1072,7 @@ struct Engine {
         }
         launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
                nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p,
-               goff == ktab_off.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr);
+               goff == ktab_off.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr, pv ? dq2.p : (uint64_t*)nullptr);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
@@ -1078,7 +1080,8 @@ struct Engine {
                   : K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
-               (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p);
+               (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
+               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace)

@@ -875,10 +875,12 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    Res* __restrict__ res,
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
-                                                   uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1) {
+                                                   uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1,
+                                                   uint64_t* __restrict__ q2) {
     unsigned long long n_steps = 0, n_blk = 0, n_pl = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
+    if (q2) q2 += (size_t)sh * qcap;
     UNIFORM_STRIDE(i, valid, P) {
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
@@ -886,9 +888,10 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
         // pv (packed direct start): input index and remaining symbols sorted along with the
         // D-mers, so neither slen nor the key chunks are read; perm is written for k_deep
         uint32_t pi, L;
-        uint64_t rem = 0;
+        uint64_t rem = 0, pvv = 0;
         if (pv) {
             const uint64_t v = valid ? pv[i] : 0ull;
+            pvv = v;
             pi = (uint32_t)(v & 0x7fffffffu);
             rem = v >> 31;
             L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
@@ -969,7 +972,10 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             }
         }
         const uint32_t at = wave_append(qcnt + sh * 32, want);
-        if (want && at < qcap) q[at] = w;
+        if (want && at < qcap) {
+            q[at] = w;
+            if (pv) q2[at] = pvv;  // k_deep reads the packed start instead of perm, slen and the key chunks
+        }
     }
     __shared__ unsigned long long ssum[4];
     stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
@@ -994,7 +1000,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
                                               const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
-                                              uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr) {
+                                              uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2) {
     unsigned long long n_steps = 0, n_hash = 0, n_blk = 0;  // n_blk: occ blocks read
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
@@ -1009,10 +1015,21 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             const uint32_t mid = (lo + hi) >> 1;
             if (spre[mid] <= (uint32_t)j) lo = mid; else hi = mid;
         }
-        const uint4 w = q[(size_t)lo * qcap + ((uint32_t)j - spre[lo])];
+        const size_t qi = (size_t)lo * qcap + ((uint32_t)j - spre[lo]);
+        const uint4 w = q[qi];
         const uint32_t i = w.x, d0 = w.y;
-        const uint32_t pi = ind ? perm[i] : i;  // slen and key chunks in input order (k_deep_fast)
-        const uint32_t L = slen[pi];
+        // q2 (packed direct start): input index and remaining symbols from the queue entry
+        uint32_t pi, L;
+        uint64_t rem = 0;
+        if (q2) {
+            const uint64_t v = q2[qi];
+            pi = (uint32_t)(v & 0x7fffffffu);
+            rem = v >> 31;
+            L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
+        } else {
+            pi = ind ? perm[i] : i;  // slen and key chunks in input order (k_deep_fast)
+            L = slen[pi];
+        }
         uint32_t cb[K], ce[K];
         uint32_t cn;
         if (w.z == ~0u) {  // from the node's items at the cutover depth
@@ -1035,7 +1052,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
         bool over = false;
         for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
-            const uint32_t code = sym.code(d);
+            const uint32_t code = q2 ? 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u) : sym.code(d);
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
@@ -1145,7 +1162,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
                     uint32_t t0 = cb[b2]; cb[b2] = cb[b2 + 1]; cb[b2 + 1] = t0;
                     t0 = ce[b2]; ce[b2] = ce[b2 + 1]; ce[b2 + 1] = t0;
                 }
-        const uint32_t o = perm[i];
+        const uint32_t o = q2 ? pi : perm[i];
         uint32_t occ = 0;
         const uint64_t at = abase + (uint64_t)i * K;
         if (cn == 1) {
