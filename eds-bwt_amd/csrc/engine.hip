@@ -165,6 +165,7 @@ struct Engine {
     bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
+    int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 20);  // ... by the D-mer's leading bits (C3 A/B: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9)
     DBuf<uint64_t> pv_in, pv_out;
     bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
@@ -1164,11 +1165,16 @@ struct Engine {
                    (uint64_t*)nullptr);
         if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
         if (packed) {
+            // the order only buys locality (neighbouring lanes read neighbouring table entries and
+            // rows): the D-mer's first direct_sort_bits bits (its leading symbols) are enough
             size_t tb = 0;
             const int endbit = (int)bits_for(E);
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, 0, endbit, stream));
+            const int beginbit = std::max(0, endbit - direct_sort_bits);
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, beginbit, endbit, stream));
             tmp.ensure(tb);
-            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, 0, endbit, stream)); });
+            timed(KC_TRIE, [&] {
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, beginbit, endbit, stream));
+            });
             sync_check(nullptr, "hipcub call in direct() (packed)");
             st.start_depth = D0;
             return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
