@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
                     }
                     key = (key << BPS) | v;
                 }
-                keys[(size_t)c * P + i] = key;
+                if (!pv) keys[(size_t)c * P + i] = key;  // the packed start needs no key chunks
                 if (c == 0) kc0 = key;
                 if (c == 1) kc1 = key;
             }
