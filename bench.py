@@ -166,7 +166,16 @@ def main():
     base, pats_path = prepare(cfg, args.workdir, rank, world, npat, barrier, args.chars)
 
     t = time.time()
-    idx = pkg.Index(base, device=local)
+    if world > 1 and ndev < world:
+        # ranks sharing a GPU (gloo rehearsal) open the index one at a time: the k-mer table
+        # build's transient workspace is sized for a whole GPU
+        idx = None
+        for r in range(world):
+            if r == rank:
+                idx = pkg.Index(base, device=local)
+            barrier()
+    else:
+        idx = pkg.Index(base, device=local)
     t_open = time.time() - t
     if args.locate == "table" and locate:
         idx.search([b"A"], table=True)  # builds the table outside the timed region

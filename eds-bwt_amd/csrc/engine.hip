@@ -234,6 +234,25 @@ struct Engine {
             for (uint32_t k = 0; k < kStatStride; k++) v[k] += pinned_stats[s * kStatStride + k];
         return v;
     }
+    // the search workspace sized by the k-mer table build (B^D patterns): given back after it,
+    // so an open index holds its tables only and searches size the workspace to their batches
+    void release_workspace() {
+        for (auto* b : {&len, &perm, &perm2, &slen, &lcp, &nid[0], &nid[1], &flag, &scan, &node_first, &node_parent, &child_first,
+                        &child_end, &ib[0], &ib[1], &ie[0], &ie[1], &iu[0], &iu[1], &ioff[0], &ioff[1], &iend[0], &iend[1], &iocb, &ioce,
+                        &hcnt, &hoff, &rflag, &rscan, &rb, &re, &ru, &doff, &dend, &docb, &doce, &tcnt, &toff, &tb, &te, &tu, &tflag,
+                        &tscan, &cb, &ce, &cu, &mflag, &mscan, &fcnt, &foff, &node_occ, &ab, &ae, &trow, &tpat, &lp, &lp2, &li, &li2,
+                        &ovf_orig, &ovf_scan, &sub_map, &lcnt, &ck_u, &ck_k, &ck_e, &gcnt, &gfill, &goff, &gend, &gb, &gee, &fv, &fv2,
+                        &fend, &hterm, &eu, &eb, &ee, &eck_u, &eck_k, &eck_e, &efv, &shpre, &fu, &fb, &fe, &fpre, &glen, &gid, &gflag,
+                        &gscan, &g_map, &dqpre, &kt_kid, &kt_cnt, &kt_pos})
+            b->release();
+        for (auto* b : {&keys, &kc, &kc2, &skey, &child_info, &lkeys, &lkeys2, &occ64, &oscan, &tc64, &tscan64, &tout, &blk_first, &lk,
+                        &lk2, &sub_len, &sub_off, &fk, &fk2, &ekeys, &efk, &g_len, &g_off, &dq2, &pv_in, &pv_out})
+            b->release();
+        for (auto* b : {&node_char, &tmp, &sub_bytes, &fin, &g_bytes}) b->release();
+        res.release(); sub_res.release(); g_res.release();
+        rec.release(); rec2.release();
+        dq.release();
+    }
     DBuf<uint8_t> hbytes;   // host-API pattern staging
     DBuf<uint64_t> hoffs;
     DBuf<uint32_t> hcounts;
@@ -702,7 +721,10 @@ struct Engine {
         count_only = was_count_only;
         st = edsbwt_stats{};
         HIPCHK(hipStreamSynchronize(stream));
-        if (c.depth < kKtabMinDepth || c.n == 0) return;
+        if (c.depth < kKtabMinDepth || c.n == 0) {
+            release_workspace();
+            return;
+        }
         const uint64_t E = pw(c.depth), n = c.n;
         DBuf<uint64_t> k1, k2;
         DBuf<uint32_t> e2;
@@ -732,6 +754,7 @@ struct Engine {
         ktab_items = n;
         ktab_entries = E;
         device_bytes += (E + 1) * 4 + n * 8;
+        release_workspace();
         if (trace) std::fprintf(stderr, "[edsbwt] k-mer start table: depth %u, %llu D-mers, %llu intervals\n", ktab_depth,
                                 (unsigned long long)E, (unsigned long long)n);
     }
