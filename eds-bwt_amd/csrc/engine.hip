@@ -173,8 +173,10 @@ struct Engine {
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
-    DBuf<uint4> rent1, rent2;
-    uint32_t r2stride = 0;
+    DBuf<uint4> rent1, rent2, rent3;
+    DBuf<uint32_t> pc3;
+    uint32_t r2stride = 0, r3stride = 0;
+    bool use_triples = env_double("EDSBWT_NO_TRIPLES", 0) == 0;
     bool use_rent = env_double("EDSBWT_NO_RANK_ENTRIES", 0) == 0;
     uint32_t PC[kPairCodes + 3] = {0};
     bool use_pairs = true;  // per search (EDSBWT_NO_PAIRS clears it)
@@ -309,6 +311,9 @@ struct Engine {
         X.rent1 = use_rent ? rent1.p : nullptr;
         X.rent2 = use_rent && use_pairs ? rent2.p : nullptr;
         X.r2stride = r2stride;
+        X.rent3 = use_rent && use_pairs && use_triples ? rent3.p : nullptr;
+        X.r3stride = r3stride;
+        X.PC3 = pc3.p;
         for (uint32_t k = 0; k < kPairCodes + 3; k++) X.PC[k] = PC[k];
         return X;
     }
@@ -677,7 +682,47 @@ struct Engine {
         HIPCHK(hipStreamSynchronize(stream));
         for (uint32_t c1 = 1; c1 < sigma; c1++)
             for (uint32_t c2 = 0; c2 < sigma; c2++) PC[1 + (c1 - 1) * sigma + c2] = C[c2] + rk[(size_t)c1 * sigma + c2];
+        code.release();
+        cscan.release();
+        build_triples();
 #endif
+    }
+
+    // rent3 (kernels.h): triple codes, their 64-row counts scanned, one entry per 32-row block
+    // and (c1, c2, c3) over the non-'#' symbols; PC3 = C[c3] + rank_c3(L, PC[(c1, c2)])
+    void build_triples() {
+        const uint32_t B = sigma - 1, nc = 1 + B * sigma * sigma;
+        const uint64_t nb32 = (uint64_t)N / 32 + 1, nblk = (uint64_t)N / 64 + 1, nrows = nblk * 64;
+        if (env_double("EDSBWT_TRIPLES", 1) == 0 || nc > 255 || (uint64_t)nc * nblk > 0x7fffffffull) return;
+        const KIdx X = kidx();
+        DBuf<uint8_t> code;
+        DBuf<uint32_t> cnt, cscan;
+        code.ensure(nrows);
+        cnt.ensure((size_t)nc * nblk);
+        launch(KC_TABLE, k_triple_codes, nrows, nrows, X, code.p);
+        launch(KC_TABLE, k_pair_counts, nrows, nblk, (const uint8_t*)code.p, nc, cnt.p);
+        scan_u32(cnt.p, cscan, (size_t)nc * nblk);
+        cnt.release();
+        r3stride = B * B * B;
+        rent3.ensure(nb32 * r3stride);
+        launch(KC_TABLE, k_rent3, nb32, nb32, nblk, (const uint8_t*)code.p, sigma, (const uint32_t*)cscan.p, rent3.p);
+        device_bytes += nb32 * r3stride * 16;
+        // PC3 from the ranks at the pair pile starts PC[(c1, c2)]
+        std::vector<uint32_t> rows((size_t)B * B), rk((size_t)B * B * sigma), h3(r3stride);
+        for (uint32_t c1 = 1; c1 < sigma; c1++)
+            for (uint32_t c2 = 1; c2 < sigma; c2++) rows[(c1 - 1) * B + (c2 - 1)] = PC[1 + (c1 - 1) * sigma + c2];
+        DBuf<uint32_t> d_rows, d_rk;
+        d_rows.ensure(rows.size());
+        d_rk.ensure(rk.size());
+        HIPCHK(hipMemcpyAsync(d_rows.p, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, stream));
+        launch(KC_TABLE, k_ranks_at, rows.size(), (uint32_t)rows.size(), (const uint32_t*)d_rows.p, X, d_rk.p);
+        HIPCHK(hipMemcpyAsync(rk.data(), d_rk.p, rk.size() * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        for (uint32_t i = 0; i < B * B; i++)
+            for (uint32_t c3 = 1; c3 < sigma; c3++) h3[i * B + (c3 - 1)] = C[c3] + rk[(size_t)i * sigma + c3];
+        pc3.ensure(r3stride);
+        HIPCHK(hipMemcpyAsync(pc3.p, h3.data(), h3.size() * 4, hipMemcpyHostToDevice, stream));
+        HIPCHK(hipStreamSynchronize(stream));
     }
 
     // k-mer start table: the order-free walk run once over every K-mer of the non-'#'

@@ -45,7 +45,10 @@ constexpr uint32_t kOccRows = 1u << kOccShift;
 // are [PC[p] + rank_p(b), PC[p] + rank_p(e+1)) for p = (c1, c2) and Q's rows [b, e], and
 //   rent2[k * (nc-1) + p-1] = {rank_p(32k), mask_p, rank_{0|q}(32k), mask_{0|q}}, q = (c1, '#'),
 // answers two steps at once when no row of [b, e] holds '#' or (c1, '#') — no link at
-// either step.
+// either step.  Triple codes (L[x], L[LF(x)], L[LF^2(x)]) give, the same way,
+//   rent3[k * (sigma-1)^3 + t] = {rank_p(32k), mask_p, rank of rows coded '#', (c1, '#') or
+//                                 (c1, c2, '#') (32k), their mask} for p = (c1, c2, c3)
+// and three steps per entry.
 constexpr uint32_t kPairCodes = 21;  // sigma = 5: 1 + 4 * 5
 
 // per-pattern result (backwardSearch's final list): archive offset of its intervals, their
@@ -78,6 +81,9 @@ struct KIdx {
     const uint4* rent1;        // single-step rank entries (nullptr: not built)
     const uint4* rent2;        // two-step rank entries (nullptr: not built or not used)
     uint32_t r2stride;         // rent2 entries per block (pair codes - 1)
+    const uint4* rent3;        // three-step rank entries (nullptr: not built or not used)
+    uint32_t r3stride;         // rent3 entries per block ((sigma-1)^3)
+    const uint32_t* PC3;       // first row of the suffixes c3 c2 c1 ... per rent3 entry
     uint32_t PC[kPairCodes + 3];  // first row of the suffixes c2 c1 ... for pair code p = (c1, c2)
 };
 

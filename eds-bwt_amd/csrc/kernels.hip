@@ -923,9 +923,34 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             bool alive = true;
             uint32_t d = D0;
             bool pair_skip = false;  // the pair entry just found '#' rows: take one step
+            uint32_t tri_from = 0;   // no three-step attempt before this depth (one just failed)
             for (; d < L; d++) {
                 const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
+                // three characters from one rank entry per end (rent3), as the pair below
+                if (X.rent3 && d >= tri_from && d + 2 < L && c != 0) {
+                    const uint32_t c2 = code_at(d + 1), c3 = code_at(d + 2);
+                    if (c2 != 0 && c2 < X.sigma && c3 != 0 && c3 < X.sigma) {
+                        const uint32_t B = X.sigma - 1;
+                        const uint32_t t = ((c - 1) * B + (c2 - 1)) * B + (c3 - 1);
+                        const uint4 v0 = X.rent3[(size_t)(b >> 5) * X.r3stride + t];
+                        const uint4 v1 = X.rent3[(size_t)((e + 1) >> 5) * X.r3stride + t];
+                        uint32_t p0, x0, p1, x1;
+                        rent_rank(v0, b, p0, x0);
+                        rent_rank(v1, e + 1, p1, x1);
+                        const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
+                        n_blk += nl;
+                        n_pl += nl;
+                        if (x1 == x0 && p1 > p0) {
+                            n_steps += 3;
+                            b = X.PC3[t] + p0;
+                            e = X.PC3[t] + p1 - 1;
+                            d += 2;
+                            continue;
+                        }
+                        tri_from = d + 3;
+                    }
+                }
                 // two characters from one rank entry per interval end, when no row of [b, e]
                 // holds '#' or (c, '#') and the pattern survives both; else one step
                 if (X.rent2 && !pair_skip && d + 1 < L && c != 0) {
@@ -1921,7 +1946,7 @@ __global__ void k_pair_counts(uint64_t nblk, const uint8_t* __restrict__ code, u
         const uint32_t lane = (uint32_t)(t & 63), k = code[t];
         for (uint32_t j = 0; j < nc; j++) {
             const uint32_t n = (uint32_t)__popcll(__ballot(k == j));
-            if (lane == j) cnt[(size_t)j * nblk + blk] = n;
+            if (lane == (j & 63u)) cnt[(size_t)j * nblk + blk] = n;
         }
     }
 }
@@ -1982,6 +2007,70 @@ __global__ void k_rent2(uint64_t nb32, uint64_t nblk, const uint8_t* __restrict_
         }
     }
 }
+
+// triple code of every row: 0 for '#'; else 1 + (c1-1)*sigma^2 + c2*sigma + c3 with c1 = L[x],
+// c2 = L[LF(x)], c3 = L[LF^2(x)] (c3 = 0 when c2 = '#'); 255 for the padding rows past N
+__global__ void k_triple_codes(uint64_t nrows, KIdx X, uint8_t* __restrict__ code) {
+    GRID_STRIDE(x, nrows) {
+        uint32_t k = 255;
+        if (x < X.N) {
+            uint32_t r;
+            const uint32_t c1 = sym_rank(X.occ, (uint32_t)x, &r);
+            if (c1 == 0) {
+                k = 0;
+            } else {
+                uint32_t r2, r3;
+                const uint32_t c2 = sym_rank(X.occ, X.C[c1] + r, &r2);
+                const uint32_t c3 = c2 == 0 ? 0u : sym_rank(X.occ, X.C[c2] + r2, &r3);
+                k = 1 + (c1 - 1) * X.sigma * X.sigma + c2 * X.sigma + c3;
+            }
+        }
+        code[x] = (uint8_t)k;
+    }
+}
+
+// rank of every symbol at n given rows: out[i * sigma + c]
+__global__ void k_ranks_at(uint32_t n, const uint32_t* __restrict__ rows, KIdx X, uint32_t* __restrict__ out) {
+    GRID_STRIDE(i, n) {
+        uint32_t r[8];
+        rank_all(X.occ, rows[i], X.sigma, r);
+        for (uint32_t c = 0; c < X.sigma; c++) out[i * X.sigma + c] = r[c];
+    }
+}
+
+// three-step rank entries (kernels.h rent3) from k_triple_codes' scanned 64-row counts
+__global__ void k_rent3(uint64_t nb32, uint64_t nblk, const uint8_t* __restrict__ code, uint32_t sigma, const uint32_t* __restrict__ scan,
+                        uint4* __restrict__ rent3) {
+    GRID_STRIDE(k, nb32) {
+        const uint64_t blk = k >> 1;
+        const bool odd = (k & 1) != 0;
+        const uint64_t* cw = reinterpret_cast<const uint64_t*>(code + blk * 64);
+        uint64_t lo[4], hi[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) { lo[t] = cw[t]; hi[t] = cw[4 + t]; }
+        const uint64_t* w = odd ? hi : lo;
+        auto rank_at = [&](uint32_t j) -> uint32_t {
+            uint32_t r = scan[(size_t)j * nblk + blk] - scan[(size_t)j * nblk];
+            if (odd) r += (uint32_t)__popc(code_mask32(lo, j));
+            return r;
+        };
+        const uint32_t B = sigma - 1, s2 = sigma * sigma;
+        const uint32_t r0 = rank_at(0), m0 = code_mask32(w, 0);
+        for (uint32_t c1 = 1; c1 < sigma; c1++) {
+            const uint32_t s1 = 1 + (c1 - 1) * s2;  // (c1, '#')
+            const uint32_t ra = r0 + rank_at(s1), ma = m0 | code_mask32(w, s1);
+            for (uint32_t c2 = 1; c2 < sigma; c2++) {
+                const uint32_t sc = s1 + c2 * sigma;  // (c1, c2, '#')
+                const uint32_t rs = ra + rank_at(sc), ms = ma | code_mask32(w, sc);
+                for (uint32_t c3 = 1; c3 < sigma; c3++) {
+                    const uint32_t p = sc + c3;
+                    rent3[k * B * B * B + ((c1 - 1) * B + (c2 - 1)) * B + (c3 - 1)] = make_uint4(rank_at(p), code_mask32(w, p), rs, ms);
+                }
+            }
+        }
+    }
+}
+
 
 // For every word w, walk LF from row w (its '#'-suffix) to the row with L='#'
 // (position 0): rows visited get DA = w and their distance from the word end.

@@ -359,6 +359,11 @@ def test_pair_blocks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             assert np.array_equal(gc2, oc) and np.array_equal(go2, oo)
             st_off = idx.stats()
             assert st_on["intervals_stepped"] == st_off["intervals_stepped"]
+    monkeypatch.setenv("EDSBWT_NO_TRIPLES", "1")  # two steps per entry at most
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert idx.stats()["intervals_stepped"] == st_on["intervals_stepped"]
     monkeypatch.setenv("EDSBWT_NO_RANK_ENTRIES", "1")  # the 64-row occ blocks only
     with edsbwt.Index(base) as idx:
         gc, go = idx.search((buf, offs))
