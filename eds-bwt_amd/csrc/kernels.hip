@@ -361,7 +361,7 @@ __global__ void k_lens(const uint64_t* __restrict__ off, uint64_t P, uint32_t* _
 // keys[c*P + i].  A block's patterns are contiguous in `bytes`, so the block stages
 // their bytes in LDS with coalesced 4-B loads (spans over kKeySpan bytes read global
 // memory directly).  Also writes len[] and counts patterns holding the end-marker '#'.
-constexpr uint32_t kKeySpan = 24576;
+constexpr uint32_t kKeySpan = 12288;  // bytes of one block-round's patterns staged in LDS (12 KB: 13 blocks per CU overlap their loads)
 template <int BPS>
 __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
                                               const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t nch, uint64_t* __restrict__ keys,
@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
             const uint32_t L = (uint32_t)(off[i + 1] - a);
             len[i] = L;
             const uint8_t* sg = bytes + a;
-            const uint8_t* sl = reinterpret_cast<const uint8_t*>(sbuf) + (a - w0);
+            const uint32_t so = (uint32_t)(a - w0);
             uint32_t term = 0;
             uint64_t kc0 = 0, kc1 = 0;
             for (uint32_t c = 0; c < nch; c++) {
@@ -409,7 +409,15 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
                     const uint32_t pos = c * SPC + t;
                     uint64_t v = 0;
                     if (pos < L) {
-                        const uint8_t ch = staged ? sl[L - 1 - pos] : sg[L - 1 - pos];
+                        // the staged bytes straight from LDS (a block-uniform branch: no flat
+                        // loads through a pointer that may be LDS or global)
+                        uint32_t ch;
+                        if (staged) {
+                            const uint32_t k = so + L - 1 - pos;
+                            ch = (sbuf[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                        } else {
+                            ch = sg[L - 1 - pos];
+                        }
                         v = scode[ch];
                         term |= ch == '#';
                     }
