@@ -1695,12 +1695,11 @@ struct Engine {
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
         zero(counters.p + 1, 8);
         zero(counters.p + 12, 16);
-        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12);
-        if (locate) {  // occurrence and task offsets: one scan of both, packed
-            occ64.ensure(P);
-            launch(KC_LOCPREP, k_res_scan_in, P, (const Res*)res.p, P, occ64.p, (uint64_t*)nullptr);
-            inclusive_scan_u64(occ64.p, oscan, P);
-        }
+        if (locate) occ64.ensure(P);
+        // counts, found, totals and (locate) the packed scan input in one pass over the results
+        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
+                      locate ? occ64.p : (uint64_t*)nullptr);
+        if (locate) inclusive_scan_u64(occ64.p, oscan, P);  // occurrence and task offsets: one scan of both
         HIPCHK(hipMemcpyAsync(pinned, counters.p + 1, 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipMemcpyAsync(pinned + 2, counters.p + 12, 16, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));

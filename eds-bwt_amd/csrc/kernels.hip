@@ -2128,12 +2128,15 @@ __global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, cons
 
 // launched with a small grid (kReduceBlocks): one atomic per block
 __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
-                                                     unsigned long long* __restrict__ found, unsigned long long* __restrict__ sums) {
+                                                     unsigned long long* __restrict__ found, unsigned long long* __restrict__ sums,
+                                                     uint64_t* __restrict__ scan_in) {
+    // scan_in (locate): the packed scan input occurrences << 32 | tasks, in the same pass
     __shared__ unsigned long long sh[4];
     unsigned long long f = 0, so = 0, st = 0;
     GRID_STRIDE(i, P) {
         const Res r = res[i];
         counts[i] = r.occ;  // backwardSearch's return value per pattern
+        if (scan_in) scan_in[i] = (uint64_t)r.occ << 32 | (r.cnt & ~kResRow);
         f += r.occ > 0;
         so += r.occ;
         st += r.cnt & ~kResRow;
