@@ -693,7 +693,9 @@ struct Engine {
     void build_triples() {
         const uint32_t B = sigma - 1, nc = 1 + B * sigma * sigma;
         const uint64_t nb32 = (uint64_t)N / 32 + 1, nblk = (uint64_t)N / 64 + 1, nrows = nblk * 64;
-        if (env_double("EDSBWT_TRIPLES", 1) == 0 || nc > 255 || (uint64_t)nc * nblk > 0x7fffffffull) return;
+        // off by default: C3 A/B (3 x 20 steps) 2.73e9 with rent3 vs 2.75e9 without — the third
+        // step per entry saves no time once two are taken, and rent3 costs 32 B per row
+        if (env_double("EDSBWT_TRIPLES", 0) == 0 || nc > 255 || (uint64_t)nc * nblk > 0x7fffffffull) return;
         const KIdx X = kidx();
         DBuf<uint8_t> code;
         DBuf<uint32_t> cnt, cscan;

@@ -339,6 +339,7 @@ def test_pair_blocks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     odd and even remaining lengths, patterns that die between the two steps and ones
     that meet '#' rows after the first — identical counts, records and step counts with
     the pair blocks on and off, and equal to the oracle."""
+    monkeypatch.setenv("EDSBWT_TRIPLES", "1")  # three-step entries too (off by default)
     rng = random.Random(355)
     segs = _covid_like(rng, 800)
     if any(w == "" for w in segs[1]):
