@@ -1,17 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark: EDS-BWT backward search on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
 
-A *step* is one pass of the hot path (MOVE_EDSBWTSearch's pattern loop + locate,
-MOVE_EDSBWTSearch.cpp:97-155) over one batch of synthetic patterns whose bytes and
-offsets are already resident in HBM: the whole trie-level search plus position
-recovery through libedsbwt.so, results (counts + occurrence records) left in HBM.
-Default workload = config C3 of SURVEY.md §8(d) (BASELINE.json configs[2]): a
-~100 Mchar COVID-like synthetic EDS, 10M planted 31-mers, full locate.  N>1 ranks
-(one per GPU, torchrun) each search their own contiguous shard of 10M patterns
-against a replicated index (weak scaling) and the per-pattern counts are gathered
-over RCCL.  rank 0 prints one JSON line.
+A *step* is one pass of the hot path — MOVE_EDSBWTSearch's pattern loop with position
+recovery (MOVE_EDSBWTSearch.cpp:97-155, 228-374) — over one batch of synthetic patterns:
+the pattern file's bytes in (page-locked) host memory go through edsbwt_search_lines,
+the library's pipelined host path (H2D of chunk k+1 overlaps the search of chunk k and the
+D2H of chunk k-1), until every count and occurrence record is back in host memory.
+`value` is therefore SURVEY.md §8(d)'s patterns/s: first H2D of the patterns to the last
+D2H of the results.  The same batch with its bytes and offsets already in HBM and the
+results left there is timed next and reported as `device_resident` (the kernel roofline
+comes from that run).
+
+Default workload = C3 (BASELINE.json configs[2]): ~100 Mchar COVID-like synthetic EDS,
+10M planted 31-mers per GPU, full locate.  C4 = the C3 index with 100M patterns in total,
+sharded over the ranks.  N>1: one process per GPU (torchrun; `--gpus N` without torchrun
+starts it), each rank searches its contiguous shard against a replicated index; the
+exchange step — sizes all-gathered, per-pattern counts gathered to rank 0 over RCCL — is
+inside the timed step.  rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -19,6 +26,7 @@ import argparse
 import importlib
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -26,67 +34,33 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-BUILD = os.path.join(ROOT, "eds-bwt_amd", "_build")
 sys.path.insert(0, ROOT)
+import workloads  # noqa: E402
 
-CONFIGS = {
-    # name: (generator config, EDS chars, EDS seed, patterns per GPU, lengths, mode, pattern seed, locate)
-    "c2": ("c2", 10_000_000, 1, 1_000_000, "20", "random", 2, False),
-    "c3": ("c3", 100_000_000, 3, 10_000_000, "31", "planted", 4, True),
-    "c5": ("c5", 1_000_000_000, 6, 200_000, "8,16,32,64", "mixed", 7, False),
-}
-WORKLOAD = {
-    "c2": "C2: 10 Mchar synthetic EDS (sigma=4, ~3 strings/segment), 1M random 20-mers per GPU, count-only",
-    "c3": "C3: ~100 Mchar COVID-like synthetic EDS, 10M planted 31-mers per GPU, full position recovery",
-    "c5": "C5: 1 Gchar synthetic EDS with 20% empty-string segments, mixed 8-64-mers per GPU, counts (a random 8-mer has ~1e4-1e5 occurrences)",
-}
 MI355X_HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
-# Practical ceiling of the rank queries' access shape — one random 64-B line per lane
-# from a table of the C3 index's size (100 MB, Infinity-Cache resident): measured on
-# MI355X by tools/calib_gather.hip (profiles/r01_calib_gather.json), 3.4-3.5 TB/s.
-GATHER64_CEILING_LINES_PER_S = 5.48e10
+MI355X_MALL_BYTES = 256 << 20  # Infinity Cache: index tables smaller than this are cache-resident
+# Practical ceilings of the deep kernels' access shape on MI355X (tools/calib_gather.hip,
+# profiles/r02_calib_gather.json): one random 16-B rank entry per lane per step from a
+# table of the C3 rank entries' size, issued as the kernel issues them.
+CALIB = os.path.join(ROOT, "profiles", "calib_gather.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def run(args, **kw):
-    subprocess.run([str(a) for a in args], check=True, **kw)
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def ensure_built():
-    need = [os.path.join(BUILD, f) for f in ("libedsbwt.so", "eds_transform", "edsbwt_gen")]
-    if not all(os.path.exists(p) for p in need):
-        run(["make", "-s", "-j", "16", "-C", os.path.join(ROOT, "eds-bwt_amd"), "all"])
-
-
-def prepare(cfg: str, workdir: str, rank: int, world: int, npat: int, barrier, chars_override: int = 0):
-    gcfg, chars, eseed, _, lens, mode, pseed, _ = CONFIGS[cfg]
-    tag = cfg
-    if chars_override:
-        chars, tag = chars_override, f"{cfg}_{chars_override}"
-    os.makedirs(workdir, exist_ok=True)
-    eds = os.path.join(workdir, f"{tag}.eds")
-    base = os.path.join(workdir, tag)
-    if rank == 0 and not os.path.exists(base + "_info.aux"):
-        t = time.time()
-        run([os.path.join(BUILD, "edsbwt_gen"), "eds", "--config", gcfg, "--chars", chars, "--seed", eseed, "--out", eds])
-        run([os.path.join(BUILD, "eds_transform"), eds, base, "--no-runs"])
-        log(f"[bench] index {base} built in {time.time() - t:.1f}s")
-    barrier()
-    pats = os.path.join(workdir, f"{tag}_pats_{npat}_r{rank}of{world}.txt")
-    if not os.path.exists(pats):
-        run([os.path.join(BUILD, "edsbwt_gen"), "patterns", "--eds", eds, "--count", npat, "--lens", lens, "--mode", mode,
-             "--seed", pseed * 1000003 + rank, "--out", pats])
-    barrier()
-    return base, pats
-
-
-def traffic_from_profile(cfg: str, kernel: str, locate: bool):
+def traffic_from_profile(cfg: str, kernel: str):
     """HBM-side bytes per launch of `kernel` from the committed rocprofv3 PMC summary of
-    this same command (profiles/traffic_<cfg>.json, written by tools/profile_summary.py
-    from separate --pmc FETCH_SIZE / WRITE_SIZE passes); None when there is none."""
+    this command (profiles/traffic_<cfg>.json, tools/profile_summary.py: separate --pmc
+    FETCH_SIZE / WRITE_SIZE passes); None when there is none."""
     path = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
     try:
         t = json.load(open(path))
@@ -96,28 +70,32 @@ def traffic_from_profile(cfg: str, kernel: str, locate: bool):
         return None, None
 
 
-def cpu_baseline(base: str, pats_path: str, sample: int, threads: int) -> dict:
-    """The oracle (faithful C restatement of MOVE_EDSBWTSearch: a-balanced M_LF,
-    literal per-pattern link/step/locate) on the first `sample` patterns."""
+def gather_ceiling():
+    try:
+        c = json.load(open(CALIB))
+        return float(c["ceiling_lines_per_s"]), c.get("shape", "")
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int) -> dict:
+    """The oracle (faithful C restatement of MOVE_EDSBWTSearch: a-balanced M_LF, literal
+    per-pattern link/step/locate, MOVE_EDSBWTSearch.cpp:228-374) on the first `sample`
+    patterns of this rank's batch, on `threads` host threads over contiguous shards; index
+    load excluded, as the reference's `bs took:` region excludes it (:109,145)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc  # checker / CPU baseline only
 
-    pkg = importlib.import_module("eds-bwt_amd")
-    buf, offs = pkg.read_pattern_file(pats_path)
-    offs = offs[: sample + 1]
-    buf = buf[: int(offs[-1])]
+    o = offs[: sample + 1]
+    b = buf[: int(o[-1])]
     t = time.time()
     eng = orc.Engine(base, 8)
     t_open = time.time() - t
     t = time.time()
-    counts, occ, ctr = eng.search(buf, offs, threads=threads)
+    counts, occ, ctr = eng.search(b, o, first_pattern_id=first_id, threads=threads)
     dt = time.time() - t
     eng.close()
-    return {"value": round(sample / dt, 3), "unit": "patterns/sec", "cores": threads, "kind": "port",
-            "sample": f"first {sample} patterns of rank 0's batch, oracle/edsbwt_oracle.c (literal MOVE_EDSBWTSearch "
-                      f"restatement, a=8 M_LF) on {threads} host threads; index load {t_open:.1f}s excluded",
-            "seconds": round(dt, 3), "lf_steps": int(ctr["step_moves"] + ctr["locate_moves"]),
-            "interval_steps": int(ctr["interval_steps"]), "occurrences": int(ctr["occurrences"])}
+    return {"value": sample / dt, "seconds": dt, "open_s": t_open, "counts": counts, "occ": occ, "ctr": ctr}
 
 
 def main():
@@ -125,31 +103,42 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (default: the config's)")
-    ap.add_argument("--chars", type=int, default=0, help="EDS size override (scaled-down parity/diagnostic runs)")
+    ap.add_argument("--config", default="c3", choices=sorted(workloads.CONFIGS))
+    ap.add_argument("--patterns", type=int, default=0, help="patterns per GPU (C4: in total; default: the config's)")
+    ap.add_argument("--chars", type=int, default=0, help="EDS size override (scaled-down diagnostic runs)")
     ap.add_argument("--locate", default="sampled", choices=("sampled", "walk", "table"),
-                    help="position recovery: LF walk to the first sampled row (default), the reference's full "
-                         "walk to '#', or the per-row (word, offset) table")
+                    help="position recovery: per-row samples (default), the reference's full walk to '#', or the per-row table")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=0)
-    ap.add_argument("--workdir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "edsbwt_bench"))
+    ap.add_argument("--no-device", action="store_true", help="skip the device-resident leg")
+    ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start torchrun as a child (nothing has touched the GPU yet)
+        port = free_port()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = max(1, torch.cuda.device_count())
     local = local % ndev  # rehearsal: several ranks may share one GPU (gloo)
+    gdev = torch.device("cpu")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            gdev = torch.device("cuda", local)
         else:
             dist.init_process_group(args.dist_backend)
         barrier = lambda: dist.barrier()  # noqa: E731
@@ -157,14 +146,25 @@ def main():
         torch.cuda.set_device(0)
         barrier = lambda: None  # noqa: E731
     if rank == 0:
-        ensure_built()
+        workloads.ensure_built()
     barrier()
     pkg = importlib.import_module("eds-bwt_amd")
-    cfg = args.config
-    npat = args.patterns or CONFIGS[cfg][3]
-    locate = CONFIGS[cfg][7]
-    base, pats_path = prepare(cfg, args.workdir, rank, world, npat, barrier, args.chars)
+    shard = importlib.import_module("eds-bwt_amd.shard")
+    w = workloads.CONFIGS[args.config]
+    locate = w.locate
 
+    # ---- inputs (outside the timed region): index, this rank's shard of the pattern stream
+    t = time.time()
+    if rank == 0:
+        eds, base = workloads.build_index(w, args.workdir, args.chars, log)
+    barrier()
+    eds, base = workloads.build_index(w, args.workdir, args.chars)
+    lo, hi = workloads.shard(w, rank, world, args.patterns)
+    pats_path = workloads.pattern_file(w, eds, args.workdir, lo, hi, tag=f"_{args.chars}" if args.chars else "")
+    barrier()
+    t_prep = time.time() - t
+    npat = hi - lo
+    first_id = lo + 1
     t = time.time()
     if world > 1 and ndev < world:
         # ranks sharing a GPU (gloo rehearsal) open the index one at a time: the k-mer table
@@ -179,73 +179,120 @@ def main():
     t_open = time.time() - t
     if args.locate == "table" and locate:
         idx.search([b"A"], table=True)  # builds the table outside the timed region
-    buf, offs = pkg.read_pattern_file(pats_path)
+    text = pkg.read_pattern_file_pinned(pats_path)
+    counts_hb = pkg.HostBuffer(4 * (npat + 1))
+    counts = counts_hb.array(np.uint32, npat + 1)
     dev = torch.device("cuda", local)
-    d_bytes = torch.from_numpy(buf).to(dev)
-    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
-    d_counts = torch.zeros(npat, dtype=torch.int32, device=dev)
-    first_id = rank * npat + 1
+    d_counts_x = torch.zeros(npat, dtype=torch.int32, device=dev)  # exchange buffer (counts gathered to rank 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    flags_kw = dict(table=args.locate == "table", walk=args.locate == "walk")
 
-    def step(profile=False):
-        return idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(),
-                                 first_pattern_id=first_id, locate=locate, table=args.locate == "table", profile=profile,
-                                 stream=stream, walk=args.locate == "walk")
+    def e2e_step(keep=False):
+        n, ptr, nocc = idx.search_lines(text.ptr, text.nbytes, counts_hb.ptr, npat + 1, first_pattern_id=first_id,
+                                        locate=locate, keep=keep)
+        assert n == npat, (n, npat)
+        return ptr, nocc
 
-    gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    gathered = torch.zeros(npat * world, dtype=torch.int32, device=gdev) if world > 1 else None
+    def exchange(nocc):
+        # the path's one exchange step: sizes all-gathered, per-pattern counts gathered to rank 0 (RCCL/xGMI)
+        if world == 1:
+            return
+        sizes = shard.exchange_sizes(npat, nocc, gdev)
+        src = d_counts_x if args.dist_backend == "nccl" else torch.from_numpy(counts[:npat].view(np.int32))
+        if args.dist_backend == "nccl":
+            d_counts_x.copy_(torch.from_numpy(counts[:npat].view(np.int32)), non_blocking=True)
+        shard.gather_counts(src, [int(x) for x in sizes[:, 0]])
 
-    def exchange():
-        # the path's one exchange: every rank's per-pattern counts, gathered over RCCL/xGMI
-        if world > 1:
-            src = d_counts if args.dist_backend == "nccl" else d_counts.cpu()
-            dist.all_gather_into_tensor(gathered, src)
-
+    # ---- timed: end-to-end (host memory -> host memory)
     for _ in range(args.warmup):
-        step()
-        exchange()
+        _, nocc = e2e_step()
+        exchange(nocc)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kstats = {}
+    search_ms = exch_ms = 0.0
+    held = (0, 0)
     total_occ = 0
-    lf_steps = 0
-    ref_loc_steps = 0
+    walls = []
     for i in range(args.steps):
-        _, nocc = step(profile="light")
-        exchange()
-        st = idx.stats()
+        ta = time.perf_counter()
+        last = i == args.steps - 1
+        ptr, nocc = e2e_step(keep=last)
+        if last:
+            held = (ptr, nocc)
+        tb = time.perf_counter()
+        exchange(nocc)
+        search_ms += 1e3 * (tb - ta)
+        exch_ms += 1e3 * (time.perf_counter() - tb)
+        walls.append(idx.stats()["ms_wall"])
         total_occ += nocc
-        lf_steps += 2 * st["intervals_stepped"] + st["locate_lf_steps"]
-        ref_loc_steps += st["locate_offsets"]
-        for k, v in st["kernels"].items():
-            a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
-            a["ms"] += v["ms"]
-            a["launches"] += v["launches"]
-            a["bytes"] += v["bytes"]
-            a["lines"] += v["lines"]
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    e2e_stats = idx.stats()
+    per_rank = [search_ms / args.steps, exch_ms / args.steps]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        agg = torch.tensor([lf_steps, total_occ, ref_loc_steps], dtype=torch.float64, device=gdev)
+        pr = torch.tensor(per_rank, dtype=torch.float64, device=gdev)
+        allpr = [torch.zeros_like(pr) for _ in range(world)]
+        dist.all_gather(allpr, pr)
+        per_rank_all = [[round(float(x), 3) for x in t_.tolist()] for t_ in allpr]
+        agg = torch.tensor([total_occ], dtype=torch.float64, device=gdev)
         dist.all_reduce(agg)
-        lf_steps, total_occ, ref_loc_steps = float(agg[0].item()), float(agg[1].item()), float(agg[2].item())
-    last = idx.stats()
+        total_occ = float(agg.item())
+    else:
+        per_rank_all = [[round(x, 3) for x in per_rank]]
+
+    # records of the last step (kept) for the parity sample
+    occ_last = idx.occ_view(*held).copy() if held[1] else np.zeros(0, pkg.OCC_DTYPE)
+    counts_last = counts[:npat].copy()
+    idx.occ_free(held[0])
+
+    # ---- timed: device-resident (bytes + offsets in HBM, results left in HBM)
+    dres = None
+    if not args.no_device:
+        buf, offs = pkg.read_pattern_file(pats_path)
+        d_bytes = torch.from_numpy(buf).to(dev)
+        d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+        d_counts = torch.zeros(npat, dtype=torch.int32, device=dev)
+
+        def dev_step(profile=False):
+            return idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(), first_pattern_id=first_id,
+                                     locate=locate, profile=profile, stream=stream, **flags_kw)
+
+        for _ in range(max(1, args.warmup)):
+            dev_step()
+        barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        kstats = {}
+        for _ in range(args.steps):
+            dev_step(profile="light")
+            st = idx.stats()
+            for k, v in st["kernels"].items():
+                a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
+                for f in a:
+                    a[f] += v[f]
+        torch.cuda.synchronize()
+        barrier()
+        d_elapsed = time.perf_counter() - t1
+        if world > 1:
+            tt = torch.tensor([d_elapsed], dtype=torch.float64, device=gdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            d_elapsed = float(tt.item())
+        dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": idx.stats(), "d_counts": d_counts}
+        if not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
+            raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")
 
     if rank == 0:
         ms_step = 1000.0 * elapsed / args.steps
-        value = npat * world * args.steps / elapsed
-        # dominant kernel class by device time over the timed region
-        dom = max((k for k in kstats if k != "scan"), key=lambda k: kstats[k]["ms"])
-        d = kstats[dom]
-        avg_ms = d["ms"] / max(1, d["launches"])
-        achieved = (d["bytes"] / d["launches"]) / (avg_ms * 1e-3) / 1e9 if d["launches"] and avg_ms > 0 else 0.0
-        line_rate = (d["lines"] / d["launches"]) / (avg_ms * 1e-3) if d["launches"] and avg_ms > 0 else 0.0
-        traffic, traffic_src = traffic_from_profile(cfg, dom, locate)
+        total_pats = npat * world if w.per_gpu else (args.patterns or w.patterns)  # every rank's shard
+        value = total_pats * args.steps / elapsed
+        rows = idx.n_rows
+        # tables the deep kernels gather from: occ blocks (1 B/row), rent1 (sigma/2 B/row), rent2 (10 B/row)
+        rank_bytes = rows * (1 + idx.sigma / 2 + (10 if idx.pair_blocks else 0))
         out = {
             "metric": "patterns/sec + LF-steps/sec, 100 Mchar EDS, 10M 31-mers, 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -255,48 +302,117 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if w.per_gpu else "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (edsbwt_gen, seeded)",
-            "config": {"workload": WORKLOAD[cfg], "config": cfg, "patterns_per_gpu": npat,
-                       "index_rows": idx.n_rows, "words": idx.n_words, "segments": idx.n_segments,
-                       "locate": {"sampled": "per-row samples (word, offset, segment, word-in-segment), one read per occurrence",
-                                  "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
-                       if locate else "count-only",
-                       "parallelism": f"pattern-shard x{world}"},
-            # LF steps the device executed (2 per interval step + locate walk moves)
-            "lf_steps_per_sec": round(lf_steps / elapsed, 1),
-            # the reference's locate walk moves for the same records (sum of offsets, :348-353)
-            "reference_locate_lf_steps_per_sec": round(ref_loc_steps / elapsed, 1),
-            "occurrences_per_step": int(total_occ / args.steps / max(1, world)) if world == 1 else int(total_occ / args.steps),
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": MI355X_HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / MI355X_HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "avg_launch_ms": round(avg_ms, 4), "launches": d["launches"],
-                         "bytes_per_launch": int(d["bytes"] / max(1, d["launches"])),
-                         # random 64-B lines: the rate the access shape is actually bound by
-                         "lines_per_launch": int(d["lines"] / max(1, d["launches"])),
-                         "lines_per_s": round(line_rate, 1),
-                         "gather_ceiling_lines_per_s": GATHER64_CEILING_LINES_PER_S,
-                         "frac_of_gather_ceiling": round(line_rate / GATHER64_CEILING_LINES_PER_S, 4)},
-            "kernel_lines_per_s": {k: round((v["lines"] / (v["ms"] * 1e-3)) if v["ms"] > 0 else 0.0, 1)
-                                   for k, v in sorted(kstats.items()) if v["lines"]},
-            "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items())},
+            "data": "synthetic (edsbwt_gen, seeded; SURVEY.md §8(d) generators)",
+            "config": {"workload": w.text, "config": w.name, "patterns_per_gpu": npat,
+                       "patterns_total": total_pats,
+                       "index_rows": rows, "words": idx.n_words, "segments": idx.n_segments,
+                       "locate": ({"sampled": "per-row samples (word, offset, segment, word-in-segment), one read per occurrence",
+                                   "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
+                                  if locate else "count-only"),
+                       "parallelism": f"pattern-shard x{world}",
+                       "timed_region": "edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> counts + records D2H "
+                                       "(SURVEY §8(d)), plus the exchange step when N>1",
+                       "ktab_depth": idx.ktab_depth, "index_device_bytes": idx.device_bytes,
+                       "cache_resident": bool(rank_bytes <= MI355X_MALL_BYTES)},
+            "occurrences_per_step": int(total_occ / args.steps),
+            "found_per_step": int(e2e_stats["found"]) if world == 1 else None,
+            "e2e": {"ms_wall_per_call": round(float(np.mean(walls)), 3), "chunks": e2e_stats["chunks"],
+                    "bytes_h2d": e2e_stats["bytes_h2d"], "bytes_d2h": e2e_stats["bytes_d2h"],
+                    "pcie_gbs": round((e2e_stats["bytes_h2d"] + e2e_stats["bytes_d2h"]) / (np.mean(walls) * 1e-3) / 1e9, 2),
+                    "device_ms_per_call": round(e2e_stats["ms_total"], 3),
+                    "per_rank_search_exchange_ms": per_rank_all},
+            "bs_took": round(elapsed / args.steps, 6),
             "index_open_s": round(t_open, 2),
-            "engine": {k: last[k] for k in ("depths", "deep_from_depth", "deep_overflow", "deep_level_rerun", "search_groups", "trie_nodes", "intervals_stepped",
-                                              "link_hash_rows", "link_ranges", "locate_lf_steps")},
-            "found_per_step": int(last["found"]),
+            "inputs_prepare_s": round(t_prep, 1),
         }
+        if dres:
+            kstats = dres["kstats"]
+            dstat = dres["stats"]
+            d_ms = 1000.0 * dres["elapsed"] / args.steps
+            dom = max((k for k in kstats if k != "scan"), key=lambda k: kstats[k]["ms"])
+            d = kstats[dom]
+            avg_ms = d["ms"] / max(1, d["launches"])
+            bpl = d["bytes"] / max(1, d["launches"])
+            lpl = d["lines"] / max(1, d["launches"])
+            achieved = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+            line_rate = lpl / (avg_ms * 1e-3) if avg_ms > 0 else 0.0
+            # SURVEY §8(d)'s per-step model: two 64-B lines per interval step (one per interval end)
+            steps_pl = dstat["intervals_stepped"] / max(1, kstats[dom]["launches"] / args.steps) if dom == "deep" else 0
+            survey_bpl = 2 * 64 * steps_pl
+            traffic, traffic_src = traffic_from_profile(w.name, dom)
+            ceil, ceil_shape = gather_ceiling()
+            out["roofline"] = {
+                "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / MI355X_HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                "avg_launch_ms": round(avg_ms, 4), "launches": d["launches"],
+                "bytes_model": "line model: the 64-B lines the class gathers (a narrow interval's two ends in one line count "
+                               "once; one 16-B two-step rank entry per end) + '#'-row reads (DESIGN.md §6)",
+                "bytes_per_launch": int(bpl),
+                "survey_model_bytes_per_launch": int(survey_bpl),
+                "survey_model_frac": round(survey_bpl / (avg_ms * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4) if avg_ms > 0 else None,
+                "lines_per_launch": int(lpl), "lines_per_s": round(line_rate, 1),
+                "gather_ceiling_lines_per_s": ceil, "gather_ceiling_shape": ceil_shape,
+                "frac_of_gather_ceiling": round(line_rate / ceil, 4) if ceil else None,
+                "from": "device_resident leg (HIP events on the library stream, EDSBWT_PROFILE_LIGHT)",
+            }
+            out["device_resident"] = {
+                "value": round(total_pats * args.steps / dres["elapsed"], 1), "ms_per_step": round(d_ms, 3),
+                "what": "pattern bytes + u64 offsets resident in HBM before the timed region; counts + records left in HBM",
+                "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items()) if v["ms"]},
+                "kernel_lines_per_s": {k: round((v["lines"] / (v["ms"] * 1e-3)) if v["ms"] > 0 else 0.0, 1)
+                                       for k, v in sorted(kstats.items()) if v["lines"]},
+                "engine": {k: dstat[k] for k in ("depths", "deep_from_depth", "deep_overflow", "deep_level_rerun", "search_groups",
+                                                 "trie_nodes", "intervals_stepped", "link_hash_rows", "start_depth",
+                                                 "locate_lf_steps")},
+                # LF steps the device executed: 2 per interval step (one per end) + locate walk moves
+                "device_lf_steps_per_sec": round((2 * dstat["intervals_stepped"] + dstat["locate_lf_steps"]) * args.steps
+                                                 / dres["elapsed"], 1),
+                "reference_locate_lf_steps_per_sec": round(dstat["locate_offsets"] * args.steps / dres["elapsed"], 1),
+            }
         if world == 1 and not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
-            sample = args.cpu_sample or (64 * threads if cfg != "c2" else 512 * threads)
-            sample = min(sample, npat)
+            buf, offs = pkg.read_pattern_file(pats_path)
+            threads = max(1, min(16, os.cpu_count() or 1))
             try:
-                out["cpu_baseline"] = cpu_baseline(base, pats_path, sample, threads)
+                samp_n = min(args.cpu_sample or (64 * threads if w.name != "c2" else 512 * threads), npat)
+                cb = cpu_baseline(base, buf, offs, first_id, samp_n, threads)
+                samp1 = max(8, samp_n // (4 * threads))
+                c1 = cpu_baseline(base, buf, offs, first_id, samp1, 1)
+                # parity of the sample: the oracle's counts and records vs the GPU's (end-to-end run)
+                k = int(cb["counts"].astype(np.int64).sum())
+                match = bool(np.array_equal(cb["counts"], counts_last[:samp_n]) and np.array_equal(cb["occ"], occ_last[:k]))
+                ctr = cb["ctr"]
+                lf_ref = (ctr["step_moves"] + ctr["locate_moves"]) / samp_n  # reference-literal M_LF moves per pattern
+                out["parity_sample"] = {"n": samp_n, "records": k, "match": match,
+                                        "what": "oracle (literal MOVE_EDSBWTSearch restatement) vs GPU end-to-end counts and "
+                                                "records, in order, for the first n patterns"}
+                out["cpu_baseline"] = {
+                    "value": round(cb["value"], 3), "unit": "patterns/sec", "cores": threads, "kind": "port",
+                    "sample": f"first {samp_n} patterns of the batch; oracle/edsbwt_oracle.c (literal MOVE_EDSBWTSearch "
+                              f"restatement, a=8 M_LF) on {threads} host threads over contiguous shards; index load "
+                              f"{cb['open_s']:.1f}s excluded",
+                    "seconds": round(cb["seconds"], 3),
+                    "single_thread": {"value": round(c1["value"], 3), "cores": 1, "sample": f"first {samp1} patterns",
+                                      "seconds": round(c1["seconds"], 3)},
+                    "host_cpus_visible": os.cpu_count(),
+                    "lf_steps_per_pattern": round(lf_ref, 1), "interval_steps_per_pattern": round(ctr["interval_steps"] / samp_n, 1),
+                }
+                # SURVEY §8(d) LF-steps: the reference-literal M_LF moves (oracle-counted on the sample)
+                # per pattern, times the measured patterns/s
+                out["lf_steps_per_sec"] = round(lf_ref * value, 1)
+                out["lf_steps_note"] = ("reference-equivalent: oracle-counted M_LF moves per pattern on the cpu_baseline "
+                                        "sample x value (SURVEY §8(d)); the device executes far fewer (device_resident."
+                                        "device_lf_steps_per_sec)")
+                out["cpu_baseline"]["lf_steps_per_sec"] = round(lf_ref * cb["value"], 1)
+                if not match:
+                    log("[bench] PARITY SAMPLE MISMATCH")
             except Exception as e:  # the GPU line is still valid
-                out["cpu_baseline"] = {"value": None, "error": str(e)}
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)
+    text.free()
+    counts_hb.free()
     idx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -67,20 +67,42 @@ class _Stats(ctypes.Structure):
                 ("bytes_kernel", ctypes.c_uint64 * 16),
                 ("lines_kernel", ctypes.c_uint64 * 16),
                 ("locate_offsets", ctypes.c_uint64),
-                ("search_groups", ctypes.c_uint64), ("start_depth", ctypes.c_uint64)]
+                ("search_groups", ctypes.c_uint64), ("start_depth", ctypes.c_uint64),
+                ("ms_wall", ctypes.c_double), ("chunks", ctypes.c_uint64), ("bytes_h2d", ctypes.c_uint64),
+                ("bytes_d2h", ctypes.c_uint64)]
 
 
 _LIB = None
+# the library's sources, in the order eds-bwt_amd/Makefile hashes them into BUILD_ID
+_SOURCES = ("csrc/engine.hip", "csrc/index_io.cpp", "csrc/format.cpp", "csrc/kernels.hip", "csrc/kernels.h", "csrc/index_io.h",
+            "../include/edsbwt.h")
+
+
+def source_build_id() -> str:
+    """sha256 (16 hex digits) of the library sources in this tree (Makefile BUILD_ID)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in _SOURCES:
+        with open(os.path.join(_HERE, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def lib() -> ctypes.CDLL:
-    """Load libedsbwt.so (built in-tree by __graft_entry__.build()); raise if absent."""
+    """Load libedsbwt.so (built in-tree by __graft_entry__.build()); raise if it is absent or
+    was built from other sources than the ones in this tree (EDSBWT_LIB overrides skip the check)."""
     global _LIB
     if _LIB is not None:
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise EdsBwtError(-4, f"{LIB_PATH} not built: run __graft_entry__.build() (make -C eds-bwt_amd)")
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    L.edsbwt_build_id.argtypes = []
+    L.edsbwt_build_id.restype = ctypes.c_char_p
+    built = L.edsbwt_build_id().decode()
+    if not os.environ.get("EDSBWT_LIB") and built != source_build_id():
+        raise EdsBwtError(-4, f"{LIB_PATH} was built from sources {built}, the tree holds {source_build_id()}: "
+                              "rebuild it (make -C eds-bwt_amd)")
     vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     L.edsbwt_index_open.argtypes = [ctypes.c_char_p, i32, u32, ctypes.POINTER(vp)]
     L.edsbwt_index_open.restype = i32
@@ -92,6 +114,13 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_search.restype = i32
     L.edsbwt_search_device.argtypes = [vp, vp, vp, u64, u32, u32, vp, ctypes.POINTER(vp), ctypes.POINTER(u64), vp]
     L.edsbwt_search_device.restype = i32
+    L.edsbwt_search_lines.argtypes = [vp, vp, u64, u32, u32, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(vp),
+                                      ctypes.POINTER(u64)]
+    L.edsbwt_search_lines.restype = i32
+    L.edsbwt_host_alloc.argtypes = [u64, ctypes.POINTER(vp)]
+    L.edsbwt_host_alloc.restype = i32
+    L.edsbwt_host_free.argtypes = [vp]
+    L.edsbwt_host_free.restype = None
     L.edsbwt_occ_free.argtypes = [vp]
     L.edsbwt_occ_free.restype = None
     L.edsbwt_last_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
@@ -138,6 +167,45 @@ def read_pattern_file(path: str) -> tuple[np.ndarray, np.ndarray]:
     keep = np.ones(data.size, dtype=bool)
     keep[nl] = False
     return np.ascontiguousarray(data[keep]), offs
+
+
+class HostBuffer:
+    """Page-locked host memory (edsbwt_host_alloc) viewed as a numpy array: pattern bytes,
+    counts and records move over PCIe at full rate from/to it."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib().edsbwt_host_alloc(int(nbytes), ctypes.byref(p)))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    def array(self, dtype=np.uint8, count: int = -1) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count < 0 else count
+        raw = (ctypes.c_char * (n * dt.itemsize)).from_address(self.ptr) if n else bytearray()
+        return np.frombuffer(raw, dtype=dt, count=n)
+
+    def free(self) -> None:
+        if getattr(self, "ptr", None):
+            lib().edsbwt_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def read_pattern_file_pinned(path: str) -> HostBuffer:
+    """The pattern file's bytes in page-locked memory (input of Index.search_lines)."""
+    n = os.path.getsize(path)
+    hb = HostBuffer(max(n, 1))
+    if n:
+        with open(path, "rb") as f:
+            f.readinto(memoryview(hb.array(np.uint8, n)).cast("B"))
+    hb.nbytes = n
+    return hb
 
 
 class Index:
@@ -204,6 +272,37 @@ class Index:
             ctypes.memmove(occ.ctypes.data, occ_p.value, n * OCC_DTYPE.itemsize)
             lib().edsbwt_occ_free(occ_p)
         return counts, occ
+
+    def search_lines(self, text_ptr: int, nbytes: int, counts_ptr: int, counts_cap: int, *, first_pattern_id: int = 1,
+                     locate: bool = True, profile: bool = False, keep: bool = False):
+        """A pattern file in host memory (ideally page-locked: HostBuffer) through the
+        pipelined host path (edsbwt_search_lines).  Returns (patterns, records pointer,
+        number of records); the records are page-locked and library-owned: pass keep=True and
+        free them with occ_free(ptr), else they are given back at once (timing runs)."""
+        pflag = {False: 0, True: PROFILE, "light": PROFILE_LIGHT}[profile]
+        flags = (LOCATE if locate else COUNT_ONLY) | pflag
+        occ_p = ctypes.c_void_p()
+        nocc = ctypes.c_uint64()
+        npat = ctypes.c_uint64()
+        _check(lib().edsbwt_search_lines(self._h, text_ptr, nbytes, first_pattern_id, flags, counts_ptr, counts_cap,
+                                         ctypes.byref(npat), ctypes.byref(occ_p), ctypes.byref(nocc)))
+        if not keep and occ_p.value:
+            lib().edsbwt_occ_free(occ_p.value)
+            return npat.value, 0, nocc.value
+        return npat.value, occ_p.value or 0, nocc.value
+
+    @staticmethod
+    def occ_view(ptr: int, n: int) -> np.ndarray:
+        """numpy view of n records at a library-owned host pointer (valid until occ_free)."""
+        if not n:
+            return np.zeros(0, OCC_DTYPE)
+        raw = (ctypes.c_char * (n * OCC_DTYPE.itemsize)).from_address(ptr)
+        return np.frombuffer(raw, dtype=OCC_DTYPE, count=n)
+
+    @staticmethod
+    def occ_free(ptr: int) -> None:
+        if ptr:
+            lib().edsbwt_occ_free(ptr)
 
     def search_device(self, d_bytes: int, d_offsets: int, npat: int, d_counts: int, *, first_pattern_id: int = 1,
                       locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,

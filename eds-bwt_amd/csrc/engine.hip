@@ -25,10 +25,15 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "index_io.h"
 #include "kernels.hip"
+
+#ifndef EDSBWT_BUILD_ID
+#define EDSBWT_BUILD_ID "unknown"
+#endif
 
 namespace edsbwt {
 
@@ -137,6 +142,19 @@ constexpr uint32_t kKtabMinDepth = 2;
 constexpr double kKtabOver = 4.0;
 // levels2() result meaning "the batch needs the ordered path"
 constexpr uint32_t kNeedOrdered = 0xFFFFFFFFu;
+
+struct Engine;
+// Occurrence buffers handed out by search_host are page-locked and owned by their engine,
+// which reuses one once edsbwt_occ_free gives it back; a buffer still held by the caller
+// when its engine moves on (a new call, close) is detached and freed by edsbwt_occ_free.
+struct OccRegistry {
+    std::mutex m;
+    std::unordered_map<const void*, std::pair<Engine*, bool>> own;  // buffer -> (engine or null, checked out)
+};
+static OccRegistry& occ_registry() {
+    static OccRegistry r;
+    return r;
+}
 
 struct Engine {
     int device = 0;
@@ -255,9 +273,36 @@ struct Engine {
         rec.release(); rec2.release();
         dq.release();
     }
-    DBuf<uint8_t> hbytes;   // host-API pattern staging
-    DBuf<uint64_t> hoffs;
-    DBuf<uint32_t> hcounts;
+    // ---- host pipeline (search_host): batches in host memory are cut into chunks; chunk k+1
+    // is uploaded on `up` while chunk k is searched on `stream` and chunk k-1's counts and
+    // records go back on `down` (two device slots per buffer, events between the streams)
+    hipStream_t up = nullptr, down = nullptr;
+    hipEvent_t up_done[2] = {}, comp_done[2] = {}, down_done[2] = {};
+    DBuf<uint8_t> hraw[2], hbytes[2];
+    DBuf<uint64_t> hoffs[2];
+    DBuf<uint32_t> hcounts[2], nlcnt, nlpre;
+    DBuf<edsbwt_occ> hrec[2];
+    struct Pinned {  // page-locked host staging (inputs or counts in pageable caller memory)
+        void* p = nullptr;
+        size_t cap = 0;
+        void ensure(size_t n) {
+            if (n <= cap && p) return;
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            if (hipHostMalloc(&p, std::max<size_t>(n, 1 << 20), hipHostMallocDefault) != hipSuccess) {
+                p = nullptr;
+                throw Fail(EDSBWT_E_NOMEM, "hipHostMalloc of " + std::to_string(n) + " bytes failed");
+            }
+            cap = std::max<size_t>(n, 1 << 20);
+        }
+        void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+    };
+    Pinned stage_in[2], stage_off[2], stage_cnt[2];
+    // the occurrence records handed to the caller (library-owned, page-locked, reused once
+    // edsbwt_occ_free gives them back: see occ_arena_*)
+    edsbwt_occ* arena = nullptr;
+    size_t arena_cap = 0;
     edsbwt_stats st{};
     // profiling
     bool prof = false;
@@ -1777,8 +1822,255 @@ struct Engine {
         return OCC;
     }
 
+    // ------------------------------------------------------------ host pipeline
+    static bool host_pinned(const void* p) {
+        if (!p) return false;
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+        return a.type == hipMemoryTypeHost;
+    }
+    // host memcpy on up to 16 threads (staging pageable caller memory)
+    static void par_copy(void* dst, const void* src, size_t n) {
+        const size_t kPer = 8u << 20;
+        const unsigned T = (unsigned)std::min<size_t>(16, std::max<size_t>(1, n / kPer));
+        if (T <= 1) { if (n) std::memcpy(dst, src, n); return; }
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < T; t++)
+            th.emplace_back([=] {
+                const size_t a = n * t / T, b = n * (t + 1) / T;
+                std::memcpy((char*)dst + a, (const char*)src + a, b - a);
+            });
+        for (auto& x : th) x.join();
+    }
+    void pipe_init() {
+        if (up) return;
+        HIPCHK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+        for (int k = 0; k < 2; k++) {
+            HIPCHK(hipEventCreateWithFlags(&up_done[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&comp_done[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&down_done[k], hipEventDisableTiming));
+        }
+    }
+    // host -> device on `up` (staged through page-locked memory when src is pageable)
+    void upload(void* dst, const void* src, size_t n, bool pinned_src, Pinned& stage, int slot) {
+        if (!n) return;
+        if (pinned_src) {
+            HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, up));
+            return;
+        }
+        HIPCHK(hipEventSynchronize(up_done[slot]));  // the slot's previous upload has left the staging buffer
+        stage.ensure(n);
+        par_copy(stage.p, src, n);
+        HIPCHK(hipMemcpyAsync(dst, stage.p, n, hipMemcpyHostToDevice, up));
+    }
+    void arena_ensure(size_t n) {  // keep the records received so far (down stream synced)
+        if (n <= arena_cap && arena) return;
+        HIPCHK(hipStreamSynchronize(down));
+        const size_t c = std::max<size_t>({n, arena_cap + arena_cap / 2, (size_t)1 << 16});
+        edsbwt_occ* q = nullptr;
+        if (hipHostMalloc((void**)&q, c * sizeof(edsbwt_occ), hipHostMallocDefault) != hipSuccess)
+            throw Fail(EDSBWT_E_NOMEM, "hipHostMalloc of the occurrence records failed");
+        if (arena) {
+            par_copy(q, arena, arena_cap * sizeof(edsbwt_occ));
+            arena_release();
+        }
+        arena = q;
+        arena_cap = c;
+        arena_register();
+    }
+    void arena_register();
+    void arena_release();
+    void arena_checkout();
+    bool arena_checked_out();
+
+    struct Chunk { uint64_t b0, b1, p0, p1; };  // byte range; pattern range (offsets mode)
+
+    // The pattern loop of MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:97-155) over a batch in host memory,
+    // timed as SURVEY §8(d) defines patterns/s: from the first H2D of the patterns to the last
+    // D2H of counts and records.  lines != 0: `text` is the pattern file as it lies on disk
+    // (getline semantics, :111: split at '\n', a last line without '\n' counts); else
+    // text/offs is a packed (bytes, offsets[npat+1]) batch.  Returns the records (page-locked,
+    // library-owned) and their number; *npat_out = patterns seen.
+    uint64_t search_host(const uint8_t* text, uint64_t len, const uint64_t* offs, uint64_t npat, bool lines, uint32_t first_id,
+                         uint32_t flags, uint32_t* counts, uint64_t counts_cap, edsbwt_occ** occ_out, uint64_t* npat_out) {
+        const auto t0 = std::chrono::steady_clock::now();
+        pipe_init();
+        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
+        const bool pin_in = host_pinned(text), pin_off = lines || host_pinned(offs), pin_cnt = host_pinned(counts);
+        // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 64 MB), cut at line ends
+        const uint64_t target = (uint64_t)(env_double("EDSBWT_CHUNK_MB", 64) * 1048576.0);
+        std::vector<Chunk> ch;
+        if (lines) {
+            uint64_t b = 0;
+            while (b < len) {
+                uint64_t e = std::min(len, b + std::max<uint64_t>(target, 1));
+                if (e < len) {
+                    const void* nl = std::memchr(text + e - 1, '\n', len - (e - 1));
+                    e = nl ? (uint64_t)((const uint8_t*)nl - text) + 1 : len;
+                }
+                ch.push_back({b, e, 0, 0});
+                b = e;
+            }
+        } else {
+            if (npat && offs[0] != 0) throw Fail(EDSBWT_E_ARG, "pat_offsets[0] must be 0");
+            uint64_t p = 0;
+            while (p < npat) {
+                // the chunk's last pattern: the first whose end passes the target
+                uint64_t lo = p + 1, hi = npat;
+                const uint64_t want = offs[p] + std::max<uint64_t>(target, 1);
+                while (lo < hi) { const uint64_t m = (lo + hi) / 2; if (offs[m] < want) lo = m + 1; else hi = m; }
+                ch.push_back({offs[p], offs[lo], p, lo});
+                p = lo;
+            }
+        }
+        if (arena_checked_out()) arena_release();  // the caller still holds the last records: start a new buffer
+        edsbwt_stats agg{};
+        uint64_t total = 0, pats = 0, h2d = 0, d2h = 0;
+        try {
+        auto issue = [&](size_t k) {
+            const Chunk& c = ch[k];
+            const int sl = (int)(k & 1);
+            const uint64_t nb = c.b1 - c.b0;
+            if (lines) {
+                hraw[sl].ensure(nb + 16);
+                upload(hraw[sl].p, text + c.b0, nb, pin_in, stage_in[sl], sl);
+            } else {
+                hbytes[sl].ensure(nb + 16);
+                hoffs[sl].ensure(c.p1 - c.p0 + 1);
+                upload(hbytes[sl].p, text + c.b0, nb, pin_in, stage_in[sl], sl);
+                upload(hoffs[sl].p, offs + c.p0, (c.p1 - c.p0 + 1) * 8, pin_off, stage_off[sl], sl);
+                h2d += (c.p1 - c.p0 + 1) * 8;
+            }
+            h2d += nb;
+            HIPCHK(hipEventRecord(up_done[sl], up));
+        };
+        if (!ch.empty()) issue(0);
+        for (size_t k = 0; k < ch.size(); k++) {
+            const Chunk& c = ch[k];
+            const int sl = (int)(k & 1);
+            if (k + 1 < ch.size()) issue(k + 1);  // overlaps this chunk's search
+            HIPCHK(hipStreamWaitEvent(stream, up_done[sl], 0));
+            HIPCHK(hipStreamWaitEvent(stream, down_done[sl], 0));  // chunk k-2's results have left the slot
+            uint64_t P;
+            if (lines) {  // the file's lines as a (bytes, offsets) batch
+                const uint64_t nb = c.b1 - c.b0;
+                const uint64_t nblk = (nb + kLineBlk - 1) / kLineBlk;
+                nlcnt.ensure(nblk + 1);
+                hbytes[sl].ensure(nb + 16);
+                launch_blocks(KC_TRIE, k_nl_count, nblk, (const uint8_t*)hraw[sl].p, nb, nlcnt.p);
+                const uint32_t nl = scan_u32(nlcnt.p, nlpre, nblk);
+                P = nl + ((nb && text[c.b1 - 1] != '\n') ? 1 : 0);
+                hoffs[sl].ensure(P + 1);
+                zero(hoffs[sl].p, 8);
+                launch_blocks(KC_TRIE, k_nl_compact, nblk, (const uint8_t*)hraw[sl].p, nb, (const uint32_t*)nlpre.p, hbytes[sl].p,
+                              hoffs[sl].p);
+                if (P > nl) {  // the last line has no '\n': it ends at the chunk's end
+                    pinned_u64()[0] = nb - nl;
+                    HIPCHK(hipMemcpyAsync(hoffs[sl].p + P, pinned_u64(), 8, hipMemcpyHostToDevice, stream));
+                    HIPCHK(hipStreamSynchronize(stream));
+                }
+            } else {
+                P = c.p1 - c.p0;
+                if (c.b0) launch(KC_TRIE, k_rebase, P + 1, hoffs[sl].p, P + 1, c.b0);
+            }
+            if (pats + P > counts_cap) throw Fail(EDSBWT_E_ARG, "counts buffer holds " + std::to_string(counts_cap) + " patterns, the batch has more");
+            hcounts[sl].ensure(P + 1);
+            std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
+            uint64_t n = 0;
+            try {
+                n = search(hbytes[sl].p, hoffs[sl].p, P, first_id + (uint32_t)pats, flags, hcounts[sl].p);
+            } catch (...) {
+                std::swap(rec, hrec[sl]);
+                throw;
+            }
+            std::swap(rec, hrec[sl]);
+            accumulate(agg, st);
+            // results back on `down`
+            HIPCHK(hipEventRecord(comp_done[sl], stream));
+            HIPCHK(hipStreamWaitEvent(down, comp_done[sl], 0));
+            if (P) {
+                if (pin_cnt) {
+                    HIPCHK(hipMemcpyAsync(counts + pats, hcounts[sl].p, P * 4, hipMemcpyDeviceToHost, down));
+                } else {
+                    HIPCHK(hipEventSynchronize(down_done[sl]));
+                    stage_cnt[sl].ensure(P * 4);
+                    HIPCHK(hipMemcpyAsync(stage_cnt[sl].p, hcounts[sl].p, P * 4, hipMemcpyDeviceToHost, down));
+                    HIPCHK(hipStreamSynchronize(down));
+                    std::memcpy(counts + pats, stage_cnt[sl].p, P * 4);
+                }
+                d2h += P * 4;
+            }
+            if (locate && n) {
+                arena_ensure(total + n);
+                HIPCHK(hipMemcpyAsync(arena + total, hrec[sl].p, n * sizeof(edsbwt_occ), hipMemcpyDeviceToHost, down));
+                d2h += n * sizeof(edsbwt_occ);
+            }
+            HIPCHK(hipEventRecord(down_done[sl], down));
+            total += n;
+            pats += P;
+        }
+        HIPCHK(hipStreamSynchronize(down));
+        HIPCHK(hipStreamSynchronize(up));
+        } catch (...) {  // no copy may still touch the caller's buffers
+            (void)hipStreamSynchronize(up);
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamSynchronize(down);
+            throw;
+        }
+        st = agg;
+        st.patterns = pats;
+        st.occurrences = total;
+        st.chunks = ch.size();
+        st.bytes_h2d = h2d;
+        st.bytes_d2h = d2h;
+        st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (npat_out) *npat_out = pats;
+        if (occ_out) {
+            *occ_out = nullptr;
+            if (locate && total) {
+                *occ_out = arena;
+                arena_checkout();
+            }
+        }
+        return total;
+    }
+    uint64_t* pinned_u64() { return reinterpret_cast<uint64_t*>(pinned + 8); }
+    template <typename K, typename... A>
+    void launch_blocks(int k, K kern, size_t blocks, A... a) {
+        if (!blocks) return;
+        timed(k, [&] { hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, a...); });
+        HIPCHK(hipGetLastError());
+        sync_check((const void*)kern);
+        st.launches_kernel[k]++;
+    }
+    static void accumulate(edsbwt_stats& a, const edsbwt_stats& b) {
+        a.found += b.found; a.not_found += b.not_found; a.occurrences += b.occurrences;
+        a.depths = std::max(a.depths, b.depths); a.trie_nodes += b.trie_nodes; a.intervals_stepped += b.intervals_stepped;
+        a.link_hash_rows += b.link_hash_rows; a.link_ranges += b.link_ranges; a.locate_lf_steps += b.locate_lf_steps;
+        a.deep_from_depth = std::max(a.deep_from_depth, b.deep_from_depth); a.deep_overflow += b.deep_overflow;
+        a.deep_level_rerun += b.deep_level_rerun; a.ms_total += b.ms_total;
+        for (int k = 0; k < 16; k++) {
+            a.ms_kernel[k] += b.ms_kernel[k]; a.launches_kernel[k] += b.launches_kernel[k];
+            a.bytes_kernel[k] += b.bytes_kernel[k]; a.lines_kernel[k] += b.lines_kernel[k];
+        }
+        a.locate_offsets += b.locate_offsets; a.search_groups = std::max(a.search_groups, b.search_groups);
+        a.start_depth = std::max(a.start_depth, b.start_depth);
+    }
+
     ~Engine() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (up) (void)hipStreamSynchronize(up);
+        if (down) (void)hipStreamSynchronize(down);
+        for (int k = 0; k < 2; k++) {
+            if (up_done[k]) (void)hipEventDestroy(up_done[k]);
+            if (comp_done[k]) (void)hipEventDestroy(comp_done[k]);
+            if (down_done[k]) (void)hipEventDestroy(down_done[k]);
+            stage_in[k].release(); stage_off[k].release(); stage_cnt[k].release();
+        }
+        if (up) (void)hipStreamDestroy(up);
+        if (down) (void)hipStreamDestroy(down);
+        arena_release();
         for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
         if (pinned) (void)hipHostFree(pinned);
         if (pinned_big) (void)hipHostFree(pinned_big);
@@ -1786,6 +2078,59 @@ struct Engine {
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
+
+void Engine::arena_register() {
+    auto& R = occ_registry();
+    std::lock_guard<std::mutex> g(R.m);
+    R.own[arena] = {this, false};
+}
+void Engine::arena_checkout() {
+    auto& R = occ_registry();
+    std::lock_guard<std::mutex> g(R.m);
+    R.own[arena] = {this, true};
+}
+bool Engine::arena_checked_out() {
+    if (!arena) return false;
+    auto& R = occ_registry();
+    std::lock_guard<std::mutex> g(R.m);
+    auto it = R.own.find(arena);
+    return it != R.own.end() && it->second.second;
+}
+void Engine::arena_release() {
+    if (!arena) return;
+    bool out = false;
+    {
+        auto& R = occ_registry();
+        std::lock_guard<std::mutex> g(R.m);
+        auto it = R.own.find(arena);
+        out = it != R.own.end() && it->second.second;
+        if (out) it->second.first = nullptr;  // detached: edsbwt_occ_free frees it
+        else if (it != R.own.end()) R.own.erase(it);
+    }
+    if (!out) (void)hipHostFree(arena);
+    arena = nullptr;
+    arena_cap = 0;
+}
+// edsbwt_occ_free: give an engine's buffer back, free a detached one, or free() a malloc'd one
+static void occ_free_any(edsbwt_occ* p) {
+    if (!p) return;
+    {
+        auto& R = occ_registry();
+        std::lock_guard<std::mutex> g(R.m);
+        auto it = R.own.find(p);
+        if (it != R.own.end()) {
+            if (it->second.first) {
+                it->second.second = false;
+                return;
+            }
+            R.own.erase(it);
+        } else {
+            std::free(p);
+            return;
+        }
+    }
+    (void)hipHostFree(p);
+}
 
 }  // namespace edsbwt
 
@@ -1859,14 +2204,13 @@ int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64
     ABI_TRY
     Engine& E = *idx->eng;
     HIPCHK(hipSetDevice(E.device));
-    hipStream_t user = (hipStream_t)stream;
-    if (user) {  // order after the caller's stream
-        hipEvent_t ev;
-        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(ev, user));
-        HIPCHK(hipStreamWaitEvent(E.stream, ev, 0));
-        (void)hipEventDestroy(ev);
-    }
+    // order after the caller's stream — the null (legacy default) stream when stream is NULL,
+    // which the engine's non-blocking stream would not wait for by itself
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev, (hipStream_t)stream));
+    HIPCHK(hipStreamWaitEvent(E.stream, ev, 0));
+    (void)hipEventDestroy(ev);
     uint64_t n = E.search(d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts);
     if (d_occ) *d_occ = n ? E.rec.p : nullptr;
     if (nocc) *nocc = n;
@@ -1882,29 +2226,47 @@ int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_
     ABI_TRY
     Engine& E = *idx->eng;
     HIPCHK(hipSetDevice(E.device));
-    const uint64_t nb = npat ? pat_offsets[npat] : 0;
-    if (npat && pat_offsets[0] != 0) throw Fail(EDSBWT_E_ARG, "pat_offsets[0] must be 0");
-    E.hbytes.ensure(nb + 1);
-    E.hoffs.ensure(npat + 1);
-    E.hcounts.ensure(npat + 1);
-    if (nb) HIPCHK(hipMemcpyAsync(E.hbytes.p, pat_bytes, nb, hipMemcpyHostToDevice, E.stream));
-    if (npat) HIPCHK(hipMemcpyAsync(E.hoffs.p, pat_offsets, (npat + 1) * 8, hipMemcpyHostToDevice, E.stream));
-    uint64_t n = E.search(E.hbytes.p, E.hoffs.p, npat, first_pattern_id, flags, E.hcounts.p);
-    if (npat) HIPCHK(hipMemcpyAsync(counts, E.hcounts.p, npat * 4, hipMemcpyDeviceToHost, E.stream));
-    edsbwt_occ* h = nullptr;
-    if (n && occ) {
-        h = (edsbwt_occ*)std::malloc(n * sizeof(edsbwt_occ));
-        if (!h) throw Fail(EDSBWT_E_NOMEM, "host allocation of occurrence records failed");
-        HIPCHK(hipMemcpyAsync(h, E.rec.p, n * sizeof(edsbwt_occ), hipMemcpyDeviceToHost, E.stream));
-    }
-    HIPCHK(hipStreamSynchronize(E.stream));
-    if (occ) *occ = h;
+    if (npat && !pat_bytes && pat_offsets[npat]) throw Fail(EDSBWT_E_ARG, "null pattern bytes");
+    uint64_t n = E.search_host((const uint8_t*)pat_bytes, npat ? pat_offsets[npat] : 0, pat_offsets, npat, false, first_pattern_id, flags,
+                               counts, npat, occ, nullptr);
     if (nocc) *nocc = n;
     return 0;
     ABI_CATCH
 }
 
-void edsbwt_occ_free(edsbwt_occ* occ) { std::free(occ); }
+int edsbwt_search_lines(edsbwt_index* idx, const char* text, uint64_t len, uint32_t first_pattern_id, uint32_t flags, uint32_t* counts,
+                        uint64_t counts_cap, uint64_t* npat, edsbwt_occ** occ, uint64_t* nocc) {
+    if (!idx || (len && (!text || !counts))) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    if (occ) *occ = nullptr;
+    if (nocc) *nocc = 0;
+    if (npat) *npat = 0;
+    ABI_TRY
+    Engine& E = *idx->eng;
+    HIPCHK(hipSetDevice(E.device));
+    uint64_t n = E.search_host((const uint8_t*)text, len, nullptr, 0, true, first_pattern_id, flags, counts, counts_cap, occ, npat);
+    if (nocc) *nocc = n;
+    return 0;
+    ABI_CATCH
+}
+
+int edsbwt_host_alloc(uint64_t bytes, void** out) {
+    if (!out) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        edsbwt::g_err = "hipHostMalloc of " + std::to_string(bytes) + " bytes failed";
+        return EDSBWT_E_NOMEM;
+    }
+    return 0;
+}
+
+void edsbwt_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+const char* edsbwt_build_id(void) { return EDSBWT_BUILD_ID; }
+
+void edsbwt_occ_free(edsbwt_occ* occ) { edsbwt::occ_free_any(occ); }
 
 int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st) {
     if (!idx || !st) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }

@@ -2323,4 +2323,70 @@ __global__ void __launch_bounds__(256) k_ktab_emit(uint32_t M, const uint32_t* _
     }
 }
 
+// ------------------------------------------- pattern-file lines (host pipeline)
+// A chunk of the pattern file as it lies on disk (MOVE_EDSBWTSearch.cpp:111 reads it with
+// getline): the '\n' bytes are dropped and the offsets of the lines are written, so the
+// search sees the (bytes, offsets) batch of edsbwt_search.  kLineBlk bytes per block of
+// 256 threads, 16 per thread: k_nl_count counts each block's '\n', a scan gives the
+// newlines before each block, k_nl_compact moves the bytes and writes line ends.
+constexpr uint32_t kLineBlk = 4096;
+// offsets of a chunk of a packed batch, rebased to its first byte
+__global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) { GRID_STRIDE(i, n) off[i] -= base; }
+__global__ void __launch_bounds__(256) k_nl_count(const uint8_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ cnt) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * kLineBlk + threadIdx.x * 16u;
+    uint32_t c = 0;
+    if (b0 + 16 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(in + b0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t x = w[k] ^ 0x0A0A0A0Au;  // a zero byte where the byte is '\n'
+            c += __builtin_popcount((x - 0x01010101u) & ~x & 0x80808080u);
+        }
+    } else {
+        for (uint64_t i = b0; i < n && i < b0 + 16; i++) c += in[i] == '\n';
+    }
+    __shared__ unsigned long long sh[4];
+    const unsigned long long t = block_sum(c, sh);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = (uint32_t)t;
+}
+
+// pre[b] = newlines before block b.  out[i - nl_before(i)] = in[i] for non-'\n' bytes; the
+// j-th newline (at i) ends line j: offs[j + 1] = i - j (offs[0] = 0 is written by the host)
+__global__ void __launch_bounds__(256) k_nl_compact(const uint8_t* __restrict__ in, uint64_t n, const uint32_t* __restrict__ pre,
+                                                    uint8_t* __restrict__ out, uint64_t* __restrict__ offs) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * kLineBlk + threadIdx.x * 16u;
+    uint8_t v[16];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        v[k] = b0 + k < n ? in[b0 + k] : (uint8_t)0;
+        c += (b0 + k < n && v[k] == '\n') ? 1u : 0u;
+    }
+    // exclusive scan of c over the block
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += y;
+    }
+    __shared__ uint32_t wsum[4];
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = pre[blockIdx.x] + incl - c;
+    for (uint32_t t = 0; t < wv; t++) before += wsum[t];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint64_t i = b0 + k;
+        if (i >= n) break;
+        if (v[k] == '\n') {
+            offs[before + 1] = i - before;
+            before++;
+        } else {
+            out[i - before] = v[k];
+        }
+    }
+}
+
 }  // namespace edsbwt

@@ -8,12 +8,17 @@
 //     c5: c2 where 20% of the segments with k>=2 replace one string by the empty word
 //   edsbwt_gen patterns --eds file.eds --count P --seed S --out file.txt
 //                       [--len L | --lens 8,16,32,64] [--mode random|planted|mixed]
+//                       [--first I] [--threads T]
+//     pattern i of the stream is drawn from its own seeded generator: --first I --count P
+//     writes stream ids [I, I+P), identical to those lines of a single larger run
 //     planted: spelled along a random path (start segment, word and offset uniform,
 //     then a uniform word of each following segment; empty words add nothing), as
 //     extract_patterns_from_msa.py:30-60 samples k-mers from real sequences.
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "eds_common.h"
@@ -63,9 +68,11 @@ static int gen_eds(const std::string& cfg, uint64_t chars, uint64_t seed, const 
     return 0;
 }
 
-static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t seed, const std::vector<uint64_t>& lens,
-                        const std::string& mode, const std::string& out) {
-    Rng R(seed);
+// Pattern i of a stream is drawn from its own generator Rng(seed, i), so any contiguous
+// shard [first, first + count) of the stream is reproducible on its own (one rank per GPU
+// generates its own shard of C4's 100M patterns) and the batch is generated in parallel.
+static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t first, uint64_t seed,
+                        const std::vector<uint64_t>& lens, const std::string& mode, const std::string& out, unsigned threads) {
     Eds E;
     std::vector<uint64_t> seg_first;  // first word of each segment
     if (mode != "random") {
@@ -81,14 +88,12 @@ static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t se
         if (l == 1 && E.text[E.wstart[w]] == 'Z') l = 0;  // the empty word
         return l;
     };
-    std::string s;
-    s.reserve(count * (lens.back() + 1));
-    std::string p;
-    for (uint64_t i = 0; i < count; i++) {
+    auto one = [&](uint64_t idx, std::string& p) {
+        Rng R(seed * 0x9E3779B97F4A7C15ull ^ (idx + 0x632BE59BD9B4E019ull));
         const uint64_t m = lens[R.below(lens.size())];
-        bool plant = (mode == "planted") || (mode == "mixed" && (R.next() & 1));
+        const bool plant = (mode == "planted") || (mode == "mixed" && (R.next() & 1));
         p.clear();
-        if (plant) {
+        if (plant && S) {
             for (int attempt = 0; attempt < 1000 && p.size() < m; attempt++) {
                 p.clear();
                 uint64_t sg = R.below(S);
@@ -109,26 +114,40 @@ static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t se
             p.clear();
             for (uint64_t t = 0; t < m; t++) p.push_back(ACGT[R.below(4)]);
         }
-        s += p;
-        s.push_back('\n');
-    }
+        p.push_back('\n');
+    };
+    threads = std::max(1u, std::min<unsigned>(threads, (unsigned)std::max<uint64_t>(1, count / 4096)));
+    std::vector<std::string> part(threads);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < threads; t++)
+        th.emplace_back([&, t] {
+            const uint64_t lo = count * t / threads, hi = count * (t + 1) / threads;
+            std::string& s = part[t];
+            s.reserve((hi - lo) * (lens.back() + 1));
+            std::string p;
+            for (uint64_t i = lo; i < hi; i++) { one(first + i, p); s += p; }
+        });
+    for (auto& x : th) x.join();
     FILE* f = std::fopen(out.c_str(), "wb");
     if (!f) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
-    std::fwrite(s.data(), 1, s.size(), f);
+    for (auto& s : part) std::fwrite(s.data(), 1, s.size(), f);
     std::fclose(f);
-    std::fprintf(stderr, "edsbwt_gen: %llu patterns (%s) -> %s\n", (unsigned long long)count, mode.c_str(), out.c_str());
+    std::fprintf(stderr, "edsbwt_gen: %llu patterns (%s, stream ids %llu..%llu) -> %s\n", (unsigned long long)count, mode.c_str(),
+                 (unsigned long long)first, (unsigned long long)(first + count), out.c_str());
     return 0;
 }
 
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s eds --config c2|c3|c5 --chars N --seed S --out F\n"
-                             "       %s patterns --eds F --count P --seed S --out F [--len L|--lens a,b,..] [--mode random|planted|mixed]\n",
+                             "       %s patterns --eds F --count P --seed S --out F [--len L|--lens a,b,..] [--mode random|planted|mixed]\n"
+                             "                   [--first I (stream id of the first pattern)] [--threads T]\n",
                      argv[0], argv[0]);
         return 1;
     }
     std::string cmd = argv[1], cfg = "c2", out, eds, mode = "random";
-    uint64_t chars = 1000000, seed = 1, count = 1000;
+    uint64_t chars = 1000000, seed = 1, count = 1000, first = 0;
+    unsigned threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<uint64_t> lens{20};
     for (int i = 2; i + 1 < argc; i += 2) {
         std::string k = argv[i], v = argv[i + 1];
@@ -138,6 +157,8 @@ int main(int argc, char** argv) {
         else if (k == "--out") out = v;
         else if (k == "--eds") eds = v;
         else if (k == "--count") count = std::stoull(v);
+        else if (k == "--first") first = std::stoull(v);
+        else if (k == "--threads") threads = (unsigned)std::stoul(v);
         else if (k == "--len") lens = {std::stoull(v)};
         else if (k == "--lens") {
             lens.clear();
@@ -153,7 +174,7 @@ int main(int argc, char** argv) {
     }
     try {
         if (cmd == "eds") return gen_eds(cfg, chars, seed, out);
-        if (cmd == "patterns") return gen_patterns(eds, count, seed, lens, mode, out);
+        if (cmd == "patterns") return gen_patterns(eds, count, first, seed, lens, mode, out, threads);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

@@ -58,30 +58,35 @@ int main(int argc, char** argv) {
                 base.c_str(), (unsigned long long)info.n_words, (unsigned long long)info.n_rows, info.sigma);
     for (uint32_t j = 0; j < info.sigma; j++) std::printf("%c\t", info.alphabet[j]);
     std::printf("\nBitVector size: %llu\n", (unsigned long long)info.n_words);
-    // patterns: std::getline semantics (:111)
+    // the pattern file, read into page-locked memory; the library splits its lines
+    // (std::getline semantics, :111) on the device
     FILE* f = std::fopen(pfile.c_str(), "rb");
     if (!f) {
         std::fprintf(stderr, "Error opening %s\n", pfile.c_str());
         return 1;
     }
-    std::vector<char> raw;
-    {
-        char buf[1 << 16];
-        size_t n;
-        while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + n);
-        std::fclose(f);
+    std::fseek(f, 0, SEEK_END);
+    const long fsz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    const uint64_t len = fsz > 0 ? (uint64_t)fsz : 0;
+    char* text = nullptr;
+    if (edsbwt_host_alloc(len + 1, (void**)&text)) {
+        std::fprintf(stderr, "%s\n", edsbwt_last_error());
+        return 1;
     }
-    std::vector<char> bytes;
-    std::vector<uint64_t> offs{0};
-    bytes.reserve(raw.size());
-    for (size_t s = 0; s < raw.size();) {
-        size_t e = s;
-        while (e < raw.size() && raw[e] != '\n') e++;
-        bytes.insert(bytes.end(), raw.begin() + s, raw.begin() + e);
-        offs.push_back(bytes.size());
-        s = e + 1;
+    if (len && std::fread(text, 1, len, f) != len) {
+        std::fprintf(stderr, "Error reading %s\n", pfile.c_str());
+        return 1;
     }
-    const uint64_t npat = offs.size() - 1;
+    std::fclose(f);
+    uint64_t nlines = 0;
+    for (const char* q = text; (q = (const char*)std::memchr(q, '\n', (size_t)(text + len - q))) != nullptr; q++) nlines++;
+    if (len && text[len - 1] != '\n') nlines++;
+    uint32_t* counts = nullptr;
+    if (edsbwt_host_alloc((nlines + 1) * 4, (void**)&counts)) {
+        std::fprintf(stderr, "%s\n", edsbwt_last_error());
+        return 1;
+    }
     const std::string out = pfile + (legacy ? "output.csv" : "output_M_LF.csv");
     FILE* fo = std::fopen(out.c_str(), "wb");
     if (!fo) {
@@ -90,12 +95,11 @@ int main(int argc, char** argv) {
     }
     std::fputs(legacy ? "#Pat\t$_i\tD[i]\tS_j\tS_j[r]\n" : "#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n", fo);
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<uint32_t> counts(npat + 1, 0);
     edsbwt_occ* occ = nullptr;
-    uint64_t nocc = 0;
+    uint64_t nocc = 0, npat = 0;
     uint32_t flags = count_only ? EDSBWT_COUNT_ONLY
                                 : (EDSBWT_LOCATE | (table ? EDSBWT_LOCATE_TABLE : 0) | (legacy ? EDSBWT_LEGACY_ORDER : 0));
-    rc = edsbwt_search(idx, bytes.data(), offs.data(), npat, 1, flags, counts.data(), &occ, &nocc);
+    rc = edsbwt_search_lines(idx, text, len, 1, flags, counts, nlines + 1, &npat, &occ, &nocc);
     if (rc) {
         std::fprintf(stderr, "%s\n", edsbwt_last_error());
         return 1;
@@ -108,14 +112,18 @@ int main(int argc, char** argv) {
     }
     std::fclose(fo);
     uint64_t found = 0;
+    const char* line = text;
     for (uint64_t i = 0; i < npat; i++) {
+        const char* nl = (const char*)std::memchr(line, '\n', (size_t)(text + len - line));
+        const char* end = nl ? nl : text + len;
         const bool ok = counts[i] > 0;
         found += ok;
         if (!quiet) {
-            const std::string p(bytes.data() + offs[i], bytes.data() + offs[i + 1]);
+            const std::string p(line, end);
             std::printf("Pattern: %s of length %zu\nnum occ %u\n", p.c_str(), p.size(), counts[i]);
             std::fprintf(stderr, "OCCORRENZA DI: %s %s\n", p.c_str(), ok ? "TROVATA" : "NON TROVATA");
         }
+        line = end + 1;
     }
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::printf("bs took:%g", secs);
@@ -124,6 +132,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, count_only ? "\nThe search is finished! \n" : "\nThe csv file is ready! \n");
     std::fprintf(stderr, "The End!\n");
     edsbwt_occ_free(occ);
+    edsbwt_host_free(counts);
+    edsbwt_host_free(text);
     edsbwt_index_close(idx);
     return 1;  // mainMove_EDSBWT.cpp:61
 }

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EDSBWT_ABI_VERSION 2
+#define EDSBWT_ABI_VERSION 3
 
 enum {
     EDSBWT_OK = 0,
@@ -106,6 +106,11 @@ typedef struct {
                                  because a depth outgrew 32-bit counts */
     uint64_t start_depth;     /* depth the trie walk started from (the k-mer start table's
                                  depth when it served the batch, else 0) */
+    /* host-memory calls (edsbwt_search, edsbwt_search_lines): the pipeline */
+    double ms_wall;           /* host wall time of the call: first H2D of the patterns to the last
+                                 D2H of counts and records (SURVEY.md §8(d)'s patterns/s clock) */
+    uint64_t chunks;          /* chunks the batch was cut into (uploads overlap searches) */
+    uint64_t bytes_h2d, bytes_d2h;
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,
@@ -121,13 +126,34 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info);
  * Patterns are pat_bytes[pat_offsets[i] .. pat_offsets[i+1]) (host memory, no
  * terminator), i < npat; pattern i is reported as #Pat = first_pattern_id + i.
  * counts[npat] (caller-owned) receives backwardSearch's return value per pattern.
- * With EDSBWT_LOCATE, *occ (library-owned, free with edsbwt_occ_free) receives
- * *nocc records in reference order: pattern-major, then interval order, rows
- * ascending — the order of <patterns>output_M_LF.csv. */
+ * With EDSBWT_LOCATE, *occ (library-owned, page-locked; give it back with
+ * edsbwt_occ_free) receives *nocc records in reference order: pattern-major, then
+ * interval order, rows ascending — the order of <patterns>output_M_LF.csv.
+ * The batch is cut into chunks (EDSBWT_CHUNK_MB, default 64 MB of pattern bytes):
+ * uploads, searches and downloads of consecutive chunks overlap on three streams.
+ * Host buffers from edsbwt_host_alloc (page-locked) are transferred directly;
+ * pageable ones are staged through page-locked buffers. */
 int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_offsets,
                   uint64_t npat, uint32_t first_pattern_id, uint32_t flags,
                   uint32_t* counts, edsbwt_occ** occ, uint64_t* nocc);
+
+/* The same over a pattern file as it lies in memory (the reference's input,
+ * MOVE_EDSBWTSearch.cpp:100-111): text[0..len) is split into lines with std::getline
+ * semantics (at '\n'; '\r' is kept; a last line without '\n' counts).  The lines go
+ * to the device as they are and are split there.  counts[counts_cap] receives one count
+ * per line (E_ARG if the file has more lines); *npat = lines. */
+int edsbwt_search_lines(edsbwt_index* idx, const char* text, uint64_t len, uint32_t first_pattern_id,
+                        uint32_t flags, uint32_t* counts, uint64_t counts_cap, uint64_t* npat,
+                        edsbwt_occ** occ, uint64_t* nocc);
 void edsbwt_occ_free(edsbwt_occ* occ);
+
+/* Page-locked host memory for pattern buffers and counts (transferred at full PCIe rate). */
+int edsbwt_host_alloc(uint64_t bytes, void** out);
+void edsbwt_host_free(void* p);
+
+/* Hash of the sources the library was built from (eds-bwt_amd/Makefile): callers compare it
+ * with the sources in their tree to refuse a stale binary. */
+const char* edsbwt_build_id(void);
 
 /* Device-resident variant (benchmarks, multi-GPU shards): d_bytes / d_offsets /
  * d_counts are device pointers on the index's device; occurrence records stay in

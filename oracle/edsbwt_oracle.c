@@ -394,15 +394,25 @@ static inline uint32_t rsl_select(const rsl_t* R, uint8_t c, uint32_t k1, int* o
  * interval holding >= 2a input starts is split at the (a+1)-th start it holds
  * (Nishimoto–Tabei balancing); repeated until none is heavy. */
 typedef struct { uint32_t p, q; } pq_t;
-static int pq_cmp(const void* a, const void* b) {
-    uint32_t x = ((const pq_t*)a)->p, y = ((const pq_t*)b)->p;
-    return (x > y) - (x < y);
+/* rank directory over the input-interval starts p_i (bit per row, ones before each
+ * 64-row word): number of starts <= x in O(1) instead of a binary search per query */
+typedef struct { uint64_t* bits; uint32_t* pre; uint32_t n; } pstart_t;
+static void pstart_build(pstart_t* R, const pq_t* v, uint32_t k, uint32_t n) {
+    uint32_t nw = n / 64 + 2;
+    R->n = n;
+    R->bits = xcalloc(nw, 8);
+    R->pre = xmalloc((size_t)nw * 4);
+    for (uint32_t j = 0; j < k; j++) R->bits[v[j].p >> 6] |= 1ull << (v[j].p & 63);
+    uint32_t acc = 0;
+    for (uint32_t w = 0; w < nw; w++) { R->pre[w] = acc; acc += (uint32_t)__builtin_popcountll(R->bits[w]); }
 }
-static uint32_t lower_bound_pq(const pq_t* v, uint32_t n, uint32_t key) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) { uint32_t m = lo + (hi - lo) / 2; if (v[m].p < key) lo = m + 1; else hi = m; }
-    return lo;
+/* number of starts < x (= lower_bound over the sorted p's) */
+static inline uint32_t pstart_lb(const pstart_t* R, uint32_t x) {
+    uint32_t w = x >> 6, o = x & 63;
+    return R->pre[w] + (o ? (uint32_t)__builtin_popcountll(R->bits[w] & ((1ull << o) - 1)) : 0u);
 }
+static void pstart_free(pstart_t* R) { free(R->bits); free(R->pre); }
+
 static void mlf_balance(pq_t** pv, uint32_t* pk, uint32_t n, uint32_t a) {
     if (a < 2) a = 2;
     pq_t* v = *pv;
@@ -410,10 +420,12 @@ static void mlf_balance(pq_t** pv, uint32_t* pk, uint32_t n, uint32_t a) {
     for (;;) {
         pq_t* add = NULL;
         size_t nadd = 0, cadd = 0;
+        pstart_t R;
+        pstart_build(&R, v, k, n);
         for (uint32_t j = 0; j < k; j++) {
             uint32_t len = ((j + 1 < k) ? v[j + 1].p : n) - v[j].p;
-            uint32_t lo = lower_bound_pq(v, k, v[j].q);
-            uint32_t hi = lower_bound_pq(v, k, v[j].q + len);
+            uint32_t lo = pstart_lb(&R, v[j].q);
+            uint32_t hi = pstart_lb(&R, v[j].q + len);
             if (hi - lo >= 2 * a) {
                 uint32_t s = v[lo + a].p;
                 uint32_t d = s - v[j].q;
@@ -423,11 +435,17 @@ static void mlf_balance(pq_t** pv, uint32_t* pk, uint32_t n, uint32_t a) {
                 nadd++;
             }
         }
+        pstart_free(&R);
         if (!nadd) { free(add); break; }
-        v = realloc(v, (k + nadd) * sizeof(pq_t));
-        memcpy(v + k, add, nadd * sizeof(pq_t));
+        /* add[] is ascending in p (one split inside each input interval j, j ascending):
+         * merge instead of re-sorting */
+        pq_t* m = xmalloc((k + nadd) * sizeof(pq_t));
+        size_t a0 = 0, b0 = 0, o = 0;
+        while (a0 < k || b0 < nadd)
+            m[o++] = (b0 == nadd || (a0 < k && v[a0].p < add[b0].p)) ? v[a0++] : add[b0++];
+        free(v);
+        v = m;
         k += (uint32_t)nadd;
-        qsort(v, k, sizeof(pq_t), pq_cmp);
         free(add);
     }
     *pv = v;
@@ -574,10 +592,11 @@ orc_engine* orc_open(const char* base, uint32_t a, int from_runs_files) {
     E->L = xcalloc(k + 1, 1);
     for (uint32_t i = 0; i < k; i++) { E->p[i] = v[i].p; E->q[i] = v[i].q; }
     E->p[k] = E->n;
-    for (uint32_t i = 0; i < k; i++) { /* idx: input interval containing q_i */
-        uint32_t lo = 0, hi = k;
-        while (hi - lo > 1) { uint32_t m = (lo + hi) / 2; if (E->p[m] <= E->q[i]) lo = m; else hi = m; }
-        E->idx[i] = lo;
+    {   /* idx: input interval containing q_i = (number of starts <= q_i) - 1 */
+        pstart_t R;
+        pstart_build(&R, v, k, E->n);
+        for (uint32_t i = 0; i < k; i++) E->idx[i] = pstart_lb(&R, E->q[i] + 1) - 1;
+        pstart_free(&R);
     }
     /* L' from the run letters (build_MLF.cpp:133-149): split pieces inherit `prev`;
      * pieces after the last run head are never assigned (left 0, recorded). */
@@ -915,5 +934,114 @@ int orc_search_file(orc_engine* E, const char* patterns_path, const char* out_cs
     clock_gettime(CLOCK_MONOTONIC, &t1);
     if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     free(pb.v); free(off); free(counts); free(occ);
+    return 0;
+}
+
+/* ------------------------------------------------ record checker (tests) */
+/* Independent of any BWT: a record (pat, word, seg, word_in_seg, offset) is sound when
+ * word/seg/word_in_seg agree with the .eds segmentation (rank1/select1 of the segment
+ * bitvector, MOVE_EDSBWTSearch.cpp:361-363), word is non-empty, offset < |word|, and the
+ * pattern can be spelled from word[offset], continuing at the start of any word of the
+ * next segment, where a segment holding the empty word may be skipped (the link()
+ * semantics of :512-625 seen forwards; tests/edsgen.py brute_occurrences). */
+typedef struct {
+    const eds_t* E;
+    const uint32_t* seg_of; /* 1-based segment of each word */
+    const uint32_t* seg_first; /* first word of segment s (1-based), [S+1] = W */
+    uint32_t W, S;
+} chk_t;
+
+static inline uint32_t chk_wlen(const chk_t* C, uint32_t w) {
+    const uint32_t e = w + 1 < C->W ? C->E->wstart.v[w + 1] - 1 : (uint32_t)C->E->text.n - 1;
+    return e - C->E->wstart.v[w];
+}
+static inline int chk_empty(const chk_t* C, uint32_t w) {
+    return chk_wlen(C, w) == 1 && C->E->text.v[C->E->wstart.v[w]] == EMPTYC;
+}
+static int chk_from_word(const chk_t* C, uint32_t w, uint32_t o, const uint8_t* P, uint32_t m, uint32_t p, uint64_t* budget);
+static int chk_from_segment(const chk_t* C, uint32_t s, const uint8_t* P, uint32_t m, uint32_t p, uint64_t* budget) {
+    if (p == m) return 1;
+    if (s > C->S || !*budget) return 0;
+    (*budget)--;
+    for (uint32_t w = C->seg_first[s]; w < C->seg_first[s + 1]; w++) {
+        if (chk_empty(C, w)) { if (chk_from_segment(C, s + 1, P, m, p, budget)) return 1; }
+        else if (chk_from_word(C, w, 0, P, m, p, budget)) return 1;
+    }
+    return 0;
+}
+static int chk_from_word(const chk_t* C, uint32_t w, uint32_t o, const uint8_t* P, uint32_t m, uint32_t p, uint64_t* budget) {
+    const uint32_t L = chk_wlen(C, w);
+    uint32_t n = L - o;
+    if (n > m - p) n = m - p;
+    if (memcmp(C->E->text.v + C->E->wstart.v[w] + o, P + p, n) != 0) return 0;
+    if (p + n == m) return 1;
+    return chk_from_segment(C, C->seg_of[w] + 1, P, m, p + n, budget);
+}
+
+typedef struct {
+    const chk_t* C;
+    const uint8_t* bytes;
+    const uint64_t* off;
+    uint64_t npat;
+    uint32_t first_id;
+    const orc_occ* rec;
+    uint64_t lo, hi, bad, first_bad;
+} chk_job;
+
+static void* chk_run(void* arg) {
+    chk_job* J = arg;
+    const chk_t* C = J->C;
+    J->first_bad = ~0ull;
+    for (uint64_t i = J->lo; i < J->hi; i++) {
+        const orc_occ r = J->rec[i];
+        int ok = r.pat >= J->first_id && (uint64_t)(r.pat - J->first_id) < J->npat && r.word < C->W;
+        if (ok) ok = C->seg_of[r.word] == r.seg && r.word - C->seg_first[r.seg] == r.word_in_seg && !chk_empty(C, r.word) &&
+                     r.offset < chk_wlen(C, r.word);
+        if (ok) {
+            const uint64_t k = r.pat - J->first_id;
+            uint64_t budget = 1u << 20;
+            ok = chk_from_word(C, r.word, r.offset, J->bytes + J->off[k], (uint32_t)(J->off[k + 1] - J->off[k]), 0, &budget);
+        }
+        if (!ok) { J->bad++; if (J->first_bad == ~0ull) J->first_bad = i; }
+    }
+    return NULL;
+}
+
+int orc_check_records(const char* eds_path, const char* bytes, const uint64_t* offsets, uint64_t npat, uint32_t first_pattern_id,
+                      const orc_occ* rec, uint64_t nocc, int threads, uint64_t* bad, uint64_t* first_bad) {
+    uint8_t* s;
+    size_t n;
+    if (read_file(eds_path, &s, &n)) return -1;
+    eds_t E;
+    int rc = eds_parse(s, n, &E);
+    free(s);
+    if (rc) return -1;
+    chk_t C = {&E, NULL, NULL, (uint32_t)E.wstart.n, 0};
+    uint32_t* so = xmalloc((size_t)C.W * 4);
+    uint32_t* sf = xmalloc(((size_t)C.W + 2) * 4);
+    for (uint32_t w = 0; w < C.W; w++) {
+        if (E.bits.v[w]) sf[++C.S] = w;
+        so[w] = C.S;
+    }
+    sf[C.S + 1] = C.W;
+    C.seg_of = so;
+    C.seg_first = sf;
+    if (threads < 1) threads = 1;
+    chk_job* J = xcalloc((size_t)threads, sizeof(chk_job));
+    pthread_t* th = xcalloc((size_t)threads, sizeof(pthread_t));
+    for (int t = 0; t < threads; t++) {
+        J[t] = (chk_job){&C, (const uint8_t*)bytes, offsets, npat, first_pattern_id, rec,
+                         nocc * (uint64_t)t / (uint64_t)threads, nocc * (uint64_t)(t + 1) / (uint64_t)threads, 0, 0};
+        pthread_create(&th[t], NULL, chk_run, &J[t]);
+    }
+    *bad = 0;
+    *first_bad = ~0ull;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        *bad += J[t].bad;
+        if (J[t].first_bad < *first_bad) *first_bad = J[t].first_bad;
+    }
+    free(J); free(th); free(so); free(sf);
+    eds_free(&E);
     return 0;
 }

@@ -75,6 +75,14 @@ void orc_free(void* p);
 int orc_search_file(orc_engine*, const char* patterns_path, const char* out_csv,
                     uint64_t limit, int threads, orc_counters* ctr, double* seconds);
 
+/* Record checker, independent of any BWT: counts records whose (word, seg, word_in_seg,
+ * offset) disagree with the .eds segmentation or from which the pattern cannot be spelled
+ * (continuing into any word of the next segment; segments holding the empty word may be
+ * skipped).  *first_bad = index of the first bad record (~0 if none). */
+int orc_check_records(const char* eds_path, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                      uint32_t first_pattern_id, const orc_occ* rec, uint64_t nocc, int threads,
+                      uint64_t* bad, uint64_t* first_bad);
+
 #ifdef __cplusplus
 }
 #endif

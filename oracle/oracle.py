@@ -61,6 +61,9 @@ def lib():
         L.orc_search_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u64, i32, ctypes.POINTER(Counters),
                                       ctypes.POINTER(ctypes.c_double)]
         L.orc_search_file.restype = i32
+        L.orc_check_records.argtypes = [ctypes.c_char_p, vp, vp, u64, u32, vp, u64, i32, ctypes.POINTER(u64),
+                                        ctypes.POINTER(u64)]
+        L.orc_check_records.restype = i32
         _L = L
     return _L
 
@@ -69,6 +72,22 @@ def transform(eds_path: str, base: str) -> None:
     """EDS-BWTransform.sh restated (naive suffix sort: small inputs only)."""
     if lib().orc_transform(eds_path.encode(), base.encode()) != 0:
         raise RuntimeError(lib().orc_last_error().decode())
+
+
+def check_records(eds_path: str, buf: np.ndarray, offs: np.ndarray, occ: np.ndarray, first_pattern_id: int = 1,
+                  threads: int = 8) -> tuple[int, int]:
+    """BWT-free soundness check of occurrence records against the .eds text (see
+    orc_check_records).  Returns (number of bad records, index of the first bad one or -1)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    occ = np.ascontiguousarray(occ, dtype=OCC_DTYPE)
+    bad, first = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().orc_check_records(eds_path.encode(), buf.ctypes.data if buf.size else None, offs.ctypes.data, offs.size - 1,
+                                 first_pattern_id, occ.ctypes.data if occ.size else None, occ.size, threads,
+                                 ctypes.byref(bad), ctypes.byref(first))
+    if rc != 0:
+        raise RuntimeError(lib().orc_last_error().decode())
+    return int(bad.value), (-1 if first.value == 2**64 - 1 else int(first.value))
 
 
 class Engine:

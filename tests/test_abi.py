@@ -19,7 +19,13 @@ def test_header_symbols_exported(edsbwt):
     assert "edsbwt_search" in names and "edsbwt_index_open" in names
     for n in names:
         assert hasattr(L, n), n
-    assert L.edsbwt_abi_version() == 2
+    assert L.edsbwt_abi_version() == 3
+
+
+def test_build_id_matches_sources(edsbwt):
+    """libedsbwt.so carries the hash of the sources it was built from; lib() refuses a stale one."""
+    L = edsbwt.lib()
+    assert L.edsbwt_build_id().decode() == edsbwt.source_build_id()
 
 
 def test_open_missing_index_fails_cleanly(edsbwt, tmp_path):

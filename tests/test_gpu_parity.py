@@ -440,3 +440,132 @@ def test_locate_sample_rates_gpu(oracle, edsbwt, tmp_path, monkeypatch, shift):
         assert st["locate_offsets"] == int(oo["offset"].astype(np.uint64).sum())
         if shift == 0:
             assert st["locate_lf_steps"] == 0  # no walk: the sample of the row itself
+
+
+def _lines_search(edsbwt, idx, text: bytes, first_id=1, locate=True, chunk_mb=None, pinned=True):
+    """edsbwt_search_lines over `text` (page-locked or pageable): counts and records."""
+    import ctypes
+    nlines = text.count(b"\n") + (1 if text and not text.endswith(b"\n") else 0)
+    if pinned:
+        hb = edsbwt.HostBuffer(max(1, len(text)))
+        hb.array(np.uint8, len(text))[:] = np.frombuffer(text, np.uint8)
+        tptr = hb.ptr
+        cb = edsbwt.HostBuffer(4 * max(1, nlines))
+        counts = cb.array(np.uint32, nlines)
+        cptr = cb.ptr
+    else:
+        arr = np.frombuffer(text, np.uint8).copy()
+        tptr = arr.ctypes.data if arr.size else None
+        counts = np.zeros(max(1, nlines), np.uint32)
+        cptr = counts.ctypes.data
+    npat, ptr, n = idx.search_lines(tptr, len(text), cptr, max(1, nlines), first_pattern_id=first_id, locate=locate, keep=True)
+    assert npat == nlines
+    occ = idx.occ_view(ptr, n).copy()
+    idx.occ_free(ptr)
+    return counts[:nlines].copy(), occ
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_search_lines_pipeline_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
+    """The pattern file in host memory through edsbwt_search_lines: lines split on the device
+    (getline semantics: '\\r' kept, empty lines, a last line without '\\n'), cut into many
+    chunks (EDSBWT_CHUNK_MB tiny) so uploads, searches and downloads overlap across slots;
+    page-locked and pageable buffers; first_pattern_id != 1 as a shard's would be."""
+    rng = random.Random(808)
+    segs = _covid_like(rng, 400)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 40)) or "ACGT" for _ in range(5000)]
+    pats += ["", "AC\r", "N", "#A"] + ["".join(rng.choice("ACGT") for _ in range(rng.randint(5, 25))) for _ in range(1000)]
+    rng.shuffle(pats)
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=77)
+    for trailing in (True, False):
+        text = ("\n".join(pats) + ("\n" if trailing else "")).encode()
+        for mb in ("0.01", "64"):
+            monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
+            with edsbwt.Index(base) as idx:
+                gc, go = _lines_search(edsbwt, idx, text, first_id=77, pinned=pinned)
+                st = idx.stats()
+                assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+                assert st["chunks"] > (5 if mb == "0.01" else 0)
+                assert st["patterns"] == len(pats) and st["occurrences"] == oo.size
+                gc2, go2 = _lines_search(edsbwt, idx, text, first_id=77, locate=False, pinned=pinned)
+                assert np.array_equal(gc2, oc) and go2.size == 0
+            # the (bytes, offsets) host path, chunked the same way
+            with edsbwt.Index(base) as idx:
+                gc3, go3 = idx.search((buf, offs), first_pattern_id=77)
+                assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)
+
+
+def test_search_lines_empty_and_held_records_gpu(oracle, edsbwt, tmp_path):
+    """An empty file; records still held by the caller when the next call runs (the engine
+    must not overwrite them) and freed after the index is closed."""
+    base = _build(oracle, tmp_path, open(os.path.join(GOLDEN, "test.eds")).read(), "test")
+    with edsbwt.Index(base) as idx:
+        c, o = _lines_search(edsbwt, idx, b"")
+        assert c.size == 0 and o.size == 0
+        hb = edsbwt.HostBuffer(64)
+        t = b"TATT\nACT\nTTAT\n"
+        hb.array(np.uint8, len(t))[:] = np.frombuffer(t, np.uint8)
+        cnt = np.zeros(3, np.uint32)
+        _, p1, n1 = idx.search_lines(hb.ptr, len(t), cnt.ctypes.data, 3, keep=True)
+        first = idx.occ_view(p1, n1).copy()
+        _, p2, n2 = idx.search_lines(hb.ptr, len(t), cnt.ctypes.data, 3, keep=True)
+        assert p2 != p1 and np.array_equal(idx.occ_view(p1, n1), first)  # the held records survive
+        assert np.array_equal(idx.occ_view(p2, n2), first)
+        idx.occ_free(p2)
+    assert np.array_equal(edsbwt.Index.occ_view(p1, n1), first)  # detached from the closed index
+    edsbwt.Index.occ_free(p1)
+    assert [tuple(int(x) for x in r) for r in first] == [(1, 3, 2, 0, 0), (1, 4, 3, 0, 1), (1, 7, 4, 0, 1), (1, 1, 1, 1, 0),
+                                                         (3, 0, 1, 0, 1), (3, 4, 3, 0, 0), (3, 7, 4, 0, 0)]
+
+
+def test_search_device_null_stream_ordering(oracle, edsbwt, tmp_path):
+    """search_device with stream=NULL after torch filled the inputs on the default stream,
+    with no synchronize in between: the engine orders itself after the null stream."""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(31)
+    segs = edsgen.random_eds(rng, 1500, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(4, 30)) or "ACGT" for _ in range(20000)]
+    buf, offs = _pack(pats)
+    oc, _, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        h_bytes = torch.from_numpy(buf.copy()).pin_memory()
+        h_offs = torch.from_numpy(offs.astype(np.int64)).pin_memory()
+        torch.cuda.synchronize()
+        d_bytes = torch.zeros(buf.size, dtype=torch.uint8, device="cuda")
+        d_offs = torch.zeros(offs.size, dtype=torch.int64, device="cuda")
+        big = torch.randn(4096, 4096, device="cuda")
+        for _ in range(8):
+            big = big @ big  # keep the null stream busy before the copies land
+        d_bytes.copy_(h_bytes, non_blocking=True)
+        d_offs.copy_(h_offs, non_blocking=True)
+        d_counts = torch.zeros(len(pats), dtype=torch.int32, device="cuda")
+        idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), len(pats), d_counts.data_ptr(), stream=0)
+        assert np.array_equal(d_counts.cpu().numpy().astype(np.uint32), oc)
+
+
+def test_shard_first_pattern_id_gpu(oracle, edsbwt, tmp_path):
+    """Two contiguous shards searched with first_pattern_id = lo + 1 (as each multi-GPU rank
+    does) concatenate to the single-call oracle output, in MOVE and legacy order."""
+    import importlib
+    shard = importlib.import_module("eds-bwt_amd.shard")
+    rng = random.Random(2024)
+    segs = edsgen.random_eds(rng, 1200, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(3, 20)) or "ACGT" for _ in range(3001)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    kp = _kpos(base)
+    legacy_ref = oo[np.lexsort((kp[oo["word"]], oo["offset"], oo["pat"]))]
+    with edsbwt.Index(base) as idx:
+        for legacy, ref in ((False, oo), (True, legacy_ref)):
+            cs, os_ = [], []
+            for r in range(2):
+                b, o, first = shard.shard_patterns(buf, offs, 2, r)
+                c, occ = idx.search((b, o), first_pattern_id=first, legacy=legacy)
+                cs.append(c)
+                os_.append(occ)
+            assert np.array_equal(np.concatenate(cs), oc)
+            assert np.array_equal(np.concatenate(os_), ref)

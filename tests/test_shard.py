@@ -36,10 +36,19 @@ def _worker(rank, world, port, base, buf, offs, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b, o, first = shard.shard_patterns(buf, offs, world, rank)
     counts, occ, _ = orc.Engine(base).search(b, o, first_pattern_id=first)  # stands in for the GPU search on CPU
-    allc = shard.gather_counts(torch.from_numpy(counts.astype(np.int64)), world, offs.size - 1)
-    allocc = shard.gather_records(occ, world)
+    # the exchange step bench.py runs over RCCL: sizes all-gathered, counts and 20-B records
+    # gathered to rank 0 as padded tensors
+    sizes = shard.exchange_sizes(counts.size, occ.size, "cpu")
+    npats = [int(x) for x in sizes[:, 0]]
+    noccs = [int(x) for x in sizes[:, 1]]
+    assert sum(npats) == offs.size - 1
+    allc = shard.gather_counts(torch.from_numpy(counts.astype(np.int32)), npats)
+    rec = torch.from_numpy(occ.view(np.uint32).reshape(-1).view(np.int32).copy())
+    allocc = shard.gather_records(rec, noccs)
     if rank == 0:
-        q.put((allc.numpy(), allocc))
+        q.put((allc.numpy(), shard.records_to_numpy(allocc)))
+    else:
+        assert allc is None and allocc is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -65,5 +74,5 @@ def test_sharded_equals_single(oracle, tmp_path, world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert np.array_equal(counts, ref_counts.astype(np.int64))
+    assert np.array_equal(counts.astype(np.uint32), ref_counts)
     assert np.array_equal(occ, ref_occ)

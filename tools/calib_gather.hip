@@ -7,7 +7,13 @@
 //         "gather128"  — one random 128-B line per lane (8 × 16-B loads);
 //         "stream16"   — coalesced 16-B-per-lane streaming read of the whole table (the
 //                        shape MI355X_MICROARCH.md calibrates FETCH_SIZE on);
-//         "stream4"    — coalesced 4-B-per-lane streaming read (the item arrays' shape).
+//         "stream4"    — coalesced 4-B-per-lane streaming read (the item arrays' shape);
+//         "chainK_wW"  — the deep walk's shape (k_deep_fast): every lane walks patterns of
+//                        8 dependent steps, each step one random 16-B load per interval end
+//                        (K = 1 or 2 loads issued together) whose address depends on the
+//                        previous step's values; W = waves per SIMD the launch is held to
+//                        (dynamic LDS), so the ceiling is measured at a kernel's occupancy.
+//   calib_gather --chain [table_MB ...]   runs only the chain shapes
 // Algorithmic bytes are known exactly, so running this under
 // `rocprofv3 --pmc FETCH_SIZE` gives the FETCH_SIZE → bytes factor for each shape, and the
 // timed rate is the practical ceiling of the rank-block gathers (vs HBM peak 8 TB/s).
@@ -16,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                        \
@@ -50,6 +57,32 @@ __global__ void __launch_bounds__(256) k_gather(const uint4* __restrict__ t, uin
     if (acc == 0x12345678u) sink[g] = acc;  // keeps the loads alive; never true in practice
 }
 
+// the deep walk's access shape: per lane, patterns of `steps` dependent steps; each step
+// issues K independent random 16-B loads (the two interval ends) and the next step's
+// addresses depend on the loaded values
+template <int K>
+__global__ void __launch_bounds__(256) k_chain(const uint4* __restrict__ t, uint32_t n16, uint32_t pats, uint32_t steps, uint32_t seed,
+                                               uint32_t* __restrict__ sink) {
+    extern __shared__ uint32_t hold[];  // occupancy limiter only
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    for (uint32_t p = 0; p < pats; p++) {
+        uint32_t h[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) h[k] = mix(g * 2654435761u ^ (seed + p * 7919u + k * 104729u));
+        for (uint32_t s = 0; s < steps; s++) {
+            uint4 v[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) v[k] = t[h[k] % n16];
+#pragma unroll
+            for (int k = 0; k < K; k++) h[k] = mix(h[k] ^ v[k].x ^ v[k].w);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) acc ^= h[k];
+    }
+    if (acc == 0x12345678u) { sink[g] = acc; hold[threadIdx.x] = acc; }
+}
+
 __global__ void __launch_bounds__(256) k_stream4(const uint32_t* __restrict__ t, size_t n4, uint32_t* __restrict__ sink) {
     uint32_t acc = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) acc ^= t[i];
@@ -65,9 +98,52 @@ __global__ void __launch_bounds__(256) k_stream(const uint4* __restrict__ t, siz
     if (acc == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
+static void chains(const std::vector<size_t>& mbs, uint32_t* sink, hipEvent_t a, hipEvent_t b) {
+    const uint32_t block = 256, steps = 8;
+    int cus = 256;
+    {
+        hipDeviceProp_t pr;
+        if (hipGetDeviceProperties(&pr, 0) == hipSuccess) cus = pr.multiProcessorCount;
+    }
+    for (size_t mb : mbs) {
+        const size_t bytes = mb << 20;
+        uint4* t;
+        CK(hipMalloc(&t, bytes));
+        CK(hipMemset(t, 3, bytes));
+        for (int K = 1; K <= 2; K++)
+            for (int waves : {2, 4, 6, 8}) {
+                // waves per SIMD = blocks per CU (a 256-thread block is one wave per SIMD)
+                const size_t lds = (160u * 1024u) / (size_t)waves - 256;
+                const uint32_t grid = (uint32_t)cus * (uint32_t)waves * 4, pats = 16;
+                float best = 1e30f;
+                for (int rep = 0; rep < 4; rep++) {
+                    CK(hipEventRecord(a));
+                    if (K == 1) hipLaunchKernelGGL(k_chain<1>, dim3(grid), dim3(block), lds, 0, t, (uint32_t)(bytes / 16), pats, steps, 5u + rep, sink);
+                    else hipLaunchKernelGGL(k_chain<2>, dim3(grid), dim3(block), lds, 0, t, (uint32_t)(bytes / 16), pats, steps, 5u + rep, sink);
+                    CK(hipGetLastError());
+                    CK(hipEventRecord(b));
+                    CK(hipEventSynchronize(b));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, a, b));
+                    if (rep > 0 && ms < best) best = ms;
+                }
+                const double loads = (double)grid * block * pats * steps * K;
+                std::printf("{\"shape\": \"chain%d_w%d\", \"table_MB\": %zu, \"loads_16B\": %.0f, \"best_ms\": %.4f, "
+                            "\"lines_per_s\": %.4g, \"dependent_steps_per_s\": %.4g}\n",
+                            K, waves, mb, loads, best, loads / (best * 1e-3), loads / K / (best * 1e-3));
+                std::fflush(stdout);
+            }
+        CK(hipFree(t));
+    }
+}
+
 int main(int argc, char** argv) {
     std::vector<size_t> mbs;
-    for (int i = 1; i < argc; i++) mbs.push_back(std::strtoull(argv[i], nullptr, 10));
+    bool chain_only = false;
+    for (int i = 1; i < argc; i++) {
+        if (std::string(argv[i]) == "--chain") chain_only = true;
+        else mbs.push_back(std::strtoull(argv[i], nullptr, 10));
+    }
     if (mbs.empty()) mbs = {16, 100, 200, 1024, 4096};
     uint32_t* sink;
     const uint32_t grid = 256 * 32, block = 256, iters = 64;
@@ -75,6 +151,8 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    chains(mbs, sink, a, b);
+    if (chain_only) return 0;
     for (size_t mb : mbs) {
         const size_t bytes = mb << 20;
         uint4* t;
