@@ -39,6 +39,7 @@ LEGACY_ORDER = 0x200
 NO_KTAB = 0x400
 NO_DIRECT = 0x800
 NO_PAIRS = 0x1000
+NO_TEXT = 0x2000
 
 OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
 CSV_HEADER = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"  # MOVE_EDSBWTSearch.cpp:59 (note the trailing space)
@@ -69,7 +70,7 @@ class _Stats(ctypes.Structure):
                 ("locate_offsets", ctypes.c_uint64),
                 ("search_groups", ctypes.c_uint64), ("start_depth", ctypes.c_uint64),
                 ("ms_wall", ctypes.c_double), ("chunks", ctypes.c_uint64), ("bytes_h2d", ctypes.c_uint64),
-                ("bytes_d2h", ctypes.c_uint64)]
+                ("bytes_d2h", ctypes.c_uint64), ("text_chars", ctypes.c_uint64), ("text_rows", ctypes.c_uint64)]
 
 
 _LIB = None
@@ -247,7 +248,7 @@ class Index:
     def search(self, patterns: Sequence[bytes | str] | tuple[np.ndarray, np.ndarray], *, first_pattern_id: int = 1,
                locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
                ordered: bool = False, wide: bool = True, walk: bool = False, legacy: bool = False,
-               ktab: bool = True, direct: bool = True, pairs: bool = True):
+               ktab: bool = True, direct: bool = True, pairs: bool = True, text: bool = True):
         """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc]).
         ``table``: (word, offset) per row from the full table; ``walk``: the reference's
         full LF walk to '#'; default: walk to the first sampled row.  ``legacy``: records in
@@ -260,7 +261,7 @@ class Index:
         flags = ((LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
                  | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0) | (0 if wide else NO_WIDE)
                  | (LOCATE_WALK if walk else 0) | (LEGACY_ORDER if legacy else 0) | (0 if ktab else NO_KTAB)
-                 | (0 if direct else NO_DIRECT) | (0 if pairs else NO_PAIRS))
+                 | (0 if direct else NO_DIRECT) | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT))
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         bp = buf.ctypes.data if buf.size else None
@@ -307,13 +308,13 @@ class Index:
     def search_device(self, d_bytes: int, d_offsets: int, npat: int, d_counts: int, *, first_pattern_id: int = 1,
                       locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
                       stream: int = 0, walk: bool = False, ktab: bool = True, direct: bool = True,
-                      pairs: bool = True):
+                      pairs: bool = True, text: bool = True):
         """Device-resident batch (pointers are device addresses, e.g. torch data_ptr()).
         Returns (device pointer of the records, number of records)."""
         pflag = {False: 0, True: PROFILE, "light": PROFILE_LIGHT}[profile]
         flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | pflag | (0 if deep else NO_DEEP) \
             | (LOCATE_WALK if walk else 0) | (0 if ktab else NO_KTAB) | (0 if direct else NO_DIRECT) \
-            | (0 if pairs else NO_PAIRS)
+            | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT)
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,

@@ -24,6 +24,9 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <condition_variable>
+#include <exception>
+#include <functional>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -171,6 +174,14 @@ struct Engine {
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
     bool have_table = false;
+    // words' text for the single-row compare (k_text_build): reversed 2-bit text, per-row text
+    // position, per-word whole-word row; built with dense samples when sigma - 1 <= 4
+    DBuf<uint64_t> rtext;
+    DBuf<uint32_t> gpos, wrow;
+    uint64_t tlen = 0;
+    bool have_text = false;
+    bool text_deep = env_double("EDSBWT_TEXT_DEEP", 1) != 0;
+    bool text_on = true;     // per search (EDSBWT_NO_TEXT, the walk and table locate modes clear it)
     DBuf<uint4> samples;     // locate samples (word, offset, segment, word in segment) of rows whose offset % 2^kSampleShift == 0
     bool have_samples = false;
     uint32_t samp_shift = 0;  // rows sampled: offset % 2^samp_shift == 0 (0: every row)
@@ -244,6 +255,15 @@ struct Engine {
     DBuf<uint4> dq;                   // k_deep_fast -> k_deep queue (pattern, depth, b, e), sharded
     DBuf<uint64_t> dq2;               // ... and, for the packed direct start, each entry's packed start
     DBuf<uint32_t> dqpre;
+    // One page-locked, device-mapped, coherent host block holds pinned, pinned_big,
+    // pinned_stats and a staging area: the search's small transfers are copied by a kernel
+    // (small_copy) on the engine stream, because a DMA copy would queue behind the host
+    // pipeline's bulk uploads / downloads on the copy engines and stall the search
+    uint8_t* hostblk = nullptr;
+    uint8_t* hostblk_dev = nullptr;
+    size_t hostblk_size = 0;
+    static constexpr size_t kStageBytes = 256 << 10;
+    uint8_t* hstage = nullptr;
     uint32_t* pinned_big = nullptr;  // host shard counters + prefix
     DBuf<unsigned long long> stats;  // kStatSlots sharded statistics counters (stat_add)
     unsigned long long* pinned_stats = nullptr;
@@ -277,11 +297,12 @@ struct Engine {
     // is uploaded on `up` while chunk k is searched on `stream` and chunk k-1's counts and
     // records go back on `down` (two device slots per buffer, events between the streams)
     hipStream_t up = nullptr, down = nullptr;
-    hipEvent_t up_done[2] = {}, comp_done[2] = {}, down_done[2] = {};
-    DBuf<uint8_t> hraw[2], hbytes[2];
-    DBuf<uint64_t> hoffs[2];
-    DBuf<uint32_t> hcounts[2], nlcnt, nlpre;
-    DBuf<edsbwt_occ> hrec[2];
+    static constexpr int kSlots = 3;  // chunk k's search never waits for chunk k-2's download
+    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {};
+    DBuf<uint8_t> hraw[kSlots], hbytes[kSlots];
+    DBuf<uint64_t> hoffs[kSlots];
+    DBuf<uint32_t> hcounts[kSlots], nlcnt, nlpre;
+    DBuf<edsbwt_occ> hrec[kSlots];
     struct Pinned {  // page-locked host staging (inputs or counts in pageable caller memory)
         void* p = nullptr;
         size_t cap = 0;
@@ -298,7 +319,7 @@ struct Engine {
         }
         void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
     };
-    Pinned stage_in[2], stage_off[2], stage_cnt[2];
+    Pinned stage_in[kSlots], stage_off[kSlots], stage_cnt[kSlots];
     // the occurrence records handed to the caller (library-owned, page-locked, reused once
     // edsbwt_occ_free gives them back: see occ_arena_*)
     edsbwt_occ* arena = nullptr;
@@ -360,6 +381,12 @@ struct Engine {
         X.r3stride = r3stride;
         X.PC3 = pc3.p;
         for (uint32_t k = 0; k < kPairCodes + 3; k++) X.PC[k] = PC[k];
+        const bool txt = have_text && text_on && X.samp_dense;
+        X.rtext = txt ? rtext.p : nullptr;
+        X.tlen = tlen;
+        X.gpos = gpos.p;
+        X.wrow = wrow.p;
+        X.text_deep = text_deep ? 1u : 0u;
         return X;
     }
 
@@ -411,18 +438,31 @@ struct Engine {
         throw Fail(EDSBWT_E_DEVICE, std::string("kernel ") + name + ": " + hipGetErrorString(e));
     }
     uint32_t read_u32(const uint32_t* d) {
-        HIPCHK(hipMemcpyAsync(pinned, d, 4, hipMemcpyDeviceToHost, stream));
+        small_copy(pinned, d, 4);
         HIPCHK(hipStreamSynchronize(stream));
         return pinned[0];
     }
     uint64_t read_u64(const void* d) {
-        HIPCHK(hipMemcpyAsync(pinned, d, 8, hipMemcpyDeviceToHost, stream));
+        small_copy(pinned, d, 8);
         HIPCHK(hipStreamSynchronize(stream));
         uint64_t v;
         std::memcpy(&v, pinned, 8);
         return v;
     }
     void zero(void* p, size_t bytes) { if (bytes) HIPCHK(hipMemsetAsync(p, 0, bytes, stream)); }
+    // small transfer on the engine stream by a kernel (see hostblk); host pointers must lie in hostblk
+    const void* dev_alias(const void* p) const {
+        const uint8_t* q = static_cast<const uint8_t*>(p);
+        return (q >= hostblk && q < hostblk + hostblk_size) ? hostblk_dev + (q - hostblk) : p;
+    }
+    void small_copy(void* dst, const void* src, size_t bytes) {
+        if (!bytes) return;
+        if (bytes % 4) throw Fail(EDSBWT_E_ARG, "small_copy of a size that is not a multiple of 4");
+        const uint32_t n = (uint32_t)(bytes / 4);
+        hipLaunchKernelGGL(k_copy_words, dim3(std::min<uint32_t>(64, (n + 255) / 256)), dim3(256), 0, stream,
+                           (const uint32_t*)dev_alias(src), (uint32_t*)const_cast<void*>(dev_alias(dst)), n);
+        HIPCHK(hipGetLastError());
+    }
 
     // reversed-code chunk of depth D for the patterns in trie order (chunk 0 is the
     // last radix pass's output, chunks 1.. were gathered by build_trie)
@@ -437,7 +477,7 @@ struct Engine {
     static constexpr uint32_t kCnt = NSHARD * 32 + 32;  // shard counters + device scalars (link runs)
     std::vector<uint32_t> hsh = std::vector<uint32_t>(kCnt, 0);
     void fetch_shards() {
-        HIPCHK(hipMemcpyAsync(pinned_big, lcnt.p, kCnt * 4, hipMemcpyDeviceToHost, stream));
+        small_copy(pinned_big, lcnt.p, kCnt * 4);
         HIPCHK(hipStreamSynchronize(stream));
         std::memcpy(hsh.data(), pinned_big, kCnt * 4);
     }
@@ -467,7 +507,7 @@ struct Engine {
         pre[0] = 0;
         for (uint32_t sh = 0; sh < NSHARD; sh++) pre[sh + 1] = pre[sh] + hsh[sh * 32 + k];
         shpre.ensure(NSHARD + 1);
-        HIPCHK(hipMemcpyAsync(shpre.p, pre, (NSHARD + 1) * 4, hipMemcpyHostToDevice, stream));
+        small_copy(shpre.p, pre, (NSHARD + 1) * 4);
     }
     template <typename A, typename B, typename C>
     void unshard3(int k, size_t cap, const A* a, const B* b, const C* c, A* oa, B* ob, C* oc, uint32_t total) {
@@ -573,9 +613,16 @@ struct Engine {
         device = dev;
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        HIPCHK(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc((void**)&pinned_big, (kCnt + 2 * (NSHARD + 8)) * 4, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc((void**)&pinned_stats, kStatSlots * 8, hipHostMallocDefault));
+        {
+            const size_t a = 256, big = ((kCnt + 2 * (NSHARD + 8)) * 4 + 255) / 256 * 256, stb = kStatSlots * 8;
+            hostblk_size = a + big + stb + kStageBytes;
+            HIPCHK(hipHostMalloc((void**)&hostblk, hostblk_size, hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer((void**)&hostblk_dev, hostblk, 0));
+            pinned = reinterpret_cast<uint32_t*>(hostblk);
+            pinned_big = reinterpret_cast<uint32_t*>(hostblk + a);
+            pinned_stats = reinterpret_cast<unsigned long long*>(hostblk + a + big);
+            hstage = hostblk + a + big + stb;
+        }
         stats.ensure(kStatSlots);
         HostIndex H;
         std::string err;
@@ -674,6 +721,8 @@ struct Engine {
         }
         up(seg_of_word, sow);
         up(seg_start, sst);
+        h_seg_of_word = sow;  // the host pipeline's record expansion (search_host)
+        h_seg_start = sst;
         up(seg_lo, slo);
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
@@ -894,8 +943,35 @@ struct Engine {
         launch(KC_TABLE, k_table_walk, W, W, X, da.p, offt.p, wl.p);
         launch(KC_TABLE, k_table_finish, N, N, (const uint32_t*)da.p, (const uint32_t*)wl.p, offt.p);
         HIPCHK(hipStreamSynchronize(stream));
+        if (!have_text && sigma >= 2 && sigma - 1 <= 4 && env_double("EDSBWT_TEXT", 1) != 0) build_text(wl);
         wl.release();
         have_table = true;
+    }
+
+    // the words' text (k_text_build) from the per-row table and the word lengths
+    void build_text(DBuf<uint32_t>& wl) {
+        DBuf<uint32_t> ws;
+        const uint32_t* wsp = nullptr;
+        {
+            DBuf<uint64_t> wl64, ws64;
+            wl64.ensure(W);
+            launch(KC_TABLE, k_u32_to_u64, W, (const uint32_t*)wl.p, (uint64_t)W, wl64.p);
+            tlen = scan_u64(wl64.p, ws64, W);
+            if (tlen >= 0xFFFFFFFFull) return;  // text positions are u32
+            ws.ensure(W);
+            launch(KC_TABLE, k_u32_of_u64, W, (const uint64_t*)ws64.p, (uint64_t)W, ws.p);
+            wsp = ws.p;
+        }
+        const uint64_t nw = tlen / 32 + 2;
+        rtext.ensure(nw);
+        zero(rtext.p, nw * 8);
+        gpos.ensure(N);
+        wrow.ensure(W);
+        launch(KC_TABLE, k_text_build, N, N, kidx(), (const uint32_t*)da.p, (const uint32_t*)offt.p, wsp, tlen, gpos.p, wrow.p,
+               (uint32_t*)rtext.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        device_bytes += nw * 8 + (size_t)N * 4 + (size_t)W * 4;
+        have_text = true;
     }
 
     // ------------------------------------------------------------ search
@@ -978,8 +1054,14 @@ struct Engine {
                 launch_reduce(KC_TRIE, k_trie_counts, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, Lmax, lhist.p, lhist.p + (Lmax + 2));
             else
                 launch(KC_TRIE, k_trie_counts_global, P, (const uint32_t*)slen.p, (const uint32_t*)lcp.p, P, lhist.p, lhist.p + (Lmax + 2));
-            HIPCHK(hipMemcpyAsync(hv.data(), lhist.p, hv.size() * 8, hipMemcpyDeviceToHost, stream));
-            HIPCHK(hipStreamSynchronize(stream));
+            if (hv.size() * 8 <= kStageBytes) {
+                small_copy(hstage, lhist.p, hv.size() * 8);
+                HIPCHK(hipStreamSynchronize(stream));
+                std::memcpy(hv.data(), hstage, hv.size() * 8);
+            } else {
+                HIPCHK(hipMemcpyAsync(hv.data(), lhist.p, hv.size() * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+            }
         };
         order(false);
         if (hv[2 * (size_t)(Lmax + 2) + 2]) {  // a tie group too large to fix in place: sort every chunk
@@ -1016,11 +1098,11 @@ struct Engine {
         {
             uint32_t h[5] = {0, N - 1, 0, 0, 1};
             std::memcpy(pinned, h, sizeof h);
-            HIPCHK(hipMemcpyAsync(ib[0].p, &pinned[0], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(ie[0].p, &pinned[1], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(iu[0].p, &pinned[2], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(ioff[0].p, &pinned[3], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(iend[0].p, &pinned[4], 4, hipMemcpyHostToDevice, stream));
+            small_copy(ib[0].p, &pinned[0], 4);
+            small_copy(ie[0].p, &pinned[1], 4);
+            small_copy(iu[0].p, &pinned[2], 4);
+            small_copy(ioff[0].p, &pinned[3], 4);
+            small_copy(iend[0].p, &pinned[4], 4);
             HIPCHK(hipStreamSynchronize(stream));
         }
         uint32_t novf = 0;
@@ -1245,7 +1327,7 @@ struct Engine {
         const uint32_t D0 = ktab_depth;
         zero(counters.p + 8, 24);
         launch_reduce(KC_TRIE, k_lminmax, d_off, P, counters.p + 8);
-        HIPCHK(hipMemcpyAsync(pinned, counters.p + 8, 16, hipMemcpyDeviceToHost, stream));
+        small_copy(pinned, counters.p + 8, 16);
         HIPCHK(hipStreamSynchronize(stream));
         uint64_t mm[2];
         std::memcpy(mm, pinned, 16);
@@ -1279,6 +1361,11 @@ struct Engine {
             launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
                    (uint64_t*)nullptr);
         if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
+        if (packed && direct_sort_bits <= 0) {  // input order (EDSBWT_DIRECT_SORT_BITS=0)
+            st.start_depth = D0;
+            return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, kid, ktab_off.p, ktab_off.p + 1,
+                            ktab_b.p, ktab_e.p, r, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_in.p);
+        }
         if (packed) {
             // the order only buys locality (neighbouring lanes read neighbouring table entries and
             // rows): the D-mer's first direct_sort_bits bits (its leading symbols) are enough
@@ -1343,9 +1430,9 @@ struct Engine {
         {
             uint32_t* h = pinned;
             h[0] = 0; h[1] = N - 1; h[2] = 0;
-            HIPCHK(hipMemcpyAsync(ib[0].p, &h[0], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(ie[0].p, &h[1], 4, hipMemcpyHostToDevice, stream));
-            HIPCHK(hipMemcpyAsync(iu[0].p, &h[2], 4, hipMemcpyHostToDevice, stream));
+            small_copy(ib[0].p, &h[0], 4);
+            small_copy(ie[0].p, &h[1], 4);
+            small_copy(iu[0].p, &h[2], 4);
         }
         uint32_t novf = 0;
         bool in_sharded = false;  // current items in fu/fb/fe shards (prefix fpre, capacity fcap)
@@ -1484,7 +1571,7 @@ struct Engine {
                     nk.release();
                     for (uint32_t sh = 0; sh < NSHARD; sh++) hsh[sh * 32 + 1] = keep_keys[sh];
                     std::memcpy(pinned_big, hsh.data(), NSHARD * 32 * 4);
-                    HIPCHK(hipMemcpyAsync(lcnt.p, pinned_big, NSHARD * 32 * 4, hipMemcpyHostToDevice, stream));
+                    small_copy(lcnt.p, pinned_big, NSHARD * 32 * 4);
                     cap_keys = ncap;
                 }
             }
@@ -1518,7 +1605,7 @@ struct Engine {
                     regrow3(eu, eb, ee, cap_next, ncap, keep_items);
                     for (uint32_t sh = 0; sh < NSHARD; sh++) hsh[sh * 32 + 0] = keep_items[sh];
                     std::memcpy(pinned_big, hsh.data(), NSHARD * 32 * 4);
-                    HIPCHK(hipMemcpyAsync(lcnt.p, pinned_big, NSHARD * 32 * 4, hipMemcpyHostToDevice, stream));
+                    small_copy(lcnt.p, pinned_big, NSHARD * 32 * 4);
                     cap_next = ncap;
                 }
                 const uint32_t R = hsh[NSHARD * 32];
@@ -1539,7 +1626,7 @@ struct Engine {
                 pre[0] = 0;
                 for (uint32_t sh = 0; sh < NSHARD; sh++) pre[sh + 1] = pre[sh] + hsh[sh * 32 + 0];
                 fpre.ensure(NSHARD + 1);
-                HIPCHK(hipMemcpyAsync(fpre.p, pre, (NSHARD + 1) * 4, hipMemcpyHostToDevice, stream));
+                small_copy(fpre.p, pre, (NSHARD + 1) * 4);
                 std::swap(fu, eu); std::swap(fb, eb); std::swap(fe, ee);
                 fcap = cap_next;
                 in_sharded = true;
@@ -1706,6 +1793,9 @@ struct Engine {
         use_ktab = (flags & EDSBWT_NO_KTAB) == 0;
         use_pairs = (flags & EDSBWT_NO_PAIRS) == 0 && env_double("EDSBWT_NO_PAIRS", 0) == 0;
         use_direct = (flags & EDSBWT_NO_DIRECT) == 0 && env_double("EDSBWT_NO_DIRECT", 0) == 0;
+        // the single-row text compare answers with (word, offset): the reference walk and table
+        // locate modes keep their row-based records
+        text_on = (flags & (EDSBWT_NO_TEXT | EDSBWT_LOCATE_WALK | EDSBWT_LOCATE_TABLE)) == 0 && env_double("EDSBWT_NO_TEXT", 0) == 0;
         if (use_table) build_table();
         st.patterns = P;
         if (P == 0) return 0;
@@ -1747,8 +1837,8 @@ struct Engine {
         launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                       locate ? occ64.p : (uint64_t*)nullptr);
         if (locate) inclusive_scan_u64(occ64.p, oscan, P);  // occurrence and task offsets: one scan of both
-        HIPCHK(hipMemcpyAsync(pinned, counters.p + 1, 8, hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(pinned + 2, counters.p + 12, 16, hipMemcpyDeviceToHost, stream));
+        small_copy(pinned, counters.p + 1, 8);
+        small_copy(pinned + 2, counters.p + 12, 16);
         HIPCHK(hipStreamSynchronize(stream));
         uint64_t rb3[3];
         std::memcpy(rb3, pinned, 24);
@@ -1773,11 +1863,11 @@ struct Engine {
                        (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p);
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
-                       (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p);
+                       (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p);
                 if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);
             }
         }
-        HIPCHK(hipMemcpyAsync(pinned_stats, stats.p, kStatSlots * 8, hipMemcpyDeviceToHost, stream));
+        small_copy(pinned_stats, stats.p, kStatSlots * 8);
         HIPCHK(hipEventRecord(e1, stream));
         HIPCHK(hipStreamSynchronize(stream));
         {
@@ -1791,6 +1881,8 @@ struct Engine {
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];
+            st.text_chars = sv[ST_TEXT_CHARS];
+            st.text_rows = sv[ST_TEXT_ROWS];
             st.locate_offsets = sv[ST_LOC_OFFSETS];
             if (trace && sv[ST_CLK_STEPS])
                 std::fprintf(stderr, "[edsbwt] k_deep lane-steps %llu (with '#' rows %llu): cycles/step rank+link %.0f, runs %.0f, rest %.0f\n",
@@ -1844,9 +1936,10 @@ struct Engine {
     }
     void pipe_init() {
         if (up) return;
+        pool.start((unsigned)std::max(0.0, env_double("EDSBWT_HOST_THREADS", 12) - 1));
         HIPCHK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < kSlots; k++) {
             HIPCHK(hipEventCreateWithFlags(&up_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&comp_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&down_done[k], hipEventDisableTiming));
@@ -1867,24 +1960,169 @@ struct Engine {
     void arena_ensure(size_t n) {  // keep the records received so far (down stream synced)
         if (n <= arena_cap && arena) return;
         HIPCHK(hipStreamSynchronize(down));
+        std::lock_guard<std::mutex> g(arena_mx);
         const size_t c = std::max<size_t>({n, arena_cap + arena_cap / 2, (size_t)1 << 16});
         edsbwt_occ* q = nullptr;
         if (hipHostMalloc((void**)&q, c * sizeof(edsbwt_occ), hipHostMallocDefault) != hipSuccess)
             throw Fail(EDSBWT_E_NOMEM, "hipHostMalloc of the occurrence records failed");
         if (arena) {
-            par_copy(q, arena, arena_cap * sizeof(edsbwt_occ));
+            pool.parallel_copy(q, arena, arena_cap * sizeof(edsbwt_occ));
             arena_release();
         }
         arena = q;
         arena_cap = c;
+        arena_dev = nullptr;
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, arena, 0) == hipSuccess) arena_dev = static_cast<edsbwt_occ*>(d);
+        else (void)hipGetLastError();
         arena_register();
+    }
+    // compact downloads: per record only (word, offset) crosses PCIe; the host rebuilds
+    // (pat, word, segment, word in segment, offset) from the counts and the segment tables
+    std::vector<uint32_t> h_seg_of_word, h_seg_start;
+    DBuf<uint2> hrec8[kSlots];
+    uint2* arena8 = nullptr;  // page-locked landing area of the compact records
+    size_t arena8_cap = 0;
+    std::mutex arena_mx;      // arena / arena8 growth vs the expander thread
+    void arena8_ensure(size_t n) {
+        if (n <= arena8_cap && arena8) return;
+        HIPCHK(hipStreamSynchronize(down));
+        const size_t c = std::max<size_t>({n, arena8_cap + arena8_cap / 2, (size_t)1 << 16});
+        uint2* q = nullptr;
+        if (hipHostMalloc((void**)&q, c * sizeof(uint2), hipHostMallocDefault) != hipSuccess)
+            throw Fail(EDSBWT_E_NOMEM, "hipHostMalloc of the compact records failed");
+        std::lock_guard<std::mutex> g(arena_mx);
+        if (arena8) {
+            pool.parallel_copy(q, arena8, arena8_cap * sizeof(uint2));
+            (void)hipHostFree(arena8);
+        }
+        arena8 = q;
+        arena8_cap = c;
+    }
+    // a few persistent host threads (EDSBWT_HOST_THREADS, default 12) for staging copies and
+    // record expansion, so the pipeline never pays thread start-up per chunk
+    struct Pool {
+        std::vector<std::thread> th;
+        std::mutex m;
+        std::condition_variable cv, done_cv;
+        std::function<void(unsigned)> fn;
+        unsigned todo = 0, next = 0, running = 0;
+        uint64_t gen = 0;
+        bool stop = false;
+        unsigned size() const { return (unsigned)th.size() + 1; }
+        void start(unsigned n) {
+            for (unsigned i = 0; i < n; i++)
+                th.emplace_back([this] {
+                    uint64_t seen = 0;
+                    for (;;) {
+                        std::unique_lock<std::mutex> lk(m);
+                        cv.wait(lk, [&] { return stop || (gen != seen && next < todo); });
+                        if (stop) return;
+                        seen = gen;
+                        while (next < todo) {
+                            const unsigned t = next++;
+                            running++;
+                            lk.unlock();
+                            fn(t);
+                            lk.lock();
+                            running--;
+                        }
+                        done_cv.notify_all();
+                    }
+                });
+        }
+        // fn(t) for t < n on the pool and the calling thread; returns when all are done
+        void run(unsigned n, const std::function<void(unsigned)>& f) {
+            if (n <= 1 || th.empty()) { for (unsigned t = 0; t < n; t++) f(t); return; }
+            std::unique_lock<std::mutex> lk(m);
+            fn = f;
+            todo = n;
+            next = 0;
+            gen++;
+            cv.notify_all();
+            while (next < todo) {
+                const unsigned t = next++;
+                running++;
+                lk.unlock();
+                fn(t);
+                lk.lock();
+                running--;
+            }
+            done_cv.wait(lk, [&] { return running == 0; });
+            todo = 0;
+        }
+        void parallel_copy(void* dst, const void* src, size_t n) {
+            const size_t kPer = 4u << 20;
+            const unsigned T = (unsigned)std::min<size_t>(size(), std::max<size_t>(1, n / kPer));
+            run(T, [&](unsigned t) {
+                const size_t a = n * t / T, b = n * (t + 1) / T;
+                std::memcpy((char*)dst + a, (const char*)src + a, b - a);
+            });
+        }
+        ~Pool() {
+            {
+                std::lock_guard<std::mutex> g(m);
+                stop = true;
+            }
+            cv.notify_all();
+            for (auto& x : th) x.join();
+        }
+    } pool;
+    // expand one chunk's compact records: pattern ids from the counts, segment and word in
+    // segment from the segment tables (MOVE_EDSBWTSearch.cpp:361-363's rank1/select1)
+    void expand_chunk(const uint32_t* counts, uint64_t p0, uint64_t P, uint64_t r0, uint64_t n, uint32_t first_id) {
+        std::lock_guard<std::mutex> g(arena_mx);
+        const unsigned T = (unsigned)std::min<uint64_t>(pool.size(), std::max<uint64_t>(1, n / 32768));
+        std::vector<uint64_t> start(T + 1, 0);
+        pool.run(T, [&](unsigned t) {
+            uint64_t sum = 0;
+            for (uint64_t p = P * t / T; p < P * (t + 1) / T; p++) sum += counts[p0 + p];
+            start[t + 1] = sum;
+        });
+        for (unsigned t = 0; t < T; t++) start[t + 1] += start[t];
+        if (start[T] != n) throw Fail(EDSBWT_E_DEVICE, "record expansion: counts do not add up to the records");
+        const uint32_t* sow = h_seg_of_word.data();
+        const uint32_t* sst = h_seg_start.data();
+        pool.run(T, [&](unsigned t) {
+            uint64_t r = r0 + start[t];
+            for (uint64_t p = P * t / T; p < P * (t + 1) / T; p++) {
+                const uint32_t c = counts[p0 + p], pid = first_id + (uint32_t)(p0 + p);
+                for (uint32_t q = 0; q < c; q++, r++) {
+                    const uint2 v = arena8[r];
+                    const uint32_t sg = sow[v.x];
+                    arena[r] = edsbwt_occ{pid, v.x, sg, v.x - sst[sg], v.y};
+                }
+            }
+        });
+    }
+    edsbwt_occ* arena_dev = nullptr;  // the arena as the device sees it (kernel-written downloads)
+    // blocks of the download kernel: few, so its PCIe stores do not crowd out the search's memory traffic
+    size_t d2h_blocks = (size_t)std::max(1.0, env_double("EDSBWT_D2H_BLOCKS", 32));
+    // device view of page-locked caller memory (nullptr: not mapped)
+    static void* host_dev_ptr(void* p) {
+        void* d = nullptr;
+        if (!p || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+        return d;
+    }
+    // device -> mapped host memory by a kernel on `down`: the copy engines take the uploads, so the
+    // downloads go over PCIe as kernel stores and both directions stream at once
+    void download(void* dst_dev, const void* src, size_t bytes) {
+        if (!bytes) return;
+        const size_t n4 = bytes / 4;
+        const unsigned blocks = (unsigned)std::min<size_t>(d2h_blocks, (n4 + 255) / 256);
+        hipLaunchKernelGGL(k_copy_out, dim3(blocks), dim3(256), 0, down, (const uint32_t*)src, (uint32_t*)dst_dev, (uint64_t)n4);
+        HIPCHK(hipGetLastError());
     }
     void arena_register();
     void arena_release();
     void arena_checkout();
     bool arena_checked_out();
 
-    struct Chunk { uint64_t b0, b1, p0, p1; };  // byte range; pattern range (offsets mode)
+    struct Chunk { uint64_t b0, b1, p0, p1, dpos; };  // byte range; pattern range (offsets mode); device place (eager)
+    DBuf<uint8_t> hin_all;                // eager uploads: every chunk of the batch
+    DBuf<uint64_t> hoff_all;
+    std::vector<hipEvent_t> chunk_ev;     // ... and their completion
+    std::vector<hipEvent_t> chunk_down_ev;  // each chunk's downloads (compact records: the expander waits on them)
 
     // The pattern loop of MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:97-155) over a batch in host memory,
     // timed as SURVEY §8(d) defines patterns/s: from the first H2D of the patterns to the last
@@ -1898,40 +2136,148 @@ struct Engine {
         pipe_init();
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
         const bool pin_in = host_pinned(text), pin_off = lines || host_pinned(offs), pin_cnt = host_pinned(counts);
-        // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 64 MB), cut at line ends
-        const uint64_t target = (uint64_t)(env_double("EDSBWT_CHUNK_MB", 64) * 1048576.0);
+        // downloads by the copy engine (EDSBWT_D2H_KERNEL=1: kernel stores to mapped host memory;
+        // measured slower on MI355X: their PCIe stores slow the search kernels running beside them)
+        const bool sdma_down = env_double("EDSBWT_D2H_KERNEL", 0) == 0;
+        uint32_t* counts_dev = pin_cnt ? static_cast<uint32_t*>(host_dev_ptr(counts)) : nullptr;
+        // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 64 MB), cut at line ends; the
+        // first and last chunks ramp up from / down to 1/8 of that (EDSBWT_CHUNK_RAMP=0: uniform),
+        // so the pipeline fills and drains fast
+        const uint64_t target = std::max<uint64_t>(1, (uint64_t)(env_double("EDSBWT_CHUNK_MB", 64) * 1048576.0));
+        std::vector<uint64_t> sizes;
+        {
+            const bool ramp = env_double("EDSBWT_CHUNK_RAMP", 1) != 0;
+            const uint64_t steps[3] = {target / 8, target / 4, target / 2};
+            std::vector<uint64_t> front, back;
+            uint64_t covered = 0;
+            for (int i = 0; covered < len; i++) {
+                const uint64_t a = std::max<uint64_t>(1, ramp && i < 3 ? steps[i] : target);
+                front.push_back(a);
+                covered += a;
+                if (covered >= len) break;
+                back.push_back(a);
+                covered += a;
+            }
+            sizes = front;
+            sizes.insert(sizes.end(), back.rbegin(), back.rend());
+        }
         std::vector<Chunk> ch;
         if (lines) {
             uint64_t b = 0;
-            while (b < len) {
-                uint64_t e = std::min(len, b + std::max<uint64_t>(target, 1));
+            for (size_t q = 0; b < len; q++) {
+                uint64_t e = q + 1 < sizes.size() ? std::min(len, b + sizes[q]) : len;
                 if (e < len) {
                     const void* nl = std::memchr(text + e - 1, '\n', len - (e - 1));
                     e = nl ? (uint64_t)((const uint8_t*)nl - text) + 1 : len;
                 }
-                ch.push_back({b, e, 0, 0});
+                ch.push_back({b, e, 0, 0, 0});
                 b = e;
             }
         } else {
             if (npat && offs[0] != 0) throw Fail(EDSBWT_E_ARG, "pat_offsets[0] must be 0");
             uint64_t p = 0;
-            while (p < npat) {
+            for (size_t q = 0; p < npat; q++) {
                 // the chunk's last pattern: the first whose end passes the target
                 uint64_t lo = p + 1, hi = npat;
-                const uint64_t want = offs[p] + std::max<uint64_t>(target, 1);
+                const uint64_t want = q + 1 < sizes.size() ? offs[p] + sizes[q] : offs[npat];
                 while (lo < hi) { const uint64_t m = (lo + hi) / 2; if (offs[m] < want) lo = m + 1; else hi = m; }
-                ch.push_back({offs[p], offs[lo], p, lo});
+                ch.push_back({offs[p], offs[lo], p, lo, 0});
                 p = lo;
+            }
+        }
+        // page-locked inputs: every chunk's upload is queued at once, into its own 256-B aligned
+        // place of one device buffer, so the copy engine never idles; pageable inputs are staged
+        // through page-locked buffers slot by slot
+        // (EDSBWT_EAGER_UP=1; off by default: uploads and downloads share one copy engine, which then
+        // serves every upload before the first download)
+        const bool eager = pin_in && pin_off && env_double("EDSBWT_EAGER_UP", 0) != 0;
+        if (eager) {
+            uint64_t at = 0;
+            for (auto& c : ch) {
+                c.dpos = at;
+                at += (c.b1 - c.b0 + 16 + 255) / 256 * 256;
+            }
+            hin_all.ensure(at + 16);
+            if (!lines) hoff_all.ensure(npat + ch.size());
+            while (chunk_ev.size() < ch.size()) {
+                hipEvent_t e;
+                HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                chunk_ev.push_back(e);
             }
         }
         if (arena_checked_out()) arena_release();  // the caller still holds the last records: start a new buffer
         edsbwt_stats agg{};
         uint64_t total = 0, pats = 0, h2d = 0, d2h = 0;
+        // compact downloads: a host thread expands each chunk's records as soon as its download has landed
+        // (EDSBWT_D2H_COMPACT=1; off by default: on the MI355X host the expansion costs more than the
+        // smaller download saves)
+        const bool compact = locate && env_double("EDSBWT_D2H_COMPACT", 0) != 0 && !h_seg_of_word.empty();
+        while (chunk_down_ev.size() < ch.size()) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            chunk_down_ev.push_back(e);
+        }
+        struct XJob { uint64_t p0, P, r0, n; hipEvent_t ev; };
+        std::vector<XJob> xjobs;
+        std::mutex xm;
+        std::condition_variable xcv;
+        bool xclosed = false;
+        std::exception_ptr xerr;
+        std::thread xth;
+        auto xpost = [&](XJob j) {
+            if (!xth.joinable())
+                xth = std::thread([&] {
+                    for (size_t q = 0;; q++) {
+                        XJob jb;
+                        {
+                            std::unique_lock<std::mutex> lk(xm);
+                            xcv.wait(lk, [&] { return xclosed || q < xjobs.size(); });
+                            if (q >= xjobs.size()) return;
+                            jb = xjobs[q];
+                        }
+                        try {
+                            HIPCHK(hipEventSynchronize(jb.ev));
+                            const auto tx = std::chrono::steady_clock::now();
+                            expand_chunk(counts, jb.p0, jb.P, jb.r0, jb.n, first_id);
+                            if (trace)
+                                std::fprintf(stderr, "[edsbwt] expand chunk %zu: %llu records in %.3f ms, done at %.3f ms\n", q,
+                                             (unsigned long long)jb.n,
+                                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx).count(),
+                                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+                        } catch (...) {
+                            std::lock_guard<std::mutex> g(xm);
+                            if (!xerr) xerr = std::current_exception();
+                        }
+                    }
+                });
+            std::lock_guard<std::mutex> g(xm);
+            xjobs.push_back(j);
+            xcv.notify_all();
+        };
+        auto xfinish = [&] {
+            {
+                std::lock_guard<std::mutex> g(xm);
+                xclosed = true;
+            }
+            xcv.notify_all();
+            if (xth.joinable()) xth.join();
+            if (xerr) std::rethrow_exception(xerr);
+        };
         try {
         auto issue = [&](size_t k) {
             const Chunk& c = ch[k];
-            const int sl = (int)(k & 1);
+            const int sl = (int)(k % kSlots);
             const uint64_t nb = c.b1 - c.b0;
+            if (eager) {
+                if (nb) HIPCHK(hipMemcpyAsync(hin_all.p + c.dpos, text + c.b0, nb, hipMemcpyHostToDevice, up));
+                if (!lines) {
+                    HIPCHK(hipMemcpyAsync(hoff_all.p + c.p0 + k, offs + c.p0, (c.p1 - c.p0 + 1) * 8, hipMemcpyHostToDevice, up));
+                    h2d += (c.p1 - c.p0 + 1) * 8;
+                }
+                h2d += nb;
+                HIPCHK(hipEventRecord(chunk_ev[k], up));
+                return;
+            }
             if (lines) {
                 hraw[sl].ensure(nb + 16);
                 upload(hraw[sl].p, text + c.b0, nb, pin_in, stage_in[sl], sl);
@@ -1945,52 +2291,74 @@ struct Engine {
             h2d += nb;
             HIPCHK(hipEventRecord(up_done[sl], up));
         };
-        if (!ch.empty()) issue(0);
+        if (eager) {
+            for (size_t k = 0; k < ch.size(); k++) issue(k);
+        } else if (!ch.empty()) {
+            issue(0);
+        }
         for (size_t k = 0; k < ch.size(); k++) {
             const Chunk& c = ch[k];
-            const int sl = (int)(k & 1);
-            if (k + 1 < ch.size()) issue(k + 1);  // overlaps this chunk's search
-            HIPCHK(hipStreamWaitEvent(stream, up_done[sl], 0));
+            const int sl = (int)(k % kSlots);
+            if (!eager && k + 1 < ch.size()) issue(k + 1);  // overlaps this chunk's search
+            const auto tc = std::chrono::steady_clock::now();
+            HIPCHK(hipStreamWaitEvent(stream, eager ? chunk_ev[k] : up_done[sl], 0));
             HIPCHK(hipStreamWaitEvent(stream, down_done[sl], 0));  // chunk k-2's results have left the slot
             uint64_t P;
+            const uint8_t* bytes_k = nullptr;
+            uint64_t* offs_k = nullptr;
             if (lines) {  // the file's lines as a (bytes, offsets) batch
                 const uint64_t nb = c.b1 - c.b0;
                 const uint64_t nblk = (nb + kLineBlk - 1) / kLineBlk;
                 nlcnt.ensure(nblk + 1);
                 hbytes[sl].ensure(nb + 16);
-                launch_blocks(KC_TRIE, k_nl_count, nblk, (const uint8_t*)hraw[sl].p, nb, nlcnt.p);
+                const uint8_t* raw = eager ? hin_all.p + c.dpos : hraw[sl].p;
+                launch_blocks(KC_TRIE, k_nl_count, nblk, raw, nb, nlcnt.p);
                 const uint32_t nl = scan_u32(nlcnt.p, nlpre, nblk);
                 P = nl + ((nb && text[c.b1 - 1] != '\n') ? 1 : 0);
                 hoffs[sl].ensure(P + 1);
                 zero(hoffs[sl].p, 8);
-                launch_blocks(KC_TRIE, k_nl_compact, nblk, (const uint8_t*)hraw[sl].p, nb, (const uint32_t*)nlpre.p, hbytes[sl].p,
-                              hoffs[sl].p);
+                launch_blocks(KC_TRIE, k_nl_compact, nblk, raw, nb, (const uint32_t*)nlpre.p, hbytes[sl].p, hoffs[sl].p);
                 if (P > nl) {  // the last line has no '\n': it ends at the chunk's end
                     pinned_u64()[0] = nb - nl;
-                    HIPCHK(hipMemcpyAsync(hoffs[sl].p + P, pinned_u64(), 8, hipMemcpyHostToDevice, stream));
+                    small_copy(hoffs[sl].p + P, pinned_u64(), 8);
                     HIPCHK(hipStreamSynchronize(stream));
                 }
+                bytes_k = hbytes[sl].p;  // (after the ensure() calls above, which may move them)
+                offs_k = hoffs[sl].p;
             } else {
                 P = c.p1 - c.p0;
-                if (c.b0) launch(KC_TRIE, k_rebase, P + 1, hoffs[sl].p, P + 1, c.b0);
+                // the chunk's bytes and offsets: where the eager uploads put them, or the slot's
+                bytes_k = eager ? hin_all.p + c.dpos : hbytes[sl].p;
+                offs_k = eager ? hoff_all.p + c.p0 + k : hoffs[sl].p;
+                if (c.b0) launch(KC_TRIE, k_rebase, P + 1, offs_k, P + 1, c.b0);
             }
             if (pats + P > counts_cap) throw Fail(EDSBWT_E_ARG, "counts buffer holds " + std::to_string(counts_cap) + " patterns, the batch has more");
             hcounts[sl].ensure(P + 1);
             std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
             uint64_t n = 0;
             try {
-                n = search(hbytes[sl].p, hoffs[sl].p, P, first_id + (uint32_t)pats, flags, hcounts[sl].p);
+                n = search(bytes_k, offs_k, P, first_id + (uint32_t)pats, flags, hcounts[sl].p);
             } catch (...) {
                 std::swap(rec, hrec[sl]);
                 throw;
             }
             std::swap(rec, hrec[sl]);
+            if (compact && locate && n) {  // (word, offset) per record for the download
+                hrec8[sl].ensure(n);
+                launch(KC_LOCATE, k_rec_compact, n, (const edsbwt_occ*)hrec[sl].p, n, hrec8[sl].p);
+            }
             accumulate(agg, st);
+            if (trace)
+                std::fprintf(stderr, "[edsbwt] chunk %zu: %llu patterns, %llu records, search %.3f ms host / %.3f ms device, at %.3f ms\n", k,
+                             (unsigned long long)P, (unsigned long long)n, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count(),
+                             st.ms_total, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
             // results back on `down`
             HIPCHK(hipEventRecord(comp_done[sl], stream));
             HIPCHK(hipStreamWaitEvent(down, comp_done[sl], 0));
             if (P) {
-                if (pin_cnt) {
+                if (counts_dev && !sdma_down) {
+                    download(counts_dev + pats, hcounts[sl].p, P * 4);
+                } else if (pin_cnt) {
                     HIPCHK(hipMemcpyAsync(counts + pats, hcounts[sl].p, P * 4, hipMemcpyDeviceToHost, down));
                 } else {
                     HIPCHK(hipEventSynchronize(down_done[sl]));
@@ -2003,16 +2371,29 @@ struct Engine {
             }
             if (locate && n) {
                 arena_ensure(total + n);
-                HIPCHK(hipMemcpyAsync(arena + total, hrec[sl].p, n * sizeof(edsbwt_occ), hipMemcpyDeviceToHost, down));
-                d2h += n * sizeof(edsbwt_occ);
+                if (compact) {
+                    arena8_ensure(total + n);
+                    HIPCHK(hipMemcpyAsync(arena8 + total, hrec8[sl].p, n * sizeof(uint2), hipMemcpyDeviceToHost, down));
+                    d2h += n * sizeof(uint2);
+                } else {
+                    if (arena_dev && !sdma_down) download(arena_dev + total, hrec[sl].p, n * sizeof(edsbwt_occ));
+                    else HIPCHK(hipMemcpyAsync(arena + total, hrec[sl].p, n * sizeof(edsbwt_occ), hipMemcpyDeviceToHost, down));
+                    d2h += n * sizeof(edsbwt_occ);
+                }
             }
             HIPCHK(hipEventRecord(down_done[sl], down));
+            if (compact && locate && n) {
+                HIPCHK(hipEventRecord(chunk_down_ev[k], down));
+                xpost({pats, P, total, n, chunk_down_ev[k]});
+            }
             total += n;
             pats += P;
         }
+        xfinish();
         HIPCHK(hipStreamSynchronize(down));
         HIPCHK(hipStreamSynchronize(up));
         } catch (...) {  // no copy may still touch the caller's buffers
+            try { xfinish(); } catch (...) {}
             (void)hipStreamSynchronize(up);
             (void)hipStreamSynchronize(stream);
             (void)hipStreamSynchronize(down);
@@ -2056,13 +2437,17 @@ struct Engine {
         }
         a.locate_offsets += b.locate_offsets; a.search_groups = std::max(a.search_groups, b.search_groups);
         a.start_depth = std::max(a.start_depth, b.start_depth);
+        a.text_chars += b.text_chars; a.text_rows += b.text_rows;
     }
 
     ~Engine() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (up) (void)hipStreamSynchronize(up);
         if (down) (void)hipStreamSynchronize(down);
-        for (int k = 0; k < 2; k++) {
+        for (auto e : chunk_ev) (void)hipEventDestroy(e);
+        for (auto e : chunk_down_ev) (void)hipEventDestroy(e);
+        if (arena8) (void)hipHostFree(arena8);
+        for (int k = 0; k < kSlots; k++) {
             if (up_done[k]) (void)hipEventDestroy(up_done[k]);
             if (comp_done[k]) (void)hipEventDestroy(comp_done[k]);
             if (down_done[k]) (void)hipEventDestroy(down_done[k]);
@@ -2072,9 +2457,7 @@ struct Engine {
         if (down) (void)hipStreamDestroy(down);
         arena_release();
         for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
-        if (pinned) (void)hipHostFree(pinned);
-        if (pinned_big) (void)hipHostFree(pinned_big);
-        if (pinned_stats) (void)hipHostFree(pinned_stats);
+        if (hostblk) (void)hipHostFree(hostblk);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };

@@ -85,6 +85,15 @@ struct KIdx {
     uint32_t r3stride;         // rent3 entries per block ((sigma-1)^3)
     const uint32_t* PC3;       // first row of the suffixes c3 c2 c1 ... per rent3 entry
     uint32_t PC[kPairCodes + 3];  // first row of the suffixes c2 c1 ... for pair code p = (c1, c2)
+    // Text of the words (sigma - 1 <= 4, every row sampled): a single-row interval is one text
+    // position, so the next characters of the pattern are compared with the text instead of
+    // stepped through the rank entries ("single rows").
+    const uint64_t* rtext;     // nullptr: off.  2-bit symbol codes - 1 of the words' characters,
+                               // concatenated in word order and reversed, 32 per u64 (char i at bits 2(i%32))
+    uint64_t tlen;             // characters in the text
+    const uint32_t* gpos;      // [N] text position of row x's suffix (word start + offset)
+    const uint32_t* wrow;      // [W] row of each word's whole-word suffix (offset 0)
+    uint32_t text_deep;        // k_deep compares single rows too (EDSBWT_TEXT_DEEP, A/B)
 };
 
 }  // namespace edsbwt

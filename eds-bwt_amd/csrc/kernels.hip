@@ -238,6 +238,23 @@ __device__ __forceinline__ uint32_t rank2_any(const KIdx& X, uint32_t x0, uint32
 // cnt | kResRow: the pattern's one interval is [off, off + occ) itself, not in the archive
 // (the deep kernels' single-interval results: no archive write, no archive read in k_tasks)
 constexpr uint32_t kResRow = 0x80000000u;
+// cnt | kResRow | kResPos: the pattern's one occurrence is the text position itself (single-row
+// text compare, k_deep_fast): off = offset << 32 | word, occ = 1 — no row, no archive
+constexpr uint32_t kResPos = 0x40000000u;
+constexpr uint32_t kResCnt = 0x3FFFFFFFu;  // the interval count in cnt
+// a kResPos result carries the whole record: cnt = kResRow | kResPos | word-in-segment (< 2^30),
+// occ = segment; its occurrence count is 1
+__device__ __forceinline__ uint32_t res_occ(const Res& r) { return (r.cnt & kResPos) ? 1u : r.occ; }
+__device__ __forceinline__ uint32_t res_cnt(const Res& r) { return (r.cnt & kResPos) ? 1u : (r.cnt & kResCnt); }
+
+// 32 characters of the reversed text from reversed index r (bits 2j = character r + j)
+__device__ __forceinline__ uint64_t rtext_window(const uint64_t* __restrict__ rt, uint64_t r) {
+    const uint64_t q = r >> 5;
+    const uint32_t sh = (uint32_t)(r & 31u) * 2u;
+    const uint64_t a = rt[q];
+    if (!sh) return a;
+    return (a >> sh) | (rt[q + 1] << (64u - sh));
+}
 // rare per-pattern events (deep-kernel overflows): lst[0] counts, the pattern ids follow
 __device__ __forceinline__ void flag_push(uint32_t* __restrict__ lst, uint32_t i) { lst[1 + atomicAdd(lst, 1u)] = i; }
 __device__ __forceinline__ void put_res(Res* __restrict__ r, size_t o, uint64_t off, uint32_t cnt, uint32_t occ) {
@@ -272,7 +289,8 @@ constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards 
 // statistic slots (zeroed once per search, folded at its end)
 enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5,
                   ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10,
-                  ST_DEEP_PAIR_LINES = 11 };  // of ST_DEEP_BLOCKS, the rank-entry lines
+                  ST_DEEP_PAIR_LINES = 11,  // of ST_DEEP_BLOCKS, the rank-entry lines
+                  ST_TEXT_CHARS = 12, ST_TEXT_ROWS = 13 };  // characters decided / single rows met by the text compare
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -885,7 +903,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
                                                    uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1,
                                                    uint64_t* __restrict__ q2) {
-    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0;
+    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     if (q2) q2 += (size_t)sh * qcap;
@@ -932,6 +950,56 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             uint32_t d = D0;
             bool pair_skip = false;  // the pair entry just found '#' rows: take one step
             uint32_t tri_from = 0;   // no three-step attempt before this depth (one just failed)
+            bool posres = false;     // answered by the text compare: (word, offset) result written
+            if (X.rtext && b == e && d < L) {
+                // One row = one text position (word w, offset o): while no '#' row is met (o > 0)
+                // each backward step keeps one row and succeeds iff the text character before it
+                // equals the pattern's, so the next k = min(o, m) characters are decided by comparing
+                // them with the text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row)
+                const uint4 s = X.samples[b];
+                const uint32_t g = X.gpos[b];
+                n_blk += 3;
+                n_trow++;
+                const uint32_t m = L - d, k = min(s.y, m);
+                bool eq = true, valid_codes = true;
+                const uint64_t r0 = X.tlen - g;  // reversed index of the text character before row b's suffix
+                for (uint32_t j = 0; j < k && eq; j += 32) {
+                    const uint32_t n = min(32u, k - j);
+                    const uint64_t mask = n == 32 ? ~0ull : ((1ull << (2 * n)) - 1ull);
+                    uint64_t want = 0;
+                    if (pv) {
+                        want = (rem >> (2 * (d + j - D0))) & mask;  // the packed start's 2-bit digits (<= 16)
+                    } else {
+                        for (uint32_t t = 0; t < n; t++) {
+                            const uint32_t c = code_at(d + j + t);
+                            if (c == 0) { valid_codes = false; break; }  // '#' in the pattern: walk it
+                            if (c >= X.sigma) { eq = false; break; }      // outside the alphabet: no match
+                            want |= (uint64_t)(c - 1) << (2 * t);
+                        }
+                        if (!valid_codes || !eq) break;
+                    }
+                    eq = ((rtext_window(X.rtext, r0 + j) ^ want) & mask) == 0;
+                }
+                if (valid_codes) {
+                    if (!eq) {
+                        alive = false;
+                        d = L;
+                    } else if (s.y >= m) {
+                        if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
+                            posres = true;
+                            n_text += m;
+                            d = L;
+                            put_res(res, pv ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                        }
+                    } else {
+                        // the word's first o characters matched: go on from its whole-word row
+                        n_text += s.y;
+                        d += s.y;
+                        b = e = X.wrow[s.x];
+                        n_blk++;
+                    }
+                }
+            }
             for (; d < L; d++) {
                 const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
@@ -997,7 +1065,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             }
             if (want) {
                 w = make_uint4((uint32_t)i, d, b, e);
-            } else {
+            } else if (!posres) {
                 const uint32_t o = pv ? pi : perm[i];
                 const uint64_t at = abase + (uint64_t)i * K;
                 if (alive) put_res(res, o, b, 1u | kResRow, e - b + 1);
@@ -1014,6 +1082,8 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
     stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
     stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
     stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
+    stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
+    stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
 }
 
 // shard prefix sums of k_deep_fast's queue counters (one block)
@@ -1034,7 +1104,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2) {
-    unsigned long long n_steps = 0, n_hash = 0, n_blk = 0;  // n_blk: occ blocks read
+    unsigned long long n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0;  // n_blk: occ blocks read
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
@@ -1082,10 +1152,50 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             ce[0] = w.w;
         }
         SymReader<BPS> sym{k0, krest, P, pi};
-        bool over = false;
+        auto code_at = [&](uint32_t dd) -> uint32_t { return q2 ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };
+        bool over = false, posres = false;
         for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
-            const uint32_t code = q2 ? 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u) : sym.code(d);
+            if (X.rtext && X.text_deep && cn == 1 && cb[0] == ce[0]) {
+                // a single row: compare with the text as k_deep_fast does
+                const uint32_t x0 = cb[0];
+                const uint4 s = X.samples[x0];
+                const uint32_t g = X.gpos[x0];
+                n_blk += 3;
+                n_trow++;
+                const uint32_t m = L - d, k = min(s.y, m);
+                bool eq = true, valid_codes = true;
+                const uint64_t r0 = X.tlen - g;
+                for (uint32_t j = 0; j < k && eq && valid_codes; j += 32) {
+                    const uint32_t n = min(32u, k - j);
+                    const uint64_t mask = n == 32 ? ~0ull : ((1ull << (2 * n)) - 1ull);
+                    uint64_t want = 0;
+                    for (uint32_t t = 0; t < n; t++) {
+                        const uint32_t c = code_at(d + j + t);
+                        if (c == 0) { valid_codes = false; break; }
+                        if (c >= X.sigma) { eq = false; break; }
+                        want |= (uint64_t)(c - 1) << (2 * t);
+                    }
+                    if (valid_codes && eq) eq = ((rtext_window(X.rtext, r0 + j) ^ want) & mask) == 0;
+                }
+                if (valid_codes) {
+                    if (!eq) { cn = 0; break; }
+                    if (s.y >= m) {
+                        if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
+                            n_text += m;
+                            posres = true;
+                            put_res(res, q2 ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                            break;
+                        }
+                    } else {
+                        n_text += s.y;
+                        d += s.y;
+                        cb[0] = ce[0] = X.wrow[s.x];
+                        n_blk++;
+                    }
+                }
+            }
+            const uint32_t code = code_at(d);
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
@@ -1186,6 +1296,7 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
             DEEP_CLK_ADD(c_hsteps, rn ? 1 : 0);
         }
         if (over) { flag_push(ovf, (uint32_t)i); continue; }
+        if (posres) continue;
         // ascending rows (the input lists may be unordered sets)
 #pragma unroll
         for (int a = 0; a < K; a++)
@@ -1215,6 +1326,8 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
     stat_add(ctr, ST_DEEP_STEPS, n_steps, sh);
     stat_add(ctr, ST_DEEP_HASH, n_hash, sh);
     stat_add(ctr, ST_DEEP_BLOCKS, n_blk, sh);
+    stat_add(ctr, ST_TEXT_CHARS, n_text, sh);
+    stat_add(ctr, ST_TEXT_ROWS, n_trow, sh);
 #ifdef EDSBWT_DEEP_CLOCKS
     stat_add(ctr, ST_CLK_RANK, c_rank, sh);
     stat_add(ctr, ST_CLK_RUNS, c_runs, sh);
@@ -1716,15 +1829,16 @@ __global__ void k_finish(uint64_t P, uint32_t D, const uint32_t* __restrict__ sl
 
 // --------------------------------------------------------------- locate
 __global__ void k_u32_to_u64(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ b) { GRID_STRIDE(i, n) b[i] = a[i]; }
+__global__ void k_u32_of_u64(const uint64_t* __restrict__ a, uint64_t n, uint32_t* __restrict__ b) { GRID_STRIDE(i, n) b[i] = (uint32_t)a[i]; }
 // scan inputs of locate: occurrences and intervals per pattern
 __global__ void k_res_scan_in(const Res* __restrict__ res, uint64_t n, uint64_t* __restrict__ occ, uint64_t* __restrict__ cnt) {
     GRID_STRIDE(i, n) {
         const Res r = res[i];
         if (cnt) {
-            occ[i] = r.occ;
-            cnt[i] = r.cnt & ~kResRow;
+            occ[i] = res_occ(r);
+            cnt[i] = res_cnt(r);
         } else {  // one scan of both (the batch's totals stay below 2^32)
-            occ[i] = (uint64_t)r.occ << 32 | (r.cnt & ~kResRow);
+            occ[i] = (uint64_t)res_occ(r) << 32 | res_cnt(r);
         }
     }
 }
@@ -1745,11 +1859,12 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
         const uint64_t t0 = tscan ? tscan[i] : (ps & 0xffffffffull);
         const Res r = res[i];
         const bool direct_row = (r.cnt & kResRow) != 0;
-        const uint32_t n = r.cnt & ~kResRow;
+        const uint32_t n = res_cnt(r);
         for (uint32_t q = 0; q < n; q++) {
             const uint64_t a = r.off + q;
-            const uint32_t row = direct_row ? (uint32_t)r.off : ab[a];
-            const uint64_t len = direct_row ? (uint64_t)r.occ : (uint64_t)(ae[a] - row) + 1;
+            // a text-position result has no row: k_locate takes (word, offset) from res
+            const uint32_t row = (r.cnt & kResPos) ? ~0u : direct_row ? (uint32_t)r.off : ab[a];
+            const uint64_t len = direct_row ? (uint64_t)res_occ(r) : (uint64_t)(ae[a] - row) + 1;
             trow[t0 + q] = row;
             tout[t0 + q] = base;
             tpat[t0 + q] = (uint32_t)i;
@@ -1768,7 +1883,8 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
 // tasks (at most kLocRun + 1, from blk_first) are staged in LDS
 __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
                                                 const uint32_t* __restrict__ tpat, const uint64_t* __restrict__ blk_first, uint32_t first_id,
-                                                KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
+                                                KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats,
+                                                const Res* __restrict__ res) {
     unsigned long long my_steps = 0, my_off = 0;
     __shared__ uint64_t s_out[kLocRun + 1];
     __shared__ uint32_t s_row[kLocRun + 1], s_pat[kLocRun + 1];
@@ -1790,8 +1906,22 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
             if (s_out[mid] <= o) lo = mid; else hi = mid;
         }
         const uint32_t pat = s_pat[lo];
-        uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
         uint32_t word, off;
+        if (s_row[lo] == ~0u) {  // text-position result (kResPos): (word, offset) from the pattern's result
+            const Res rr = res[pat];
+            word = (uint32_t)rr.off;
+            off = (uint32_t)(rr.off >> 32);
+            my_off += off;
+            edsbwt_occ r;
+            r.pat = first_id + pat;
+            r.word = word;
+            r.seg = rr.occ;
+            r.word_in_seg = rr.cnt & kResCnt;
+            r.offset = off;
+            rec[o] = r;
+            continue;
+        }
+        uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
         if (mode == 2 && X.samp_dense) {  // every row sampled: the record straight from row x's sample
             const uint4 s = X.samples[x];
             my_off += s.y;
@@ -2125,6 +2255,26 @@ __global__ void k_table_walk(uint32_t W, KIdx X, uint32_t* __restrict__ da, uint
 __global__ void k_table_finish(uint32_t N, const uint32_t* __restrict__ da, const uint32_t* __restrict__ wlen, uint32_t* __restrict__ off) {
     GRID_STRIDE(x, N) off[x] = wlen[da[x]] - off[x];
 }
+// text of the words from the per-row table (index open): row x is position (w, o) = (da[x],
+// offt[x]); gpos[x] = wstart[w] + o; L[x] is the character at (w, o - 1) when o > 0, stored
+// at reversed index tlen - gpos[x]; the row with o = 0 is the word's whole-word suffix
+__global__ void k_text_build(uint32_t N, KIdx X, const uint32_t* __restrict__ da, const uint32_t* __restrict__ offt,
+                             const uint32_t* __restrict__ wstart, uint64_t tlen, uint32_t* __restrict__ gpos,
+                             uint32_t* __restrict__ wrow, uint32_t* __restrict__ rt32) {
+    GRID_STRIDE(x, N) {
+        const uint32_t w = da[x], o = offt[x];
+        const uint32_t g = wstart[w] + o;
+        gpos[x] = g;
+        if (o == 0) {
+            wrow[w] = (uint32_t)x;
+        } else {
+            uint32_t rk;
+            const uint32_t c = sym_rank(X.occ, (uint32_t)x, &rk);
+            const uint64_t r = tlen - g;
+            atomicOr(rt32 + (r >> 4), (uint32_t)((c - 1u) & 3u) << (2u * (uint32_t)(r & 15u)));
+        }
+    }
+}
 
 // launched with a small grid (kReduceBlocks): one atomic per block
 __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
@@ -2135,11 +2285,12 @@ __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res
     unsigned long long f = 0, so = 0, st = 0;
     GRID_STRIDE(i, P) {
         const Res r = res[i];
-        counts[i] = r.occ;  // backwardSearch's return value per pattern
-        if (scan_in) scan_in[i] = (uint64_t)r.occ << 32 | (r.cnt & ~kResRow);
-        f += r.occ > 0;
-        so += r.occ;
-        st += r.cnt & ~kResRow;
+        const uint32_t oc = res_occ(r);
+        counts[i] = oc;  // backwardSearch's return value per pattern
+        if (scan_in) scan_in[i] = (uint64_t)oc << 32 | res_cnt(r);
+        f += oc > 0;
+        so += oc;
+        st += res_cnt(r);
     }
     f = block_sum(f, sh);
     so = block_sum(so, sh);
@@ -2330,6 +2481,21 @@ __global__ void __launch_bounds__(256) k_ktab_emit(uint32_t M, const uint32_t* _
 // 256 threads, 16 per thread: k_nl_count counts each block's '\n', a scan gives the
 // newlines before each block, k_nl_compact moves the bytes and writes line ends.
 constexpr uint32_t kLineBlk = 4096;
+// small host<->device transfers on the engine stream (engine.hip small_copy)
+__global__ void k_copy_words(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+// downloads of the host pipeline: device -> mapped page-locked host memory as kernel stores
+__global__ void __launch_bounds__(256) k_copy_out(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+// compact download of a chunk's records: (word, offset); the host restores the rest
+__global__ void k_rec_compact(const edsbwt_occ* __restrict__ rec, uint64_t n, uint2* __restrict__ out) {
+    GRID_STRIDE(i, n) {
+        const edsbwt_occ r = rec[i];
+        out[i] = make_uint2(r.word, r.offset);
+    }
+}
 // offsets of a chunk of a packed batch, rebased to its first byte
 __global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) { GRID_STRIDE(i, n) off[i] -= base; }
 __global__ void __launch_bounds__(256) k_nl_count(const uint8_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ cnt) {

@@ -59,6 +59,8 @@ enum {
                                     start straight from its k-mer table list (tests: same results) */
 #define EDSBWT_NO_PAIRS     0x1000u/* deep walk one character per rank line instead of two from the
                                     pair blocks (sigma <= 5; tests: same results) */
+#define EDSBWT_NO_TEXT      0x2000u/* step single-row intervals through the rank entries instead of
+                                    comparing the pattern with the words' text (tests: same results) */
 
 typedef struct edsbwt_index edsbwt_index;
 
@@ -111,6 +113,8 @@ typedef struct {
                                  D2H of counts and records (SURVEY.md §8(d)'s patterns/s clock) */
     uint64_t chunks;          /* chunks the batch was cut into (uploads overlap searches) */
     uint64_t bytes_h2d, bytes_d2h;
+    uint64_t text_chars;      /* pattern characters decided by the single-row text compare */
+    uint64_t text_rows;       /* single-row intervals the text compare met */
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,

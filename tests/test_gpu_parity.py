@@ -57,6 +57,8 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         assert np.array_equal(gt, oc) and np.array_equal(got, oo)
         gp, gop = idx.search((buf, offs), pairs=False)   # one character per rank line in k_deep_fast
         assert np.array_equal(gp, oc) and np.array_equal(gop, oo)
+        gx, gox = idx.search((buf, offs), text=False)    # single rows stepped, not compared with the text
+        assert np.array_equal(gx, oc) and np.array_equal(gox, oo)
         for deep in (True, False):                       # reference-ordered lists at every depth
             gc5, go5 = idx.search((buf, offs), ordered=True, deep=deep)
             assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
@@ -401,10 +403,48 @@ def test_packed_direct_start_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         with edsbwt.Index(base) as idx:
             gc, go = idx.search((buf, offs))
             assert idx.stats()["start_depth"] == D0 and idx.stats()["trie_nodes"] == 0  # direct start
+            assert idx.stats()["text_rows"] > 0  # single rows compared with the text
             assert np.array_equal(gc, oc) and np.array_equal(go, oo)
             got[packed] = (gc, go)
             gp, gop = idx.search((buf, offs), pairs=False)
             assert np.array_equal(gp, oc) and np.array_equal(gop, oo)
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, direct):
+    """Single-row intervals decided by comparing the pattern with the words' text: patterns
+    ending inside a word, crossing into earlier segments (the compare stops at the word start
+    and the walk goes on from the whole-word row), mismatching before or after the jump, with
+    bytes outside the alphabet; count-only and locate; identical to the oracle and to the walk
+    with the text compare off, and the compare really ran."""
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
+    rng = random.Random(7331)
+    segs = _covid_like(rng, 700)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(3000)]
+    pats += [edsgen.planted(rng, segs, rng.randint(D0 + 17, D0 + 60)) or "ACGT" * 20 for _ in range(1000)]
+    pats += [p[:-3] + rng.choice("ACGT") + p[-2:] for p in pats[:500]]       # a mismatch near the end
+    pats += [rng.choice("ACGT") + p[1:] for p in pats[500:1000]]            # ... at the start
+    pats += [p[:5] + "N" + p[6:] for p in pats[1000:1100]]                  # outside the alphabet
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        for locate in (True, False):
+            gc, go = idx.search((buf, offs), direct=direct, locate=locate)
+            st = idx.stats()
+            assert np.array_equal(gc, oc)
+            if locate:
+                assert np.array_equal(go, oo)
+                assert st["locate_offsets"] == int(oo["offset"].astype(np.uint64).sum())
+            assert st["text_rows"] > 1000 and st["text_chars"] > 10000, st
+            gc2, go2 = idx.search((buf, offs), direct=direct, locate=locate, text=False)
+            assert np.array_equal(gc2, oc) and idx.stats()["text_rows"] == 0
+            if locate:
+                assert np.array_equal(go2, oo)
 
 
 def test_split_locate_scans_gpu(oracle, edsbwt, tmp_path, monkeypatch):
