@@ -42,7 +42,7 @@ MI355X_MALL_BYTES = 256 << 20  # Infinity Cache: index tables smaller than this 
 # Practical ceilings of the deep kernels' access shape on MI355X (tools/calib_gather.hip,
 # profiles/r02_calib_gather.json): one random 16-B rank entry per lane per step from a
 # table of the C3 rank entries' size, issued as the kernel issues them.
-CALIB = os.path.join(ROOT, "profiles", "calib_gather.json")
+CALIB = os.path.join(ROOT, "profiles", "r02_calib_chain.json")
 
 
 def log(*a):
@@ -71,9 +71,14 @@ def traffic_from_profile(cfg: str, kernel: str):
 
 
 def gather_ceiling():
+    """Line-rate ceiling of the deep walk's own access shape: chain2 = each lane walks
+    dependent steps of two random 16-B rank-entry loads (one per interval end), several
+    patterns per lane in flight, from a 1 GB table (the C3 rent2 entries' size)."""
     try:
-        c = json.load(open(CALIB))
-        return float(c["ceiling_lines_per_s"]), c.get("shape", "")
+        rows = [json.loads(x) for x in open(CALIB) if x.strip()]
+        best = max((r for r in rows if r["shape"].startswith("chain2") and r["table_MB"] >= 1024),
+                   key=lambda r: r["lines_per_s"])
+        return float(best["lines_per_s"]), f"{best['shape']} over {best['table_MB']} MB ({os.path.basename(CALIB)})"
     except (OSError, KeyError, ValueError):
         return None, None
 

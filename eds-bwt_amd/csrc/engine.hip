@@ -393,6 +393,11 @@ struct Engine {
     // ------------------------------------------------------------ helpers
     static unsigned grid_for(size_t n) { return (unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 16384)); }
 
+    // timing events of an attempt that will not be reported go back to the pool
+    void discard_attempt() {
+        for (auto& e : evs) ev_pool.push_back(e);
+        evs.clear();
+    }
     Ev ev_get(int k) {
         Ev e;
         if (!ev_pool.empty()) { e = ev_pool.back(); ev_pool.pop_back(); }
@@ -1799,10 +1804,20 @@ struct Engine {
         if (use_table) build_table();
         st.patterns = P;
         if (P == 0) return 0;
-        hipEvent_t e0, e1;
-        HIPCHK(hipEventCreate(&e0));
-        HIPCHK(hipEventCreate(&e1));
+        struct EvPair {  // released on every exit, including exceptions
+            hipEvent_t a = nullptr, b = nullptr;
+            ~EvPair() { if (a) (void)hipEventDestroy(a); if (b) (void)hipEventDestroy(b); }
+        } ep;
+        HIPCHK(hipEventCreate(&ep.a));
+        HIPCHK(hipEventCreate(&ep.b));
+        hipEvent_t e0 = ep.a, e1 = ep.b;
         HIPCHK(hipEventRecord(e0, stream));
+        // a search that throws leaves no timing events behind for the next call
+        struct EvRecycle {
+            Engine* E;
+            bool done = false;
+            ~EvRecycle() { if (!done) E->discard_attempt(); }
+        } recycle{this};
         const KIdx X = kidx();
         res.ensure(P);
         zero(res.p, P * sizeof(Res));
@@ -1821,6 +1836,13 @@ struct Engine {
             // later batches on this index start grouped (sticky_groups)
             for (uint32_t k = std::max(2u, sticky_groups + 1);; k++) {
                 try {
+                    // the failed attempt's counters and timings are not this search's
+                    discard_attempt();
+                    st = edsbwt_stats{};
+                    st.patterns = P;
+                    zero(res.p, P * sizeof(Res));
+                    zero(stats.p, kStatSlots * 8);
+                    abase = 0;
                     run_grouped(d_bytes, d_off, P, allow_deep, ordered, k, abase);
                     sticky_groups = k;
                     break;
@@ -1899,8 +1921,7 @@ struct Engine {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         st.ms_total = ms;
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        recycle.done = true;
         if (prof) {
             for (auto& e : evs) {
                 float t = 0;
