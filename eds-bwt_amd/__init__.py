@@ -70,7 +70,8 @@ class _Stats(ctypes.Structure):
                 ("locate_offsets", ctypes.c_uint64),
                 ("search_groups", ctypes.c_uint64), ("start_depth", ctypes.c_uint64),
                 ("ms_wall", ctypes.c_double), ("chunks", ctypes.c_uint64), ("bytes_h2d", ctypes.c_uint64),
-                ("bytes_d2h", ctypes.c_uint64), ("text_chars", ctypes.c_uint64), ("text_rows", ctypes.c_uint64)]
+                ("bytes_d2h", ctypes.c_uint64), ("text_chars", ctypes.c_uint64), ("text_rows", ctypes.c_uint64),
+                ("redo_searches", ctypes.c_uint64)]
 
 
 _LIB = None

@@ -196,6 +196,10 @@ struct Engine {
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
     int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 20);  // ... by the D-mer's leading bits (C3 A/B: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9)
     DBuf<uint64_t> pv_in, pv_out;
+    DBuf<uint32_t> bhist, bscan;  // direct start buckets (k_keys histogram, its scan / scatter cursors)
+    // (measured on C3, 10M patterns: k_keys' histogram atomics +0.2 ms and the scatter 0.69 ms
+    // against 0.34 ms for the radix sort: off by default)
+    bool use_buckets = env_double("EDSBWT_BUCKETS", 0) != 0;
     bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     DBuf<uint64_t> ktab_one;  // per D-mer: its one interval inline, else list length and offset (k_ktab_one)
@@ -297,8 +301,17 @@ struct Engine {
     // is uploaded on `up` while chunk k is searched on `stream` and chunk k-1's counts and
     // records go back on `down` (two device slots per buffer, events between the streams)
     hipStream_t up = nullptr, down = nullptr;
-    static constexpr int kSlots = 3;  // chunk k's search never waits for chunk k-2's download
-    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {};
+    // chunk k reuses chunk k-kSlots's device buffers, so its search waits for that chunk's
+    // download: five slots keep the searches clear of a download backlog
+    static constexpr int kSlots = 5;
+    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {}, prep_done[kSlots] = {};
+    // per-slot prep on `up` after each upload: the chunk's lines split (lines mode) or its offsets
+    // rebased, and its pattern count and longest / shortest pattern measured, so the search
+    // itself reads nothing back before its final check
+    DBuf<uint32_t> nlcnt_s[kSlots], nlpre_s[kSlots];
+    DBuf<uint8_t> ptmp[kSlots];
+    DBuf<unsigned long long> prep_mm[kSlots];
+    uint32_t* prep_host(int sl) { return pinned + 64 + 8 * sl; }  // P, max, ~min as u64 (in hostblk)
     DBuf<uint8_t> hraw[kSlots], hbytes[kSlots];
     DBuf<uint64_t> hoffs[kSlots];
     DBuf<uint32_t> hcounts[kSlots], nlcnt, nlpre;
@@ -346,8 +359,40 @@ struct Engine {
     }  // EDSBWT_NO_WIDE (tests): overflowed deep patterns go straight to the level path
     uint32_t prof_mask = ~0u;  // kernel classes timed with events when profiling
     bool trace = std::getenv("EDSBWT_TRACE") != nullptr;
+    // EDSBWT_TRACE=2: host time of every launch inside a search (what the host spends per call)
+    bool trace2 = env_double("EDSBWT_TRACE", 0) >= 2;
+    std::chrono::steady_clock::time_point t_search0;
+    void hmark(const char* what) {
+        if (trace2)
+            std::fprintf(stderr, "[edsbwt]   +%7.1f us %s\n",
+                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_search0).count(), what);
+    }
+    void hmark_kern(const void* kern) {
+        if (!trace2) return;
+        Dl_info di{};
+        hmark(kern && dladdr(kern, &di) && di.dli_sname ? di.dli_sname : "?");
+    }
     struct Ev { int k; hipEvent_t a, b; };
     std::vector<Ev> evs, ev_pool;
+    // deferred checks (direct start): the search runs without read-backs between its stages;
+    // what they decided ('#' in a pattern, overflow lists, record totals) is read once at the
+    // end, and a batch that fails a check is searched again on the checked path
+    bool defer_ok = env_double("EDSBWT_NO_DEFER", 0) == 0;  // per call (cleared for a redo)
+    bool defer = false;                                      // the current search deferred its checks
+    bool defer_call = false;                                 // ... may defer them (set by search())
+    static constexpr uint32_t kFlagNoDefer = 0x80000000u;    // internal flag: the checked path
+    uint32_t defer_wide_cap = 0;
+    const uint32_t* defer_ovf2 = nullptr;
+    static constexpr uint32_t kWideCap = 16384;  // k_deep_wide lanes launched without a count read-back
+    uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
+    uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
+    // pinned + 32..: the deferred checks' landing slots (u32 words)
+    static constexpr uint32_t kChkTerm = 0, kChkOvf = 2, kChkOvf2 = 3, kChkOflow = 4, kChkFound = 6, kChkSums = 8;
+    uint32_t* chk() { return pinned + 32; }
+    double occ_per_pat = 0, tasks_per_pat = 0;  // record and task rates seen so far (deferred buffer sizing)
+    // lengths of the batch's patterns measured by the caller (host pipeline prep): no k_lminmax read-back
+    bool known_len = false;
+    uint32_t known_lmin = 0, known_lmax = 0;
 
     // bits needed for values 0..v
     static uint32_t bits_for(uint64_t v) {
@@ -420,6 +465,7 @@ struct Engine {
     void launch_reduce(int k, K kern, A... a) {
         timed(k, [&] { hipLaunchKernelGGL(kern, dim3(kReduceBlocks), dim3(256), 0, stream, a...); });
         HIPCHK(hipGetLastError());
+        hmark_kern((const void*)kern);
         sync_check((const void*)kern);
         st.launches_kernel[k]++;
     }
@@ -428,6 +474,7 @@ struct Engine {
         if (!n) return;
         timed(k, [&] { hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(256), 0, stream, a...); });
         HIPCHK(hipGetLastError());
+        hmark_kern((const void*)kern);
         sync_check((const void*)kern);
         st.launches_kernel[k]++;
     }
@@ -454,17 +501,44 @@ struct Engine {
         std::memcpy(&v, pinned, 8);
         return v;
     }
-    void zero(void* p, size_t bytes) { if (bytes) HIPCHK(hipMemsetAsync(p, 0, bytes, stream)); }
+    // zeroing by our own kernel: hipMemsetAsync's fill kernel ran at PCIe-like rates beside the
+    // host pipeline's download blits (0.4-0.7 ms for a 32 MB result array)
+    void zero(void* p, size_t bytes) { zero_on(p, bytes, stream); }
+    // several (4-B multiple) ranges in one launch
+    void zero_many(std::initializer_list<std::pair<void*, size_t>> rs) {
+        ZeroSet z{};
+        uint32_t n = 0;
+        uint64_t mx = 0;
+        for (auto& r : rs) {
+            if (!r.second) continue;
+            if (n == 8) throw Fail(EDSBWT_E_ARG, "zero_many: more than 8 ranges");
+            z.p[n] = static_cast<uint32_t*>(r.first);
+            z.n4[n] = r.second / 4;
+            mx = std::max<uint64_t>(mx, z.n4[n]);
+            n++;
+        }
+        if (!n) return;
+        const unsigned gx = (unsigned)std::min<uint64_t>(1024, std::max<uint64_t>(1, (mx + 1023) / 1024));
+        hipLaunchKernelGGL(k_zero_multi, dim3(gx, n), dim3(256), 0, stream, z);
+        HIPCHK(hipGetLastError());
+    }
+    static void zero_on(void* p, size_t bytes, hipStream_t s) {
+        if (!bytes) return;
+        const unsigned g = (unsigned)std::min<size_t>(2048, std::max<size_t>(1, (bytes / 16 + 255) / 256));
+        hipLaunchKernelGGL(k_zero_bytes, dim3(g), dim3(256), 0, s, (uint8_t*)p, (uint64_t)bytes);
+        HIPCHK(hipGetLastError());
+    }
     // small transfer on the engine stream by a kernel (see hostblk); host pointers must lie in hostblk
     const void* dev_alias(const void* p) const {
         const uint8_t* q = static_cast<const uint8_t*>(p);
         return (q >= hostblk && q < hostblk + hostblk_size) ? hostblk_dev + (q - hostblk) : p;
     }
-    void small_copy(void* dst, const void* src, size_t bytes) {
+    void small_copy(void* dst, const void* src, size_t bytes) { small_copy_on(dst, src, bytes, stream); }
+    void small_copy_on(void* dst, const void* src, size_t bytes, hipStream_t s) {
         if (!bytes) return;
         if (bytes % 4) throw Fail(EDSBWT_E_ARG, "small_copy of a size that is not a multiple of 4");
         const uint32_t n = (uint32_t)(bytes / 4);
-        hipLaunchKernelGGL(k_copy_words, dim3(std::min<uint32_t>(64, (n + 255) / 256)), dim3(256), 0, stream,
+        hipLaunchKernelGGL(k_copy_words, dim3(std::min<uint32_t>(64, (n + 255) / 256)), dim3(256), 0, s,
                            (const uint32_t*)dev_alias(src), (uint32_t*)const_cast<void*>(dev_alias(dst)), n);
         HIPCHK(hipGetLastError());
     }
@@ -573,9 +647,9 @@ struct Engine {
     }
 
     // out[0..n] = exclusive prefix sum (out[0] = 0, out[n] = total), no read-back
-    void inclusive_scan_u64(const uint64_t* in, DBuf<uint64_t>& out, size_t n) {
+    void inclusive_scan_u64(const uint64_t* in, DBuf<uint64_t>& out, size_t n, bool zero_first = true) {
         out.ensure(n + 1);
-        zero(out.p, 8);
+        if (zero_first) zero(out.p, 8);
         if (!n) return;
         if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
         size_t tb = 0;
@@ -619,7 +693,7 @@ struct Engine {
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         {
-            const size_t a = 256, big = ((kCnt + 2 * (NSHARD + 8)) * 4 + 255) / 256 * 256, stb = kStatSlots * 8;
+            const size_t a = 512, big = ((kCnt + 2 * (NSHARD + 8)) * 4 + 255) / 256 * 256, stb = kStatSlots * 8;
             hostblk_size = a + big + stb + kStageBytes;
             HIPCHK(hipHostMalloc((void**)&hostblk, hostblk_size, hipHostMallocMapped | hipHostMallocCoherent));
             HIPCHK(hipHostGetDevicePointer((void**)&hostblk_dev, hostblk, 0));
@@ -731,7 +805,7 @@ struct Engine {
         up(seg_lo, slo);
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
-        counters.ensure(16);
+        counters.ensure(32);
         {  // segment link table (k_deep)
             const KIdx X0 = kidx();
             segtab.ensure((size_t)(S + 2) * X0.seg_stride);
@@ -1003,10 +1077,10 @@ struct Engine {
         keys.ensure((size_t)nch * P);
         if (bps == 3)
             launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, 0u, 0u,
-                   (uint32_t*)nullptr, (uint64_t*)nullptr);
+                   (uint32_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr, 0u);
         else
             launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, 0u, 0u,
-                   (uint32_t*)nullptr, (uint64_t*)nullptr);
+                   (uint32_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr, 0u);
         perm.ensure(P);
         perm2.ensure(P);
         kc.ensure(P);
@@ -1256,7 +1330,7 @@ struct Engine {
         const uint32_t D = d + 1;
         DBuf<uint32_t>& ovf = tflag;  // flag_push list of sorted patterns k_deep could not hold
         ovf.ensure(P + 1);
-        zero(ovf.p, 4);
+        if (!defer) zero(ovf.p, 4);
         const uint32_t K = deep_k;
         ab.grow_keep(abase + (uint64_t)P * K, stream);
         ae.grow_keep(abase + (uint64_t)P * K, stream);
@@ -1266,7 +1340,7 @@ struct Engine {
         if (pv) dq2.ensure(qcap * NSHARD);
         dqpre.ensure(NSHARD + 1);
         lcnt.ensure(NSHARD * 32 + 32);
-        zero(lcnt.p, NSHARD * 32 * 4);
+        if (!defer) zero(lcnt.p, NSHARD * 32 * 4);
         // the patterns' remaining symbols come from the sorted key chunks (chunk 0, then skey)
         if (!k0) {
             k0 = sorted_chunk(1, P);
@@ -1292,6 +1366,25 @@ struct Engine {
                          read_u32(dqpre.p + NSHARD));
         st.bytes_kernel[KC_DEEP] += (uint64_t)P * 24;  // + interval steps and '#' rows, folded at the end of search()
         // lists that outgrew k_deep's registers: retry those patterns with wide lists
+        if (defer) {
+            // no read-back: k_deep_wide takes the list's length from the device, up to
+            // kWideCap patterns; a longer list, or any pattern the wide lists cannot hold
+            // either, fails search()'s final check and the batch is searched again
+            DBuf<uint32_t>& ovf2 = hcnt;
+            const uint32_t wcap = (uint32_t)std::min<uint64_t>(P, wide_cap);
+            ovf2.ensure((size_t)wcap + 1);  // (count zeroed by search())
+            if (!no_wide) {
+                ab.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
+                ae.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
+                launch(KC_DEEP, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
+                       d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
+                       (const uint32_t*)ovf.p);
+                abase += (uint64_t)wcap * kDeepWide;
+            }
+            defer_ovf2 = no_wide ? ovf.p : ovf2.p;  // gathered by finish_deferred
+            defer_wide_cap = no_wide ? 0 : wcap;
+            return 0;
+        }
         const uint32_t nw = read_u32(ovf.p);
         uint32_t novf = nw;
         const uint32_t* list = ovf.p + 1;
@@ -1302,7 +1395,8 @@ struct Engine {
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
-                   d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p);
+                   d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
+                   (const uint32_t*)nullptr);
             abase += (uint64_t)nw * kDeepWide;
             st.deep_overflow += nw;
             novf = read_u32(ovf2.p);
@@ -1325,18 +1419,33 @@ struct Engine {
     // kNotDirect when the batch does not qualify (nothing was written), kNeedOrdered for
     // patterns holding '#', else k_deep's overflow count as run_deep.
     static constexpr uint32_t kNotDirect = 0xFFFFFFFEu;
+    // buckets of the direct start's grouping (0: the radix sort path or no direct start)
+    uint64_t direct_buckets() const {
+        if (!ktab_depth || !use_buckets || direct_sort_bits <= 0) return 0;
+        const uint64_t E = ktab_entries;
+        const int shift = std::max(0, (int)bits_for(E) - direct_sort_bits);
+        const uint64_t nb = (E >> shift) + 1;
+        return nb <= (1u << 22) ? nb : 0;
+    }
     uint32_t direct(const uint64_t* d_off, const uint8_t* d_bytes, uint64_t P, Res* r,
                     uint64_t& abase, uint32_t* ovf_orig) {
         if (cap || !use_ktab || !use_direct || !ktab_depth || (double)ktab_items > direct_items * (double)ktab_entries) return kNotDirect;
         if (P > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^31 patterns in one call");
         const uint32_t D0 = ktab_depth;
-        zero(counters.p + 8, 24);
-        launch_reduce(KC_TRIE, k_lminmax, d_off, P, counters.p + 8);
-        small_copy(pinned, counters.p + 8, 16);
-        HIPCHK(hipStreamSynchronize(stream));
-        uint64_t mm[2];
-        std::memcpy(mm, pinned, 16);
-        const uint32_t Lmax = (uint32_t)mm[0], Lmin = ~(uint32_t)mm[1];
+        if (!defer_call) zero(counters.p + 8, 24);
+        uint32_t Lmax, Lmin;
+        if (known_len) {  // the host pipeline measured the chunk's lines beside the previous search
+            Lmax = known_lmax;
+            Lmin = known_lmin;
+        } else {
+            launch_reduce(KC_TRIE, k_lminmax, d_off, P, counters.p + 8);
+            small_copy(pinned, counters.p + 8, 16);
+            HIPCHK(hipStreamSynchronize(stream));
+            uint64_t mm[2];
+            std::memcpy(mm, pinned, 16);
+            Lmax = (uint32_t)mm[0];
+            Lmin = ~(uint32_t)mm[1];
+        }
         if (Lmin <= D0) return kNotDirect;
         bps = sigma + 2 <= 8 ? 3u : 4u;
         const uint32_t nch = (Lmax + 64 / bps - 1) / (64 / bps);
@@ -1358,18 +1467,40 @@ struct Engine {
             pv_in.ensure(P);
             pv_out.ensure(P);
         }
+        // the packed start's grouping by the D-mer's leading bits: a bucket histogram from k_keys,
+        // a scan, one scatter (EDSBWT_BUCKETS=0: hipcub radix sort over those bits instead)
+        const int endbit_e = (int)bits_for(E);
+        const uint32_t hshift = (uint32_t)std::max(0, endbit_e - direct_sort_bits);
+        const uint64_t nbkt = direct_buckets();
+        const bool buckets = packed && nbkt;
+        if (buckets && !defer_call) {
+            bhist.ensure(nbkt + 1);
+            zero(bhist.p, (nbkt + 1) * 4);
+        }
         // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass
         if (bps == 3)
             launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
-                   packed ? pv_in.p : (uint64_t*)nullptr);
+                   packed ? pv_in.p : (uint64_t*)nullptr, buckets ? bhist.p : (uint32_t*)nullptr, hshift);
         else
             launch(KC_TRIE, k_keys<4>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
-                   (uint64_t*)nullptr);
-        if (read_u64(d_nterm)) return kNeedOrdered;  // '#' in a pattern: lists may overlap, use levels()
+                   (uint64_t*)nullptr, (uint32_t*)nullptr, 0u);
+        // '#' in a pattern: lists may overlap, use levels().  Deferred: read with the final check
+        // (a batch holding '#' is then searched again on the ordered path)
+        defer = defer_call && packed && direct_sort_bits > 0;
+        if (!defer && read_u64(d_nterm)) return kNeedOrdered;
         if (packed && direct_sort_bits <= 0) {  // input order (EDSBWT_DIRECT_SORT_BITS=0)
             st.start_depth = D0;
             return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, kid, ktab_off.p, ktab_off.p + 1,
                             ktab_b.p, ktab_e.p, r, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_in.p);
+        }
+        if (buckets) {
+            bscan.ensure(nbkt + 1);
+            exclusive_scan(bhist.p, bscan.p, nbkt);
+            hmark("bucket scan");
+            launch(KC_TRIE, k_bucket_scatter, P, (uint64_t)P, (const uint32_t*)kid, (const uint64_t*)pv_in.p, hshift, bscan.p, nid[0].p, pv_out.p);
+            st.start_depth = D0;
+            return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, nid[0].p, ktab_off.p, ktab_off.p + 1,
+                            ktab_b.p, ktab_e.p, r, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_out.p);
         }
         if (packed) {
             // the order only buys locality (neighbouring lanes read neighbouring table entries and
@@ -1786,6 +1917,7 @@ struct Engine {
 
     // d_bytes/d_off/d_counts are device pointers; returns number of records
     uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
+        t_search0 = std::chrono::steady_clock::now();
         st = edsbwt_stats{};
         prof = (flags & (EDSBWT_PROFILE | EDSBWT_PROFILE_LIGHT)) != 0;
         prof_mask = (flags & EDSBWT_PROFILE) ? ~0u : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_LOCATE) | (1u << KC_LINKSORT));
@@ -1803,6 +1935,8 @@ struct Engine {
         text_on = (flags & (EDSBWT_NO_TEXT | EDSBWT_LOCATE_WALK | EDSBWT_LOCATE_TABLE)) == 0 && env_double("EDSBWT_NO_TEXT", 0) == 0;
         if (use_table) build_table();
         st.patterns = P;
+        defer = false;
+        defer_call = defer_ok && !(flags & (kFlagNoDefer | EDSBWT_LEGACY_ORDER)) && !force_groups && !sticky_groups;
         if (P == 0) return 0;
         struct EvPair {  // released on every exit, including exceptions
             hipEvent_t a = nullptr, b = nullptr;
@@ -1812,6 +1946,7 @@ struct Engine {
         HIPCHK(hipEventCreate(&ep.b));
         hipEvent_t e0 = ep.a, e1 = ep.b;
         HIPCHK(hipEventRecord(e0, stream));
+        hmark("events");
         // a search that throws leaves no timing events behind for the next call
         struct EvRecycle {
             Engine* E;
@@ -1820,9 +1955,22 @@ struct Engine {
         } recycle{this};
         const KIdx X = kidx();
         res.ensure(P);
-        zero(res.p, P * sizeof(Res));
-        zero(stats.p, kStatSlots * 8);
         ovf_orig.ensure(P);
+        if (defer_call) {
+            // one zeroing launch for everything the deferred direct start counts into (see
+            // direct(), run_deep(), finish_deferred(); they skip their own zeroing when defer)
+            tflag.ensure(P + 1);
+            hcnt.ensure((size_t)std::min<uint64_t>(P, wide_cap) + 1);
+            lcnt.ensure(NSHARD * 32 + 32);
+            oscan.ensure(P + 1);
+            const uint64_t nb = direct_buckets();
+            if (nb) bhist.ensure(nb + 1);
+            zero_many({{res.p, P * sizeof(Res)}, {stats.p, kStatSlots * 8}, {counters.p, 24 * 8}, {tflag.p, 4}, {hcnt.p, 4},
+                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}});
+        } else {
+            zero(res.p, P * sizeof(Res));
+            zero(stats.p, kStatSlots * 8);
+        }
         uint64_t abase = 0;
         // patterns holding '#' make the reference's lists overlap: they take the ordered path
         const bool ordered = (flags & EDSBWT_ORDERED) != 0;
@@ -1838,6 +1986,7 @@ struct Engine {
                 try {
                     // the failed attempt's counters and timings are not this search's
                     discard_attempt();
+                    defer_call = defer = false;
                     st = edsbwt_stats{};
                     st.patterns = P;
                     zero(res.p, P * sizeof(Res));
@@ -1850,6 +1999,19 @@ struct Engine {
                     if (k >= 4) throw;
                 }
             }
+        }
+        if (defer) {
+            const uint64_t n = finish_deferred(P, first_id, locate, loc_mode, d_counts, e1);
+            if (n != kRedo) {
+                recycle.done = true;
+                return finish_stats(P, locate, use_table, loc_mode, n, e0, e1);
+            }
+            // a deferred check failed: the batch again on the checked path (inputs are untouched)
+            discard_attempt();
+            recycle.done = true;
+            const uint64_t m = search(d_bytes, d_off, P, first_id, flags | kFlagNoDefer, d_counts);
+            st.redo_searches++;
+            return m;
         }
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
         zero(counters.p + 1, 8);
@@ -1882,16 +2044,25 @@ struct Engine {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
                 blk_first.ensure(OCC / kLocRun + 1);
                 launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, tsc,
-                       (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p);
+                       (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p,
+                       ~0ull, ~0ull, (uint32_t*)(counters.p + 20));
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
-                       (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p);
+                       (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p,
+                       (const unsigned long long*)nullptr, (const uint32_t*)nullptr);
                 if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);
             }
         }
         small_copy(pinned_stats, stats.p, kStatSlots * 8);
         HIPCHK(hipEventRecord(e1, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        recycle.done = true;
+        return finish_stats(P, locate, use_table, loc_mode, OCC, e0, e1);
+    }
+
+    // the end of search(): device statistics (already copied to pinned_stats), timings
+    uint64_t finish_stats(uint64_t P, bool locate, bool use_table, int loc_mode, uint64_t OCC, hipEvent_t e0, hipEvent_t e1) {
+        (void)P;
         {
             const std::vector<uint64_t> sv = fold_pinned_stats();
             st.intervals_stepped += sv[ST_DEEP_STEPS];
@@ -1921,7 +2092,6 @@ struct Engine {
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         st.ms_total = ms;
-        recycle.done = true;
         if (prof) {
             for (auto& e : evs) {
                 float t = 0;
@@ -1932,6 +2102,65 @@ struct Engine {
             evs.clear();
         }
         st.occurrences = OCC;
+        return OCC;
+    }
+
+    // Deferred checks (direct start): counts, and with locate the tasks and records into
+    // buffers sized from earlier batches (at least 2 per pattern), then ONE read-back of
+    // everything the search postponed.  Returns the record count, or kRedo when a check
+    // failed ('#' in a pattern, more overflow patterns than k_deep_wide's launch covered or
+    // lists longer than its limit, totals past the buffers).
+    static constexpr uint64_t kRedo = ~0ull;
+    uint64_t finish_deferred(uint64_t P, uint32_t first_id, bool locate, int loc_mode, uint32_t* d_counts, hipEvent_t e1) {
+        const KIdx X = kidx();
+        // (counters, the scan's first slot and the check words were zeroed by search())
+        uint64_t occ_cap = std::min<uint64_t>(0xffffffffull, std::max<uint64_t>({rec.cap, 2 * P + 65536, (uint64_t)(occ_per_pat * 1.25 * (double)P)}));
+        uint64_t task_cap = std::min<uint64_t>(0xffffffffull, std::max<uint64_t>({trow.cap, 2 * P + 65536, (uint64_t)(tasks_per_pat * 1.25 * (double)P)}));
+        if (defer_cap) occ_cap = task_cap = defer_cap;
+        if (locate) occ64.ensure(P);
+        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
+                      locate ? occ64.p : (uint64_t*)nullptr);
+        uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
+        if (locate) {
+            inclusive_scan_u64(occ64.p, oscan, P, false);  // packed: occurrences << 32 | tasks (totals checked below)
+            hmark("locate scan");
+            trow.ensure(task_cap); tout.ensure(task_cap); tpat.ensure(task_cap);
+            blk_first.ensure(occ_cap / kLocRun + 2);
+            rec.ensure(occ_cap);
+            launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, (const uint64_t*)nullptr, (const uint64_t*)oscan.p, (const uint32_t*)ab.p,
+                   (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p, occ_cap, task_cap, oflow);
+            launch(KC_LOCATE, k_locate, occ_cap, occ_cap, task_cap, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
+                   (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p,
+                   (const unsigned long long*)(counters.p + 12), (const uint32_t*)oflow);
+        }
+        uint32_t* ck = chk();
+        hipLaunchKernelGGL(k_gather_checks, dim3(kStatSlots / 256), dim3(256), 0, stream, (const unsigned long long*)counters.p,
+                           (const uint32_t*)tflag.p, defer_ovf2, (const unsigned long long*)stats.p, kStatSlots,
+                           (uint32_t*)dev_alias(ck), (unsigned long long*)dev_alias(pinned_stats));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e1, stream));
+        hmark("gather queued");
+        HIPCHK(hipStreamSynchronize(stream));
+        hmark("synced");
+        uint64_t term, found, sums[2];
+        std::memcpy(&term, ck + kChkTerm, 8);
+        std::memcpy(&found, ck + kChkFound, 8);
+        std::memcpy(sums, ck + kChkSums, 16);
+        const bool ok = term == 0 && ck[kChkOvf] <= defer_wide_cap && ck[kChkOvf2] == 0 && ck[kChkOflow] == 0 &&
+                        (!locate || (sums[0] <= occ_cap && sums[1] <= task_cap));
+        if (trace)
+            std::fprintf(stderr, "[edsbwt] deferred checks: '#' %llu, overflow %u (wide cap %u), wide overflow %u, buffers %s -> %s\n",
+                                    (unsigned long long)term, ck[kChkOvf], defer_wide_cap, ck[kChkOvf2], ck[kChkOflow] ? "short" : "ok", ok ? "ok" : "redo");
+        if (!ok) return kRedo;
+        const uint32_t nw = ck[kChkOvf];
+        st.deep_overflow += nw;
+        st.found = found;
+        st.not_found = P - found;
+        const uint64_t OCC = locate ? sums[0] : 0;
+        if (locate) {
+            occ_per_pat = std::max(occ_per_pat, (double)sums[0] / (double)P);
+            tasks_per_pat = std::max(tasks_per_pat, (double)sums[1] / (double)P);
+        }
         return OCC;
     }
 
@@ -1959,11 +2188,33 @@ struct Engine {
         if (up) return;
         pool.start((unsigned)std::max(0.0, env_double("EDSBWT_HOST_THREADS", 12) - 1));
         HIPCHK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+        // downloads: hipMemcpyAsync into page-locked host memory runs as a blit kernel that fills
+        // every CU with waves waiting on PCIe stores, and the search kernels beside it then wait
+        // for CUs (measured: a 4-byte zeroing kernel took 0.56 ms behind a 34 MB download).  The
+        // download stream is therefore confined to a few CUs spread over the XCDs
+        // (EDSBWT_DOWN_CUS, 0: no mask)
+        {
+            hipDeviceProp_t prop{};
+            HIPCHK(hipGetDeviceProperties(&prop, device));
+            const int ncu = prop.multiProcessorCount;
+            const int want = (int)env_double("EDSBWT_DOWN_CUS", 32);
+            if (want > 0 && want < ncu) {
+                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+                const bool spread = env_double("EDSBWT_DOWN_CU_SPREAD", 1) != 0;
+                const int stride = std::max(1, ncu / want);
+                int got = 0;
+                for (int i = 0; i < ncu && got < want; i++)
+                    if (!spread || i % stride == 0) { mask[i / 32] |= 1u << (i % 32); got++; }
+                HIPCHK(hipExtStreamCreateWithCUMask(&down, (uint32_t)mask.size(), mask.data()));
+            } else {
+                HIPCHK(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+            }
+        }
         for (int k = 0; k < kSlots; k++) {
             HIPCHK(hipEventCreateWithFlags(&up_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&comp_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&down_done[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&prep_done[k], hipEventDisableTiming));
         }
     }
     // host -> device on `up` (staged through page-locked memory when src is pageable)
@@ -2140,6 +2391,50 @@ struct Engine {
     bool arena_checked_out();
 
     struct Chunk { uint64_t b0, b1, p0, p1, dpos; };  // byte range; pattern range (offsets mode); device place (eager)
+    // chunk prep on `up` (after its upload into slot sl): lines mode splits the raw bytes into
+    // (bytes, offsets) — k_nl_count, a scan, k_nl_compact — and k_line_fin writes the pattern
+    // count, the unterminated last line's end and the longest / shortest line; offsets mode
+    // rebases the offsets and measures the lengths.  Results land in prep_host(sl).
+    void prep(const Chunk& c, int sl, bool lines, const uint8_t* text) {
+        prep_mm[sl].ensure(4);
+        zero_on(prep_mm[sl].p, 32, up);
+        if (lines) {
+            const uint64_t nb = c.b1 - c.b0;
+            const uint64_t nblk = std::max<uint64_t>(1, (nb + kLineBlk - 1) / kLineBlk);
+            const uint32_t tail = (nb && text[c.b1 - 1] != '\n') ? 1u : 0u;
+            nlcnt_s[sl].ensure(nblk + 1);
+            nlpre_s[sl].ensure(nblk + 1);
+            hbytes[sl].ensure(nb + 16);
+            hoffs[sl].ensure(nb + 2);  // at most one line per byte, plus the unterminated last line
+            zero_on(nlpre_s[sl].p, 4, up);
+            zero_on(hoffs[sl].p, 8, up);
+            if (nb) {
+                hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nblk), dim3(256), 0, up, (const uint8_t*)hraw[sl].p, nb, nlcnt_s[sl].p);
+                HIPCHK(hipGetLastError());
+                size_t tb = 0;
+                HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, nlcnt_s[sl].p, nlpre_s[sl].p + 1, (int)nblk, up));
+                ptmp[sl].ensure(tb);
+                HIPCHK(hipcub::DeviceScan::InclusiveSum(ptmp[sl].p, tb, nlcnt_s[sl].p, nlpre_s[sl].p + 1, (int)nblk, up));
+                hipLaunchKernelGGL(k_nl_compact, dim3((unsigned)nblk), dim3(256), 0, up, (const uint8_t*)hraw[sl].p, nb,
+                                   (const uint32_t*)nlpre_s[sl].p, hbytes[sl].p, hoffs[sl].p);
+                HIPCHK(hipGetLastError());
+                hipLaunchKernelGGL(k_line_fin, dim3(kReduceBlocks), dim3(256), 0, up, hoffs[sl].p, (const uint32_t*)(nlpre_s[sl].p + nblk), tail,
+                                   nb, prep_mm[sl].p);
+                HIPCHK(hipGetLastError());
+            }
+        } else {
+            const uint64_t P = c.p1 - c.p0;
+            if (c.b0) {
+                hipLaunchKernelGGL(k_rebase, dim3(grid_for(P + 1)), dim3(256), 0, up, hoffs[sl].p, P + 1, c.b0);
+                HIPCHK(hipGetLastError());
+            }
+            if (P) {  // (offsets mode knows P: prep_host's count slot stays 0)
+                hipLaunchKernelGGL(k_lminmax, dim3(kReduceBlocks), dim3(256), 0, up, (const uint64_t*)hoffs[sl].p, P, prep_mm[sl].p + 1);
+                HIPCHK(hipGetLastError());
+            }
+        }
+        small_copy_on(prep_host(sl), prep_mm[sl].p, 24, up);
+    }
     DBuf<uint8_t> hin_all;                // eager uploads: every chunk of the batch
     DBuf<uint64_t> hoff_all;
     std::vector<hipEvent_t> chunk_ev;     // ... and their completion
@@ -2168,19 +2463,29 @@ struct Engine {
         std::vector<uint64_t> sizes;
         {
             const bool ramp = env_double("EDSBWT_CHUNK_RAMP", 1) != 0;
-            const uint64_t steps[3] = {target / 8, target / 4, target / 2};
-            std::vector<uint64_t> front, back;
-            uint64_t covered = 0;
-            for (int i = 0; covered < len; i++) {
-                const uint64_t a = std::max<uint64_t>(1, ramp && i < 3 ? steps[i] : target);
-                front.push_back(a);
-                covered += a;
-                if (covered >= len) break;
-                back.push_back(a);
-                covered += a;
+            const uint64_t steps[3] = {std::max<uint64_t>(1, target / 8), std::max<uint64_t>(1, target / 4), std::max<uint64_t>(1, target / 2)};
+            const uint64_t rsum = steps[0] + steps[1] + steps[2];
+            if (ramp && len > 2 * rsum) {
+                // ramp up, uniform middle chunks of at most `target`, ramp down: the last
+                // chunk's search and download (the drain) stay short
+                const uint64_t mid = len - 2 * rsum, nm = (mid + target - 1) / target;
+                sizes = {steps[0], steps[1], steps[2]};
+                for (uint64_t q = 0; q < nm; q++) sizes.push_back(mid * (q + 1) / nm - mid * q / nm);
+                sizes.insert(sizes.end(), {steps[2], steps[1], steps[0]});
+            } else {
+                std::vector<uint64_t> front, back;
+                uint64_t covered = 0;
+                for (int i = 0; covered < len; i++) {
+                    const uint64_t a = std::max<uint64_t>(1, ramp && i < 3 ? steps[i] : target);
+                    front.push_back(a);
+                    covered += a;
+                    if (covered >= len) break;
+                    back.push_back(a);
+                    covered += a;
+                }
+                sizes = front;
+                sizes.insert(sizes.end(), back.rbegin(), back.rend());
             }
-            sizes = front;
-            sizes.insert(sizes.end(), back.rbegin(), back.rend());
         }
         std::vector<Chunk> ch;
         if (lines) {
@@ -2211,7 +2516,7 @@ struct Engine {
         // through page-locked buffers slot by slot
         // (EDSBWT_EAGER_UP=1; off by default: uploads and downloads share one copy engine, which then
         // serves every upload before the first download)
-        const bool eager = pin_in && pin_off && env_double("EDSBWT_EAGER_UP", 0) != 0;
+        const bool eager = !lines && pin_in && pin_off && env_double("EDSBWT_EAGER_UP", 0) != 0;
         if (eager) {
             uint64_t at = 0;
             for (auto& c : ch) {
@@ -2311,48 +2616,53 @@ struct Engine {
             }
             h2d += nb;
             HIPCHK(hipEventRecord(up_done[sl], up));
+            prep(c, sl, lines, text);
+            HIPCHK(hipEventRecord(prep_done[sl], up));
         };
+        // EDSBWT_TRACE: host timeline of the pipeline (printed at the end)
+        std::vector<std::tuple<const char*, size_t, double>> marks;
+        auto mark = [&](const char* what, size_t k) {
+            if (trace) marks.emplace_back(what, k, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        };
+        // uploads run two chunks ahead of the search: chunk k+2's upload and prep overlap
+        // chunk k's search and chunk k-1's download
+        const size_t ahead = (size_t)std::max(1.0, std::min<double>(kSlots - 2, env_double("EDSBWT_AHEAD", 2)));
+        size_t issued = 0;
         if (eager) {
             for (size_t k = 0; k < ch.size(); k++) issue(k);
-        } else if (!ch.empty()) {
-            issue(0);
+            issued = ch.size();
         }
         for (size_t k = 0; k < ch.size(); k++) {
             const Chunk& c = ch[k];
             const int sl = (int)(k % kSlots);
-            if (!eager && k + 1 < ch.size()) issue(k + 1);  // overlaps this chunk's search
+            while (issued < ch.size() && issued <= k + ahead) { mark("issue", issued); issue(issued++); }
+            mark("issued", k);
             const auto tc = std::chrono::steady_clock::now();
-            HIPCHK(hipStreamWaitEvent(stream, eager ? chunk_ev[k] : up_done[sl], 0));
-            HIPCHK(hipStreamWaitEvent(stream, down_done[sl], 0));  // chunk k-2's results have left the slot
             uint64_t P;
             const uint8_t* bytes_k = nullptr;
             uint64_t* offs_k = nullptr;
-            if (lines) {  // the file's lines as a (bytes, offsets) batch
-                const uint64_t nb = c.b1 - c.b0;
-                const uint64_t nblk = (nb + kLineBlk - 1) / kLineBlk;
-                nlcnt.ensure(nblk + 1);
-                hbytes[sl].ensure(nb + 16);
-                const uint8_t* raw = eager ? hin_all.p + c.dpos : hraw[sl].p;
-                launch_blocks(KC_TRIE, k_nl_count, nblk, raw, nb, nlcnt.p);
-                const uint32_t nl = scan_u32(nlcnt.p, nlpre, nblk);
-                P = nl + ((nb && text[c.b1 - 1] != '\n') ? 1 : 0);
-                hoffs[sl].ensure(P + 1);
-                zero(hoffs[sl].p, 8);
-                launch_blocks(KC_TRIE, k_nl_compact, nblk, raw, nb, (const uint32_t*)nlpre.p, hbytes[sl].p, hoffs[sl].p);
-                if (P > nl) {  // the last line has no '\n': it ends at the chunk's end
-                    pinned_u64()[0] = nb - nl;
-                    small_copy(hoffs[sl].p + P, pinned_u64(), 8);
-                    HIPCHK(hipStreamSynchronize(stream));
-                }
-                bytes_k = hbytes[sl].p;  // (after the ensure() calls above, which may move them)
-                offs_k = hoffs[sl].p;
-            } else {
+            if (eager) {
+                HIPCHK(hipStreamWaitEvent(stream, chunk_ev[k], 0));
                 P = c.p1 - c.p0;
-                // the chunk's bytes and offsets: where the eager uploads put them, or the slot's
-                bytes_k = eager ? hin_all.p + c.dpos : hbytes[sl].p;
-                offs_k = eager ? hoff_all.p + c.p0 + k : hoffs[sl].p;
+                bytes_k = hin_all.p + c.dpos;
+                offs_k = hoff_all.p + c.p0 + k;
                 if (c.b0) launch(KC_TRIE, k_rebase, P + 1, offs_k, P + 1, c.b0);
+                known_len = false;
+            } else {
+                // the prep's pattern count and lengths (it ran on `up` right after the upload)
+                HIPCHK(hipEventSynchronize(prep_done[sl]));
+                mark("prep_ready", k);
+                HIPCHK(hipStreamWaitEvent(stream, prep_done[sl], 0));
+                uint64_t pm[3];
+                std::memcpy(pm, prep_host(sl), 24);
+                P = lines ? pm[0] : c.p1 - c.p0;
+                known_len = P > 0;
+                known_lmax = (uint32_t)pm[1];
+                known_lmin = ~(uint32_t)pm[2];
+                bytes_k = hbytes[sl].p;
+                offs_k = hoffs[sl].p;
             }
+            HIPCHK(hipStreamWaitEvent(stream, down_done[sl], 0));  // chunk k-3's results have left the slot
             if (pats + P > counts_cap) throw Fail(EDSBWT_E_ARG, "counts buffer holds " + std::to_string(counts_cap) + " patterns, the batch has more");
             hcounts[sl].ensure(P + 1);
             std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
@@ -2360,14 +2670,17 @@ struct Engine {
             try {
                 n = search(bytes_k, offs_k, P, first_id + (uint32_t)pats, flags, hcounts[sl].p);
             } catch (...) {
+                known_len = false;
                 std::swap(rec, hrec[sl]);
                 throw;
             }
+            known_len = false;
             std::swap(rec, hrec[sl]);
             if (compact && locate && n) {  // (word, offset) per record for the download
                 hrec8[sl].ensure(n);
                 launch(KC_LOCATE, k_rec_compact, n, (const edsbwt_occ*)hrec[sl].p, n, hrec8[sl].p);
             }
+            mark("searched", k);
             accumulate(agg, st);
             if (trace)
                 std::fprintf(stderr, "[edsbwt] chunk %zu: %llu patterns, %llu records, search %.3f ms host / %.3f ms device, at %.3f ms\n", k,
@@ -2403,6 +2716,7 @@ struct Engine {
                 }
             }
             HIPCHK(hipEventRecord(down_done[sl], down));
+            mark("d2h_queued", k);
             if (compact && locate && n) {
                 HIPCHK(hipEventRecord(chunk_down_ev[k], down));
                 xpost({pats, P, total, n, chunk_down_ev[k]});
@@ -2413,6 +2727,8 @@ struct Engine {
         xfinish();
         HIPCHK(hipStreamSynchronize(down));
         HIPCHK(hipStreamSynchronize(up));
+        mark("drained", ch.size());
+        for (auto& m : marks) std::fprintf(stderr, "[edsbwt] t %8.3f ms  %-10s chunk %zu\n", std::get<2>(m), std::get<0>(m), std::get<1>(m));
         } catch (...) {  // no copy may still touch the caller's buffers
             try { xfinish(); } catch (...) {}
             (void)hipStreamSynchronize(up);
@@ -2458,7 +2774,7 @@ struct Engine {
         }
         a.locate_offsets += b.locate_offsets; a.search_groups = std::max(a.search_groups, b.search_groups);
         a.start_depth = std::max(a.start_depth, b.start_depth);
-        a.text_chars += b.text_chars; a.text_rows += b.text_rows;
+        a.text_chars += b.text_chars; a.text_rows += b.text_rows; a.redo_searches += b.redo_searches;
     }
 
     ~Engine() {

@@ -384,7 +384,8 @@ template <int BPS>
 __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
                                               const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t nch, uint64_t* __restrict__ keys,
                                               uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term,
-                                              uint32_t D, uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
+                                              uint32_t D, uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv,
+                                              uint32_t* __restrict__ hist, uint32_t hshift) {
     // kid / pv (direct start), from the chunks still in registers: kid = the D-mer id of the
     // pattern's last D symbols (last character least significant digit, as k_ktab_count reads
     // a node's); a D-mer holding '#' or a byte outside the alphabet has no list: kid = E
@@ -470,6 +471,7 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
                     pv[i] = rem << 31 | (uint64_t)i;
                 }
                 kid[i] = ok ? x : E;
+                if (hist) atomicAdd(&hist[(ok ? x : E) >> hshift], 1u);  // bucket sizes for k_bucket_scatter
             }
         }
     }
@@ -478,6 +480,21 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
 }
 
 __global__ void k_iota(uint32_t* __restrict__ a, uint64_t n) { GRID_STRIDE(i, n) a[i] = (uint32_t)i; }
+
+// direct start: patterns grouped by their D-mer's leading bits (kid >> shift) for locality —
+// neighbouring lanes then read neighbouring table entries and rows.  cur[] holds each
+// bucket's first slot (exclusive scan of k_keys' histogram) and is advanced by atomics, so
+// the order inside a bucket is arbitrary: nothing downstream depends on it (results are
+// written by input index, carried in the packed start)
+__global__ void k_bucket_scatter(uint64_t P, const uint32_t* __restrict__ kid, const uint64_t* __restrict__ pv, uint32_t shift,
+                                 uint32_t* __restrict__ cur, uint32_t* __restrict__ kid_out, uint64_t* __restrict__ pv_out) {
+    GRID_STRIDE(i, P) {
+        const uint32_t k = kid[i];
+        const uint32_t at = atomicAdd(&cur[k >> shift], 1u);
+        kid_out[at] = k;
+        pv_out[at] = pv[i];
+    }
+}
 
 // group of a pattern = its last k characters' sort codes (0 past the pattern's start),
 // i.e. its depth-k node of the reversed-pattern trie, in base sigma+2
@@ -1347,8 +1364,11 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
                                                   const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
                                                   const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                                   uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
-                                                  uint32_t* __restrict__ ovf2) {
+                                                  uint32_t* __restrict__ ovf2, const uint32_t* __restrict__ ntodo_dev) {
     (void)P;
+    // ntodo_dev (deferred checks): the list's length lives on the device; ntodo is the grid's
+    // capacity, and a longer list is caught by the caller's final check
+    if (ntodo_dev) ntodo = min(ntodo, *ntodo_dev);
     GRID_STRIDE(j, ntodo) {
         const uint32_t i = todo[j];
         const uint32_t L = slen[ind ? perm[i] : i];
@@ -1851,13 +1871,16 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
                         const uint64_t* __restrict__ tscan, const uint64_t* __restrict__ oscan,
                         const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                         uint32_t* __restrict__ trow, uint64_t* __restrict__ tout, uint32_t* __restrict__ tpat,
-                        uint64_t* __restrict__ blk_first) {
+                        uint64_t* __restrict__ blk_first, uint64_t occ_cap, uint64_t task_cap, uint32_t* __restrict__ oflow) {
     GRID_STRIDE(i, P) {
         // tscan null: oscan holds the packed scan (occurrences << 32 | tasks)
         const uint64_t ps = oscan[i];
         uint64_t base = tscan ? ps : ps >> 32;
         const uint64_t t0 = tscan ? tscan[i] : (ps & 0xffffffffull);
         const Res r = res[i];
+        // buffers sized before the totals were read (deferred checks): a pattern whose tasks or
+        // records pass them flags the batch, and the caller searches it again with exact sizes
+        if (t0 + res_cnt(r) > task_cap || base + res_occ(r) > occ_cap) { atomicOr(oflow, 1u); continue; }
         const bool direct_row = (r.cnt & kResRow) != 0;
         const uint32_t n = res_cnt(r);
         for (uint32_t q = 0; q < n; q++) {
@@ -1884,12 +1907,21 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
 __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
                                                 const uint32_t* __restrict__ tpat, const uint64_t* __restrict__ blk_first, uint32_t first_id,
                                                 KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats,
-                                                const Res* __restrict__ res) {
+                                                const Res* __restrict__ res, const unsigned long long* __restrict__ tot_dev,
+                                                const uint32_t* __restrict__ oflow) {
+    // tot_dev (deferred checks): OCC and TT are the batch's totals on the device, the launch
+    // arguments the buffers' capacities; nothing runs when k_tasks found them too small
+    if (tot_dev) {
+        if (*oflow) return;
+        OCC = min(OCC, (uint64_t)tot_dev[0]);
+        TT = min(TT, (uint64_t)tot_dev[1]);
+    }
     unsigned long long my_steps = 0, my_off = 0;
     __shared__ uint64_t s_out[kLocRun + 1];
     __shared__ uint32_t s_row[kLocRun + 1], s_pat[kLocRun + 1];
     for (uint64_t o0 = (uint64_t)blockIdx.x * kLocRun; o0 < OCC; o0 += (uint64_t)gridDim.x * kLocRun) {  // block-uniform
         const uint64_t t0 = blk_first[o0 / kLocRun];
+        if (t0 >= TT) continue;  // (block-uniform) only a batch that fails its deferred checks gets here
         const uint32_t nt = (uint32_t)min((uint64_t)kLocRun + 1, TT - t0);
         __syncthreads();  // the previous pass is done with the staged tasks
         for (uint32_t j = threadIdx.x; j < nt; j += blockDim.x) {
@@ -1922,6 +1954,7 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
             continue;
         }
         uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
+        if (x >= X.N) continue;  // as above: rows of a valid task are < N
         if (mode == 2 && X.samp_dense) {  // every row sampled: the record straight from row x's sample
             const uint4 s = X.samples[x];
             my_off += s.y;
@@ -2482,6 +2515,34 @@ __global__ void __launch_bounds__(256) k_ktab_emit(uint32_t M, const uint32_t* _
 // newlines before each block, k_nl_compact moves the bytes and writes line ends.
 constexpr uint32_t kLineBlk = 4096;
 // small host<->device transfers on the engine stream (engine.hip small_copy)
+// zero up to 8 ranges (byte sizes multiples of 4, 4-B aligned) in one launch: blockIdx.y = range
+struct ZeroSet {
+    uint32_t* p[8];
+    uint64_t n4[8];
+};
+__global__ void __launch_bounds__(256) k_zero_multi(ZeroSet z) {
+    uint32_t* p = z.p[blockIdx.y];
+    const uint64_t n = z.n4[blockIdx.y];
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) p[i] = 0u;
+}
+// the deferred checks and the statistics shards of a search, to page-locked host memory in
+// one launch (engine.hip finish_deferred: chk layout kChk*)
+__global__ void k_gather_checks(const unsigned long long* __restrict__ counters, const uint32_t* __restrict__ ovf,
+                                const uint32_t* __restrict__ ovf2, const unsigned long long* __restrict__ stats, uint32_t nstats,
+                                uint32_t* __restrict__ chk, unsigned long long* __restrict__ pstats) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        const unsigned long long term = counters[10], found = counters[1], occ = counters[12], tasks = counters[13];
+        chk[0] = (uint32_t)term; chk[1] = (uint32_t)(term >> 32);
+        chk[2] = *ovf;
+        chk[3] = *ovf2;
+        chk[4] = *reinterpret_cast<const uint32_t*>(counters + 20);
+        chk[6] = (uint32_t)found; chk[7] = (uint32_t)(found >> 32);
+        chk[8] = (uint32_t)occ; chk[9] = (uint32_t)(occ >> 32);
+        chk[10] = (uint32_t)tasks; chk[11] = (uint32_t)(tasks >> 32);
+    }
+    for (uint32_t i = t; i < nstats; i += gridDim.x * blockDim.x) pstats[i] = stats[i];
+}
 __global__ void k_copy_words(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t n) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
 }
@@ -2495,6 +2556,49 @@ __global__ void k_rec_compact(const edsbwt_occ* __restrict__ rec, uint64_t n, ui
         const edsbwt_occ r = rec[i];
         out[i] = make_uint2(r.word, r.offset);
     }
+}
+// zero n bytes at p: 16-B stores over the aligned interior, byte stores at both ends
+__global__ void __launch_bounds__(256) k_zero_bytes(uint8_t* __restrict__ p, uint64_t n) {
+    const uint64_t head = min(n, (uint64_t)((16u - ((uintptr_t)p & 15u)) & 15u));
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    if (tid < head) p[tid] = 0;
+    uint4* q = reinterpret_cast<uint4*>(p + head);
+    const uint64_t n16 = (n - head) / 16;
+    for (uint64_t i = tid; i < n16; i += nt) q[i] = make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t t0 = head + n16 * 16;
+    if (tid < n - t0) p[t0 + tid] = 0;
+}
+// a chunk's lines after k_nl_compact: P = newlines + (1 if the chunk does not end with
+// '\n'); that last line's end; P and the longest and shortest line into out[0..2]
+// (out[1] = max, out[2] = ~min, both by atomicMax; out zeroed before) — no host round trip
+__global__ void __launch_bounds__(256) k_line_fin(uint64_t* __restrict__ offs, const uint32_t* __restrict__ nl_total, uint32_t tail,
+                                                  uint64_t nb, unsigned long long* __restrict__ out) {
+    const uint32_t nl = *nl_total;
+    const uint64_t P = (uint64_t)nl + tail;
+    const uint64_t tail_end = nb - nl;  // compacted bytes: the last line ends there
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid == 0) {
+        out[0] = P;
+        if (tail) offs[P] = tail_end;
+    }
+    __shared__ unsigned int smx, smn;
+    if (threadIdx.x == 0) smx = smn = 0;
+    __syncthreads();
+    uint32_t mx = 0, nmn = 0;
+    GRID_STRIDE(i, P) {
+        const uint64_t e = (tail && i == P - 1) ? tail_end : offs[i + 1];
+        const uint32_t L = (uint32_t)(e - offs[i]);
+        mx = max(mx, L);
+        nmn = max(nmn, ~L);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+        nmn = max(nmn, (uint32_t)__shfl_xor(nmn, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) { atomicMax(&smx, mx); atomicMax(&smn, nmn); }
+    __syncthreads();
+    if (threadIdx.x == 0) { atomicMax(out + 1, (unsigned long long)smx); atomicMax(out + 2, (unsigned long long)smn); }
 }
 // offsets of a chunk of a packed batch, rebased to its first byte
 __global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) { GRID_STRIDE(i, n) off[i] -= base; }

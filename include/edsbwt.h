@@ -115,6 +115,9 @@ typedef struct {
     uint64_t bytes_h2d, bytes_d2h;
     uint64_t text_chars;      /* pattern characters decided by the single-row text compare */
     uint64_t text_rows;       /* single-row intervals the text compare met */
+    uint64_t redo_searches;   /* searches (chunks) run again on the checked path because a
+                                 deferred check failed ('#' in a pattern, long overflow lists,
+                                 more records than the pre-sized buffers) */
 } edsbwt_stats;
 
 /* Replaces recoverInfo + retrieve_MLF + bitvector load (MOVE_EDSBWTSearch.cpp:23-95,

@@ -609,3 +609,74 @@ def test_shard_first_pattern_id_gpu(oracle, edsbwt, tmp_path):
                 os_.append(occ)
             assert np.array_equal(np.concatenate(cs), oc)
             assert np.array_equal(np.concatenate(os_), ref)
+
+
+def test_deferred_checks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The packed direct start defers its checks to one read-back at the end ('#' in a pattern,
+    k_deep overflow lists and the wide retry, record / task totals vs pre-sized buffers).  A
+    batch that fails one is searched again on the checked path: forced here by a '#' pattern,
+    tiny buffer caps, a tiny wide-retry cap and no wide retry.  Identical to the oracle each time,
+    and the redo is visible in the stats."""
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
+    rng = random.Random(4242)
+    # (a) COVID-like: no overflow; the deferred path completes without a redo
+    segs = _covid_like(rng, 600)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs), "cov")
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    assert D0 >= 2
+    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(3000)]
+    pats = [p[: D0 + 16] if len(p) > D0 + 16 else p for p in pats]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(D0 + 1, D0 + 16))) for _ in range(500)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        for locate in (True, False):
+            gc, go = idx.search((buf, offs), locate=locate)
+            st = idx.stats()
+            assert np.array_equal(gc, oc) and (not locate or np.array_equal(go, oo))
+            assert st["start_depth"] == D0 and st["trie_nodes"] == 0 and st["redo_searches"] == 0, st
+    monkeypatch.setenv("EDSBWT_DEFER_CAP", "64")  # records and tasks pass the pre-sized buffers
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert idx.stats()["redo_searches"] == 1
+    monkeypatch.delenv("EDSBWT_DEFER_CAP")
+    # a pattern holding '#' (the ordered path), found only at the final check
+    pats2 = pats[:500] + ["A" * D0 + "#AC"] + pats[500:1000]
+    buf2, offs2 = _pack(pats2)
+    oc2, oo2, _ = oracle.Engine(base, 8).search(buf2, offs2)
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf2, offs2))
+        assert np.array_equal(gc, oc2) and np.array_equal(go, oo2)
+        assert idx.stats()["redo_searches"] == 1
+    # (b) one repeated motif: k_deep overflows (some past the wide lists too)
+    motif = ["AC", "ACA", "CA", "A", "", "CAC"]
+    segs = [[rng.choice(motif) or "A" for _ in range(rng.randint(1, 5))] for _ in range(3000)]
+    for s in segs:
+        if rng.random() < 0.3 and len(s) > 1:
+            s[0] = ""
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs), "motif")
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    pats = ["".join(rng.choice("AC") for _ in range(rng.randint(D0 + 1, D0 + 16))) for _ in range(2000)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs))
+        st = idx.stats()
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert st["start_depth"] == D0 and st["deep_overflow"] > 0, st
+        gc, go = idx.search((buf, offs), wide=False)  # every overflow fails the check
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        assert idx.stats()["redo_searches"] == 1
+    monkeypatch.setenv("EDSBWT_WIDE_CAP", "1")
+    with edsbwt.Index(base) as idx:
+        for locate in (True, False):
+            gc, go = idx.search((buf, offs), locate=locate)
+            assert np.array_equal(gc, oc) and (not locate or np.array_equal(go, oo))
+            assert idx.stats()["redo_searches"] == 1
