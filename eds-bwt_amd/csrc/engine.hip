@@ -12,6 +12,8 @@
 // one depth per launch group: every distinct pattern suffix is searched once.
 // DESIGN.md §Search walks through the phases and why each equals the reference.
 #include <hipcub/hipcub.hpp>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <dlfcn.h>
 
@@ -25,6 +27,8 @@
 #include <stdexcept>
 #include <string>
 #include <condition_variable>
+#include <deque>
+#include <tuple>
 #include <exception>
 #include <functional>
 #include <thread>
@@ -2440,25 +2444,10 @@ struct Engine {
     std::vector<hipEvent_t> chunk_ev;     // ... and their completion
     std::vector<hipEvent_t> chunk_down_ev;  // each chunk's downloads (compact records: the expander waits on them)
 
-    // The pattern loop of MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:97-155) over a batch in host memory,
-    // timed as SURVEY §8(d) defines patterns/s: from the first H2D of the patterns to the last
-    // D2H of counts and records.  lines != 0: `text` is the pattern file as it lies on disk
-    // (getline semantics, :111: split at '\n', a last line without '\n' counts); else
-    // text/offs is a packed (bytes, offsets[npat+1]) batch.  Returns the records (page-locked,
-    // library-owned) and their number; *npat_out = patterns seen.
-    uint64_t search_host(const uint8_t* text, uint64_t len, const uint64_t* offs, uint64_t npat, bool lines, uint32_t first_id,
-                         uint32_t flags, uint32_t* counts, uint64_t counts_cap, edsbwt_occ** occ_out, uint64_t* npat_out) {
-        const auto t0 = std::chrono::steady_clock::now();
-        pipe_init();
-        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
-        const bool pin_in = host_pinned(text), pin_off = lines || host_pinned(offs), pin_cnt = host_pinned(counts);
-        // downloads by the copy engine (EDSBWT_D2H_KERNEL=1: kernel stores to mapped host memory;
-        // measured slower on MI355X: their PCIe stores slow the search kernels running beside them)
-        const bool sdma_down = env_double("EDSBWT_D2H_KERNEL", 0) == 0;
-        uint32_t* counts_dev = pin_cnt ? static_cast<uint32_t*>(host_dev_ptr(counts)) : nullptr;
-        // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 64 MB), cut at line ends; the
-        // first and last chunks ramp up from / down to 1/8 of that (EDSBWT_CHUNK_RAMP=0: uniform),
-        // so the pipeline fills and drains fast
+    // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 64 MB), cut at line ends; the
+    // first and last chunks ramp up from / down to 1/8 of that (EDSBWT_CHUNK_RAMP=0: uniform),
+    // so the pipeline fills and drains fast
+    std::vector<Chunk> cut_chunks(const uint8_t* text, uint64_t len, const uint64_t* offs, uint64_t npat, bool lines) {
         const uint64_t target = std::max<uint64_t>(1, (uint64_t)(env_double("EDSBWT_CHUNK_MB", 64) * 1048576.0));
         std::vector<uint64_t> sizes;
         {
@@ -2510,6 +2499,339 @@ struct Engine {
                 ch.push_back({offs[p], offs[lo], p, lo, 0});
                 p = lo;
             }
+        }
+        return ch;
+    }
+
+    // ---- bulk transfers on explicit SDMA engines: uploads on one, downloads on another, each
+    // driven by its own host thread.  Through hipMemcpyAsync the runtime gave both directions
+    // the same engine here, which then served them in turn (tools/hsa_duplex.hip on MI355X:
+    // 56 GB/s on one engine, 95 GB/s on two).  EDSBWT_HSA_COPY=0: the HIP-stream pipeline.
+    bool hsa_tried = false, hsa_ok = false;
+    hsa_agent_t hsa_gpu{}, hsa_cpu{};
+    uint32_t eng_up = 0, eng_down = 0;
+    bool hsa_init() {
+        if (hsa_tried) return hsa_ok;
+        hsa_tried = true;
+        if (env_double("EDSBWT_HSA_COPY", 1) == 0) return false;
+        struct Ctx {
+            int bus = -1, dev = -1, dom = -1;
+            hsa_agent_t gpu{}, cpu{};
+            bool g = false, c = false;
+        } cx;
+        if (hipDeviceGetAttribute(&cx.bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+            hipDeviceGetAttribute(&cx.dev, hipDeviceAttributePciDeviceId, device) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (hipDeviceGetAttribute(&cx.dom, hipDeviceAttributePciDomainId, device) != hipSuccess) { (void)hipGetLastError(); cx.dom = -1; }
+        auto cb = [](hsa_agent_t a, void* d) -> hsa_status_t {
+            Ctx* c = static_cast<Ctx*>(d);
+            hsa_device_type_t t;
+            if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+            if (t == HSA_DEVICE_TYPE_CPU && !c->c) { c->cpu = a; c->c = true; }
+            if (t == HSA_DEVICE_TYPE_GPU && !c->g) {
+                uint32_t bdf = 0, domain = 0;
+                if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+                (void)hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &domain);
+                if ((int)((bdf >> 8) & 0xff) == c->bus && (int)((bdf >> 3) & 0x1f) == c->dev && (c->dom < 0 || (int)domain == c->dom)) {
+                    c->gpu = a;
+                    c->g = true;
+                }
+            }
+            return HSA_STATUS_SUCCESS;
+        };
+        if (hsa_iterate_agents(cb, &cx) != HSA_STATUS_SUCCESS || !cx.g || !cx.c) return false;
+        uint32_t m_up = 0, m_down = 0;
+        if (hsa_amd_memory_copy_engine_status(cx.gpu, cx.cpu, &m_up) != HSA_STATUS_SUCCESS ||
+            hsa_amd_memory_copy_engine_status(cx.cpu, cx.gpu, &m_down) != HSA_STATUS_SUCCESS)
+            return false;
+        const uint32_t want_up = (uint32_t)env_double("EDSBWT_SDMA_UP", 0x1), want_down = (uint32_t)env_double("EDSBWT_SDMA_DOWN", 0x2);
+        auto pick = [](uint32_t avail, uint32_t want, uint32_t avoid) -> uint32_t {
+            if (want && (avail & want) && want != avoid && !(want & (want - 1))) return want;
+            for (uint32_t b = 1; b && b <= 0x8000u; b <<= 1)
+                if ((avail & b) && b != avoid) return b;
+            return 0;
+        };
+        eng_up = pick(m_up, want_up, 0);
+        eng_down = pick(m_down, want_down, eng_up);
+        if (!eng_up || !eng_down) return false;
+        hsa_gpu = cx.gpu;
+        hsa_cpu = cx.cpu;
+        hsa_ok = true;
+        if (trace) std::fprintf(stderr, "[edsbwt] host pipeline: SDMA engine 0x%x up, 0x%x down\n", eng_up, eng_down);
+        return true;
+    }
+    // n bytes on engine `eng`, waiting for the copy (the caller is that direction's thread)
+    void hsa_copy(void* dst, const void* src, size_t n, bool to_host, uint32_t eng, hsa_signal_t sig) {
+        if (!n) return;
+        hsa_signal_store_relaxed(sig, 1);
+        const hsa_status_t r = hsa_amd_memory_async_copy_on_engine(dst, to_host ? hsa_cpu : hsa_gpu, src, to_host ? hsa_gpu : hsa_cpu, n, 0, nullptr,
+                                                                   sig, (hsa_amd_sdma_engine_id_t)eng, true);
+        if (r != HSA_STATUS_SUCCESS) {
+            const char* m = nullptr;
+            hsa_status_string(r, &m);
+            throw Fail(EDSBWT_E_DEVICE, std::string("hsa_amd_memory_async_copy_on_engine: ") + (m ? m : "?"));
+        }
+        while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) >= 1) {}
+    }
+
+    // search_host over explicit SDMA engines: an upload thread (chunk k+ahead: copy, then its prep
+    // on `up`), this thread (chunk k's search on `stream`), a download thread (chunk k-1's counts
+    // and records).  Chunk k reuses slot k % kSlots: its upload waits for chunk k-kSlots's search,
+    // its search for chunk k-kSlots's download.
+    uint64_t search_host_hsa(const std::vector<Chunk>& ch, const uint8_t* text, const uint64_t* offs, bool lines, bool pin_in, bool pin_off,
+                             bool pin_cnt, uint32_t first_id, uint32_t flags, uint32_t* counts, uint64_t counts_cap, bool locate,
+                             edsbwt_occ** occ_out, uint64_t* npat_out, std::chrono::steady_clock::time_point t0) {
+        const size_t nch = ch.size();
+        const size_t ahead = (size_t)std::max(1.0, std::min<double>(kSlots - 2, env_double("EDSBWT_AHEAD", 3)));
+        std::mutex m;
+        std::condition_variable cv;
+        size_t uploaded = 0, searched = 0, downloaded = 0;
+        bool stop = false, closed = false;
+        std::exception_ptr err;
+        struct Job {
+            size_t k;
+            uint64_t P, n, pats, total;
+        };
+        std::deque<Job> jobs;
+        uint64_t h2d = 0, d2h = 0;
+        std::vector<std::tuple<const char*, size_t, double>> marks;
+        std::mutex mark_m;
+        auto mark = [&](const char* what, size_t k) {
+            if (!trace) return;
+            std::lock_guard<std::mutex> g(mark_m);
+            marks.emplace_back(what, k, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        };
+        auto fail = [&](std::exception_ptr e) {
+            std::lock_guard<std::mutex> g(m);
+            if (!err) err = e;
+            stop = true;
+            cv.notify_all();
+        };
+        if (arena_checked_out()) arena_release();  // the caller still holds the last records: start a new buffer
+        std::thread tu([&] {
+            hsa_signal_t sig{};
+            bool have_sig = false;
+            try {
+                HIPCHK(hipSetDevice(device));
+                if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) throw Fail(EDSBWT_E_DEVICE, "hsa_signal_create failed");
+                have_sig = true;
+                for (size_t k = 0; k < nch; k++) {
+                    {
+                        std::unique_lock<std::mutex> lk(m);
+                        cv.wait(lk, [&] { return stop || (k <= searched + ahead && k < searched + kSlots); });
+                        if (stop) break;
+                    }
+                    const Chunk& c = ch[k];
+                    const int sl = (int)(k % kSlots);
+                    const uint64_t nb = c.b1 - c.b0;
+                    mark("upload", k);
+                    uint64_t up_bytes = nb;
+                    uint8_t* dst = nullptr;
+                    if (lines) {
+                        hraw[sl].ensure(nb + 16);
+                        dst = hraw[sl].p;
+                    } else {
+                        hbytes[sl].ensure(nb + 16);
+                        hoffs[sl].ensure(c.p1 - c.p0 + 1);
+                        dst = hbytes[sl].p;
+                    }
+                    const uint8_t* src = text + c.b0;
+                    if (!pin_in && nb) {
+                        stage_in[sl].ensure(nb);
+                        par_copy(stage_in[sl].p, src, nb);
+                        src = static_cast<const uint8_t*>(stage_in[sl].p);
+                    }
+                    hsa_copy(dst, src, nb, false, eng_up, sig);
+                    if (!lines) {
+                        const size_t ob = (c.p1 - c.p0 + 1) * 8;
+                        const void* osrc = offs + c.p0;
+                        if (!pin_off) {
+                            stage_off[sl].ensure(ob);
+                            par_copy(stage_off[sl].p, osrc, ob);
+                            osrc = stage_off[sl].p;
+                        }
+                        hsa_copy(hoffs[sl].p, osrc, ob, false, eng_up, sig);
+                        up_bytes += ob;
+                    }
+                    prep(c, sl, lines, text);
+                    HIPCHK(hipEventRecord(prep_done[sl], up));
+                    mark("uploaded", k);
+                    {
+                        std::lock_guard<std::mutex> g(m);
+                        uploaded = k + 1;
+                        h2d += up_bytes;
+                    }
+                    cv.notify_all();
+                }
+            } catch (...) {
+                fail(std::current_exception());
+            }
+            if (have_sig) hsa_signal_destroy(sig);
+        });
+        std::thread td([&] {
+            hsa_signal_t sig{};
+            bool have_sig = false;
+            try {
+                HIPCHK(hipSetDevice(device));
+                if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) throw Fail(EDSBWT_E_DEVICE, "hsa_signal_create failed");
+                have_sig = true;
+                for (;;) {
+                    Job j;
+                    {
+                        std::unique_lock<std::mutex> lk(m);
+                        cv.wait(lk, [&] { return stop || closed || !jobs.empty(); });
+                        if (stop || jobs.empty()) break;
+                        j = jobs.front();
+                        jobs.pop_front();
+                    }
+                    const int sl = (int)(j.k % kSlots);
+                    mark("download", j.k);
+                    uint64_t dn = 0;
+                    if (j.P) {
+                        if (pin_cnt) {
+                            hsa_copy(counts + j.pats, hcounts[sl].p, j.P * 4, true, eng_down, sig);
+                        } else {
+                            stage_cnt[sl].ensure(j.P * 4);
+                            hsa_copy(stage_cnt[sl].p, hcounts[sl].p, j.P * 4, true, eng_down, sig);
+                            std::memcpy(counts + j.pats, stage_cnt[sl].p, j.P * 4);
+                        }
+                        dn += j.P * 4;
+                    }
+                    if (locate && j.n) {
+                        hsa_copy(arena + j.total, hrec[sl].p, j.n * sizeof(edsbwt_occ), true, eng_down, sig);
+                        dn += j.n * sizeof(edsbwt_occ);
+                    }
+                    mark("downloaded", j.k);
+                    {
+                        std::lock_guard<std::mutex> g(m);
+                        downloaded = j.k + 1;
+                        d2h += dn;
+                    }
+                    cv.notify_all();
+                }
+            } catch (...) {
+                fail(std::current_exception());
+            }
+            if (have_sig) hsa_signal_destroy(sig);
+        });
+        edsbwt_stats agg{};
+        uint64_t total = 0, pats = 0;
+        try {
+            for (size_t k = 0; k < nch; k++) {
+                const Chunk& c = ch[k];
+                const int sl = (int)(k % kSlots);
+                {
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [&] { return stop || (uploaded > k && (k < (size_t)kSlots || downloaded > k - kSlots)); });
+                    if (stop) break;
+                }
+                HIPCHK(hipEventSynchronize(prep_done[sl]));
+                mark("search", k);
+                uint64_t pm[3];
+                std::memcpy(pm, prep_host(sl), 24);
+                const uint64_t P = lines ? pm[0] : c.p1 - c.p0;
+                known_len = P > 0;
+                known_lmax = (uint32_t)pm[1];
+                known_lmin = ~(uint32_t)pm[2];
+                HIPCHK(hipStreamWaitEvent(stream, prep_done[sl], 0));
+                if (pats + P > counts_cap) throw Fail(EDSBWT_E_ARG, "counts buffer holds " + std::to_string(counts_cap) + " patterns, the batch has more");
+                hcounts[sl].ensure(P + 1);
+                std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
+                uint64_t n = 0;
+                try {
+                    n = search(hbytes[sl].p, hoffs[sl].p, P, first_id + (uint32_t)pats, flags, hcounts[sl].p);
+                } catch (...) {
+                    known_len = false;
+                    std::swap(rec, hrec[sl]);
+                    throw;
+                }
+                known_len = false;
+                std::swap(rec, hrec[sl]);
+                mark("searched", k);
+                accumulate(agg, st);
+                if (locate && n && total + n > arena_cap) {
+                    // the arena grows: every earlier chunk's records must have landed first
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [&] { return stop || downloaded == k; });
+                    if (stop) break;
+                    lk.unlock();
+                    arena_ensure(total + n);
+                }
+                {
+                    std::lock_guard<std::mutex> g(m);
+                    jobs.push_back(Job{k, P, n, pats, total});
+                    searched = k + 1;
+                }
+                cv.notify_all();
+                total += n;
+                pats += P;
+            }
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return stop || downloaded == nch; });
+                closed = true;
+            }
+            cv.notify_all();
+        } catch (...) {
+            fail(std::current_exception());
+        }
+        {
+            std::lock_guard<std::mutex> g(m);
+            closed = true;
+        }
+        cv.notify_all();
+        tu.join();
+        td.join();
+        (void)hipStreamSynchronize(up);
+        if (err) {
+            (void)hipStreamSynchronize(stream);  // no kernel may still touch the slots
+            std::rethrow_exception(err);
+        }
+        mark("drained", nch);
+        for (auto& mk : marks) std::fprintf(stderr, "[edsbwt] t %8.3f ms  %-10s chunk %zu\n", std::get<2>(mk), std::get<0>(mk), std::get<1>(mk));
+        st = agg;
+        st.patterns = pats;
+        st.occurrences = total;
+        st.chunks = nch;
+        st.bytes_h2d = h2d;
+        st.bytes_d2h = d2h;
+        st.ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (npat_out) *npat_out = pats;
+        if (occ_out) {
+            *occ_out = nullptr;
+            if (locate && total) {
+                *occ_out = arena;
+                arena_checkout();
+            }
+        }
+        return total;
+    }
+
+    // The pattern loop of MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:97-155) over a batch in host memory,
+    // timed as SURVEY §8(d) defines patterns/s: from the first H2D of the patterns to the last
+    // D2H of counts and records.  lines != 0: `text` is the pattern file as it lies on disk
+    // (getline semantics, :111: split at '\n', a last line without '\n' counts); else
+    // text/offs is a packed (bytes, offsets[npat+1]) batch.  Returns the records (page-locked,
+    // library-owned) and their number; *npat_out = patterns seen.
+    uint64_t search_host(const uint8_t* text, uint64_t len, const uint64_t* offs, uint64_t npat, bool lines, uint32_t first_id,
+                         uint32_t flags, uint32_t* counts, uint64_t counts_cap, edsbwt_occ** occ_out, uint64_t* npat_out) {
+        const auto t0 = std::chrono::steady_clock::now();
+        pipe_init();
+        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
+        const bool pin_in = host_pinned(text), pin_off = lines || host_pinned(offs), pin_cnt = host_pinned(counts);
+        // downloads by the copy engine (EDSBWT_D2H_KERNEL=1: kernel stores to mapped host memory;
+        // measured slower on MI355X: their PCIe stores slow the search kernels running beside them)
+        const bool sdma_down = env_double("EDSBWT_D2H_KERNEL", 0) == 0;
+        uint32_t* counts_dev = pin_cnt ? static_cast<uint32_t*>(host_dev_ptr(counts)) : nullptr;
+        std::vector<Chunk> ch = cut_chunks(text, len, offs, npat, lines);
+        {
+            const bool eager_req = !lines && pin_in && pin_off && env_double("EDSBWT_EAGER_UP", 0) != 0;
+            const bool compact_req = locate && env_double("EDSBWT_D2H_COMPACT", 0) != 0;
+            if (!eager_req && !compact_req && sdma_down && hsa_init())
+                return search_host_hsa(ch, text, offs, lines, pin_in, pin_off, pin_cnt, first_id, flags, counts, counts_cap, locate, occ_out,
+                                       npat_out, t0);
         }
         // page-locked inputs: every chunk's upload is queued at once, into its own 256-B aligned
         // place of one device buffer, so the copy engine never idles; pageable inputs are staged
