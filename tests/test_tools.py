@@ -70,3 +70,117 @@ def test_generator_reproducible_and_planted(oracle, tmp_path, cfg):
     offs = np.arange(0, 201 * 12, 12, dtype=np.uint64)
     counts, _, _ = oracle.Engine(str(tmp_path / "g")).search(buf, offs)
     assert (counts > 0).all()  # every planted pattern occurs
+
+
+def _string_check(tmp_path, data: bytes):
+    src = tmp_path / "in.txt"
+    src.write_bytes(data)
+    out = tmp_path / "norm"
+    if (tmp_path / "norm.eds").exists():
+        (tmp_path / "norm.eds").unlink()
+    r = subprocess.run([os.path.join(BUILD, "stringCheck"), str(src), str(out)], capture_output=True)
+    got = (tmp_path / "norm.eds").read_bytes() if (tmp_path / "norm.eds").exists() else None
+    return got, r
+
+
+def test_string_check_examples(tmp_path):
+    """stringCheck (stringCheck.cpp:11-106): brackets around solid stretches, comments dropped,
+    'Z' rejected; the console lines of the reference."""
+    cases = {
+        b"ACGT{A,C}GG{T,}A": b"{ACGT}{A,C}{GG}{T,}{A}",
+        b"{A,C}G": b"{A,C}{G}",
+        b"AC<note>{G,T}": b"{AC}{G,T}",
+        b"{A,C}{G}": b"{A,C}{G}",
+        b"{A,}T\n": b"{A,}{T\n}",       # the reference closes after a trailing newline
+        b"": b"",
+    }
+    for src, want in cases.items():
+        got, r = _string_check(tmp_path, src)
+        assert r.returncode == 0 and got == want, (src, got, r.stderr)
+        if src:
+            assert r.stdout.decode().startswith("stringCheck on ") and r.stdout.decode().endswith("Done.\n")
+    for bad in (b"Z", b"{A,Z}", b"AC<unclosed"):
+        got, r = _string_check(tmp_path, bad)
+        assert r.returncode == 1, bad
+    r = subprocess.run([os.path.join(BUILD, "stringCheck"), "only-one-arg"], capture_output=True)
+    assert r.returncode == 1 and b"usage:" in r.stderr
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_string_check_matches_restatement(tmp_path, seed):
+    """Random malformed inputs (missing brackets, comments, empty words, newlines, 0xFF, 'Z'):
+    the tool's bytes and exit code equal the line-by-line restatement (oracle/string_check.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import string_check as sc  # test infrastructure: the checker
+    rng = random.Random(500 + seed)
+    for _ in range(60):
+        parts = []
+        for _ in range(rng.randint(0, 12)):
+            k = rng.random()
+            if k < 0.35:
+                parts.append("".join(rng.choice("ACGT") for _ in range(rng.randint(1, 6))))
+            elif k < 0.75:
+                ws = ["".join(rng.choice("ACGTE") for _ in range(rng.randint(0, 3))) for _ in range(rng.randint(1, 4))]
+                parts.append("{" + ",".join(ws) + "}")
+            elif k < 0.85:
+                parts.append("<" + "".join(rng.choice("ACGT {},Z") for _ in range(rng.randint(0, 5))) + ">")
+            elif k < 0.9:
+                parts.append("\n")
+            elif k < 0.95:
+                parts.append("\xff")
+            else:
+                parts.append(rng.choice(["Z", "<", "}", "{"]))
+        data = "".join(parts).encode("latin-1")
+        want, code = sc.string_check(data)
+        got, r = _string_check(tmp_path, data)
+        assert r.returncode == code, (data, r.stderr)
+        if code == 0:
+            assert got == want, (data, got, want)
+
+
+def test_string_check_then_index(oracle, tmp_path):
+    """A bracket-less EDS normalised by stringCheck indexes and searches exactly like the
+    hand-bracketed one (EDS-BWTransform.sh's order: stringCheck, then the index writer)."""
+    raw = b"ACGT{A,C}GG{T,}ACAT{G,GA,}TTA"
+    (tmp_path / "raw.txt").write_bytes(raw)
+    subprocess.run([os.path.join(BUILD, "stringCheck"), str(tmp_path / "raw.txt"), str(tmp_path / "n")], check=True, capture_output=True)
+    (tmp_path / "h.eds").write_bytes(b"{ACGT}{A,C}{GG}{T,}{ACAT}{G,GA,}{TTA}")
+    assert (tmp_path / "n.eds").read_bytes() == (tmp_path / "h.eds").read_bytes()
+    _run("eds_transform", tmp_path / "n.eds", tmp_path / "ni")
+    oracle.transform(str(tmp_path / "h.eds"), str(tmp_path / "hi"))
+    for f in FILES:
+        assert (tmp_path / ("ni" + f)).read_bytes() == (tmp_path / ("hi" + f)).read_bytes(), f
+
+
+def test_msa_pattern_sampler(tmp_path):
+    """extract_patterns_from_msa (extract_patterns_from_msa.py:7-71): gaps removed, windows of
+    every long-enough record, NUM drawn without replacement, no trailing newline; with a seed the
+    draw equals random.sample over the materialised window list (the reference's way)."""
+    rng = random.Random(11)
+    recs = []
+    for r in range(7):
+        seq = "".join(rng.choice("ACGT-") for _ in range(rng.randint(5, 120)))
+        recs.append(f">seq{r} some header\n" + "\n".join(seq[i:i + 60] for i in range(0, len(seq), 60)) + "\n")
+    (tmp_path / "m.fa").write_text("".join(recs))
+    tool = os.path.join(ROOT, "eds-bwt_amd", "tools", "extract_patterns_from_msa.py")
+    subprocess.run(["python3", tool, str(tmp_path / "m.fa"), str(tmp_path / "p.txt"), "-l", "12", "-n", "40", "--seed", "5"], check=True)
+    got = (tmp_path / "p.txt").read_text()
+    assert not got.endswith("\n")
+    lines = got.split("\n")
+    # the reference's own steps, materialised
+    seqs, cur = [], []
+    for line in (tmp_path / "m.fa").read_text().splitlines(keepends=True):
+        if line.startswith(">"):
+            if cur:
+                seqs.append("".join(cur)); cur = []
+            continue
+        cur.append(line.strip().replace("-", ""))
+    if cur:
+        seqs.append("".join(cur))
+    pats = [s[i:i + 12] for s in seqs if len(s) >= 12 for i in range(len(s) - 12 + 1)]
+    assert lines == random.Random(5).sample(pats, 40)
+    assert len(set(map(tuple, [[i] for i in lines]))) <= 40 and all(len(p) == 12 and "-" not in p for p in lines)
+    r = subprocess.run(["python3", tool, str(tmp_path / "m.fa"), str(tmp_path / "q.txt"), "-l", "12", "-n", str(len(pats) + 1)],
+                       capture_output=True)
+    assert r.returncode != 0  # more than the windows: random.sample refuses, as in the reference
