@@ -2546,7 +2546,9 @@ struct Engine {
         if (hsa_amd_memory_copy_engine_status(cx.gpu, cx.cpu, &m_up) != HSA_STATUS_SUCCESS ||
             hsa_amd_memory_copy_engine_status(cx.cpu, cx.gpu, &m_down) != HSA_STATUS_SUCCESS)
             return false;
-        const uint32_t want_up = (uint32_t)env_double("EDSBWT_SDMA_UP", 0x1), want_down = (uint32_t)env_double("EDSBWT_SDMA_DOWN", 0x2);
+        // engines 2 and 3: measured fastest for this pair on MI355X (0 and 1 also carry the runtime's own
+        // copies; 4 and up reach the host at a fraction of the rate: tools/gpu_ab.sh sweeps)
+        const uint32_t want_up = (uint32_t)env_double("EDSBWT_SDMA_UP", 0x4), want_down = (uint32_t)env_double("EDSBWT_SDMA_DOWN", 0x8);
         auto pick = [](uint32_t avail, uint32_t want, uint32_t avoid) -> uint32_t {
             if (want && (avail & want) && want != avoid && !(want & (want - 1))) return want;
             for (uint32_t b = 1; b && b <= 0x8000u; b <<= 1)
