@@ -118,6 +118,10 @@ def main():
     ap.add_argument("--no-device", action="store_true", help="skip the device-resident leg")
     ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
+    ap.add_argument("--gather", default="none", choices=("none", "counts"),
+                    help="N>1 exchange: the (patterns, records) sizes are all-gathered (each rank's output offsets: every "
+                         "rank keeps its counts and records as its slice of the output); 'counts' also gathers the "
+                         "per-pattern counts to rank 0 over RCCL inside the timed step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -199,14 +203,17 @@ def main():
         return ptr, nocc
 
     def exchange(nocc):
-        # the path's one exchange step: sizes all-gathered, per-pattern counts gathered to rank 0 (RCCL/xGMI)
+        # the path's exchange step: every rank's (patterns, records) all-gathered — its offsets in
+        # the output (each rank writes its slice); --gather counts also gathers the
+        # per-pattern counts to rank 0 (RCCL/xGMI)
         if world == 1:
             return
         sizes = shard.exchange_sizes(npat, nocc, gdev)
-        src = d_counts_x if args.dist_backend == "nccl" else torch.from_numpy(counts[:npat].view(np.int32))
-        if args.dist_backend == "nccl":
-            d_counts_x.copy_(torch.from_numpy(counts[:npat].view(np.int32)), non_blocking=True)
-        shard.gather_counts(src, [int(x) for x in sizes[:, 0]])
+        if args.gather == "counts":
+            src = d_counts_x if args.dist_backend == "nccl" else torch.from_numpy(counts[:npat].view(np.int32))
+            if args.dist_backend == "nccl":
+                d_counts_x.copy_(torch.from_numpy(counts[:npat].view(np.int32)), non_blocking=True)
+            shard.gather_counts(src, [int(x) for x in sizes[:, 0]])
 
     # ---- timed: end-to-end (host memory -> host memory)
     for _ in range(args.warmup):
@@ -320,6 +327,9 @@ def main():
                        "parallelism": f"pattern-shard x{world}",
                        "timed_region": "edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> counts + records D2H "
                                        "(SURVEY §8(d)), plus the exchange step when N>1",
+                       "exchange": ("none (one GPU)" if world == 1 else
+                                    "sizes all-gathered (each rank keeps its counts + records as its output slice)"
+                                    + (" + counts gathered to rank 0 over RCCL" if args.gather == "counts" else "")),
                        "ktab_depth": idx.ktab_depth, "index_device_bytes": idx.device_bytes,
                        "cache_resident": bool(rank_bytes <= MI355X_MALL_BYTES)},
             "occurrences_per_step": int(total_occ / args.steps),
