@@ -143,10 +143,14 @@ constexpr int kDeepWide = 64;
 // shallowest depth worth a table
 constexpr double kKtabK = 15;  // D-mer ids stay below 2^32 (B^15 = 2^30 for B = 4)
 constexpr uint64_t kKtabMaxEntries = 1ull << 31;  // 8 GiB of offsets at most
-constexpr double kKtabItems = 268435456.0;  // 2^28 intervals (2 GiB)
+constexpr double kKtabItems = 268435456.0;  // at least 2^28 intervals (2 GiB) ...
+constexpr double kKtabHbmShare = 0.15;      // ... or as many as kKtabHbmShare of the free HBM holds at
+constexpr double kKtabBuildBytes = 40.0;    // the build's transient bytes per interval (capture + sort)
 constexpr uint32_t kKtabMinDepth = 2;
-// ... and no deeper than B^(K-1) <= kKtabOver * N: most longer D-mers do not occur
-constexpr double kKtabOver = 4.0;
+// ... and no deeper than B^(K-1) <= kKtabOver * N: most longer D-mers do not occur (an
+// entry is 12 B; C2, 12.5M rows: depth 15 = 12.9 GB of the 288 GB, searches 4.6x faster
+// than at depth 11)
+constexpr double kKtabOver = 64.0;
 // levels2() result meaning "the batch needs the ordered path"
 constexpr uint32_t kNeedOrdered = 0xFFFFFFFFu;
 
@@ -911,7 +915,11 @@ struct Engine {
     void build_ktab() {
         const uint32_t B = sigma - 1;
         uint32_t K = (uint32_t)env_double("EDSBWT_KTAB_K", kKtabK);
-        const uint64_t budget = (uint64_t)env_double("EDSBWT_KTAB_ITEMS", kKtabItems);
+        // the interval budget scales with the device's free HBM (EDSBWT_KTAB_ITEMS overrides)
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); free_b = 0; }
+        const double by_hbm = kKtabHbmShare * (double)free_b / kKtabBuildBytes;
+        const uint64_t budget = (uint64_t)env_double("EDSBWT_KTAB_ITEMS", std::max(kKtabItems, by_hbm));
         K = std::min(K, 16u);  // a search reads a node's D-mer from its sorted key chunk 0 (>= 16 symbols)
         if (B < 1 || K < 2) return;
         auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
@@ -1603,8 +1611,12 @@ struct Engine {
                    sorted_chunk(1, P), (const uint32_t*)ktab_off.p, kt_kid.p, kt_cnt.p);
             const uint32_t n0 = scan_u32(kt_cnt.p, kt_pos, M0);
             iu[1].ensure(n0); ib[1].ensure(n0); ie[1].ensure(n0);
-            launch(KC_NODES, k_ktab_emit, ((size_t)M0 + 63) / 64 * 64, M0, (const uint32_t*)kt_kid.p, (const uint32_t*)kt_pos.p, (const uint32_t*)ktab_off.p,
-                   (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p, iu[1].p, ib[1].p, ie[1].p);
+            if ((uint64_t)n0 > 256ull * M0)  // few nodes, long lists: one thread per item
+                launch(KC_NODES, k_ktab_emit_flat, n0, n0, M0, (const uint32_t*)kt_kid.p, (const uint32_t*)kt_pos.p, (const uint32_t*)ktab_off.p,
+                       (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p, iu[1].p, ib[1].p, ie[1].p);
+            else
+                launch(KC_NODES, k_ktab_emit, ((size_t)M0 + 63) / 64 * 64, M0, (const uint32_t*)kt_kid.p, (const uint32_t*)kt_pos.p,
+                       (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p, iu[1].p, ib[1].p, ie[1].p);
             cur = 1;
             Mcur = M0;
             ncur = n0;

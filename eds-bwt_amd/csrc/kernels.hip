@@ -2507,6 +2507,27 @@ __global__ void __launch_bounds__(256) k_ktab_emit(uint32_t M, const uint32_t* _
     }
 }
 
+// the same items, one thread per item: for a few nodes with long lists (a shallow table
+// start of a grouped search holds millions of intervals per node, which k_ktab_emit would
+// copy 64 at a time per wave).  pos[0..M] = exclusive scan of the list lengths; item q
+// belongs to the last node u with pos[u] <= q (nodes with empty lists share their pos)
+__global__ void __launch_bounds__(256) k_ktab_emit_flat(uint32_t n0, uint32_t M, const uint32_t* __restrict__ kid, const uint32_t* __restrict__ pos,
+                                                        const uint32_t* __restrict__ toff, const uint32_t* __restrict__ tb,
+                                                        const uint32_t* __restrict__ te, uint32_t* __restrict__ iu, uint32_t* __restrict__ ib,
+                                                        uint32_t* __restrict__ ie) {
+    GRID_STRIDE(q, n0) {
+        uint32_t lo = 0, hi = M;  // pos[lo] <= q < pos[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pos[mid] <= (uint32_t)q) lo = mid; else hi = mid;
+        }
+        const uint32_t src = toff[kid[lo]] + ((uint32_t)q - pos[lo]);
+        iu[q] = lo;
+        ib[q] = tb[src];
+        ie[q] = te[src];
+    }
+}
+
 // ------------------------------------------- pattern-file lines (host pipeline)
 // A chunk of the pattern file as it lies on disk (MOVE_EDSBWTSearch.cpp:111 reads it with
 // getline): the '\n' bytes are dropped and the offsets of the lines are written, so the
