@@ -3213,6 +3213,113 @@ struct edsbwt_index {
         return EDSBWT_E_DEVICE;                                          \
     }
 
+namespace edsbwt {
+// ------------------------------------------------------------ index writer: GPU suffix sort
+// The generalized suffix array eds_transform needs (gsufsort's order over word·'#',
+// EDS-BWTransform.sh:26): suffixes compared up to and including their word's '#' ('#' = code 0,
+// the smallest), equal ones by text position (= word id).  Prefix doubling over ranks: the
+// first key packs each suffix's next cpw codes (zeros after its '#'); round h sorts by
+// (rank[t], rank[t+h]) — or (rank[t], 0) when t's '#' lies within its first h codes — stably,
+// from the previous order, so equal keys keep position order; it stops once h passes the
+// longest word.  O(log(longest word)) radix sorts of N 64-bit keys.
+__global__ void k_gsa_dist(const uint64_t* __restrict__ ends, uint64_t W, uint64_t n, uint32_t* __restrict__ dist) {
+    GRID_STRIDE(t, n) {
+        uint64_t lo = 0, hi = W;  // first '#' at or after t
+        while (lo < hi) {
+            const uint64_t m = (lo + hi) >> 1;
+            if (ends[m] < t) lo = m + 1; else hi = m;
+        }
+        dist[t] = (uint32_t)(ends[lo] - t);
+    }
+}
+__global__ void k_gsa_key0(const uint8_t* __restrict__ codes, const uint32_t* __restrict__ dist, uint64_t n, uint32_t b, uint32_t cpw,
+                           uint64_t* __restrict__ key, uint32_t* __restrict__ pos) {
+    GRID_STRIDE(t, n) {
+        const uint32_t m = min(dist[t] + 1, cpw);  // codes through the '#', at most cpw
+        uint64_t k = 0;
+        for (uint32_t j = 0; j < cpw; j++) k = (k << b) | (j < m ? (uint64_t)codes[t + j] : 0ull);
+        key[t] = k;
+        pos[t] = (uint32_t)t;
+    }
+}
+// group-start index of sorted entry i (heads by key inequality), as rank of its suffix
+__global__ void k_gsa_heads(const uint64_t* __restrict__ key, uint64_t n, uint32_t* __restrict__ head) {
+    GRID_STRIDE(i, n) head[i] = (i == 0 || key[i] != key[i - 1]) ? (uint32_t)i : 0u;
+}
+__global__ void k_gsa_rank(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ grp, uint64_t n, uint32_t* __restrict__ rank) {
+    GRID_STRIDE(i, n) rank[sa[i]] = grp[i];
+}
+__global__ void k_gsa_key(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ rank, const uint32_t* __restrict__ dist, uint64_t n,
+                          uint64_t h, uint64_t* __restrict__ key) {
+    GRID_STRIDE(i, n) {
+        const uint32_t t = sa[i];
+        key[i] = (uint64_t)rank[t] << 32 | (dist[t] < h ? 0ull : (uint64_t)rank[t + h] + 1ull);
+    }
+}
+struct MaxOp {
+    __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+
+static void gsa_sort(const uint8_t* h_codes, uint64_t n, const uint64_t* h_ends, uint64_t W, uint32_t b, int device, uint32_t* h_sa,
+                     double* ms_out) {
+    if (!n) return;
+    if (n >= 0xFFFFFFFFull) throw Fail(EDSBWT_E_UNSUPPORTED, "text longer than 2^32-1 symbols");
+    if (b < 1 || b > 8) throw Fail(EDSBWT_E_ARG, "bits per code must be 1..8");
+    if (!W || h_ends[W - 1] != n - 1) throw Fail(EDSBWT_E_ARG, "the text must end with a word's '#'");
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    struct StreamGuard { hipStream_t s; ~StreamGuard() { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); } } sg{s};
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t cpw = 64 / b;
+    DBuf<uint8_t> codes;
+    DBuf<uint64_t> ends, k1, k2;
+    DBuf<uint32_t> dist, sa1, sa2, grp, rank;
+    DBuf<uint8_t> tmp;
+    codes.ensure(n + cpw);
+    ends.ensure(W);
+    HIPCHK(hipMemcpyAsync(codes.p, h_codes, n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(codes.p + n, 0, cpw, s));
+    HIPCHK(hipMemcpyAsync(ends.p, h_ends, W * 8, hipMemcpyHostToDevice, s));
+    dist.ensure(n); k1.ensure(n); k2.ensure(n); sa1.ensure(n); sa2.ensure(n); grp.ensure(n); rank.ensure(n);
+    const unsigned G = (unsigned)std::min<uint64_t>(65535, (n + 255) / 256);
+    hipLaunchKernelGGL(k_gsa_dist, dim3(G), dim3(256), 0, s, (const uint64_t*)ends.p, W, n, dist.p);
+    hipLaunchKernelGGL(k_gsa_key0, dim3(G), dim3(256), 0, s, (const uint8_t*)codes.p, (const uint32_t*)dist.p, n, b, cpw, k1.p, sa1.p);
+    HIPCHK(hipGetLastError());
+    const int nbits = (int)std::max<uint32_t>(1, 64 - __builtin_clzll((unsigned long long)n));  // ranks < n
+    auto sort = [&](int end_bit) {
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, sa1.p, sa2.p, (int)n, 0, end_bit, s));
+        tmp.ensure(tb);
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, sa1.p, sa2.p, (int)n, 0, end_bit, s));
+        std::swap(k1.p, k2.p); std::swap(k1.cap, k2.cap);
+        std::swap(sa1.p, sa2.p); std::swap(sa1.cap, sa2.cap);
+    };
+    auto ranks = [&]() {
+        hipLaunchKernelGGL(k_gsa_heads, dim3(G), dim3(256), 0, s, (const uint64_t*)k1.p, n, sa2.p);
+        size_t tb = 0;
+        HIPCHK(hipcub::DeviceScan::InclusiveScan(nullptr, tb, sa2.p, grp.p, MaxOp{}, (int)n, s));
+        tmp.ensure(tb);
+        HIPCHK(hipcub::DeviceScan::InclusiveScan(tmp.p, tb, sa2.p, grp.p, MaxOp{}, (int)n, s));
+        hipLaunchKernelGGL(k_gsa_rank, dim3(G), dim3(256), 0, s, (const uint32_t*)sa1.p, (const uint32_t*)grp.p, n, rank.p);
+        HIPCHK(hipGetLastError());
+    };
+    sort((int)(b * cpw));
+    // longest word (with its '#'): the rounds stop once h passes it
+    uint64_t maxw = 0, prev = 0;
+    for (uint64_t w = 0; w < W; w++) { maxw = std::max<uint64_t>(maxw, h_ends[w] + 1 - prev); prev = h_ends[w] + 1; }
+    for (uint64_t h = cpw; h < maxw; h *= 2) {
+        ranks();
+        hipLaunchKernelGGL(k_gsa_key, dim3(G), dim3(256), 0, s, (const uint32_t*)sa1.p, (const uint32_t*)rank.p, (const uint32_t*)dist.p, n, h, k1.p);
+        HIPCHK(hipGetLastError());
+        sort(std::min(64, 32 + nbits + 1));
+    }
+    HIPCHK(hipMemcpyAsync(h_sa, sa1.p, n * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (ms_out) *ms_out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace edsbwt
+
 extern "C" {
 
 int edsbwt_abi_version(void) { return EDSBWT_ABI_VERSION; }
@@ -3328,6 +3435,15 @@ int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st) {
     if (!idx || !st) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
     *st = idx->eng->st;
     return 0;
+}
+
+int edsbwt_gsa(const uint8_t* codes, uint64_t n, const uint64_t* word_ends, uint64_t n_words, uint32_t bits, int device,
+               uint32_t* sa, double* ms) {
+    if ((n && (!codes || !word_ends || !sa))) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    edsbwt::gsa_sort(codes, n, word_ends, n_words, bits, device, sa, ms);
+    return 0;
+    ABI_CATCH
 }
 
 }  // extern "C"

@@ -14,9 +14,11 @@
 // compared up to and including their word's '#', '#' smallest, equal suffixes by
 // word id.  Built here by a parallel LSD radix sort on packed prefixes of
 // floor(64/b) symbols (b = bits per symbol code), ties on unterminated prefixes
-// refined chunk by chunk.  OpenMP, no GPU.
+// refined chunk by chunk (OpenMP), or with --gpu [device] on an MI355X by prefix
+// doubling in libedsbwt.so (edsbwt_gsa: O(log longest word) radix sorts); both give
+// the same order, so the same files.
 //
-// usage: eds_transform <file.eds> <base> [--no-runs] [--threads T]
+// usage: eds_transform <file.eds> <base> [--no-runs] [--threads T] [--gpu [device]]
 #include <omp.h>
 
 #include <algorithm>
@@ -27,6 +29,7 @@
 #include <vector>
 
 #include "eds_common.h"
+#include "../../include/edsbwt.h"
 
 using namespace edsbwt_tools;
 
@@ -104,9 +107,11 @@ int main(int argc, char** argv) {
     const std::string in = argv[1], base = argv[2];
     bool runs = true;
     int T = omp_get_max_threads();
+    int gpu = -1;
     for (int i = 3; i < argc; i++) {
         if (!std::strcmp(argv[i], "--no-runs")) runs = false;
         else if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) T = std::max(1, std::atoi(argv[++i]));
+        else if (!std::strcmp(argv[i], "--gpu")) gpu = (i + 1 < argc && argv[i + 1][0] != '-') ? std::atoi(argv[++i]) : 0;
     }
     try {
         double t0 = now();
@@ -132,6 +137,23 @@ int main(int argc, char** argv) {
         const int cpw = 64 / b;
         const uint64_t lastmask = (1ull << b) - 1;
         const int top = b * (cpw - 1);
+        std::vector<KP> kp(tot);
+        size_t ngroups = 0;
+        double gpu_ms = -1;
+        if (gpu >= 0) {
+            // the suffix sort on the GPU (edsbwt_gsa): codes with '#' = 0 and the words' ends
+            std::vector<uint8_t> codes(tot);
+            std::vector<uint64_t> ends(W);
+#pragma omp parallel for num_threads(T)
+            for (int64_t i = 0; i < (int64_t)tot; i++) codes[i] = (uint8_t)code[Tx[i]];
+#pragma omp parallel for num_threads(T)
+            for (int64_t w = 0; w < (int64_t)W; w++) ends[w] = (w + 1 < (int64_t)W ? E.wstart[w + 1] : tot) - 1;
+            std::vector<uint32_t> sa(tot);
+            if (edsbwt_gsa(codes.data(), tot, ends.data(), W, (uint32_t)b, gpu, sa.data(), &gpu_ms) != 0)
+                throw std::runtime_error(std::string("edsbwt_gsa: ") + edsbwt_last_error());
+#pragma omp parallel for num_threads(T)
+            for (int64_t i = 0; i < (int64_t)tot; i++) kp[i] = KP{0, sa[i], 0};
+        } else {
         // packed prefix of every suffix (right to left inside each word)
         std::vector<uint64_t> key0(tot);
 #pragma omp parallel for schedule(dynamic, 4096) num_threads(T)
@@ -145,7 +167,6 @@ int main(int argc, char** argv) {
                 key0[t] = key;
             }
         }
-        std::vector<KP> kp(tot);
 #pragma omp parallel for num_threads(T)
         for (int64_t i = 0; i < (int64_t)tot; i++) kp[i] = KP{key0[i], (uint32_t)i, 0};
         radix_sort(kp, b * cpw, T);
@@ -169,7 +190,8 @@ int main(int argc, char** argv) {
         };
 #pragma omp parallel for schedule(dynamic, 1) num_threads(T)
         for (int64_t g = 0; g < (int64_t)groups.size(); g++) std::sort(kp.begin() + groups[g].first, kp.begin() + groups[g].second, cmp);
-        std::vector<uint64_t>().swap(key0);
+        ngroups = groups.size();
+        }
         double t1 = now();
         // rows: drop the 'Z#' suffixes of empty words (remove_empty_symbols, :397,:438)
         const uint64_t N = tot - E.empty;
@@ -279,8 +301,13 @@ int main(int argc, char** argv) {
             write_file(base + "_runs.txt", rt.data(), rt.size());
         }
         double t2 = now();
-        std::fprintf(stderr, "eds_transform: %llu words, %llu rows, sigma %u, %zu tie groups; sort %.2fs, write %.2fs (%d threads)\n",
-                     (unsigned long long)W, (unsigned long long)N, sigma, groups.size(), t1 - t0, t2 - t1, T);
+        if (gpu >= 0)
+            std::fprintf(stderr, "eds_transform: %llu words, %llu rows, sigma %u; GPU suffix sort %.3fs (device %d, %.1f ms on the device), "
+                                 "sort total %.2fs, write %.2fs (%d threads)\n",
+                         (unsigned long long)W, (unsigned long long)N, sigma, gpu_ms / 1e3, gpu, gpu_ms, t1 - t0, t2 - t1, T);
+        else
+            std::fprintf(stderr, "eds_transform: %llu words, %llu rows, sigma %u, %zu tie groups; sort %.2fs, write %.2fs (%d threads)\n",
+                         (unsigned long long)W, (unsigned long long)N, sigma, ngroups, t1 - t0, t2 - t1, T);
         std::fprintf(stderr, "File %s done.\n", in.c_str());
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());

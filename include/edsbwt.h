@@ -180,6 +180,16 @@ const char* edsbwt_kernel_name(int k);
 uint64_t edsbwt_format_csv(const edsbwt_occ* occ, uint64_t nocc, char* buf, uint64_t cap, int threads);
 
 const char* edsbwt_last_error(void);
+
+/* Index writer support (eds_transform --gpu; replaces gsufsort's suffix sort, EDS-BWTransform.sh:26
+ * and gsufsort --da over eds_to_fasta's output): the generalized suffix array of the words'
+ * texts, each word followed by its terminator.  codes[n]: symbol codes, the terminator '#' = 0
+ * and the other symbols 1..2^bits-1 in byte order; word_ends[n_words]: positions of the
+ * terminators, ascending, the last one n-1.  sa[n] receives the text positions in suffix
+ * order: suffixes compared up to and including their word's terminator, equal ones by
+ * position.  *ms (optional): device time including the transfers. */
+int edsbwt_gsa(const uint8_t* codes, uint64_t n, const uint64_t* word_ends, uint64_t n_words, uint32_t bits, int device,
+               uint32_t* sa, double* ms);
 int edsbwt_abi_version(void);
 
 #ifdef __cplusplus
