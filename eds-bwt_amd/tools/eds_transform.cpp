@@ -7,8 +7,8 @@
 //   <base>_info.aux   N, nText, sigma, alphabet, EOF ids, tableOcc  da_to_everything.cpp:150-254
 //   <base>_bwt_<j>.aux  pile j of the BWT                      da_to_everything.cpp:185-213
 //   <base>_runs.aux / <base>_runs.txt  run heads and LF(run head)  da_to_everything.cpp:62-109,414-443
-// (_bv_<j>.aux, the sdsl rrr_vector copies of "L=='#'" per pile, are not written:
-// every reader here takes numEOF[j] from tableOcc.)
+//   <base>_bv_<j>.aux   pile j's "L == '#'" as sdsl rrr_vector<63>  da_to_everything.cpp:170-171,218-236
+//                       (tools/sdsl_rrr.h; parity unpinned: the search reads numEOF[j] from tableOcc)
 //
 // Suffix order (gsufsort's generalized suffix array over word·'#'): suffixes are
 // compared up to and including their word's '#', '#' smallest, equal suffixes by
@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "eds_common.h"
+#include "sdsl_rrr.h"
 #include "../../include/edsbwt.h"
 
 using namespace edsbwt_tools;
@@ -242,6 +243,14 @@ int main(int argc, char** argv) {
             for (int t = 0; t < T; t++)
                 for (uint32_t h = 0; h < sigma; h++) tocc[(size_t)j * sigma + h] += part[t][h];
             write_file(base + "_bwt_" + std::to_string(j) + ".aux", L.data() + lo, n);
+            {  // _bv_<j>.aux: the pile's '#' rows
+                std::vector<uint64_t> bits((n + 63) / 64 + 1, 0);
+                for (uint64_t i = 0; i < n; i++)
+                    if (L[lo + i] == '#') bits[i >> 6] |= 1ull << (i & 63);
+                static const Rrr63 rrr;
+                const std::vector<uint8_t> bytes = rrr.build(bits, n);
+                write_file(base + "_bv_" + std::to_string(j) + ".aux", bytes.data(), bytes.size());
+            }
         }
         write_file(base + ".ebwt", L.data(), N);
         {

@@ -184,3 +184,92 @@ def test_msa_pattern_sampler(tmp_path):
     r = subprocess.run(["python3", tool, str(tmp_path / "m.fa"), str(tmp_path / "q.txt"), "-l", "12", "-n", str(len(pats) + 1)],
                        capture_output=True)
     assert r.returncode != 0  # more than the windows: random.sample refuses, as in the reference
+
+
+def _rrr63_decode(raw: bytes):
+    """Decode an sdsl rrr_vector<63, int_vector<>, 32> as tools/sdsl_rrr.h writes it (member order
+    m_size, bt, btnr, btnrp, rank, invert): the bits, the rank samples and the total."""
+    from math import comb
+    import struct
+    at = 0
+
+    def u64():
+        nonlocal at
+        v = struct.unpack_from("<Q", raw, at)[0]
+        at += 8
+        return v
+
+    def intvec(var):
+        nonlocal at
+        nbits = u64()
+        w = raw[at] if var else 1
+        at += 1 if var else 0
+        nw = (nbits + 63) // 64
+        words = struct.unpack_from(f"<{nw}Q", raw, at)
+        at += 8 * nw
+        big = 0
+        for i, x in enumerate(words):
+            big |= x << (64 * i)
+        return big, nbits, w
+
+    m = u64()
+    bt, btb, btw = intvec(True)
+    btnr, btnrb, _ = intvec(False)
+    btnrp, pb, pw = intvec(True)
+    rank, rb, rw = intvec(True)
+    inv, ib, _ = intvec(False)
+    assert at == len(raw) and btw == 6 and inv == 0
+    get = lambda big, i, w: (big >> (i * w)) & ((1 << w) - 1)
+    nb = btb // btw
+    assert nb == (m + 63) // 63
+    space = [0 if comb(63, k) == 1 else (comb(63, k)).bit_length() for k in range(64)]
+    bits, pos, ones = 0, 0, 0
+    samples = []
+    for i in range(nb):
+        if i % 32 == 0:
+            assert get(btnrp, i // 32, pw) == pos or i * 63 >= m
+            samples.append(get(rank, i // 32, rw))
+        k = get(bt, i, btw)
+        sp = space[k]
+        nr = (btnr >> pos) & ((1 << sp) - 1) if sp else 0
+        pos += sp
+        blk, kk, nn = 0, k, 63
+        if k == 63:
+            blk = (1 << 63) - 1
+        else:
+            for p in range(63):  # inverse of bin_to_nr
+                if kk == 0:
+                    break
+                c = comb(nn - 1, kk)
+                if nr >= c:
+                    blk |= 1 << p
+                    nr -= c
+                    kk -= 1
+                nn -= 1
+        assert bin(blk).count("1") == k
+        bits |= blk << (63 * i)
+        ones += k
+    assert get(rank, rb // rw - 1, rw) == ones
+    return bits, m, samples, ones
+
+
+def test_rrr_bv_files(oracle, tmp_path):
+    """<base>_bv_<j>.aux (da_to_everything.cpp:170-171,218-236): every pile's '#' rows as an sdsl
+    rrr_vector<63>.  The search never reads them; the byte layout follows sdsl-lite 2.x and is
+    unpinned (no sdsl here), so this decodes every block back and checks the piles and ranks."""
+    rng = random.Random(31)
+    for t in range(4):
+        segs = edsgen.random_eds(rng, rng.randint(1, 2500), p_empty=0.3 if t % 2 else 0.0, lmax=3 + 9 * t)
+        eds = tmp_path / f"x{t}.eds"
+        eds.write_text(edsgen.eds_text(segs))
+        _run("eds_transform", eds, tmp_path / f"p{t}")
+        info = (tmp_path / f"p{t}_info.aux").read_bytes()
+        sigma = info[8]
+        for j in range(sigma):
+            pile = (tmp_path / f"p{t}_bwt_{j}.aux").read_bytes()
+            bits, m, samples, ones = _rrr63_decode((tmp_path / f"p{t}_bv_{j}.aux").read_bytes())
+            assert m == len(pile)
+            want = sum(1 << i for i, c in enumerate(pile) if c == ord("#"))
+            assert bits == want and ones == pile.count(b"#")
+            for s_i, r in enumerate(samples):
+                assert r == pile[: min(len(pile), s_i * 32 * 63)].count(b"#")
