@@ -1113,10 +1113,11 @@ struct Engine {
             for (int c = full ? (int)nch - 1 : 0; c >= 0; c--) {
                 const uint32_t nsym = std::min(spc, Lmax - (uint32_t)c * spc);
                 // rocPRIM (ROCm 7.2) mis-sorts u64 keys over [begin_bit, 64) when begin_bit > 0
-                // (measured: tools/diag/sort_check.hip): 4-bit codes fill all 64 bits, so their
-                // partial chunks are sorted over the whole word
+                // (measured: tools/diag/sort_check.hip): every chunk is sorted from bit 0 (the
+                // zero digits below a partial chunk's symbols cost passes, not correctness)
                 const int end_bit = (int)(bps * spc);
-                const int begin_bit = end_bit == 64 ? 0 : (int)(bps * (spc - nsym));
+                const int begin_bit = 0;
+                (void)nsym;
                 const uint64_t* kin = keys.p + (size_t)c * P;
                 if (full && c != (int)nch - 1) {  // later passes sort the chunk in the current order
                     launch(KC_TRIE, k_gather_key, P, kin, (const uint32_t*)perm.p, P, kc.p);

@@ -680,3 +680,20 @@ def test_deferred_checks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             gc, go = idx.search((buf, offs), locate=locate)
             assert np.array_equal(gc, oc) and (not locate or np.array_equal(go, oo))
             assert idx.stats()["redo_searches"] == 1
+
+
+def test_short_patterns_3bit_many_gpu(oracle, edsbwt, tmp_path):
+    """More than 2000 patterns shorter than one 3-bit key chunk (21 symbols), so the trie-order
+    radix sort runs over partial chunks of many keys, on the trie path (direct=False) and the
+    ordered path: identical to the oracle (rocPRIM partial bit ranges)."""
+    rng = random.Random(2121)
+    segs = edsgen.random_eds(rng, 3000, lmax=8, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(2, 20)) or "ACG" for _ in range(2500)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(1, 20))) for _ in range(2500)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    with edsbwt.Index(base) as idx:
+        for kw in ({"direct": False}, {"ordered": True}, {"direct": False, "ktab": False}):
+            gc, go = idx.search((buf, offs), **kw)
+            assert np.array_equal(gc, oc) and np.array_equal(go, oo), kw
