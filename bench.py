@@ -116,6 +116,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=0)
     ap.add_argument("--no-device", action="store_true", help="skip the device-resident leg")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="profiling runs: only the device-resident leg (its kernel averages then match a rocprofv3 "
+                         "trace of the whole run); the line's value is then the device-resident rate")
     ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
     ap.add_argument("--gather", default="none", choices=("none", "counts"),
@@ -216,7 +219,7 @@ def main():
             shard.gather_counts(src, [int(x) for x in sizes[:, 0]])
 
     # ---- timed: end-to-end (host memory -> host memory)
-    for _ in range(args.warmup):
+    for _ in range(0 if args.no_e2e else args.warmup):
         _, nocc = e2e_step()
         exchange(nocc)
     barrier()
@@ -226,7 +229,7 @@ def main():
     held = (0, 0)
     total_occ = 0
     walls = []
-    for i in range(args.steps):
+    for i in range(0 if args.no_e2e else args.steps):
         ta = time.perf_counter()
         last = i == args.steps - 1
         ptr, nocc = e2e_step(keep=last)
@@ -242,6 +245,9 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     e2e_stats = idx.stats()
+    if args.no_e2e:
+        e2e_stats = dict(e2e_stats, ms_wall=0.0, found=0)
+        walls = [0.0]
     per_rank = [search_ms / args.steps, exch_ms / args.steps]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
@@ -295,12 +301,15 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d_elapsed = float(tt.item())
         dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": idx.stats(), "d_counts": d_counts}
-        if not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
+        if not args.no_e2e and not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
             raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")
 
     if rank == 0:
         ms_step = 1000.0 * elapsed / args.steps
         total_pats = npat * world if w.per_gpu else (args.patterns or w.patterns)  # every rank's shard
+        if args.no_e2e:  # profiling run: the device-resident rate stands in (labelled below)
+            elapsed = dres["elapsed"] if dres else 1.0
+            ms_step = 1000.0 * elapsed / args.steps
         value = total_pats * args.steps / elapsed
         rows = idx.n_rows
         # tables the deep kernels gather from: occ blocks (1 B/row), rent1 (sigma/2 B/row), rent2 (10 B/row)
@@ -325,8 +334,9 @@ def main():
                                    "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
                                   if locate else "count-only"),
                        "parallelism": f"pattern-shard x{world}",
-                       "timed_region": "edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> counts + records D2H "
-                                       "(SURVEY §8(d)), plus the exchange step when N>1",
+                       "timed_region": ("device-resident leg only (--no-e2e profiling run)" if args.no_e2e else
+                                        "edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> counts + records D2H "
+                                        "(SURVEY §8(d)), plus the exchange step when N>1"),
                        "exchange": ("none (one GPU)" if world == 1 else
                                     "sizes all-gathered (each rank keeps its counts + records as its output slice)"
                                     + (" + counts gathered to rank 0 over RCCL" if args.gather == "counts" else "")),
@@ -336,7 +346,7 @@ def main():
             "found_per_step": int(e2e_stats["found"]) if world == 1 else None,
             "e2e": {"ms_wall_per_call": round(float(np.mean(walls)), 3), "chunks": e2e_stats["chunks"],
                     "bytes_h2d": e2e_stats["bytes_h2d"], "bytes_d2h": e2e_stats["bytes_d2h"],
-                    "pcie_gbs": round((e2e_stats["bytes_h2d"] + e2e_stats["bytes_d2h"]) / (np.mean(walls) * 1e-3) / 1e9, 2),
+                    "pcie_gbs": round((e2e_stats["bytes_h2d"] + e2e_stats["bytes_d2h"]) / max(1e-9, np.mean(walls) * 1e-3) / 1e9, 2),
                     "device_ms_per_call": round(e2e_stats["ms_total"], 3),
                     "per_rank_search_exchange_ms": per_rank_all},
             "bs_took": round(elapsed / args.steps, 6),
