@@ -188,6 +188,7 @@ struct Engine {
     DBuf<uint32_t> gpos, wrow;
     uint64_t tlen = 0;
     bool have_text = false;
+    bool kt1_pos = false;  // k_ktab_one's one-row entries carry the row's text position (kernels.h KIdx)
     bool text_deep = env_double("EDSBWT_TEXT_DEEP", 1) != 0;
     bool text_on = true;     // per search (EDSBWT_NO_TEXT, the walk and table locate modes clear it)
     DBuf<uint4> samples;     // locate samples (word, offset, segment, word in segment) of rows whose offset % 2^kSampleShift == 0
@@ -440,6 +441,7 @@ struct Engine {
         X.gpos = gpos.p;
         X.wrow = wrow.p;
         X.text_deep = text_deep ? 1u : 0u;
+        X.kt1_pos = kt1_pos ? 1u : 0u;
         return X;
     }
 
@@ -977,8 +979,9 @@ struct Engine {
         HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
         if (N < 0x80000000u) {  // inline single intervals need bit 63 free
             ktab_one.ensure(E + 1);
+            kt1_pos = have_text && gpos.p && N < 0x40000000u && tlen < 0x80000000ull && env_double("EDSBWT_KT1_POS", 1) != 0;
             launch(KC_TABLE, k_ktab_one, E + 1, E, (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p,
-                   ktab_one.p);
+                   ktab_one.p, kt1_pos ? (const uint32_t*)gpos.p : (const uint32_t*)nullptr);
             device_bytes += (E + 1) * 8;
         }
         HIPCHK(hipStreamSynchronize(stream));

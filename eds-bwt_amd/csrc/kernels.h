@@ -94,6 +94,8 @@ struct KIdx {
     const uint32_t* gpos;      // [N] text position of row x's suffix (word start + offset)
     const uint32_t* wrow;      // [W] row of each word's whole-word suffix (offset 0)
     uint32_t text_deep;        // k_deep compares single rows too (EDSBWT_TEXT_DEEP, A/B)
+    uint32_t kt1_pos;          // the direct start's inline D-mer entries of ONE row hold that row's
+                               // text position too (k_ktab_one): bit 62 set, gpos in bits [31, 62)
 };
 
 }  // namespace edsbwt

@@ -952,9 +952,15 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             w = make_uint4((uint32_t)i, D0, ~0u, 0u);
         } else if (n0 == 1) {
             uint32_t b, e;
+            uint32_t g1 = ~0u;  // the row's text position when the table entry holds it
             if (kt1) {
-                b = (uint32_t)ent;
-                e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+                if (X.kt1_pos && ((ent >> 62) & 1)) {
+                    b = e = (uint32_t)ent & 0x7fffffffu;
+                    g1 = (uint32_t)(ent >> 31) & 0x7fffffffu;
+                } else {
+                    b = (uint32_t)ent;
+                    e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+                }
             } else {
                 b = ib[ioff[u]];
                 e = ie[ioff[u]];
@@ -974,8 +980,8 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                 // equals the pattern's, so the next k = min(o, m) characters are decided by comparing
                 // them with the text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row)
                 const uint4 s = X.samples[b];
-                const uint32_t g = X.gpos[b];
-                n_blk += 3;
+                const uint32_t g = g1 != ~0u ? g1 : X.gpos[b];
+                n_blk += g1 != ~0u ? 2 : 3;
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 bool eq = true, valid_codes = true;
@@ -2430,11 +2436,17 @@ __global__ void k_ktab_bounds(uint64_t E, const uint64_t* __restrict__ key, uint
 
 // per D-mer: its one interval inline (bit 63 | e << 32 | b; rows < 2^31) or its list's
 // length << 32 | offset — one 8-B read per pattern at the direct start
+// gpos (N < 2^30, text < 2^31): a one-row interval's entry also holds that row's text position,
+// so the single-row text compare of the direct start reads no gpos line: bit 63 | bit 62 |
+// gpos << 31 | row (other inline intervals keep e < 2^30 in bits [32, 62), bit 62 clear)
 __global__ void k_ktab_one(uint64_t E, const uint32_t* __restrict__ off, const uint32_t* __restrict__ b, const uint32_t* __restrict__ e,
-                           uint64_t* __restrict__ one) {
+                           uint64_t* __restrict__ one, const uint32_t* __restrict__ gpos) {
     GRID_STRIDE(u, E + 1) {
         const uint32_t o = off[u], n = off[u + 1] - o;
-        one[u] = n == 1 ? (1ull << 63 | (uint64_t)e[o] << 32 | b[o]) : ((uint64_t)n << 32 | o);
+        if (n == 1 && gpos && b[o] == e[o])
+            one[u] = 3ull << 62 | (uint64_t)(gpos[b[o]] & 0x7fffffffu) << 31 | (b[o] & 0x7fffffffu);
+        else
+            one[u] = n == 1 ? (1ull << 63 | (uint64_t)e[o] << 32 | b[o]) : ((uint64_t)n << 32 | o);
     }
 }
 
