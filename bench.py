@@ -83,6 +83,29 @@ def gather_ceiling():
         return None, None
 
 
+def pin_to_gpu_numa(torch, dev: int):
+    """Run this rank's host threads (and so place its page-locked buffers) on the NUMA node of its
+    GPU's PCIe root, within the CPUs the process may use: the host pipeline's DMA then stays off
+    the inter-socket link.  Returns the node, or None when the platform does not say."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read().strip())
+        if node < 0:
+            return None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        allowed = os.sched_getaffinity(0) & cpus
+        if not allowed:
+            return None
+        os.sched_setaffinity(0, allowed)
+        return node
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int) -> dict:
     """The oracle (faithful C restatement of MOVE_EDSBWTSearch: a-balanced M_LF, literal
     per-pattern link/step/locate, MOVE_EDSBWTSearch.cpp:228-374) on the first `sample`
@@ -157,6 +180,7 @@ def main():
     else:
         torch.cuda.set_device(0)
         barrier = lambda: None  # noqa: E731
+    numa = pin_to_gpu_numa(torch, local) if torch.cuda.is_available() else None
     if rank == 0:
         workloads.ensure_built()
     barrier()
@@ -341,6 +365,7 @@ def main():
                                     "sizes all-gathered (each rank keeps its counts + records as its output slice)"
                                     + (" + counts gathered to rank 0 over RCCL" if args.gather == "counts" else "")),
                        "ktab_depth": idx.ktab_depth, "index_device_bytes": idx.device_bytes,
+                       "host_numa_node": numa,
                        "cache_resident": bool(rank_bytes <= MI355X_MALL_BYTES)},
             "occurrences_per_step": int(total_occ / args.steps),
             "found_per_step": int(e2e_stats["found"]) if world == 1 else None,
