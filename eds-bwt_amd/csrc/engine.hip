@@ -203,7 +203,8 @@ struct Engine {
     bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
-    int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 20);  // ... by the D-mer's leading bits (C3 A/B: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9)
+    int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 20);
+    uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);  // C3 chunks: 7.84 ms per call against 7.92-8.06 sorting every chunk  // ... by the D-mer's leading bits (C3 A/B: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9)
     DBuf<uint64_t> pv_in, pv_out;
     DBuf<uint32_t> bhist, bscan;  // direct start buckets (k_keys histogram, its scan / scatter cursors)
     // (measured on C3, 10M patterns: k_keys' histogram atomics +0.2 ms and the scatter 0.69 ms
@@ -1502,9 +1503,11 @@ struct Engine {
                    (uint64_t*)nullptr, (uint32_t*)nullptr, 0u);
         // '#' in a pattern: lists may overlap, use levels().  Deferred: read with the final check
         // (a batch holding '#' is then searched again on the ordered path)
-        defer = defer_call && packed && direct_sort_bits > 0;
+        defer = defer_call && packed;
         if (!defer && read_u64(d_nterm)) return kNeedOrdered;
-        if (packed && direct_sort_bits <= 0) {  // input order (EDSBWT_DIRECT_SORT_BITS=0)
+        // input order (EDSBWT_DIRECT_SORT_BITS=0, or a batch too small for the grouping to pay:
+        // its ~20 sort launches cost more than the locality saves below EDSBWT_DIRECT_SORT_MIN)
+        if (packed && (direct_sort_bits <= 0 || P < direct_sort_min)) {
             st.start_depth = D0;
             return run_deep(D0, (uint32_t)std::min<uint64_t>(P, 0xffffffffu), P, P, d_bytes, d_off, kid, ktab_off.p, ktab_off.p + 1,
                             ktab_b.p, ktab_e.p, r, abase, ovf_orig, keys.p, keys.p + P, len.p, 1u, pv_in.p);
