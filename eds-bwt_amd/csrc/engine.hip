@@ -204,7 +204,9 @@ struct Engine {
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
     int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 20);
-    uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);  // C3 chunks: 7.84 ms per call against 7.92-8.06 sorting every chunk  // ... by the D-mer's leading bits (C3 A/B: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9)
+    // ... for batches of at least this many patterns (C3 pipeline chunks: 7.84 ms per call against
+    // 7.92-8.06 sorting every chunk)
+    uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);
     DBuf<uint64_t> pv_in, pv_out;
     DBuf<uint32_t> bhist, bscan;  // direct start buckets (k_keys histogram, its scan / scatter cursors)
     // (measured on C3, 10M patterns: k_keys' histogram atomics +0.2 ms and the scatter 0.69 ms
