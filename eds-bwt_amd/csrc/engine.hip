@@ -203,10 +203,11 @@ struct Engine {
     bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
-    int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 20);  // ... by the D-mer's leading bits (C3 A/B: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9)
+    int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 16);  // ... by the D-mer's leading bits (C3 A/B, round 1: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9; round 2: 16 bits 3.115 ms against 20 bits 3.145)
     // ... for batches of at least this many patterns (C3 pipeline chunks: 7.84 ms per call against
     // 7.92-8.06 sorting every chunk)
     uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);
+    bool keys_packed = env_double("EDSBWT_KEYS_PACKED", 1) != 0;
     DBuf<uint64_t> pv_in, pv_out;
     DBuf<uint32_t> bhist, bscan;  // direct start buckets (k_keys histogram, its scan / scatter cursors)
     // (measured on C3, 10M patterns: k_keys' histogram atomics +0.2 ms and the scatter 0.69 ms
@@ -1496,8 +1497,11 @@ struct Engine {
             bhist.ensure(nbkt + 1);
             zero(bhist.p, (nbkt + 1) * 4);
         }
-        // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass
-        if (bps == 3)
+        // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass; the
+        // packed start needs no chunks (EDSBWT_KEYS_PACKED=0: k_keys for it too)
+        if (packed && !buckets && keys_packed)
+            launch(KC_TRIE, k_keys_packed, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, len.p, d_nterm, D0, E, kid, pv_in.p);
+        else if (bps == 3)
             launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
                    packed ? pv_in.p : (uint64_t*)nullptr, buckets ? bhist.p : (uint32_t*)nullptr, hshift);
         else

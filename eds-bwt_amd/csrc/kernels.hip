@@ -481,6 +481,70 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
 
 __global__ void k_iota(uint32_t* __restrict__ a, uint64_t n) { GRID_STRIDE(i, n) a[i] = (uint32_t)i; }
 
+// The packed direct start's keys straight from the bytes (k_keys builds the 3-bit sort chunks
+// first and reads kid / pv back out of them): per pattern, reading its characters from the end,
+// the D-mer id of the last D symbols (last character least significant digit), the packed
+// start (input index, then the remaining <= 16 symbols as 2-bit digits closed by a 1 bit), the
+// length, and whether it holds '#'.  A symbol outside the B <= 4 non-'#' symbols gives kid = E.
+__global__ void __launch_bounds__(256) k_keys_packed(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
+                                                     const uint8_t* __restrict__ code_of, uint32_t sigma, uint32_t* __restrict__ len,
+                                                     unsigned long long* __restrict__ n_term, uint32_t D, uint32_t E,
+                                                     uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
+    __shared__ uint32_t sbuf[kKeySpan / 4 + 2];
+    __shared__ uint8_t scode[256];
+    __shared__ unsigned long long sh[4];
+    const uint32_t B = sigma - 1;
+    for (uint32_t t = threadIdx.x; t < 256; t += blockDim.x) {
+        const uint32_t c = code_of[t];
+        // digit + 1 for the B non-'#' symbols, 0 for '#' and bytes outside the alphabet
+        scode[t] = (uint8_t)(c >= 1 && c < sigma ? c : 0);
+    }
+    unsigned long long nt = 0;
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < P; base += (size_t)gridDim.x * blockDim.x) {
+        const size_t nb = min((size_t)blockDim.x, (size_t)P - base);
+        const uint64_t s0 = off[base], s1 = off[base + nb];
+        const uint64_t w0 = s0 & ~3ull;
+        const bool staged = s1 - w0 <= kKeySpan && ((uintptr_t)bytes & 3) == 0;
+        __syncthreads();
+        if (staged) {
+            const uint32_t nw = (uint32_t)((s1 - w0 + 3) / 4);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(bytes + w0);
+            for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x) sbuf[t] = src[t];
+        }
+        __syncthreads();
+        const size_t i = base + threadIdx.x;
+        if (i < P) {
+            const uint64_t a = off[i];
+            const uint32_t L = (uint32_t)(off[i + 1] - a);
+            len[i] = L;
+            const uint32_t so = (uint32_t)(a - w0);
+            uint32_t x = 0, mul = 1, n = 0;
+            uint64_t rem = 0;
+            bool ok = true, term = false;
+            for (uint32_t t = 0; t < L; t++) {
+                const uint32_t k = L - 1 - t;
+                const uint32_t ch = staged ? (sbuf[(so + k) >> 2] >> (8 * ((so + k) & 3))) & 0xffu : bytes[a + k];
+                const uint32_t v = scode[ch];
+                term |= ch == '#';
+                ok &= v != 0;
+                if (t < D) {
+                    x += (v - 1) * mul;
+                    mul *= B;
+                } else {
+                    rem |= (uint64_t)((v - 1) & 3u) << (2 * n);
+                    n++;
+                }
+            }
+            nt += term;
+            rem |= 1ull << (2 * n);
+            pv[i] = rem << 31 | (uint64_t)i;
+            kid[i] = ok ? x : E;
+        }
+    }
+    nt = block_sum(nt, sh);
+    if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
+}
+
 // direct start: patterns grouped by their D-mer's leading bits (kid >> shift) for locality —
 // neighbouring lanes then read neighbouring table entries and rows.  cur[] holds each
 // bucket's first slot (exclusive scan of k_keys' histogram) and is advanced by atomics, so
