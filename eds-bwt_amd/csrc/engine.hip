@@ -208,6 +208,8 @@ struct Engine {
     // 7.92-8.06 sorting every chunk)
     uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);
     bool keys_packed = env_double("EDSBWT_KEYS_PACKED", 1) != 0;
+    bool locate_pp = env_double("EDSBWT_LOCATE_TASKS", 0) == 0;  // deferred path: per-pattern locate
+    DBuf<uint32_t> lbig;  // patterns with more than kLocBig records (k_locate_big)
     DBuf<uint64_t> pv_in, pv_out;
     DBuf<uint32_t> bhist, bscan;  // direct start buckets (k_keys histogram, its scan / scatter cursors)
     // (measured on C3, 10M patterns: k_keys' histogram atomics +0.2 ms and the scatter 0.69 ms
@@ -2150,7 +2152,24 @@ struct Engine {
         launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                       locate ? occ64.p : (uint64_t*)nullptr);
         uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
-        if (locate) {
+        // dense samples: records straight from each pattern's result (k_locate_pp / k_locate_big),
+        // no tasks (EDSBWT_LOCATE_TASKS=1: the task path as for every other search)
+        const bool per_pattern = locate && loc_mode == 2 && X.samp_dense && locate_pp;
+        if (per_pattern) {
+            inclusive_scan_u64(occ64.p, oscan, P, false);
+            hmark("locate scan");
+            rec.ensure(occ_cap);
+            lbig.ensure(P + 1);
+            zero(lbig.p, 4);
+            launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, (const uint64_t*)oscan.p, first_id, X, (const uint32_t*)ab.p,
+                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p);
+            timed(KC_LOCATE, [&] {
+                hipLaunchKernelGGL(k_locate_big, dim3(256), dim3(256), 0, stream, (const uint32_t*)lbig.p, (const Res*)res.p,
+                                   (const uint64_t*)oscan.p, first_id, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
+            });
+            HIPCHK(hipGetLastError());
+            task_cap = ~0ull;  // no task buffers in this path
+        } else if (locate) {
             inclusive_scan_u64(occ64.p, oscan, P, false);  // packed: occurrences << 32 | tasks (totals checked below)
             hmark("locate scan");
             trow.ensure(task_cap); tout.ensure(task_cap); tpat.ensure(task_cap);
@@ -2176,7 +2195,7 @@ struct Engine {
         std::memcpy(&found, ck + kChkFound, 8);
         std::memcpy(sums, ck + kChkSums, 16);
         const bool ok = term == 0 && ck[kChkOvf] <= defer_wide_cap && ck[kChkOvf2] == 0 && ck[kChkOflow] == 0 &&
-                        (!locate || (sums[0] <= occ_cap && sums[1] <= task_cap));
+                        (!locate || (sums[0] <= occ_cap && sums[1] <= task_cap && sums[1] < (1ull << 32)));
         if (trace)
             std::fprintf(stderr, "[edsbwt] deferred checks: '#' %llu, overflow %u (wide cap %u), wide overflow %u, buffers %s -> %s\n",
                                     (unsigned long long)term, ck[kChkOvf], defer_wide_cap, ck[kChkOvf2], ck[kChkOflow] ? "short" : "ok", ok ? "ok" : "redo");

@@ -2093,6 +2093,83 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
     stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
 }
 
+// Locate for dense samples without tasks (the deferred direct start's results: single
+// intervals, text positions, or at most kDeepWide archived intervals per pattern): one lane per
+// pattern writes its records from oscan's offset; a pattern with more than kLocBig records is
+// listed for k_locate_big instead (a block per pattern), so no lane walks a long run alone.
+constexpr uint32_t kLocBig = 64;
+__device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o, uint32_t pat, uint32_t word, uint32_t seg, uint32_t wis,
+                                        uint32_t off) {
+    edsbwt_occ r;
+    r.pat = pat;
+    r.word = word;
+    r.seg = seg;
+    r.word_in_seg = wis;
+    r.offset = off;
+    rec[o] = r;
+}
+__global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, const uint64_t* __restrict__ oscan, uint32_t first_id,
+                                                   KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
+                                                   edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
+                                                   uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats) {
+    unsigned long long my_off = 0;
+    GRID_STRIDE(i, P) {
+        const Res r = res[i];
+        const uint32_t occ = res_occ(r);
+        if (!occ) continue;
+        const uint64_t base = oscan[i] >> 32;  // the packed scan: occurrences << 32 | tasks
+        if (base + occ > occ_cap) { atomicOr(oflow, 1u); continue; }
+        const uint32_t pat = first_id + (uint32_t)i;
+        if (r.cnt & kResPos) {
+            const uint32_t off = (uint32_t)(r.off >> 32);
+            put_rec(rec, base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
+            my_off += off;
+            continue;
+        }
+        if (occ > kLocBig) { flag_push(big, (uint32_t)i); continue; }
+        uint64_t o = base;
+        const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
+        for (uint32_t t = 0; t < n; t++) {
+            const uint32_t b = (r.cnt & kResRow) ? (uint32_t)r.off : ab[r.off + t];
+            const uint32_t e = (r.cnt & kResRow) ? (uint32_t)r.off + occ - 1 : ae[r.off + t];
+            for (uint32_t x = b; x <= e; x++, o++) {
+                const uint4 sm = X.samples[x];
+                put_rec(rec, o, pat, sm.x, sm.z, sm.w, sm.y);
+                my_off += sm.y;
+            }
+        }
+    }
+    __shared__ unsigned long long sh[4];
+    stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
+}
+__global__ void __launch_bounds__(256) k_locate_big(const uint32_t* __restrict__ big, const Res* __restrict__ res,
+                                                    const uint64_t* __restrict__ oscan, uint32_t first_id, KIdx X,
+                                                    const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
+                                                    edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
+    unsigned long long my_off = 0;
+    const uint32_t nbig = big[0];
+    for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {  // block-uniform
+        const uint32_t i = big[1 + j];
+        const Res r = res[i];
+        const uint32_t occ = res_occ(r), pat = first_id + i;
+        const uint64_t base = oscan[i] >> 32;
+        const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
+        uint64_t start = 0;
+        for (uint32_t t = 0; t < n; t++) {
+            const uint32_t b = (r.cnt & kResRow) ? (uint32_t)r.off : ab[r.off + t];
+            const uint32_t e = (r.cnt & kResRow) ? (uint32_t)r.off + occ - 1 : ae[r.off + t];
+            for (uint32_t q = threadIdx.x; q <= e - b; q += blockDim.x) {
+                const uint4 sm = X.samples[b + q];
+                put_rec(rec, base + start + q, pat, sm.x, sm.z, sm.w, sm.y);
+                my_off += sm.y;
+            }
+            start += (uint64_t)(e - b) + 1;
+        }
+    }
+    __shared__ unsigned long long sh[4];
+    stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
+}
+
 // ---------------------------------------------- locate samples (index open)
 #if EDSBWT_OCC_ROWS == 64
 // per 64-row block: the sampled-row plane (offset % 2^shift == 0) and its count
