@@ -249,6 +249,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    c0 = time.process_time()
     search_ms = exch_ms = 0.0
     held = (0, 0)
     total_occ = 0
@@ -268,6 +269,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    host_cores = (time.process_time() - c0) / max(1e-9, elapsed)  # host CPU the pipeline kept busy
     e2e_stats = idx.stats()
     if args.no_e2e:
         e2e_stats = dict(e2e_stats, ms_wall=0.0, found=0)
@@ -369,7 +371,8 @@ def main():
                        "cache_resident": bool(rank_bytes <= MI355X_MALL_BYTES)},
             "occurrences_per_step": int(total_occ / args.steps),
             "found_per_step": int(e2e_stats["found"]) if world == 1 else None,
-            "e2e": {"ms_wall_per_call": round(float(np.mean(walls)), 3), "chunks": e2e_stats["chunks"],
+            "e2e": {"ms_wall_per_call": round(float(np.mean(walls)), 3), "ms_wall_median": round(float(np.median(walls)), 3),
+                    "ms_wall_min": round(float(np.min(walls)), 3), "host_cores": round(host_cores, 2), "chunks": e2e_stats["chunks"],
                     "bytes_h2d": e2e_stats["bytes_h2d"], "bytes_d2h": e2e_stats["bytes_d2h"],
                     "pcie_gbs": round((e2e_stats["bytes_h2d"] + e2e_stats["bytes_d2h"]) / max(1e-9, np.mean(walls) * 1e-3) / 1e9, 2),
                     "device_ms_per_call": round(e2e_stats["ms_total"], 3),

@@ -18,6 +18,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +38,10 @@
 
 #include "index_io.h"
 #include "kernels.hip"
+
+// format.cpp: the 2-bit packer of fixed-length pattern lines (host side of k_unpack_lines)
+extern "C" uint64_t edsbwt_lines_fixed(const uint8_t* s, uint64_t nb, uint32_t* L_out);
+extern "C" int edsbwt_pack_lines(const uint8_t* s, uint64_t nb, uint32_t L, uint64_t p0, uint64_t p1, const uint8_t* end, uint8_t* out);
 
 #ifndef EDSBWT_BUILD_ID
 #define EDSBWT_BUILD_ID "unknown"
@@ -319,7 +324,7 @@ struct Engine {
     // chunk k reuses chunk k-kSlots's device buffers, so its search waits for that chunk's
     // download: five slots keep the searches clear of a download backlog
     static constexpr int kSlots = 5;
-    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {}, prep_done[kSlots] = {};
+    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {}, prep_done[kSlots] = {}, c8_done[kSlots] = {};
     // per-slot prep on `up` after each upload: the chunk's lines split (lines mode) or its offsets
     // rebased, and its pattern count and longest / shortest pattern measured, so the search
     // itself reads nothing back before its final check
@@ -327,7 +332,7 @@ struct Engine {
     DBuf<uint8_t> ptmp[kSlots];
     DBuf<unsigned long long> prep_mm[kSlots];
     uint32_t* prep_host(int sl) { return pinned + 64 + 8 * sl; }  // P, max, ~min as u64 (in hostblk)
-    DBuf<uint8_t> hraw[kSlots], hbytes[kSlots];
+    DBuf<uint8_t> hraw[kSlots], hbytes[kSlots], hpack[kSlots];  // hpack: a packed chunk (k_unpack_lines)
     DBuf<uint64_t> hoffs[kSlots];
     DBuf<uint32_t> hcounts[kSlots], nlcnt, nlpre;
     DBuf<edsbwt_occ> hrec[kSlots];
@@ -347,7 +352,9 @@ struct Engine {
         }
         void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
     };
-    Pinned stage_in[kSlots], stage_off[kSlots], stage_cnt[kSlots];
+    Pinned stage_in[kSlots], stage_off[kSlots], stage_cnt[kSlots], stage_pack[kSlots], stage_c8[kSlots], stage_exc[kSlots];
+    DBuf<uint8_t> hc8[kSlots];  // a chunk's counts as bytes, then the number of larger ones (k_counts_u8)
+    DBuf<uint2> hexc[kSlots];   // ... and those: (pattern, count)
     // the occurrence records handed to the caller (library-owned, page-locked, reused once
     // edsbwt_occ_free gives them back: see occ_arena_*)
     edsbwt_occ* arena = nullptr;
@@ -2235,6 +2242,7 @@ struct Engine {
     void pipe_init() {
         if (up) return;
         pool.start((unsigned)std::max(0.0, env_double("EDSBWT_HOST_THREADS", 12) - 1));
+        cpool.start((unsigned)std::max(0.0, env_double("EDSBWT_COUNT_THREADS", 4) - 1));
         HIPCHK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         // downloads: hipMemcpyAsync into page-locked host memory runs as a blit kernel that fills
         // every CU with waves waiting on PCIe stores, and the search kernels beside it then wait
@@ -2263,6 +2271,7 @@ struct Engine {
             HIPCHK(hipEventCreateWithFlags(&comp_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&down_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&prep_done[k], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&c8_done[k], hipEventDisableTiming));
         }
     }
     // host -> device on `up` (staged through page-locked memory when src is pageable)
@@ -2329,6 +2338,7 @@ struct Engine {
         unsigned todo = 0, next = 0, running = 0;
         uint64_t gen = 0;
         bool stop = false;
+        std::mutex run_mx;  // one run at a time (the upload thread packs while this thread may grow the arena)
         unsigned size() const { return (unsigned)th.size() + 1; }
         void start(unsigned n) {
             for (unsigned i = 0; i < n; i++)
@@ -2354,6 +2364,7 @@ struct Engine {
         // fn(t) for t < n on the pool and the calling thread; returns when all are done
         void run(unsigned n, const std::function<void(unsigned)>& f) {
             if (n <= 1 || th.empty()) { for (unsigned t = 0; t < n; t++) f(t); return; }
+            std::lock_guard<std::mutex> one(run_mx);
             std::unique_lock<std::mutex> lk(m);
             fn = f;
             todo = n;
@@ -2387,7 +2398,23 @@ struct Engine {
             cv.notify_all();
             for (auto& x : th) x.join();
         }
-    } pool;
+    } pool, cpool;  // cpool: the counts thread's (expand_c8)
+    // With records the counts cross PCIe as one byte each (k_counts_u8: most are small), the
+    // few of 255 and more as (pattern, count) pairs, and a host thread widens them into the
+    // caller's counts while the next chunk downloads: a quarter of the counts' PCIe bytes.
+    // EDSBWT_SMALL_COUNTS=0: 4 bytes each.
+    bool small_counts = env_double("EDSBWT_SMALL_COUNTS", 1) != 0;
+    static uint64_t c8_bytes(uint64_t P) { return (P + 7) / 8 * 8 + 8; }  // bytes, then the exception count (u32)
+    void expand_c8(uint32_t* c, const uint8_t* c8, uint64_t P, const uint2* exc, uint32_t nexc) {
+        const unsigned T = (unsigned)std::min<uint64_t>(cpool.size(), std::max<uint64_t>(1, P / 262144));
+        cpool.run(T, [&](unsigned t) {
+            for (uint64_t p = P * t / T, e = P * (t + 1) / T; p < e; p++) c[p] = c8[p];
+        });
+        for (uint32_t i = 0; i < nexc; i++) {
+            if (exc[i].x >= P) throw Fail(EDSBWT_E_DEVICE, "counts: an exception outside the chunk");
+            c[exc[i].x] = exc[i].y;
+        }
+    }
     // expand one chunk's compact records: pattern ids from the counts, segment and word in
     // segment from the segment tables (MOVE_EDSBWTSearch.cpp:361-363's rank1/select1)
     void expand_chunk(const uint32_t* counts, uint64_t p0, uint64_t P, uint64_t r0, uint64_t n, uint32_t first_id) {
@@ -2481,6 +2508,39 @@ struct Engine {
                 HIPCHK(hipGetLastError());
             }
         }
+        small_copy_on(prep_host(sl), prep_mm[sl].p, 24, up);
+    }
+    // a chunk of fixed-length A/C/G/T lines packed to 2 bits per base on the host (format.cpp),
+    // into stage_pack[sl]: returns its lines (0: the chunk is not of that form; send the bytes).
+    // EDSBWT_PACK_LINES=0 turns it off.
+    bool pack_lines = env_double("EDSBWT_PACK_LINES", 1) != 0;
+    uint64_t pack_chunk(const uint8_t* s, uint64_t nb, const uint8_t* end, int sl, uint32_t* L_out) {
+        if (!pack_lines) return 0;
+        uint32_t L = 0;
+        const uint64_t P = edsbwt_lines_fixed(s, nb, &L);
+        if (!P) return 0;
+        const uint64_t S = (L + 3) / 4;
+        stage_pack[sl].ensure(P * S + 16);
+        uint8_t* out = static_cast<uint8_t*>(stage_pack[sl].p);
+        const unsigned T = (unsigned)std::min<uint64_t>(pool.size(), std::max<uint64_t>(1, P / 16384));
+        std::atomic<int> bad{0};
+        pool.run(T, [&](unsigned t) {
+            if (!edsbwt_pack_lines(s, nb, L, P * t / T, P * (t + 1) / T, end, out)) bad.store(1, std::memory_order_relaxed);
+        });
+        if (bad.load()) return 0;
+        *L_out = L;
+        return P;
+    }
+    // prep of a packed chunk on `up`: its bytes and offsets back (k_unpack_lines), P and the
+    // line length into prep_host(sl) as prep() leaves them
+    void prep_packed(int sl, uint64_t nb, uint64_t P, uint32_t L) {
+        prep_mm[sl].ensure(4);
+        hbytes[sl].ensure(nb + 16);
+        hoffs[sl].ensure(P + 2);
+        const uint64_t n16 = (P * L + 15) / 16;
+        hipLaunchKernelGGL(k_unpack_lines, dim3((unsigned)std::min<uint64_t>(std::max<uint64_t>(1, (n16 + 255) / 256), 4096)), dim3(256), 0, up,
+                           (const uint8_t*)hpack[sl].p, P, L, (uint32_t)((L + 3) / 4), hbytes[sl].p, hoffs[sl].p, prep_mm[sl].p);
+        HIPCHK(hipGetLastError());
         small_copy_on(prep_host(sl), prep_mm[sl].p, 24, up);
     }
     DBuf<uint8_t> hin_all;                // eager uploads: every chunk of the batch
@@ -2611,6 +2671,13 @@ struct Engine {
     // n bytes on engine `eng`, waiting for the copy (the caller is that direction's thread)
     void hsa_copy(void* dst, const void* src, size_t n, bool to_host, uint32_t eng, hsa_signal_t sig) {
         if (!n) return;
+        hsa_copy_start(dst, src, n, to_host, eng, sig);
+        hsa_wait(sig);
+    }
+    void hsa_wait(hsa_signal_t sig) {
+        while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) >= 1) {}
+    }
+    void hsa_copy_start(void* dst, const void* src, size_t n, bool to_host, uint32_t eng, hsa_signal_t sig) {
         hsa_signal_store_relaxed(sig, 1);
         const hsa_status_t r = hsa_amd_memory_async_copy_on_engine(dst, to_host ? hsa_cpu : hsa_gpu, src, to_host ? hsa_gpu : hsa_cpu, n, 0, nullptr,
                                                                    sig, (hsa_amd_sdma_engine_id_t)eng, true);
@@ -2619,7 +2686,6 @@ struct Engine {
             hsa_status_string(r, &m);
             throw Fail(EDSBWT_E_DEVICE, std::string("hsa_amd_memory_async_copy_on_engine: ") + (m ? m : "?"));
         }
-        while (hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_ACTIVE) >= 1) {}
     }
 
     // search_host over explicit SDMA engines: an upload thread (chunk k+ahead: copy, then its prep
@@ -2639,9 +2705,16 @@ struct Engine {
         struct Job {
             size_t k;
             uint64_t P, n, pats, total;
+            uint32_t nexc;  // small counts: the chunk's counts of 255 and more
         };
         std::deque<Job> jobs;
-        uint64_t h2d = 0, d2h = 0;
+        uint64_t h2d = 0, d2h = 0, packed = 0;
+        // small counts (expand_c8): widened on a thread of their own, chunk by chunk as they
+        // land, so the downloads never wait for it
+        const bool derive_counts = small_counts;
+        size_t counted = 0;
+        std::vector<Job> landed;
+        const uint8_t* text_end = text + (nch ? ch.back().b1 : 0);
         std::vector<std::tuple<const char*, size_t, double>> marks;
         std::mutex mark_m;
         auto mark = [&](const char* what, size_t k) {
@@ -2673,6 +2746,24 @@ struct Engine {
                     const int sl = (int)(k % kSlots);
                     const uint64_t nb = c.b1 - c.b0;
                     mark("upload", k);
+                    uint32_t L = 0;
+                    const uint64_t Pk = lines ? pack_chunk(text + c.b0, nb, text_end, sl, &L) : 0;
+                    if (Pk) {  // 2 bits per base over PCIe, unpacked on the device
+                        const uint64_t pb = Pk * ((L + 3) / 4);
+                        hpack[sl].ensure(pb + 16);
+                        hsa_copy(hpack[sl].p, stage_pack[sl].p, pb, false, eng_up, sig);
+                        prep_packed(sl, nb, Pk, L);
+                        HIPCHK(hipEventRecord(prep_done[sl], up));
+                        mark("uploaded", k);
+                        {
+                            std::lock_guard<std::mutex> g(m);
+                            uploaded = k + 1;
+                            h2d += pb;
+                            packed++;
+                        }
+                        cv.notify_all();
+                        continue;
+                    }
                     uint64_t up_bytes = nb;
                     uint8_t* dst = nullptr;
                     if (lines) {
@@ -2735,7 +2826,33 @@ struct Engine {
                     const int sl = (int)(j.k % kSlots);
                     mark("download", j.k);
                     uint64_t dn = 0;
-                    if (j.P) {
+                    if (j.P && derive_counts) {
+                        // the previous user of this slot's staging must have been widened
+                        if (j.k >= (size_t)kSlots) {
+                            std::unique_lock<std::mutex> lk(m);
+                            cv.wait(lk, [&] { return stop || counted > j.k - kSlots; });
+                            if (stop) break;
+                        }
+                        if (locate && j.n) {  // the records first: the byte counts were computed meanwhile
+                            hsa_copy(arena + j.total, hrec[sl].p, j.n * sizeof(edsbwt_occ), true, eng_down, sig);
+                            dn += j.n * sizeof(edsbwt_occ);
+                            j.n = 0;
+                        }
+                        HIPCHK(hipEventSynchronize(c8_done[sl]));
+                        const uint64_t cb = c8_bytes(j.P);
+                        stage_c8[sl].ensure(cb);
+                        hsa_copy(stage_c8[sl].p, hc8[sl].p, cb, true, eng_down, sig);
+                        dn += cb;
+                        uint32_t ne = 0;
+                        std::memcpy(&ne, static_cast<const uint8_t*>(stage_c8[sl].p) + cb - 8, 4);
+                        if (ne > j.P) throw Fail(EDSBWT_E_DEVICE, "counts: more exceptions than patterns");
+                        if (ne) {
+                            stage_exc[sl].ensure((size_t)ne * 8);
+                            hsa_copy(stage_exc[sl].p, hexc[sl].p, (size_t)ne * 8, true, eng_down, sig);
+                            dn += (uint64_t)ne * 8;
+                        }
+                        j.nexc = ne;
+                    } else if (j.P) {
                         if (pin_cnt) {
                             hsa_copy(counts + j.pats, hcounts[sl].p, j.P * 4, true, eng_down, sig);
                         } else {
@@ -2754,6 +2871,7 @@ struct Engine {
                         std::lock_guard<std::mutex> g(m);
                         downloaded = j.k + 1;
                         d2h += dn;
+                        if (derive_counts) landed.push_back(j);
                     }
                     cv.notify_all();
                 }
@@ -2762,6 +2880,33 @@ struct Engine {
             }
             if (have_sig) hsa_signal_destroy(sig);
         });
+        std::thread tc;
+        if (derive_counts)
+            tc = std::thread([&] {
+                try {
+                    for (size_t k = 0; k < nch; k++) {
+                        Job j;
+                        {
+                            std::unique_lock<std::mutex> lk(m);
+                            cv.wait(lk, [&] { return stop || landed.size() > k; });
+                            if (stop) break;
+                            j = landed[k];
+                        }
+                        const int sl = (int)(j.k % kSlots);
+                        if (j.P)
+                            expand_c8(counts + j.pats, static_cast<const uint8_t*>(stage_c8[sl].p), j.P,
+                                      static_cast<const uint2*>(stage_exc[sl].p), j.nexc);
+                        mark("counted", j.k);
+                        {
+                            std::lock_guard<std::mutex> g(m);
+                            counted = k + 1;
+                        }
+                        cv.notify_all();
+                    }
+                } catch (...) {
+                    fail(std::current_exception());
+                }
+            });
         edsbwt_stats agg{};
         uint64_t total = 0, pats = 0;
         try {
@@ -2795,6 +2940,16 @@ struct Engine {
                 }
                 known_len = false;
                 std::swap(rec, hrec[sl]);
+                if (derive_counts && P) {
+                    hc8[sl].ensure(c8_bytes(P));
+                    hexc[sl].ensure(P);
+                    uint32_t* ne = reinterpret_cast<uint32_t*>(hc8[sl].p + c8_bytes(P) - 8);
+                    zero_on(ne, 8, stream);
+                    hipLaunchKernelGGL(k_counts_u8, dim3((unsigned)std::min<uint64_t>(2048, (P + 1023) / 1024)), dim3(256), 0, stream,
+                                       (const uint32_t*)hcounts[sl].p, P, hc8[sl].p, hexc[sl].p, ne);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipEventRecord(c8_done[sl], stream));
+                }
                 mark("searched", k);
                 accumulate(agg, st);
                 if (locate && n && total + n > arena_cap) {
@@ -2807,7 +2962,7 @@ struct Engine {
                 }
                 {
                     std::lock_guard<std::mutex> g(m);
-                    jobs.push_back(Job{k, P, n, pats, total});
+                    jobs.push_back(Job{k, P, n, pats, total, 0});
                     searched = k + 1;
                 }
                 cv.notify_all();
@@ -2816,7 +2971,7 @@ struct Engine {
             }
             {
                 std::unique_lock<std::mutex> lk(m);
-                cv.wait(lk, [&] { return stop || downloaded == nch; });
+                cv.wait(lk, [&] { return stop || (downloaded == nch && (!derive_counts || counted == nch)); });
                 closed = true;
             }
             cv.notify_all();
@@ -2830,12 +2985,14 @@ struct Engine {
         cv.notify_all();
         tu.join();
         td.join();
+        if (tc.joinable()) tc.join();
         (void)hipStreamSynchronize(up);
         if (err) {
             (void)hipStreamSynchronize(stream);  // no kernel may still touch the slots
             std::rethrow_exception(err);
         }
         mark("drained", nch);
+        if (trace) std::fprintf(stderr, "[edsbwt] host pipeline: %llu of %zu chunks went packed (2 bits per base)\n", (unsigned long long)packed, nch);
         for (auto& mk : marks) std::fprintf(stderr, "[edsbwt] t %8.3f ms  %-10s chunk %zu\n", std::get<2>(mk), std::get<0>(mk), std::get<1>(mk));
         st = agg;
         st.patterns = pats;
@@ -3156,7 +3313,7 @@ struct Engine {
             if (up_done[k]) (void)hipEventDestroy(up_done[k]);
             if (comp_done[k]) (void)hipEventDestroy(comp_done[k]);
             if (down_done[k]) (void)hipEventDestroy(down_done[k]);
-            stage_in[k].release(); stage_off[k].release(); stage_cnt[k].release();
+            stage_in[k].release(); stage_off[k].release(); stage_cnt[k].release(); stage_pack[k].release(); stage_c8[k].release(); stage_exc[k].release();
         }
         if (up) (void)hipStreamDestroy(up);
         if (down) (void)hipStreamDestroy(down);

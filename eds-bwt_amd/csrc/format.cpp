@@ -1,5 +1,9 @@
-// eds-bwt_amd/csrc/format.cpp — multi-threaded CSV body formatter for the records
-// of <patterns>output_M_LF.csv ("%u\t%u\t%u\t%u\t%u\n", MOVE_EDSBWTSearch.cpp:365).
+// eds-bwt_amd/csrc/format.cpp — host byte work around the search: the multi-threaded CSV
+// body formatter for the records of <patterns>output_M_LF.csv ("%u\t%u\t%u\t%u\t%u\n",
+// MOVE_EDSBWTSearch.cpp:365), and the 2-bit packer of fixed-length DNA pattern lines that
+// shrinks the host pipeline's uploads four-fold (engine.hip search_host_hsa).
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cstring>
 #include <thread>
@@ -56,4 +60,70 @@ extern "C" uint64_t edsbwt_format_csv(const edsbwt_occ* occ, uint64_t nocc, char
         });
     for (auto& x : th) x.join();
     return sz[T];
+}
+
+// ---- fixed-length line packing.  A chunk of the pattern file (getline lines,
+// MOVE_EDSBWTSearch.cpp:111) whose lines all hold exactly L bytes of A/C/G/T (1 <= L <= 32),
+// each ended by '\n' (the chunk's last line may lack it), goes over PCIe as 2 bits per base:
+// code (byte >> 1) & 3 (A 0, C 1, T 2, G 3), line p at out + p*S with S = ceil(L/4) bytes,
+// base j at bits 2*(j%4) of byte j/4.  The device restores the same bytes (kernels.hip
+// k_unpack_lines), so the search sees what the unpacked chunk would have given it.
+
+// lines of such a chunk (0: the chunk does not have that form at its first line / its size)
+extern "C" uint64_t edsbwt_lines_fixed(const uint8_t* s, uint64_t nb, uint32_t* L_out) {
+    if (!nb) return 0;
+    const void* nl = std::memchr(s, '\n', std::min<uint64_t>(nb, 33));
+    if (!nl) return 0;
+    const uint64_t L = (uint64_t)((const uint8_t*)nl - s);
+    if (L == 0 || L > 32) return 0;
+    uint64_t P = nb / (L + 1);
+    const uint64_t r = nb % (L + 1);
+    if (r == L) P++;            // a last line without '\n'
+    else if (r != 0) return 0;
+    *L_out = (uint32_t)L;
+    return P;
+}
+
+namespace {
+__attribute__((target("avx2"))) int pack_avx2(const uint8_t* s, uint64_t nb, uint32_t L, uint64_t p0, uint64_t p1, const uint8_t* end,
+                                              uint8_t* out) {
+    const __m256i cA = _mm256_set1_epi8('A'), cC = _mm256_set1_epi8('C'), cG = _mm256_set1_epi8('G'), cT = _mm256_set1_epi8('T');
+    const __m256i k3 = _mm256_set1_epi8(3), m1 = _mm256_set1_epi16(0x0401), m2 = _mm256_set1_epi32(0x00100001);
+    const __m256i shuf = _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,  //
+                                          0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+    const uint32_t need = L == 32 ? 0xFFFFFFFFu : (1u << L) - 1u;
+    const uint64_t cmask = L == 32 ? ~0ull : (1ull << (2 * L)) - 1ull;
+    const uint64_t stride = L + 1, S = (L + 3) / 4;
+    for (uint64_t p = p0; p < p1; p++) {
+        const uint8_t* q = s + p * stride;
+        __m256i v;
+        if (q + 32 <= end) {
+            v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(q));
+        } else {  // the caller's buffer ends within 32 bytes
+            alignas(32) uint8_t tmp[32] = {0};
+            std::memcpy(tmp, q, (size_t)(end - q));
+            v = _mm256_load_si256(reinterpret_cast<const __m256i*>(tmp));
+        }
+        const __m256i acgt = _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(v, cA), _mm256_cmpeq_epi8(v, cC)),
+                                             _mm256_or_si256(_mm256_cmpeq_epi8(v, cG), _mm256_cmpeq_epi8(v, cT)));
+        if (((uint32_t)_mm256_movemask_epi8(acgt) & need) != need) return 0;
+        if (p * stride + L < nb ? q[L] != '\n' : p + 1 != p1) return 0;
+        const __m256i x = _mm256_and_si256(_mm256_srli_epi16(v, 1), k3);                  // a code per byte
+        const __m256i z = _mm256_madd_epi16(_mm256_maddubs_epi16(x, m1), m2);             // 4 codes per u32
+        const __m256i w = _mm256_shuffle_epi8(z, shuf);                                   // ... their low bytes
+        const uint64_t codes = (((uint64_t)(uint32_t)_mm_cvtsi128_si32(_mm256_extracti128_si256(w, 1)) << 32) |
+                                (uint32_t)_mm_cvtsi128_si32(_mm256_castsi256_si128(w))) & cmask;
+        if (p + 1 < p1) std::memcpy(out + p * S, &codes, 8);  // the next line's bytes follow
+        else std::memcpy(out + p * S, &codes, S);             // the range's last line: its own bytes only
+    }
+    return 1;
+}
+}  // namespace
+
+// pack lines [p0, p1) of a chunk edsbwt_lines_fixed accepted (L bases each); `end` is the first
+// byte of the caller's buffer that may not be read.  Returns 0 when a line is not L A/C/G/T bytes
+// then '\n' (or the CPU lacks AVX2): the caller then sends the raw bytes.
+extern "C" int edsbwt_pack_lines(const uint8_t* s, uint64_t nb, uint32_t L, uint64_t p0, uint64_t p1, const uint8_t* end, uint8_t* out) {
+    if (L == 0 || L > 32 || !__builtin_cpu_supports("avx2")) return 0;
+    return pack_avx2(s, nb, L, p0, p1, end, out);
 }

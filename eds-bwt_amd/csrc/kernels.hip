@@ -2774,6 +2774,57 @@ __global__ void __launch_bounds__(256) k_line_fin(uint64_t* __restrict__ offs, c
     __syncthreads();
     if (threadIdx.x == 0) { atomicMax(out + 1, (unsigned long long)smx); atomicMax(out + 2, (unsigned long long)smn); }
 }
+// a chunk the host packed to 2 bits per base (format.cpp edsbwt_pack_lines: P lines of L
+// bases, line p's codes at pk + p*S, code (byte >> 1) & 3): the line bytes back, without
+// their '\n' as k_nl_compact leaves them, the line offsets, and P / longest / ~shortest into
+// mm[0..2] as k_line_fin writes them.  16 output bytes per thread.
+__global__ void __launch_bounds__(256) k_unpack_lines(const uint8_t* __restrict__ pk, uint64_t P, uint32_t L, uint32_t S,
+                                                      uint8_t* __restrict__ out, uint64_t* __restrict__ offs,
+                                                      unsigned long long* __restrict__ mm) {
+    const uint64_t nbytes = P * L, n16 = (nbytes + 15) / 16;
+    const uint32_t base = 0x47544341u;  // "ACTG": the byte of code c is byte c of this word
+    GRID_STRIDE(i, n16) {
+        const uint64_t pos = i * 16;
+        uint64_t p = pos / L;
+        uint32_t j = (uint32_t)(pos - p * L);
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        const uint32_t m = (uint32_t)min<uint64_t>(16, nbytes - pos);
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t c = (pk[p * S + (j >> 2)] >> ((j & 3u) * 2u)) & 3u;
+            w[k >> 2] |= ((base >> (c * 8u)) & 0xFFu) << ((k & 3u) * 8u);
+            if (++j == L) { j = 0; p++; }
+        }
+        if (m == 16) {
+            *reinterpret_cast<uint4*>(out + pos) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            for (uint32_t k = 0; k < m; k++) out[pos + k] = (uint8_t)(w[k >> 2] >> ((k & 3u) * 8u));
+        }
+    }
+    GRID_STRIDE(q, P + 1) offs[q] = q * L;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        mm[0] = P;
+        mm[1] = L;
+        mm[2] = (unsigned long long)(~L);
+    }
+}
+// a chunk's counts as one byte each for the download (engine.hip expand_c8): 255 marks a
+// count of 255 or more, listed as (pattern, count) in exc (room for P) after the *nexc
+// counter (zeroed before).  4 counts per thread.
+__global__ void __launch_bounds__(256) k_counts_u8(const uint32_t* __restrict__ c, uint64_t P, uint8_t* __restrict__ c8,
+                                                   uint2* __restrict__ exc, uint32_t* __restrict__ nexc) {
+    GRID_STRIDE(i, (P + 3) / 4) {
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint64_t p = i * 4 + k;
+            if (p >= P) break;
+            const uint32_t v = c[p];
+            if (v >= 255u) exc[atomicAdd(nexc, 1u)] = make_uint2((uint32_t)p, v);
+            w |= min(v, 255u) << (8 * k);
+        }
+        *reinterpret_cast<uint32_t*>(c8 + i * 4) = w;
+    }
+}
 // offsets of a chunk of a packed batch, rebased to its first byte
 __global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) { GRID_STRIDE(i, n) off[i] -= base; }
 __global__ void __launch_bounds__(256) k_nl_count(const uint8_t* __restrict__ in, uint64_t n, uint32_t* __restrict__ cnt) {

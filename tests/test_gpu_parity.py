@@ -537,6 +537,41 @@ def test_search_lines_pipeline_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned
                 assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)
 
 
+@pytest.mark.parametrize("pinned", [True, False])
+def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
+    """Fixed-length A/C/G/T lines go over PCIe at 2 bits per base (format.cpp packer,
+    k_unpack_lines): the same counts and records as the oracle for several lengths, with a
+    stray 'N' line that sends its chunk raw beside packed ones, a last line without '\\n',
+    and the packer switched off (EDSBWT_PACK_LINES=0) for comparison."""
+    rng = random.Random(909)
+    segs = _covid_like(rng, 400)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    for L in (1, 7, 20, 31, 32):
+        pats = []
+        for _ in range(4000):
+            p = edsgen.planted(rng, segs, L)
+            pats.append(p if p and len(p) == L and set(p) <= set("ACGT") else "".join(rng.choice("ACGT") for _ in range(L)))
+        stray = list(pats)
+        stray[len(stray) // 2] = "N" * L
+        for lines, trailing in ((pats, True), (pats, False), (stray, True)):
+            buf, offs = _pack(lines)
+            oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=5)
+            text = ("\n".join(lines) + ("\n" if trailing else "")).encode()
+            for pack in ("1", "0"):
+                monkeypatch.setenv("EDSBWT_PACK_LINES", pack)
+                monkeypatch.setenv("EDSBWT_CHUNK_MB", "0.02")
+                with edsbwt.Index(base) as idx:
+                    gc, go = _lines_search(edsbwt, idx, text, first_id=5, pinned=pinned)
+                    st = idx.stats()
+                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack)
+                if pack == "1" and lines is pats:
+                    assert st["bytes_h2d"] <= len(lines) * ((L + 3) // 4)  # every chunk went packed
+                elif pack == "1":
+                    assert len(lines) * ((L + 3) // 4) < st["bytes_h2d"] < len(text)  # one chunk raw, the rest packed
+                else:
+                    assert st["bytes_h2d"] == len(text)
+
+
 def test_search_lines_empty_and_held_records_gpu(oracle, edsbwt, tmp_path):
     """An empty file; records still held by the caller when the next call runs (the engine
     must not overwrite them) and freed after the index is closed."""
