@@ -213,6 +213,8 @@ struct Engine {
     // 7.92-8.06 sorting every chunk)
     uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);
     bool keys_packed = env_double("EDSBWT_KEYS_PACKED", 1) != 0;
+    bool acgt_alpha = false;  // the alphabet is {#, A, C, G, T}: k_keys_acgt (EDSBWT_KEYS_SWAR=0: k_keys_packed)
+    bool keys_swar = env_double("EDSBWT_KEYS_SWAR", 1) != 0;
     bool locate_pp = env_double("EDSBWT_LOCATE_TASKS", 0) == 0;  // deferred path: per-pattern locate
     DBuf<uint32_t> lbig;  // patterns with more than kLocBig records (k_locate_big)
     DBuf<uint64_t> pv_in, pv_out;
@@ -324,7 +326,7 @@ struct Engine {
     // chunk k reuses chunk k-kSlots's device buffers, so its search waits for that chunk's
     // download: five slots keep the searches clear of a download backlog
     static constexpr int kSlots = 5;
-    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {}, prep_done[kSlots] = {}, c8_done[kSlots] = {};
+    hipEvent_t up_done[kSlots] = {}, comp_done[kSlots] = {}, down_done[kSlots] = {}, prep_done[kSlots] = {};
     // per-slot prep on `up` after each upload: the chunk's lines split (lines mode) or its offsets
     // rebased, and its pattern count and longest / shortest pattern measured, so the search
     // itself reads nothing back before its final check
@@ -735,6 +737,8 @@ struct Engine {
         N = H.N; W = H.W; S = H.S; sigma = H.sigma;
         for (uint32_t j = 0; j < sigma; j++) alpha[j] = H.alpha[j];
         std::memcpy(h_code_of, H.code_of, 256);
+        acgt_alpha = H.sigma == 5 && H.code_of[(uint8_t)'#'] == 0 && H.code_of[(uint8_t)'A'] == 1 && H.code_of[(uint8_t)'C'] == 2 &&
+                     H.code_of[(uint8_t)'G'] == 3 && H.code_of[(uint8_t)'T'] == 4;
         if (W > N) throw Fail(EDSBWT_E_FORMAT, "more words than rows");
         // occ blocks (parallel over block ranges)
         const size_t nblk = (size_t)N / kOccRows + 1;
@@ -1508,7 +1512,9 @@ struct Engine {
         }
         // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass; the
         // packed start needs no chunks (EDSBWT_KEYS_PACKED=0: k_keys for it too)
-        if (packed && !buckets && keys_packed)
+        if (packed && !buckets && keys_packed && acgt_alpha && keys_swar)
+            launch(KC_TRIE, k_keys_acgt, P, d_bytes, d_off, P, len.p, d_nterm, D0, E, kid, pv_in.p);
+        else if (packed && !buckets && keys_packed)
             launch(KC_TRIE, k_keys_packed, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, len.p, d_nterm, D0, E, kid, pv_in.p);
         else if (bps == 3)
             launch(KC_TRIE, k_keys<3>, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, nch, keys.p, len.p, d_nterm, D0, E, kid,
@@ -2058,6 +2064,7 @@ struct Engine {
         // counts, found, totals and (locate) the packed scan input in one pass over the results
         launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                       locate ? occ64.p : (uint64_t*)nullptr);
+        emit_c8(P, d_counts);
         if (locate) inclusive_scan_u64(occ64.p, oscan, P);  // occurrence and task offsets: one scan of both
         small_copy(pinned, counters.p + 1, 8);
         small_copy(pinned + 2, counters.p + 12, 16);
@@ -2149,6 +2156,20 @@ struct Engine {
     // failed ('#' in a pattern, more overflow patterns than k_deep_wide's launch covered or
     // lists longer than its limit, totals past the buffers).
     static constexpr uint64_t kRedo = ~0ull;
+    // the host pipeline's byte-wide counts (k_counts_u8), queued with the search that makes
+    // the counts so they are ready when it returns (c8_out.c8 null: none)
+    struct C8Out {
+        uint8_t* c8 = nullptr;
+        uint2* exc = nullptr;
+        uint32_t* ne = nullptr;
+    } c8_out;
+    void emit_c8(uint64_t P, const uint32_t* d_counts) {
+        if (!c8_out.c8 || !P) return;
+        zero(c8_out.ne, 8);
+        hipLaunchKernelGGL(k_counts_u8, dim3((unsigned)std::min<uint64_t>(2048, (P + 1023) / 1024)), dim3(256), 0, stream, d_counts, P,
+                           c8_out.c8, c8_out.exc, c8_out.ne);
+        HIPCHK(hipGetLastError());
+    }
     uint64_t finish_deferred(uint64_t P, uint32_t first_id, bool locate, int loc_mode, uint32_t* d_counts, hipEvent_t e1) {
         const KIdx X = kidx();
         // (counters, the scan's first slot and the check words were zeroed by search())
@@ -2158,6 +2179,7 @@ struct Engine {
         if (locate) occ64.ensure(P);
         launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                       locate ? occ64.p : (uint64_t*)nullptr);
+        emit_c8(P, d_counts);
         uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
         // dense samples: records straight from each pattern's result (k_locate_pp / k_locate_big),
         // no tasks (EDSBWT_LOCATE_TASKS=1: the task path as for every other search)
@@ -2271,7 +2293,6 @@ struct Engine {
             HIPCHK(hipEventCreateWithFlags(&comp_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&down_done[k], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&prep_done[k], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&c8_done[k], hipEventDisableTiming));
         }
     }
     // host -> device on `up` (staged through page-locked memory when src is pageable)
@@ -2548,11 +2569,11 @@ struct Engine {
     std::vector<hipEvent_t> chunk_ev;     // ... and their completion
     std::vector<hipEvent_t> chunk_down_ev;  // each chunk's downloads (compact records: the expander waits on them)
 
-    // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 64 MB), cut at line ends; the
+    // chunks of about EDSBWT_CHUNK_MB of pattern bytes (default 40 MB: tools/ab_calls.py on C3, 40 against 32-64), cut at line ends; the
     // first and last chunks ramp up from / down to 1/8 of that (EDSBWT_CHUNK_RAMP=0: uniform),
     // so the pipeline fills and drains fast
     std::vector<Chunk> cut_chunks(const uint8_t* text, uint64_t len, const uint64_t* offs, uint64_t npat, bool lines) {
-        const uint64_t target = std::max<uint64_t>(1, (uint64_t)(env_double("EDSBWT_CHUNK_MB", 64) * 1048576.0));
+        const uint64_t target = std::max<uint64_t>(1, (uint64_t)(env_double("EDSBWT_CHUNK_MB", 40) * 1048576.0));
         std::vector<uint64_t> sizes;
         {
             const bool ramp = env_double("EDSBWT_CHUNK_RAMP", 1) != 0;
@@ -2838,7 +2859,6 @@ struct Engine {
                             dn += j.n * sizeof(edsbwt_occ);
                             j.n = 0;
                         }
-                        HIPCHK(hipEventSynchronize(c8_done[sl]));
                         const uint64_t cb = c8_bytes(j.P);
                         stage_c8[sl].ensure(cb);
                         hsa_copy(stage_c8[sl].p, hc8[sl].p, cb, true, eng_down, sig);
@@ -2931,25 +2951,22 @@ struct Engine {
                 hcounts[sl].ensure(P + 1);
                 std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
                 uint64_t n = 0;
+                if (derive_counts && P) {
+                    hc8[sl].ensure(c8_bytes(P));
+                    hexc[sl].ensure(P);
+                    c8_out = C8Out{hc8[sl].p, hexc[sl].p, reinterpret_cast<uint32_t*>(hc8[sl].p + c8_bytes(P) - 8)};
+                }
                 try {
                     n = search(hbytes[sl].p, hoffs[sl].p, P, first_id + (uint32_t)pats, flags, hcounts[sl].p);
                 } catch (...) {
                     known_len = false;
+                    c8_out = C8Out{};
                     std::swap(rec, hrec[sl]);
                     throw;
                 }
                 known_len = false;
+                c8_out = C8Out{};
                 std::swap(rec, hrec[sl]);
-                if (derive_counts && P) {
-                    hc8[sl].ensure(c8_bytes(P));
-                    hexc[sl].ensure(P);
-                    uint32_t* ne = reinterpret_cast<uint32_t*>(hc8[sl].p + c8_bytes(P) - 8);
-                    zero_on(ne, 8, stream);
-                    hipLaunchKernelGGL(k_counts_u8, dim3((unsigned)std::min<uint64_t>(2048, (P + 1023) / 1024)), dim3(256), 0, stream,
-                                       (const uint32_t*)hcounts[sl].p, P, hc8[sl].p, hexc[sl].p, ne);
-                    HIPCHK(hipGetLastError());
-                    HIPCHK(hipEventRecord(c8_done[sl], stream));
-                }
                 mark("searched", k);
                 accumulate(agg, st);
                 if (locate && n && total + n > arena_cap) {

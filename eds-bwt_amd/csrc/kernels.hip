@@ -545,6 +545,96 @@ __global__ void __launch_bounds__(256) k_keys_packed(const uint8_t* __restrict__
     if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
 }
 
+// per byte of x: 0x80 where the byte is zero, else 0 (exact, no borrow between bytes)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) { return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u; }
+// k_keys_packed for the alphabet {#, A, C, G, T} (codes 0..4: DNA, C3's): four characters per
+// LDS word, their digits by byte compares (SWAR) instead of one table lookup and one
+// multiply-add per character.  The pattern's digits form V (its last character least
+// significant): kid = the low 2D bits, the packed start = the rest, closed by a 1 bit — the same
+// values k_keys_packed writes (its per-character loop is kept for patterns over 32 characters).
+__global__ void __launch_bounds__(256) k_keys_acgt(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
+                                                   uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term, uint32_t D,
+                                                   uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
+    __shared__ uint4 sbuf4[kKeySpan / 16 + 2];
+    __shared__ unsigned long long sh[4];
+    const uint32_t* sbuf = reinterpret_cast<const uint32_t*>(sbuf4);
+    unsigned long long nt = 0;
+    for (size_t base = (size_t)blockIdx.x * blockDim.x; base < P; base += (size_t)gridDim.x * blockDim.x) {
+        const size_t nb = min((size_t)blockDim.x, (size_t)P - base);
+        const uint64_t s0 = off[base], s1 = off[base + nb];
+        const uint64_t w0 = s0 & ~15ull;
+        const bool staged = s1 - w0 + 16 <= kKeySpan && ((uintptr_t)bytes & 15) == 0;
+        __syncthreads();
+        if (staged) {
+            const uint32_t nw = (uint32_t)((s1 - w0 + 15) / 16);
+            const uint4* src = reinterpret_cast<const uint4*>(bytes + w0);
+            for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x) sbuf4[t] = src[t];
+        }
+        __syncthreads();
+        const size_t i = base + threadIdx.x;
+        if (i < P) {
+            const uint64_t a = off[i];
+            const uint32_t L = (uint32_t)(off[i + 1] - a);
+            len[i] = L;
+            uint64_t V = 0;
+            bool ok = true, term = false;
+            if (L <= 32) {
+                const uint32_t so = (uint32_t)(a - w0);
+                for (uint32_t j = 0; j < L; j += 4) {
+                    const uint32_t n = min(4u, L - j);
+                    uint32_t w;
+                    if (staged) {
+                        const uint32_t o = so + j;
+                        w = __builtin_amdgcn_alignbyte(sbuf[(o >> 2) + 1], sbuf[o >> 2], o & 3u);
+                    } else {
+                        w = 0;
+                        for (uint32_t t = 0; t < n; t++) w |= (uint32_t)bytes[a + j + t] << (8 * t);
+                    }
+                    const uint32_t live = n == 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - n)));  // the n bytes in the pattern
+                    const uint32_t mC = zero_bytes(w ^ 0x43434343u), mG = zero_bytes(w ^ 0x47474747u), mT = zero_bytes(w ^ 0x54545454u);
+                    const uint32_t hit = zero_bytes(w ^ 0x41414141u) | mC | mG | mT;
+                    ok &= (hit & live) == live;
+                    term |= (zero_bytes(w ^ 0x23232323u) & live) != 0;
+                    const uint32_t bad = ~hit & 0x80808080u;  // '#' or outside the alphabet: digit 3, as (0 - 1) & 3
+                    const uint32_t q = ((mC | mT | bad) >> 7) | ((mG | mT | bad) >> 6);  // digit (A 0, C 1, G 2, T 3) per byte
+                    const uint32_t pk = ((q & 3u) << 6) | (((q >> 8) & 3u) << 4) | (((q >> 16) & 3u) << 2) | ((q >> 24) & 3u);
+                    V = (V << (2 * n)) | (pk >> (8 - 2 * n));
+                }
+            } else {  // rare: longer patterns keep k_keys_packed's per-character order
+                uint32_t x = 0, mul = 1, nn = 0;
+                uint64_t rem = 0;
+                for (uint32_t t = 0; t < L; t++) {
+                    const uint32_t ch = bytes[a + L - 1 - t];
+                    const uint32_t v = ch == 'A' ? 1u : ch == 'C' ? 2u : ch == 'G' ? 3u : ch == 'T' ? 4u : 0u;
+                    term |= ch == '#';
+                    ok &= v != 0;
+                    if (t < D) { x += (v - 1) * mul; mul *= 4u; }
+                    else { rem |= (uint64_t)((v - 1) & 3u) << (2 * nn); nn++; }
+                }
+                nt += term;
+                rem |= 1ull << (2 * nn);
+                pv[i] = rem << 31 | (uint64_t)i;
+                kid[i] = ok ? x : E;
+                continue;
+            }
+            nt += term;
+            uint32_t x;
+            uint64_t rem;
+            if (L <= D) {
+                x = (uint32_t)V;
+                rem = 1ull;
+            } else {
+                x = (uint32_t)(V & ((1ull << (2 * D)) - 1ull));
+                rem = (V >> (2 * D)) | (1ull << (2 * (L - D)));
+            }
+            pv[i] = rem << 31 | (uint64_t)i;
+            kid[i] = ok ? x : E;
+        }
+    }
+    nt = block_sum(nt, sh);
+    if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
+}
+
 // direct start: patterns grouped by their D-mer's leading bits (kid >> shift) for locality —
 // neighbouring lanes then read neighbouring table entries and rows.  cur[] holds each
 // bucket's first slot (exclusive scan of k_keys' histogram) and is advanced by atomics, so
