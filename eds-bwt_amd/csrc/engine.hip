@@ -2575,7 +2575,13 @@ struct Engine {
     std::vector<Chunk> cut_chunks(const uint8_t* text, uint64_t len, const uint64_t* offs, uint64_t npat, bool lines) {
         const uint64_t target = std::max<uint64_t>(1, (uint64_t)(env_double("EDSBWT_CHUNK_MB", 40) * 1048576.0));
         std::vector<uint64_t> sizes;
-        {
+        // a batch of at most EDSBWT_CHUNK_SINGLE_MB (default 24) is one chunk: every chunk pays
+        // a search's fixed cost, which small batches (C2's 21 MB, C5's 7 MB of grouped search)
+        // do not win back by overlapping their transfers
+        const uint64_t single = (uint64_t)(env_double("EDSBWT_CHUNK_SINGLE_MB", 24) * 1048576.0);
+        if (len <= single) {
+            sizes = {len};
+        } else {
             const bool ramp = env_double("EDSBWT_CHUNK_RAMP", 1) != 0;
             const uint64_t steps[3] = {std::max<uint64_t>(1, target / 8), std::max<uint64_t>(1, target / 4), std::max<uint64_t>(1, target / 2)};
             const uint64_t rsum = steps[0] + steps[1] + steps[2];

@@ -773,7 +773,19 @@ __global__ void __launch_bounds__(256) k_lminmax(const uint64_t* __restrict__ of
     if (threadIdx.x == 0) smx = smn = 0;
     __syncthreads();
     uint32_t mx = 0, nmn = 0;
-    GRID_STRIDE(i, P) {
+    // four lengths per thread and round: two 16-B loads and the next group's first offset
+    // (a 16-B aligned array; else one offset pair at a time)
+    const uint64_t P4 = ((uintptr_t)off & 15) == 0 ? P / 4 : 0;
+    const ulonglong2* o2 = reinterpret_cast<const ulonglong2*>(off);
+    GRID_STRIDE(g, P4) {
+        const ulonglong2 a = o2[2 * g], b = o2[2 * g + 1];
+        const uint64_t c = off[4 * g + 4];
+        const uint32_t l0 = (uint32_t)(a.y - a.x), l1 = (uint32_t)(b.x - a.y), l2 = (uint32_t)(b.y - b.x), l3 = (uint32_t)(c - b.y);
+        mx = max(max(mx, max(l0, l1)), max(l2, l3));
+        nmn = max(max(nmn, max(~l0, ~l1)), max(~l2, ~l3));
+    }
+    GRID_STRIDE(j, P - 4 * P4) {
+        const uint64_t i = 4 * P4 + j;
         const uint32_t L = (uint32_t)(off[i + 1] - off[i]);
         mx = max(mx, L);
         nmn = max(nmn, ~L);

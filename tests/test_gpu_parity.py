@@ -523,6 +523,7 @@ def test_search_lines_pipeline_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned
         text = ("\n".join(pats) + ("\n" if trailing else "")).encode()
         for mb in ("0.01", "64"):
             monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
+            monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")  # small batches would otherwise be one chunk
             with edsbwt.Index(base) as idx:
                 gc, go = _lines_search(edsbwt, idx, text, first_id=77, pinned=pinned)
                 st = idx.stats()
@@ -560,6 +561,7 @@ def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
             for pack in ("1", "0"):
                 monkeypatch.setenv("EDSBWT_PACK_LINES", pack)
                 monkeypatch.setenv("EDSBWT_CHUNK_MB", "0.02")
+                monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
                 with edsbwt.Index(base) as idx:
                     gc, go = _lines_search(edsbwt, idx, text, first_id=5, pinned=pinned)
                     st = idx.stats()

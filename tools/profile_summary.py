@@ -29,7 +29,7 @@ CLASSES = {
     # average per launch is comparable with bench.py's event-timed class average
     "deep": ("k_deep_fast", "k_deep", "k_deep_wide", "k_list_flagged", "k_ovf_lens",
              "k_group_end", "k_group_count", "k_group_scatter", "k_sub_build", "k_sub_bytes", "k_sub_scatter"),
-    "locate": ("k_locate",),
+    "locate": ("k_locate", "k_locate_pp", "k_locate_big"),
 }
 FETCH_FACTOR_GATHER64 = 1.0
 
