@@ -73,6 +73,22 @@ def main():
             pmc[k][key] += FETCH_FACTOR_GATHER64 * v if key == "fetch_bytes" else v
             if key == "fetch_bytes":
                 pmc[k]["dispatches"] += 1
+    # registers, LDS and the occupancy they allow, per kernel (kernel trace columns).  gfx950:
+    # 512 VGPRs per lane per SIMD shared by the arch and accumulation registers (granule 8),
+    # at most 8 waves per SIMD, 160 KB of LDS per CU (4 SIMDs)
+    res = {}
+    for r in csv.DictReader(open(first_csv(a.trace_dir, "kernel_trace.csv"))):
+        k = short(r["Kernel_Name"])
+        if k in res:
+            continue
+        v, acc = int(r["VGPR_Count"]), int(r.get("Accum_VGPR_Count") or 0)
+        lds, wg = int(r["LDS_Block_Size"]), max(1, int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"]))
+        regs = max(8, -(-(v + acc) // 8) * 8)
+        w_reg = min(8, 512 // regs)
+        waves_per_wg = -(-wg // 64)
+        w_lds = 8 if lds == 0 else min(8, (160 * 1024 // lds) * waves_per_wg // 4)
+        res[k] = {"vgpr": v, "agpr": acc, "sgpr": int(r["SGPR_Count"]), "lds_bytes": lds, "scratch_bytes": int(r["Scratch_Size"]),
+                  "workgroup": wg, "waves_per_simd": min(w_reg, w_lds), "occupancy_limit": "vgpr" if w_reg <= w_lds else "lds"}
     bench = json.load(open(a.bench_json))
     classes = {}
     for c, ks in CLASSES.items():
@@ -87,7 +103,7 @@ def main():
     out_d = {"bench": {k: bench.get(k) for k in ("value", "ms_per_step", "roofline", "kernel_ms_per_step")},
              "fetch_factor": FETCH_FACTOR_GATHER64,
              "classes": classes,
-             "kernels": {k: {**per[k], **pmc.get(k, {})} for k in sorted(per, key=lambda k: -per[k]["total_ms"])}}
+             "kernels": {k: {**per[k], **pmc.get(k, {}), **res.get(k, {})} for k in sorted(per, key=lambda k: -per[k]["total_ms"])}}
     json.dump(out_d, open(a.out, "w"), indent=1)
     if a.traffic:
         json.dump({"source": a.source, "fetch_factor": FETCH_FACTOR_GATHER64, "classes": classes}, open(a.traffic, "w"), indent=1)
