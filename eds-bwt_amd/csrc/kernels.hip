@@ -2210,38 +2210,84 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
     r.offset = off;
     rec[o] = r;
 }
+// records of one block's 256 patterns are one contiguous range of the output: staged in LDS
+// (up to kLocStage records) and written out as 16-B stores, instead of five strided 4-B stores
+// per record from every lane (records of patterns left to k_locate_big, which runs next on the
+// stream, are written over by it)
+constexpr uint32_t kLocStage = 1024;
 __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, const uint64_t* __restrict__ oscan, uint32_t first_id,
                                                    KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
                                                    uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats) {
+    __shared__ uint32_t sw[kLocStage * 5];
+    __shared__ uint64_t s_lo, s_hi;
+    __shared__ unsigned long long sh[4];
     unsigned long long my_off = 0;
-    GRID_STRIDE(i, P) {
-        const Res r = res[i];
-        const uint32_t occ = res_occ(r);
-        if (!occ) continue;
-        const uint64_t base = oscan[i] >> 32;  // the packed scan: occurrences << 32 | tasks
-        if (base + occ > occ_cap) { atomicOr(oflow, 1u); continue; }
-        const uint32_t pat = first_id + (uint32_t)i;
-        if (r.cnt & kResPos) {
-            const uint32_t off = (uint32_t)(r.off >> 32);
-            put_rec(rec, base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
-            my_off += off;
-            continue;
+    uint32_t* recw = reinterpret_cast<uint32_t*>(rec);
+    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < P; p0 += (uint64_t)gridDim.x * blockDim.x) {  // block-uniform
+        const uint64_t i = p0 + threadIdx.x, plast = min(P, p0 + blockDim.x) - 1;
+        Res r{};
+        uint32_t occ = 0;
+        uint64_t base = 0;
+        if (i < P) {
+            r = res[i];
+            occ = res_occ(r);
+            base = oscan[i] >> 32;  // the packed scan: occurrences << 32 | tasks
         }
-        if (occ > kLocBig) { flag_push(big, (uint32_t)i); continue; }
-        uint64_t o = base;
-        const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
-        for (uint32_t t = 0; t < n; t++) {
-            const uint32_t b = (r.cnt & kResRow) ? (uint32_t)r.off : ab[r.off + t];
-            const uint32_t e = (r.cnt & kResRow) ? (uint32_t)r.off + occ - 1 : ae[r.off + t];
-            for (uint32_t x = b; x <= e; x++, o++) {
-                const uint4 sm = X.samples[x];
-                put_rec(rec, o, pat, sm.x, sm.z, sm.w, sm.y);
-                my_off += sm.y;
+        if (threadIdx.x == 0) s_lo = base;
+        if (i == plast) s_hi = base + occ;
+        __syncthreads();
+        const uint64_t lo = s_lo, hi = min(s_hi, occ_cap);
+        const bool stage = hi >= lo && hi - lo <= kLocStage;
+        auto emit = [&](uint64_t o, uint32_t pat, uint32_t word, uint32_t seg, uint32_t wis, uint32_t off) {
+            if (stage) {
+                uint32_t* d = sw + (o - lo) * 5;
+                d[0] = pat; d[1] = word; d[2] = seg; d[3] = wis; d[4] = off;
+            } else {
+                put_rec(rec, o, pat, word, seg, wis, off);
+            }
+        };
+        if (i < P && occ) {
+            const uint32_t pat = first_id + (uint32_t)i;
+            if (base + occ > occ_cap) {
+                atomicOr(oflow, 1u);
+            } else if (r.cnt & kResPos) {
+                const uint32_t off = (uint32_t)(r.off >> 32);
+                emit(base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
+                my_off += off;
+            } else if (occ > kLocBig) {
+                flag_push(big, (uint32_t)i);
+            } else {
+                uint64_t o = base;
+                const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
+                for (uint32_t t = 0; t < n; t++) {
+                    const uint32_t b = (r.cnt & kResRow) ? (uint32_t)r.off : ab[r.off + t];
+                    const uint32_t e = (r.cnt & kResRow) ? (uint32_t)r.off + occ - 1 : ae[r.off + t];
+                    for (uint32_t x = b; x <= e; x++, o++) {
+                        const uint4 sm = X.samples[x];
+                        emit(o, pat, sm.x, sm.z, sm.w, sm.y);
+                        my_off += sm.y;
+                    }
+                }
             }
         }
+        __syncthreads();
+        if (stage && hi > lo) {
+            // words [lo*5, hi*5) of the output: 4-B stores up to a 16-B boundary, 16-B stores, 4-B tail
+            const uint64_t g0 = lo * 5, nw = (hi - lo) * 5;
+            const uint32_t head = (uint32_t)min<uint64_t>(nw, (4u - (uint32_t)(g0 & 3u)) & 3u);
+            const uint64_t nq = (nw - head) / 4;
+            if (threadIdx.x < head) recw[g0 + threadIdx.x] = sw[threadIdx.x];
+            uint4* dst = reinterpret_cast<uint4*>(recw + g0 + head);
+            for (uint64_t q = threadIdx.x; q < nq; q += blockDim.x) {
+                const uint32_t* s4 = sw + head + 4 * q;
+                dst[q] = make_uint4(s4[0], s4[1], s4[2], s4[3]);
+            }
+            const uint64_t t0 = head + nq * 4;
+            if (threadIdx.x < nw - t0) recw[g0 + t0 + threadIdx.x] = sw[t0 + threadIdx.x];
+        }
+        __syncthreads();
     }
-    __shared__ unsigned long long sh[4];
     stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
 }
 __global__ void __launch_bounds__(256) k_locate_big(const uint32_t* __restrict__ big, const Res* __restrict__ res,
