@@ -2176,25 +2176,32 @@ struct Engine {
         uint64_t occ_cap = std::min<uint64_t>(0xffffffffull, std::max<uint64_t>({rec.cap, 2 * P + 65536, (uint64_t)(occ_per_pat * 1.25 * (double)P)}));
         uint64_t task_cap = std::min<uint64_t>(0xffffffffull, std::max<uint64_t>({trow.cap, 2 * P + 65536, (uint64_t)(tasks_per_pat * 1.25 * (double)P)}));
         if (defer_cap) occ_cap = task_cap = defer_cap;
-        if (locate) occ64.ensure(P);
-        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
-                      locate ? occ64.p : (uint64_t*)nullptr);
-        emit_c8(P, d_counts);
-        uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
         // dense samples: records straight from each pattern's result (k_locate_pp / k_locate_big),
         // no tasks (EDSBWT_LOCATE_TASKS=1: the task path as for every other search)
         const bool per_pattern = locate && loc_mode == 2 && X.samp_dense && locate_pp;
+        if (locate && !per_pattern) occ64.ensure(P);
+        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
+                      locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
+        emit_c8(P, d_counts);
+        uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
         if (per_pattern) {
-            inclusive_scan_u64(occ64.p, oscan, P, false);
+            // record offsets: a u32 scan of the counts themselves (a total past 2^32 fails the
+            // occ_cap check below); o32[0] = 0 from search()'s zeroing of oscan's first 8 bytes
+            oscan.ensure(P + 1);
+            uint32_t* o32 = reinterpret_cast<uint32_t*>(oscan.p);
+            size_t tb = 0;
+            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_counts, o32 + 1, (int)P, stream));
+            tmp.ensure(tb);
+            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, d_counts, o32 + 1, (int)P, stream)); });
             hmark("locate scan");
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);
             zero(lbig.p, 4);
-            launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, (const uint64_t*)oscan.p, first_id, X, (const uint32_t*)ab.p,
+            launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p);
             timed(KC_LOCATE, [&] {
                 hipLaunchKernelGGL(k_locate_big, dim3(256), dim3(256), 0, stream, (const uint32_t*)lbig.p, (const Res*)res.p,
-                                   (const uint64_t*)oscan.p, first_id, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
+                                   (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
             });
             HIPCHK(hipGetLastError());
             task_cap = ~0ull;  // no task buffers in this path

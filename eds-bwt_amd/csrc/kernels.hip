@@ -2215,7 +2215,7 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
 // per record from every lane (records of patterns left to k_locate_big, which runs next on the
 // stream, are written over by it)
 constexpr uint32_t kLocStage = 1024;
-__global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, const uint64_t* __restrict__ oscan, uint32_t first_id,
+__global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, const uint32_t* __restrict__ oscan, uint32_t first_id,
                                                    KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
                                                    uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats) {
@@ -2232,7 +2232,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
         if (i < P) {
             r = res[i];
             occ = res_occ(r);
-            base = oscan[i] >> 32;  // the packed scan: occurrences << 32 | tasks
+            base = oscan[i];  // exclusive scan of the counts
         }
         if (threadIdx.x == 0) s_lo = base;
         if (i == plast) s_hi = base + occ;
@@ -2291,7 +2291,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
     stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
 }
 __global__ void __launch_bounds__(256) k_locate_big(const uint32_t* __restrict__ big, const Res* __restrict__ res,
-                                                    const uint64_t* __restrict__ oscan, uint32_t first_id, KIdx X,
+                                                    const uint32_t* __restrict__ oscan, uint32_t first_id, KIdx X,
                                                     const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                     edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
     unsigned long long my_off = 0;
@@ -2300,7 +2300,7 @@ __global__ void __launch_bounds__(256) k_locate_big(const uint32_t* __restrict__
         const uint32_t i = big[1 + j];
         const Res r = res[i];
         const uint32_t occ = res_occ(r), pat = first_id + i;
-        const uint64_t base = oscan[i] >> 32;
+        const uint64_t base = oscan[i];
         const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
         uint64_t start = 0;
         for (uint32_t t = 0; t < n; t++) {
