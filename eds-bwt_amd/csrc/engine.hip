@@ -2749,6 +2749,7 @@ struct Engine {
         size_t counted = 0;
         std::vector<Job> landed;
         const uint8_t* text_end = text + (nch ? ch.back().b1 : 0);
+        const bool prepack = env_double("EDSBWT_PREPACK", 1) != 0;
         std::vector<std::tuple<const char*, size_t, double>> marks;
         std::mutex mark_m;
         auto mark = [&](const char* what, size_t k) {
@@ -2770,6 +2771,9 @@ struct Engine {
                 HIPCHK(hipSetDevice(device));
                 if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) throw Fail(EDSBWT_E_DEVICE, "hsa_signal_create failed");
                 have_sig = true;
+                size_t pre_k = ~size_t(0);  // the chunk packed ahead (pre_P lines of pre_L bases; 0: raw)
+                uint64_t pre_P = 0;
+                uint32_t pre_L = 0;
                 for (size_t k = 0; k < nch; k++) {
                     {
                         std::unique_lock<std::mutex> lk(m);
@@ -2781,11 +2785,21 @@ struct Engine {
                     const uint64_t nb = c.b1 - c.b0;
                     mark("upload", k);
                     uint32_t L = 0;
-                    const uint64_t Pk = lines ? pack_chunk(text + c.b0, nb, text_end, sl, &L) : 0;
+                    uint64_t Pk = 0;
+                    if (lines) Pk = pre_k == k ? (L = pre_L, pre_P) : pack_chunk(text + c.b0, nb, text_end, sl, &L);
+                    pre_k = ~size_t(0);
                     if (Pk) {  // 2 bits per base over PCIe, unpacked on the device
                         const uint64_t pb = Pk * ((L + 3) / 4);
                         hpack[sl].ensure(pb + 16);
-                        hsa_copy(hpack[sl].p, stage_pack[sl].p, pb, false, eng_up, sig);
+                        hsa_copy_start(hpack[sl].p, stage_pack[sl].p, pb, false, eng_up, sig);
+                        if (k + 1 < nch && prepack) {
+                            // the next chunk packed while this one crosses PCIe (its staging buffer's
+                            // last upload has finished)
+                            const Chunk& c2 = ch[k + 1];
+                            pre_P = pack_chunk(text + c2.b0, c2.b1 - c2.b0, text_end, (int)((k + 1) % kSlots), &pre_L);
+                            pre_k = k + 1;
+                        }
+                        hsa_wait(sig);
                         prep_packed(sl, nb, Pk, L);
                         HIPCHK(hipEventRecord(prep_done[sl], up));
                         mark("uploaded", k);
