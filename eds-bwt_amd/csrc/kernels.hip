@@ -1140,14 +1140,14 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             bool pair_skip = false;  // the pair entry just found '#' rows: take one step
             uint32_t tri_from = 0;   // no three-step attempt before this depth (one just failed)
             bool posres = false;     // answered by the text compare: (word, offset) result written
-            if (X.rtext && b == e && d < L) {
+            for (bool first = true; X.rtext && b == e && d < L; first = false) {
                 // One row = one text position (word w, offset o): while no '#' row is met (o > 0)
                 // each backward step keeps one row and succeeds iff the text character before it
                 // equals the pattern's, so the next k = min(o, m) characters are decided by comparing
                 // them with the text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row)
                 const uint4 s = X.samples[b];
-                const uint32_t g = g1 != ~0u ? g1 : X.gpos[b];
-                n_blk += g1 != ~0u ? 2 : 3;
+                const uint32_t g = first && g1 != ~0u ? g1 : X.gpos[b];
+                n_blk += first && g1 != ~0u ? 2 : 3;
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 bool eq = true, valid_codes = true;
@@ -1169,25 +1169,50 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                     }
                     eq = ((rtext_window(X.rtext, r0 + j) ^ want) & mask) == 0;
                 }
-                if (valid_codes) {
-                    if (!eq) {
-                        alive = false;
-                        d = L;
-                    } else if (s.y >= m) {
-                        if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
-                            posres = true;
-                            n_text += m;
-                            d = L;
-                            put_res(res, pv ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
-                        }
-                    } else {
-                        // the word's first o characters matched: go on from its whole-word row
-                        n_text += s.y;
-                        d += s.y;
-                        b = e = X.wrow[s.x];
-                        n_blk++;
-                    }
+                if (!valid_codes) break;  // '#' in the pattern: the walk below takes it
+                if (!eq) {
+                    alive = false;
+                    d = L;
+                    break;
                 }
+                if (s.y >= m) {
+                    if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
+                        posres = true;
+                        n_text += m;
+                        d = L;
+                        put_res(res, pv ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                    }
+                    break;
+                }
+                // the word's first o characters matched: its whole-word row is the '#' row of word
+                // s.x, so the next step is the link (:512-563) from ONE segment, s.z — the words of
+                // segments [seg_lo[s.z], s.z - 1] by the next character, one interval from the
+                // segment table (what k_deep would do after a rank and an eof_seg read)
+                n_text += s.y;
+                d += s.y;
+                const uint32_t c = code_at(d);
+                if (c == 0 || c >= X.sigma) {  // '#' or outside the alphabet: the walk below decides
+                    b = e = X.wrow[s.x];
+                    n_blk++;
+                    break;
+                }
+                if (s.z < 2) {  // the first segment: no previous words (eof_seg 0)
+                    alive = false;
+                    d = L;
+                    break;
+                }
+                const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
+                const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
+                n_blk++;
+                n_steps++;
+                if (ry <= rx) {
+                    alive = false;
+                    d = L;
+                    break;
+                }
+                b = X.C[c] + rx;
+                e = X.C[c] + ry - 1;
+                d++;
             }
             for (; d < L; d++) {
                 const uint32_t c = code_at(d);
@@ -1379,6 +1404,19 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
                     } else {
                         n_text += s.y;
                         d += s.y;
+                        // the whole word matched: the link from its one segment, as in k_deep_fast
+                        const uint32_t c = code_at(d);
+                        if (c != 0 && c < X.sigma) {
+                            if (s.z < 2) { cn = 0; break; }
+                            const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
+                            const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
+                            n_blk++;
+                            n_steps++;
+                            if (ry <= rx) { cn = 0; break; }
+                            cb[0] = X.C[c] + rx;
+                            ce[0] = X.C[c] + ry - 1;
+                            continue;  // the loop's d++ consumes c
+                        }
                         cb[0] = ce[0] = X.wrow[s.x];
                         n_blk++;
                     }
