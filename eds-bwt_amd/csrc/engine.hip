@@ -213,7 +213,10 @@ struct Engine {
     // 7.92-8.06 sorting every chunk)
     uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);
     bool keys_packed = env_double("EDSBWT_KEYS_PACKED", 1) != 0;
-    bool acgt_alpha = false;  // the alphabet is {#, A, C, G, T}: k_keys_acgt (EDSBWT_KEYS_SWAR=0: k_keys_packed)
+    bool acgt_alpha = false;
+    // direct(): lengths assumed rather than measured (deferred); a batch that failed the guess
+    // turns it off for this index (mixed-length batches then measure first, as before)
+    bool len_guess = env_double("EDSBWT_LEN_GUESS", 1) != 0, guessed_len = false;  // the alphabet is {#, A, C, G, T}: k_keys_acgt (EDSBWT_KEYS_SWAR=0: k_keys_packed)
     bool keys_swar = env_double("EDSBWT_KEYS_SWAR", 1) != 0;
     bool locate_pp = env_double("EDSBWT_LOCATE_TASKS", 0) == 0;  // deferred path: per-pattern locate
     DBuf<uint32_t> lbig;  // patterns with more than kLocBig records (k_locate_big)
@@ -1467,9 +1470,17 @@ struct Engine {
         const uint32_t D0 = ktab_depth;
         if (!defer_call) zero(counters.p + 8, 24);
         uint32_t Lmax, Lmin;
+        bool unmeasured = false;
         if (known_len) {  // the host pipeline measured the chunk's lines beside the previous search
             Lmax = known_lmax;
             Lmin = known_lmin;
+        } else if (defer_call && len_guess && acgt_alpha && keys_packed && keys_swar && use_packed && direct_sort && !use_buckets && sigma == 5) {
+            // deferred: assume the packed start's lengths (D0 + 1 .. D0 + 16) and let k_keys_acgt
+            // count the patterns outside them with the '#' check (no read-back here)
+            Lmin = D0 + 1;
+            Lmax = D0 + 16;
+            unmeasured = true;
+            guessed_len = true;
         } else {
             launch_reduce(KC_TRIE, k_lminmax, d_off, P, counters.p + 8);
             small_copy(pinned, counters.p + 8, 16);
@@ -1513,7 +1524,8 @@ struct Engine {
         // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass; the
         // packed start needs no chunks (EDSBWT_KEYS_PACKED=0: k_keys for it too)
         if (packed && !buckets && keys_packed && acgt_alpha && keys_swar)
-            launch(KC_TRIE, k_keys_acgt, P, d_bytes, d_off, P, len.p, d_nterm, D0, E, kid, pv_in.p);
+            launch(KC_TRIE, k_keys_acgt, P, d_bytes, d_off, P, len.p, d_nterm, D0, E, kid, pv_in.p, unmeasured ? D0 + 1 : 0u,
+                   unmeasured ? D0 + 16 : 0u);
         else if (packed && !buckets && keys_packed)
             launch(KC_TRIE, k_keys_packed, P, d_bytes, d_off, P, (const uint8_t*)code_of.p, sigma, len.p, d_nterm, D0, E, kid, pv_in.p);
         else if (bps == 3)
@@ -1963,6 +1975,7 @@ struct Engine {
     uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
         t_search0 = std::chrono::steady_clock::now();
         st = edsbwt_stats{};
+        guessed_len = false;
         prof = (flags & (EDSBWT_PROFILE | EDSBWT_PROFILE_LIGHT)) != 0;
         prof_mask = (flags & EDSBWT_PROFILE) ? ~0u : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_LOCATE) | (1u << KC_LINKSORT));
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
@@ -2051,6 +2064,7 @@ struct Engine {
                 return finish_stats(P, locate, use_table, loc_mode, n, e0, e1);
             }
             // a deferred check failed: the batch again on the checked path (inputs are untouched)
+            if (guessed_len) len_guess = false;
             discard_attempt();
             recycle.done = true;
             const uint64_t m = search(d_bytes, d_off, P, first_id, flags | kFlagNoDefer, d_counts);

@@ -554,7 +554,10 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) { return ~(((x & 0x7f
 // values k_keys_packed writes (its per-character loop is kept for patterns over 32 characters).
 __global__ void __launch_bounds__(256) k_keys_acgt(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
                                                    uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term, uint32_t D,
-                                                   uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv) {
+                                                   uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv, uint32_t lmin,
+                                                   uint32_t lmax) {
+    // lmax != 0: the batch's lengths were not measured (no k_lminmax read-back); a pattern outside
+    // [lmin, lmax] counts as one holding '#', so the deferred check sends the batch to the checked path
     __shared__ uint4 sbuf4[kKeySpan / 16 + 2];
     __shared__ unsigned long long sh[4];
     const uint32_t* sbuf = reinterpret_cast<const uint32_t*>(sbuf4);
@@ -577,7 +580,7 @@ __global__ void __launch_bounds__(256) k_keys_acgt(const uint8_t* __restrict__ b
             const uint32_t L = (uint32_t)(off[i + 1] - a);
             len[i] = L;
             uint64_t V = 0;
-            bool ok = true, term = false;
+            bool ok = true, term = lmax != 0 && (L < lmin || L > lmax);
             if (L <= 32) {
                 const uint32_t so = (uint32_t)(a - w0);
                 for (uint32_t j = 0; j < L; j += 4) {
