@@ -574,6 +574,26 @@ def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
                     assert st["bytes_h2d"] == len(text)
 
 
+def test_search_lines_hip_streams_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The host pipeline without explicit SDMA engines (EDSBWT_HSA_COPY=0: HIP-stream copies,
+    the fallback when the HSA agents cannot be matched): same counts and records."""
+    rng = random.Random(4242)
+    segs = _covid_like(rng, 300)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 40)) or "ACGT" for _ in range(3000)] + ["", "AC\r", "N"]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=3)
+    monkeypatch.setenv("EDSBWT_HSA_COPY", "0")
+    monkeypatch.setenv("EDSBWT_CHUNK_MB", "0.01")
+    monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+    text = ("\n".join(pats) + "\n").encode()
+    for pinned in (True, False):
+        with edsbwt.Index(base) as idx:
+            gc, go = _lines_search(edsbwt, idx, text, first_id=3, pinned=pinned)
+            assert idx.stats()["chunks"] > 5
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+
+
 def test_search_lines_empty_and_held_records_gpu(oracle, edsbwt, tmp_path):
     """An empty file; records still held by the caller when the next call runs (the engine
     must not overwrite them) and freed after the index is closed."""
