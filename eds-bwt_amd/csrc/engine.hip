@@ -2284,7 +2284,7 @@ struct Engine {
     }
     void pipe_init() {
         if (up) return;
-        pool.start((unsigned)std::max(0.0, env_double("EDSBWT_HOST_THREADS", 16) - 1));
+        pool.start((unsigned)std::max(0.0, env_double("EDSBWT_HOST_THREADS", 12) - 1));
         cpool.start((unsigned)std::max(0.0, env_double("EDSBWT_COUNT_THREADS", 4) - 1));
         HIPCHK(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
         // downloads: hipMemcpyAsync into page-locked host memory runs as a blit kernel that fills
@@ -2370,7 +2370,7 @@ struct Engine {
         arena8 = q;
         arena8_cap = c;
     }
-    // a few persistent host threads (EDSBWT_HOST_THREADS, default 16: C3 A/B 5.81 ms against 5.91 with 12) for staging copies and
+    // a few persistent host threads (EDSBWT_HOST_THREADS, default 12: bench.py on C3 5.74 ms against 6.0 with 16 — more threads than the 16-CPU share throttles; an in-process A/B had favoured 16) for staging copies and
     // record expansion, so the pipeline never pays thread start-up per chunk
     struct Pool {
         std::vector<std::thread> th;
