@@ -106,11 +106,12 @@ def pin_to_gpu_numa(torch, dev: int):
         return None
 
 
-def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int) -> dict:
+def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int, trie: bool = False) -> dict:
     """The oracle (faithful C restatement of MOVE_EDSBWTSearch: a-balanced M_LF, literal
     per-pattern link/step/locate, MOVE_EDSBWTSearch.cpp:228-374) on the first `sample`
     patterns of this rank's batch, on `threads` host threads over contiguous shards; index
-    load excluded, as the reference's `bs took:` region excludes it (:109,145)."""
+    load excluded, as the reference's `bs took:` region excludes it (:109,145).  trie=True: the
+    trie-sharing variant (orc_search_batch_trie: common pattern suffixes searched once)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc  # checker / CPU baseline only
 
@@ -120,7 +121,7 @@ def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int)
     eng = orc.Engine(base, 8)
     t_open = time.time() - t
     t = time.time()
-    counts, occ, ctr = eng.search(b, o, first_pattern_id=first_id, threads=threads)
+    counts, occ, ctr = eng.search(b, o, first_pattern_id=first_id, threads=threads, trie=trie)
     dt = time.time() - t
     eng.close()
     return {"value": sample / dt, "seconds": dt, "open_s": t_open, "counts": counts, "occ": occ, "ctr": ctr}
@@ -459,6 +460,25 @@ def main():
                                         "sample x value (SURVEY §8(d)); the device executes far fewer (device_resident."
                                         "device_lf_steps_per_sec)")
                 out["cpu_baseline"]["lf_steps_per_sec"] = round(lf_ref * cb["value"], 1)
+                # the trie-sharing CPU variant on the same sample, and §8(d)'s
+                # algorithmic bytes from its deduplicated counters
+                ct = cpu_baseline(base, buf, offs, first_id, samp_n, threads, trie=True)
+                tc = ct["ctr"]
+                plen = int(offs[samp_n] - offs[0])
+                B = (64 * (2 * tc["interval_steps"] + 2 * tc["pdf_calls"] + tc["locate_moves"] + 3 * tc["occurrences"])
+                     + 4 * tc["eof_reads"] + plen + samp_n + 4 * samp_n + 20 * tc["occurrences"])
+                out["cpu_baseline"]["trie_sharing"] = {
+                    "value": round(ct["value"], 3), "cores": threads, "seconds": round(ct["seconds"], 3),
+                    "sample": f"first {samp_n} patterns, sorted by reversed pattern, each thread a contiguous range of "
+                              "that order (orc_search_batch_trie)",
+                    "match_literal": bool(np.array_equal(ct["counts"], cb["counts"]) and np.array_equal(ct["occ"], cb["occ"])),
+                    "interval_steps_per_pattern": round(tc["interval_steps"] / samp_n, 1),
+                }
+                out.setdefault("roofline", {})["survey_oracle_bytes_per_pattern"] = round(B / samp_n, 1)
+                out["roofline"]["survey_oracle_note"] = (
+                    "SURVEY §8(d) B = 64(2 S_steps + 2 K_pdf + W_lf + 3 O) + 4 D_eof + sum(|P|+1) + 4 N_pat + 20 O from the "
+                    "trie-sharing oracle's deduplicated counters on the cpu_baseline sample; a sample shares far fewer "
+                    "suffixes than the full batch, so this overstates the batch's per-pattern bytes")
                 if not match:
                     log("[bench] PARITY SAMPLE MISMATCH")
             except Exception as e:  # the GPU line is still valid

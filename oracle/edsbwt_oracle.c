@@ -770,45 +770,11 @@ static void link_(const orc_engine* E, ctx_t* X) {
     for (size_t i = 0, j = D->n ? D->n - 1 : 0; i < j; i++, j--) { rng_t t = D->v[i]; D->v[i] = D->v[j]; D->v[j] = t; }
 }
 
-/* backwardSearch (:228-374); occurrences appended to X->out */
-static uint32_t backward_search(const orc_engine* E, ctx_t* X, uint32_t n_kmer, const uint8_t* kmer, uint32_t len) {
+/* LOCATE (:328-369): every row of the final list walks M_LF to its '#' */
+static uint32_t locate_list(const orc_engine* E, ctx_t* X, uint32_t n_kmer, const rvec* V) {
     uint32_t num_occ = 0;
-    if (len == 0) return 0; /* kmer[len-1] is undefined behaviour in the reference (:239) */
-    X->other.n = 0;
-    X->dollar.n = 0;
-    rng_t first = {0, E->n - 1, 0, E->r - 1}; /* init_backward_search (:220-225) */
-    VEC_PUSH(&X->other, first);
-    if (!bs_step(E, X, kmer[len - 1], &X->other)) return 0;
-    for (uint32_t pos = len - 1; pos > 0; pos--) {
-        int found = 0;
-        link_(E, X);
-        uint8_t sym = kmer[pos - 1];
-        if (X->dollar.n) {
-            if (bs_step(E, X, sym, &X->dollar)) found = 1;
-        }
-        if (bs_step(E, X, sym, &X->other)) found = 1;
-        if (!found) return 0;
-        for (size_t i = 0; i < X->other.n; i++) VEC_PUSH(&X->dollar, X->other.v[i]); /* :300 */
-        { rvec t = X->other; X->other = X->dollar; X->dollar = t; }
-        X->dollar.n = 0;
-        if (X->other.n > 1) { /* adjacency merge (:309-324) */
-            X->merged.n = 0;
-            VEC_PUSH(&X->merged, X->other.v[0]);
-            for (size_t i = 1; i < X->other.n; i++) {
-                rng_t* last = &X->merged.v[X->merged.n - 1];
-                if (X->other.v[i].b == last->e + 1) {
-                    last->e = X->other.v[i].e;
-                    last->ei = X->other.v[i].ei;
-                } else {
-                    VEC_PUSH(&X->merged, X->other.v[i]);
-                }
-            }
-            rvec t = X->other; X->other = X->merged; X->merged = t;
-        }
-    }
-    /* LOCATE (:328-369) */
-    for (size_t i = 0; i < X->other.n; i++) {
-        rng_t iv = X->other.v[i];
+    for (size_t i = 0; i < V->n; i++) {
+        rng_t iv = V->v[i];
         uint32_t prev_copy = iv.bi, prevII = iv.bi;
         num_occ += iv.e - iv.b + 1;
         for (uint32_t j = iv.b; j <= iv.e; j++) {
@@ -831,6 +797,50 @@ static uint32_t backward_search(const orc_engine* E, ctx_t* X, uint32_t n_kmer, 
         }
     }
     return num_occ;
+}
+
+/* One iteration of backwardSearch's character loop (:241-325): link the '#' rows of the
+ * list, step both lists by sym, concatenate (:300) and merge adjacent intervals (:309-324).
+ * Returns 0 when neither step found anything (the search ends with count 0). */
+static int bs_level(const orc_engine* E, ctx_t* X, uint8_t sym) {
+    int found = 0;
+    link_(E, X);
+    if (X->dollar.n) {
+        if (bs_step(E, X, sym, &X->dollar)) found = 1;
+    }
+    if (bs_step(E, X, sym, &X->other)) found = 1;
+    if (!found) return 0;
+    for (size_t i = 0; i < X->other.n; i++) VEC_PUSH(&X->dollar, X->other.v[i]); /* :300 */
+    { rvec t = X->other; X->other = X->dollar; X->dollar = t; }
+    X->dollar.n = 0;
+    if (X->other.n > 1) { /* adjacency merge (:309-324) */
+        X->merged.n = 0;
+        VEC_PUSH(&X->merged, X->other.v[0]);
+        for (size_t i = 1; i < X->other.n; i++) {
+            rng_t* last = &X->merged.v[X->merged.n - 1];
+            if (X->other.v[i].b == last->e + 1) {
+                last->e = X->other.v[i].e;
+                last->ei = X->other.v[i].ei;
+            } else {
+                VEC_PUSH(&X->merged, X->other.v[i]);
+            }
+        }
+        rvec t = X->other; X->other = X->merged; X->merged = t;
+    }
+    return 1;
+}
+
+/* backwardSearch (:228-374); occurrences appended to X->out */
+static uint32_t backward_search(const orc_engine* E, ctx_t* X, uint32_t n_kmer, const uint8_t* kmer, uint32_t len) {
+    if (len == 0) return 0; /* kmer[len-1] is undefined behaviour in the reference (:239) */
+    X->other.n = 0;
+    X->dollar.n = 0;
+    rng_t first = {0, E->n - 1, 0, E->r - 1}; /* init_backward_search (:220-225) */
+    VEC_PUSH(&X->other, first);
+    if (!bs_step(E, X, kmer[len - 1], &X->other)) return 0;
+    for (uint32_t pos = len - 1; pos > 0; pos--)
+        if (!bs_level(E, X, kmer[pos - 1])) return 0;
+    return locate_list(E, X, n_kmer, &X->other);
 }
 
 typedef struct {
@@ -893,6 +903,141 @@ int orc_search_batch(orc_engine* E, const char* bytes, const uint64_t* offsets, 
     if (nocc) *nocc = tot;
     for (int t = 0; t < threads; t++) { if (ctr) add_ctr(ctr, &J[t].X.c); ctx_free(&J[t].X); }
     free(J); free(th);
+    return 0;
+}
+
+/* ---------------------------------------------------------- trie-sharing variant
+ * backwardSearch's list after the last q characters of a pattern depends only on those q
+ * characters, so a batch sorted by reversed pattern shares every common suffix: each thread
+ * walks its contiguous range of the sorted order keeping the list of every depth of the
+ * current path, and a pattern resumes from the deepest list it shares with the previous one.
+ * Same counts and records as orc_search_batch; the counters count each distinct suffix once
+ * (SURVEY §8(d)'s deduplicated work). */
+typedef struct {
+    const uint8_t* bytes;
+    const uint64_t* off;
+} rsort_arg;
+
+static int rev_cmp(const void* pa, const void* pb, void* arg) {
+    const rsort_arg* A = arg;
+    uint64_t i = *(const uint64_t*)pa, j = *(const uint64_t*)pb;
+    const uint8_t *x = A->bytes + A->off[i], *y = A->bytes + A->off[j];
+    uint64_t m = A->off[i + 1] - A->off[i], n = A->off[j + 1] - A->off[j];
+    for (uint64_t k = 0; k < m && k < n; k++) {
+        uint8_t a = x[m - 1 - k], b = y[n - 1 - k];
+        if (a != b) return (a > b) - (a < b);
+    }
+    if (m != n) return (m > n) - (m < n);
+    return (i > j) - (i < j);
+}
+
+typedef struct {
+    const orc_engine* E;
+    const uint8_t* bytes;
+    const uint64_t* off;
+    const uint64_t* order;
+    uint64_t lo, hi;
+    uint32_t first_id;
+    uint32_t* counts;
+    uint64_t* rec_at; /* per pattern: its first record in X.out */
+    ctx_t X;
+} tjob_t;
+
+static void* tjob_run(void* arg) {
+    tjob_t* J = arg;
+    const orc_engine* E = J->E;
+    ctx_t* X = &J->X;
+    rvec* st = NULL;   /* st[d]: the list after d characters of the current path */
+    size_t nst = 0;
+    uint32_t top = 0;  /* depths 1..top of st hold the previous pattern's path */
+    uint32_t dead = 0; /* the previous path's search ended at this depth (0: it did not) */
+    const uint8_t* prev = NULL;
+    uint64_t prev_len = 0;
+    for (uint64_t k = J->lo; k < J->hi; k++) {
+        uint64_t i = J->order[k];
+        const uint8_t* P = J->bytes + J->off[i];
+        uint32_t len = (uint32_t)(J->off[i + 1] - J->off[i]);
+        uint32_t h = 0; /* shared reversed prefix with the previous pattern */
+        while (h < len && h < prev_len && h < top && P[len - 1 - h] == prev[prev_len - 1 - h]) h++;
+        prev = P; prev_len = len;
+        J->rec_at[i] = X->out.n;
+        uint32_t r = 0;
+        if (len == 0) { top = 0; dead = 0; goto done; }
+        if (dead && dead <= h) { top = dead; goto done; } /* a shared suffix already failed */
+        dead = 0;
+        if (nst < (size_t)len + 1) {
+            st = realloc(st, ((size_t)len + 1) * sizeof(rvec));
+            memset(st + nst, 0, ((size_t)len + 1 - nst) * sizeof(rvec));
+            nst = (size_t)len + 1;
+        }
+        X->dollar.n = 0;
+        if (h == 0) {
+            X->other.n = 0;
+            rng_t first = {0, E->n - 1, 0, E->r - 1}; /* init_backward_search (:220-225) */
+            VEC_PUSH(&X->other, first);
+            bs_step(E, X, P[len - 1], &X->other);
+            h = 1;
+        } else {
+            X->other.n = 0;
+            for (size_t t = 0; t < st[h].n; t++) VEC_PUSH(&X->other, st[h].v[t]);
+        }
+        for (uint32_t d = h;; d++) {
+            st[d].n = 0;
+            for (size_t t = 0; t < X->other.n; t++) VEC_PUSH(&st[d], X->other.v[t]);
+            top = d;
+            if (d == len) break;
+            if (!bs_level(E, X, P[len - 1 - d])) { dead = d + 1; top = d + 1; goto done; }
+        }
+        r = locate_list(E, X, J->first_id + (uint32_t)i, &X->other);
+    done:
+        J->counts[i] = r;
+        if (r > 0) X->c.found++; else X->c.not_found++;
+    }
+    for (size_t d = 0; d < nst; d++) free(st[d].v);
+    free(st);
+    return NULL;
+}
+
+int orc_search_batch_trie(orc_engine* E, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                          uint32_t first_pattern_id, int threads, uint32_t* counts,
+                          orc_occ** occ, uint64_t* nocc, orc_counters* ctr) {
+    if (threads < 1) threads = 1;
+    if (threads > 255) threads = 255;
+    if ((uint64_t)threads > npat) threads = npat ? (int)npat : 1;
+    uint64_t* order = xmalloc((size_t)npat * 8 + 8);
+    uint64_t* rec_at = xmalloc((size_t)npat * 8 + 8);
+    uint8_t* owner = xmalloc((size_t)npat + 1);
+    for (uint64_t i = 0; i < npat; i++) order[i] = i;
+    rsort_arg A = {(const uint8_t*)bytes, offsets};
+    qsort_r(order, npat, 8, rev_cmp, &A);
+    tjob_t* J = xcalloc((size_t)threads, sizeof(tjob_t));
+    pthread_t* th = xcalloc((size_t)threads, sizeof(pthread_t));
+    for (int t = 0; t < threads; t++) {
+        J[t].E = E; J[t].bytes = (const uint8_t*)bytes; J[t].off = offsets; J[t].order = order;
+        J[t].lo = npat * (uint64_t)t / (uint64_t)threads;
+        J[t].hi = npat * (uint64_t)(t + 1) / (uint64_t)threads;
+        J[t].first_id = first_pattern_id; J[t].counts = counts; J[t].rec_at = rec_at;
+        for (uint64_t k = J[t].lo; k < J[t].hi; k++) owner[order[k]] = (uint8_t)t;
+    }
+    if (threads == 1) tjob_run(&J[0]);
+    else {
+        for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, tjob_run, &J[t]);
+        for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    }
+    uint64_t tot = 0;
+    for (int t = 0; t < threads; t++) tot += J[t].X.out.n;
+    if (ctr) memset(ctr, 0, sizeof *ctr);
+    if (occ) { /* pattern order, as the reference writes them */
+        *occ = xmalloc((size_t)tot * sizeof(orc_occ) + sizeof(orc_occ));
+        uint64_t at = 0;
+        for (uint64_t i = 0; i < npat; i++) {
+            memcpy(*occ + at, J[owner[i]].X.out.v + rec_at[i], (size_t)counts[i] * sizeof(orc_occ));
+            at += counts[i];
+        }
+    }
+    if (nocc) *nocc = tot;
+    for (int t = 0; t < threads; t++) { if (ctr) add_ctr(ctr, &J[t].X.c); ctx_free(&J[t].X); }
+    free(J); free(th); free(order); free(rec_at); free(owner);
     return 0;
 }
 

@@ -68,6 +68,12 @@ void orc_mlf_arrays(const orc_engine*, uint32_t* p, uint32_t* q, uint32_t* idx, 
 int orc_search_batch(orc_engine*, const char* bytes, const uint64_t* offsets, uint64_t npat,
                      uint32_t first_pattern_id, int threads, uint32_t* counts,
                      orc_occ** occ, uint64_t* nocc, orc_counters* ctr);
+/* The same batch searched with the reversed-suffix trie shared (sorted by reversed
+ * pattern, each thread a contiguous range of that order): identical counts and records
+ * (pattern-major, pattern order); counters count each distinct suffix once. */
+int orc_search_batch_trie(orc_engine*, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                          uint32_t first_pattern_id, int threads, uint32_t* counts,
+                          orc_occ** occ, uint64_t* nocc, orc_counters* ctr);
 void orc_free(void* p);
 
 /* Same loop over a pattern file (getline semantics), writing <out_csv>

@@ -57,6 +57,8 @@ def lib():
         L.orc_search_batch.argtypes = [vp, vp, vp, u64, u32, i32, vp, ctypes.POINTER(vp), ctypes.POINTER(u64),
                                        ctypes.POINTER(Counters)]
         L.orc_search_batch.restype = i32
+        L.orc_search_batch_trie.argtypes = L.orc_search_batch.argtypes
+        L.orc_search_batch_trie.restype = i32
         L.orc_free.argtypes = [vp]
         L.orc_search_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u64, i32, ctypes.POINTER(Counters),
                                       ctypes.POINTER(ctypes.c_double)]
@@ -129,7 +131,10 @@ class Engine:
         lib().orc_mlf_arrays(self._h, p.ctypes.data, q.ctypes.data, idx.ctypes.data, L.ctypes.data)
         return p, q, idx, L
 
-    def search(self, buf: np.ndarray, offs: np.ndarray, first_pattern_id: int = 1, threads: int = 1):
+    def search(self, buf: np.ndarray, offs: np.ndarray, first_pattern_id: int = 1, threads: int = 1,
+               trie: bool = False):
+        """The reference's pattern loop over the batch; trie=True shares common pattern suffixes
+        (orc_search_batch_trie: same results, deduplicated counters)."""
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         npat = offs.size - 1
@@ -137,9 +142,9 @@ class Engine:
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         c = Counters()
-        rc = lib().orc_search_batch(self._h, buf.ctypes.data if buf.size else None, offs.ctypes.data, npat,
-                                    first_pattern_id, threads, counts.ctypes.data, ctypes.byref(occ_p),
-                                    ctypes.byref(nocc), ctypes.byref(c))
+        fn = lib().orc_search_batch_trie if trie else lib().orc_search_batch
+        rc = fn(self._h, buf.ctypes.data if buf.size else None, offs.ctypes.data, npat,
+                first_pattern_id, threads, counts.ctypes.data, ctypes.byref(occ_p), ctypes.byref(nocc), ctypes.byref(c))
         if rc != 0:
             raise RuntimeError(lib().orc_last_error().decode())
         occ = np.zeros(nocc.value, OCC_DTYPE)

@@ -151,3 +151,31 @@ def test_mlf_is_lf(oracle, tmp_path, a):
         length = int(p[i + 1] - p[i])
         lo, hi = np.searchsorted(p[:-1], [q[i], q[i] + length])
         assert hi - lo < 2 * a
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_trie_variant_equals_literal(oracle, tmp_path, seed):
+    """orc_search_batch_trie (the trie-sharing CPU variant) gives the literal
+    pattern loop's counts and records in the same order, including '#' patterns, empty lines,
+    duplicates and patterns that are suffixes of others; its interval steps never exceed the
+    literal's."""
+    rng = random.Random(100 + seed)
+    segs = edsgen.random_eds(rng, rng.randint(10, 80), p_empty=0.0 if seed % 4 == 0 else 0.25)
+    base = _index(oracle, tmp_path, edsgen.eds_text(segs, use_E=(seed % 2 == 1)), text=True)
+    eng = oracle.Engine(base, 2 + seed % 5)
+    pats = []
+    for _ in range(300):
+        m = rng.randint(0, 12)
+        p = edsgen.planted(rng, segs, m) if m and rng.random() < 0.6 else None
+        p = p or "".join(rng.choice("ACGT#" if rng.random() < 0.05 else "ACGT") for _ in range(m))
+        pats.append(p)
+        if rng.random() < 0.2:
+            pats.append(p[rng.randint(0, len(p)):] if p else p)  # a suffix (or a duplicate)
+    buf = np.frombuffer("".join(pats).encode(), np.uint8)
+    offs = np.concatenate(([0], np.cumsum([len(p) for p in pats]))).astype(np.uint64)
+    lc, lo, lctr = eng.search(buf, offs, first_pattern_id=5)
+    for threads in (1, 3):
+        tc, to, tctr = eng.search(buf, offs, first_pattern_id=5, threads=threads, trie=True)
+        assert np.array_equal(tc, lc) and np.array_equal(to, lo)
+        assert tctr["occurrences"] == lctr["occurrences"] and tctr["found"] == lctr["found"]
+        assert tctr["interval_steps"] <= lctr["interval_steps"]
