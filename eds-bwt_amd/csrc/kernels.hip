@@ -1934,13 +1934,27 @@ __global__ void __launch_bounds__(256) k_fin_emit(uint32_t n, const uint32_t* __
         }
         // fk == nullptr (count only): the occurrence sums are all that is kept
         uint32_t at = wave_append(cnt + 4, fk ? f : 0u);
+        uint32_t v = 0;
         if (f) {
             if (fk && at < cap) {
                 fk[at] = ((uint64_t)u << rowbits) | nb[i];
                 fv[at] = ne[i];
             }
-            atomicAdd(node_occ + u, ne[i] - nb[i] + 1);
+            v = ne[i] - nb[i] + 1;
         }
+        // neighbouring items mostly belong to one node: sum each run of equal nodes over the
+        // wave (segmented scan) and let the run's last lane add it, one atomic per run
+        const int lane = threadIdx.x & 63;
+        const uint32_t key = f ? u : 0xffffffffu;
+        const uint32_t kprev = __shfl_up(key, 1, 64);
+        uint32_t head = (lane == 0 || kprev != key) ? 1u : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t pv = __shfl_up(v, o, 64), ph = __shfl_up(head, o, 64);
+            if (lane >= o && !head) { v += pv; head = ph; }
+        }
+        const uint32_t knext = __shfl_down(key, 1, 64);
+        if (key != 0xffffffffu && (lane == 63 || knext != key) && v) atomicAdd(node_occ + u, v);
     }
 }
 
