@@ -1843,18 +1843,16 @@ struct Engine {
             }
             // finish patterns of length D: their node's items, sorted by row
             if (finishing) {
-                const uint32_t ncur_saved = ncur;
-                ncur = nnext;
-                pack_items(nxt);
-                ncur = ncur_saved;
+                // the items stay in their shards (k_fin_emit reads them in place, as the next
+                // depth's k_lvl_items does)
                 launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
                 const size_t cap_fin = count_only ? 0 : shard_bound(nnext, 1);
                 if (!count_only) { efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD); }
                 // count only: per-node occurrence sums, no interval archive (C5-scale batches
                 // finish billions of intervals)
-                launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)iu[nxt].p, (const uint32_t*)ib[nxt].p, (const uint32_t*)ie[nxt].p,
+                launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)fu.p, (const uint32_t*)fb.p, (const uint32_t*)fe.p,
                        (const uint8_t*)fin.p, lcnt.p, count_only ? (uint64_t*)nullptr : efk.p, count_only ? (uint32_t*)nullptr : efv.p,
-                       (uint32_t)cap_fin, node_occ.p, X.rowbits);
+                       (uint32_t)cap_fin, node_occ.p, X.rowbits, (const uint32_t*)fpre.p, (uint32_t)fcap);
                 uint32_t F = 0;
                 if (!count_only) {
                     fetch_shards();

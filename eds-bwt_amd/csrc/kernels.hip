@@ -913,7 +913,10 @@ __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const
         uint32_t f = 1;
         if (t) {
             const uint64_t kp = keys[t - 1];
-            if ((kp >> sb) == (k >> sb) && seg_lo[(uint32_t)(k & sm)] <= (uint32_t)(kp & sm)) f = 0;
+            // seg_lo[s] <= s - 1: a key one segment after (or equal to) its predecessor
+            // continues the run without the seg_lo gather
+            const uint32_t s = (uint32_t)(k & sm), sp = (uint32_t)(kp & sm);
+            if ((kp >> sb) == (k >> sb) && (sp + 1 >= s || seg_lo[s] <= sp)) f = 0;
         }
         flag[t] = f;
     }
@@ -1922,40 +1925,75 @@ __global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__
 __global__ void __launch_bounds__(256) k_fin_emit(uint32_t n, const uint32_t* __restrict__ nu, const uint32_t* __restrict__ nb,
                                                   const uint32_t* __restrict__ ne, const uint8_t* __restrict__ fin, uint32_t* __restrict__ cnt_all,
                                                   uint64_t* __restrict__ fk, uint32_t* __restrict__ fv, uint32_t cap,
-                                                  uint32_t* __restrict__ node_occ, uint32_t rowbits) {
+                                                  uint32_t* __restrict__ node_occ, uint32_t rowbits, const uint32_t* __restrict__ ipre,
+                                                  uint32_t icap) {
+    // ipre != nullptr: the items are still in the step's NSHARD regions (as k_lvl_items reads them)
+    __shared__ uint32_t spre[NSHARD + 1];
+    // the block's occurrence sums per finishing node (open addressing; full: global atomics)
+    constexpr uint32_t kH = 1024;
+    __shared__ uint32_t hk[kH], hv[kH];
+    for (uint32_t t = threadIdx.x; t < kH; t += blockDim.x) { hk[t] = 0xffffffffu; hv[t] = 0; }
+    if (ipre)
+        for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) spre[t] = ipre[t];
+    __syncthreads();
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
     if (fk) { fk += (size_t)sh * cap; fv += (size_t)sh * cap; }
     UNIFORM_STRIDE(i, valid, n) {
         uint32_t f = 0, u = 0;
+        size_t src = i;
         if (valid) {
-            u = nu[i];
+            if (ipre) {
+                uint32_t lo = 0, hi = NSHARD;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (spre[mid] <= (uint32_t)i) lo = mid; else hi = mid;
+                }
+                src = (size_t)lo * icap + ((uint32_t)i - spre[lo]);
+            }
+            u = nu[src];
             f = fin[u];
         }
         // fk == nullptr (count only): the occurrence sums are all that is kept
         uint32_t at = wave_append(cnt + 4, fk ? f : 0u);
         uint32_t v = 0;
         if (f) {
+            const uint32_t b = nb[src], e = ne[src];
             if (fk && at < cap) {
-                fk[at] = ((uint64_t)u << rowbits) | nb[i];
-                fv[at] = ne[i];
+                fk[at] = ((uint64_t)u << rowbits) | b;
+                fv[at] = e;
             }
-            v = ne[i] - nb[i] + 1;
+            v = e - b + 1;
         }
-        // neighbouring items mostly belong to one node: sum each run of equal nodes over the
-        // wave (segmented scan) and let the run's last lane add it, one atomic per run
+        // a few finishing nodes can hold millions of items each (C5: a group's depth-8 nodes):
+        // per-item atomics on one address serialise in L2.  The wave sums each distinct node
+        // first (up to 8 of them; lanes left over add their own) into the block's LDS table,
+        // which goes to memory once at the end.
         const int lane = threadIdx.x & 63;
         const uint32_t key = f ? u : 0xffffffffu;
-        const uint32_t kprev = __shfl_up(key, 1, 64);
-        uint32_t head = (lane == 0 || kprev != key) ? 1u : 0u;
+        uint64_t todo = __ballot(key != 0xffffffffu && v != 0);
+        for (int it = 0; it < 8 && todo; it++) {
+            const int l = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t kl = __shfl(key, l, 64);
+            const bool m = key == kl;
+            uint32_t sum = m ? v : 0u;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t pv = __shfl_up(v, o, 64), ph = __shfl_up(head, o, 64);
-            if (lane >= o && !head) { v += pv; head = ph; }
+            for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+            if (lane == l) {
+                uint32_t slot = (kl * 2654435761u) >> 22, q = 0;
+                for (; q < 16; q++, slot = (slot + 1) & (kH - 1)) {
+                    const uint32_t old = atomicCAS(&hk[slot], 0xffffffffu, kl);
+                    if (old == 0xffffffffu || old == kl) { atomicAdd(&hv[slot], sum); break; }
+                }
+                if (q == 16) atomicAdd(node_occ + kl, sum);
+            }
+            todo &= ~__ballot(m);
         }
-        const uint32_t knext = __shfl_down(key, 1, 64);
-        if (key != 0xffffffffu && (lane == 63 || knext != key) && v) atomicAdd(node_occ + u, v);
+        if ((todo >> lane) & 1) atomicAdd(node_occ + u, v);
     }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < kH; t += blockDim.x)
+        if (hv[t]) atomicAdd(node_occ + hk[t], hv[t]);
 }
 
 // pack shard regions: item t of the packed array lives in shard s = last with
