@@ -908,17 +908,39 @@ __global__ void k_link_emit(uint64_t H, const uint32_t* __restrict__ hoff, uint6
 __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ seg_lo, uint32_t sb,
                             uint32_t* __restrict__ flag) {
     const uint64_t sm = (1ull << sb) - 1;
-    GRID_STRIDE(t, V) {
-        const uint64_t k = keys[t];
-        uint32_t f = 1;
-        if (t) {
-            const uint64_t kp = keys[t - 1];
-            // seg_lo[s] <= s - 1: a key one segment after (or equal to) its predecessor
-            // continues the run without the seg_lo gather
-            const uint32_t s = (uint32_t)(k & sm), sp = (uint32_t)(kp & sm);
-            if ((kp >> sb) == (k >> sb) && (sp + 1 >= s || seg_lo[s] <= sp)) f = 0;
+    // four keys per lane, a grid stride apart: their seg_lo gathers (random, L2-missing) are
+    // independent and in flight together
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < V; t0 += 4 * stride) {
+        uint32_t f[4], s[4], sp[4];
+        bool need[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const size_t t = t0 + q * stride;
+            f[q] = 1;
+            need[q] = false;
+            s[q] = sp[q] = 0;
+            if (t < V && t) {
+                const uint64_t k = keys[t], kp = keys[t - 1];
+                s[q] = (uint32_t)(k & sm);
+                sp[q] = (uint32_t)(kp & sm);
+                if ((kp >> sb) == (k >> sb)) {
+                    // seg_lo[s] <= s - 1: a key one segment after (or equal to) its
+                    // predecessor continues the run without the gather
+                    if (sp[q] + 1 >= s[q]) f[q] = 0;
+                    else need[q] = true;
+                }
+            }
         }
-        flag[t] = f;
+        uint32_t lo[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) lo[q] = need[q] ? seg_lo[s[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const size_t t = t0 + q * stride;
+            if (need[q] && lo[q] <= sp[q]) f[q] = 0;
+            if (t < V) flag[t] = f[q];
+        }
     }
 }
 
