@@ -60,6 +60,13 @@ struct TooBig : Fail {
     explicit TooBig(const std::string& m) : Fail(EDSBWT_E_UNSUPPORTED, m) {}
 };
 
+// hipcub / rocPRIM take int item counts: a count past 2^31 - 1 is refused (TooBig: a search
+// retries in trie-subtree groups) rather than wrapping negative
+static inline int cub_n(uint64_t n) {
+    if (n > 0x7fffffffull) throw TooBig("hipcub call over more than 2^31-1 items");
+    return (int)n;
+}
+
 #define HIPCHK(x)                                                                                 \
     do {                                                                                          \
         hipError_t e_ = (x);                                                                      \
@@ -649,17 +656,17 @@ struct Engine {
         using It = hipcub::TransformInputIterator<uint32_t, NodeFlag, hipcub::CountingInputIterator<uint32_t>>;
         It in(hipcub::CountingInputIterator<uint32_t>(0), NodeFlag{slen.p, lcp.p, D});
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, scan.p, (int)P, stream));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, scan.p, cub_n(P), stream));
         tmp.ensure(tb);
-        timed(KC_NODES, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, scan.p, (int)P, stream)); });
+        timed(KC_NODES, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, scan.p, cub_n(P), stream)); });
         sync_check(nullptr, "hipcub call at engine.hip:396");
     }
 
     void sort_link_keys(const uint64_t* in, uint64_t* out, size_t n, int end_bit) {
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, in, out, (int)n, 0, end_bit, stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, in, out, cub_n(n), 0, end_bit, stream));
         tmp.ensure(tb);
-        timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, in, out, (int)n, 0, end_bit, stream)); });
+        timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, in, out, cub_n(n), 0, end_bit, stream)); });
         sync_check(nullptr, "link key sort");
     }
 
@@ -668,9 +675,9 @@ struct Engine {
         if (!n) return;
         if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, stream));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, cub_n(n), stream));
         tmp.ensure(tb);
-        timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, out, (int)n, stream)); });
+        timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, in, out, cub_n(n), stream)); });
         sync_check(nullptr, "hipcub call at engine.hip:414");
     }
 
@@ -681,9 +688,9 @@ struct Engine {
         if (!n) return;
         if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
+        HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, cub_n(n), stream));
         tmp.ensure(tb);
-        timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+        timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, cub_n(n), stream)); });
         sync_check(nullptr, "hipcub call at engine.hip:426");
     }
 
@@ -694,9 +701,9 @@ struct Engine {
         if (n) {
             if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
             size_t tb = 0;
-            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
+            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, cub_n(n), stream));
             tmp.ensure(tb);
-            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, cub_n(n), stream)); });
             sync_check(nullptr, "hipcub call at engine.hip:438");
         }
         return read_u32(out.p + n);
@@ -707,9 +714,9 @@ struct Engine {
         if (n) {
             if (n > 0x7fffffffull) throw TooBig("scan over >2^31 items");
             size_t tb = 0;
-            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, (int)n, stream));
+            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out.p + 1, cub_n(n), stream));
             tmp.ensure(tb);
-            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, (int)n, stream)); });
+            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, out.p + 1, cub_n(n), stream)); });
             sync_check(nullptr, "hipcub call at engine.hip:450");
         }
         return read_u64(out.p + n);
@@ -986,9 +993,9 @@ struct Engine {
         launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
         size_t tb = 0;
         const int endbit = 32 + (int)bits_for(E);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, (int)n, 0, endbit, stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
         tmp.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, (int)n, 0, endbit, stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
         sync_check(nullptr, "hipcub call at engine.hip:624");
         ktab_off.ensure(E + 2);  // [E, E+1): the empty list of D-mers outside the alphabet (direct start)
         ktab_b.ensure(n);
@@ -1147,10 +1154,10 @@ struct Engine {
                     kin = kc.p;
                 }
                 size_t tb = 0;
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kc2.p, perm.p, perm2.p, cub_n(P), begin_bit, end_bit, stream));
                 tmp.ensure(tb);
                 timed(KC_TRIE, [&] {
-                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kin, kc2.p, perm.p, perm2.p, (int)P, begin_bit, end_bit, stream));
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kin, kc2.p, perm.p, perm2.p, cub_n(P), begin_bit, end_bit, stream));
                     sync_check(nullptr, "hipcub call at engine.hip:739");
                 });
                 std::swap(perm.p, perm2.p);
@@ -1276,9 +1283,9 @@ struct Engine {
                     if (V) {
                         size_t tb = 0;
                         // sentinels (~0) sort last; only the first V keys are used
-                        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream));
+                        HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, lkeys.p, lkeys2.p, cub_n(Hn), 0, 64, stream));
                         tmp.ensure(tb);
-                        timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, (int)Hn, 0, 64, stream)); });
+                        timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, cub_n(Hn), 0, 64, stream)); });
                         sync_check(nullptr, "hipcub call at engine.hip:862");
                         rflag.ensure(V);
                         launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, 32u, rflag.p);
@@ -1560,10 +1567,10 @@ struct Engine {
             size_t tb = 0;
             const int endbit = (int)bits_for(E);
             const int beginbit = std::max(0, endbit - direct_sort_bits);
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, beginbit, endbit, stream));
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, pv_in.p, pv_out.p, cub_n(P), beginbit, endbit, stream));
             tmp.ensure(tb);
             timed(KC_TRIE, [&] {
-                HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, pv_in.p, pv_out.p, (int)P, beginbit, endbit, stream));
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, pv_in.p, pv_out.p, cub_n(P), beginbit, endbit, stream));
             });
             sync_check(nullptr, "hipcub call in direct() (packed)");
             st.start_depth = D0;
@@ -1576,9 +1583,9 @@ struct Engine {
             // their first steps (their lengths and key chunks stay in input order, read via perm)
             size_t tb = 0;
             const int endbit = (int)bits_for(E);
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, perm2.p, perm.p, (int)P, 0, endbit, stream));
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kid, nid[0].p, perm2.p, perm.p, cub_n(P), 0, endbit, stream));
             tmp.ensure(tb);
-            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, perm2.p, perm.p, (int)P, 0, endbit, stream)); });
+            timed(KC_TRIE, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kid, nid[0].p, perm2.p, perm.p, cub_n(P), 0, endbit, stream)); });
             sync_check(nullptr, "hipcub call in direct()");
         }
         st.start_depth = D0;
@@ -1864,9 +1871,9 @@ struct Engine {
                     fk2.ensure(F); fv2.ensure(F);
                     const int endbit = (int)std::min<uint32_t>(64, X.rowbits + bits_for(M));
                     size_t tb = 0;
-                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream));
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, fk.p, fk2.p, fv.p, fv2.p, cub_n(F), 0, endbit, stream));
                     tmp.ensure(tb);
-                    timed(KC_FINISH, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, fk.p, fk2.p, fv.p, fv2.p, (int)F, 0, endbit, stream)); });
+                    timed(KC_FINISH, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, fk.p, fk2.p, fv.p, fv2.p, cub_n(F), 0, endbit, stream)); });
                     sync_check(nullptr, "hipcub call at engine.hip:1257");
                     launch(KC_FINISH, k_fin_bounds, F, F, (const uint64_t*)fk2.p, X.rowbits, foff.p, fend.p);
                     ab.grow_keep(abase + F, stream);
@@ -1951,17 +1958,17 @@ struct Engine {
         lk.ensure(n); lk2.ensure(n); lp.ensure(n); lp2.ensure(n); li.ensure(n); li2.ensure(n);
         launch(KC_LOCATE, k_legacy_keys, n, (uint64_t)n, (const edsbwt_occ*)rec.p, (const uint32_t*)kpos.p, kbits, lk.p, lp.p, li.p);
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lk.p, lk2.p, li.p, li2.p, (int)n, 0, (int)(kbits + obits), stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lk.p, lk2.p, li.p, li2.p, cub_n(n), 0, (int)(kbits + obits), stream));
         tmp.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lk.p, lk2.p, li.p, li2.p, (int)n, 0, (int)(kbits + obits), stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lk.p, lk2.p, li.p, li2.p, cub_n(n), 0, (int)(kbits + obits), stream));
         sync_check(nullptr, "hipcub call at engine.hip:1351");
         // stable by pattern: gather the pattern ids in key order, then sort them carrying the indices
         launch(KC_LOCATE, k_gather_u32, n, (const uint32_t*)lp.p, (const uint32_t*)li2.p, (uint64_t)n, lp2.p);
         const int pbits = (int)bits_for((uint64_t)first_id + P);
         tb = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lp2.p, lp.p, li2.p, li.p, (int)n, 0, pbits, stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lp2.p, lp.p, li2.p, li.p, cub_n(n), 0, pbits, stream));
         tmp.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lp2.p, lp.p, li2.p, li.p, (int)n, 0, pbits, stream));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, lp2.p, lp.p, li2.p, li.p, cub_n(n), 0, pbits, stream));
         sync_check(nullptr, "hipcub call at engine.hip:1358");
         rec2.ensure(n);
         launch(KC_LOCATE, k_gather_rec, n, (uint64_t)n, (const uint32_t*)li.p, (const edsbwt_occ*)rec.p, rec2.p);
@@ -2202,9 +2209,9 @@ struct Engine {
             oscan.ensure(P + 1);
             uint32_t* o32 = reinterpret_cast<uint32_t*>(oscan.p);
             size_t tb = 0;
-            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_counts, o32 + 1, (int)P, stream));
+            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_counts, o32 + 1, cub_n(P), stream));
             tmp.ensure(tb);
-            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, d_counts, o32 + 1, (int)P, stream)); });
+            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, d_counts, o32 + 1, cub_n(P), stream)); });
             hmark("locate scan");
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);
@@ -2527,9 +2534,9 @@ struct Engine {
                 hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nblk), dim3(256), 0, up, (const uint8_t*)hraw[sl].p, nb, nlcnt_s[sl].p);
                 HIPCHK(hipGetLastError());
                 size_t tb = 0;
-                HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, nlcnt_s[sl].p, nlpre_s[sl].p + 1, (int)nblk, up));
+                HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, nlcnt_s[sl].p, nlpre_s[sl].p + 1, cub_n(nblk), up));
                 ptmp[sl].ensure(tb);
-                HIPCHK(hipcub::DeviceScan::InclusiveSum(ptmp[sl].p, tb, nlcnt_s[sl].p, nlpre_s[sl].p + 1, (int)nblk, up));
+                HIPCHK(hipcub::DeviceScan::InclusiveSum(ptmp[sl].p, tb, nlcnt_s[sl].p, nlpre_s[sl].p + 1, cub_n(nblk), up));
                 hipLaunchKernelGGL(k_nl_compact, dim3((unsigned)nblk), dim3(256), 0, up, (const uint8_t*)hraw[sl].p, nb,
                                    (const uint32_t*)nlpre_s[sl].p, hbytes[sl].p, hoffs[sl].p);
                 HIPCHK(hipGetLastError());
@@ -3510,7 +3517,7 @@ struct MaxOp {
 static void gsa_sort(const uint8_t* h_codes, uint64_t n, const uint64_t* h_ends, uint64_t W, uint32_t b, int device, uint32_t* h_sa,
                      double* ms_out) {
     if (!n) return;
-    if (n >= 0xFFFFFFFFull) throw Fail(EDSBWT_E_UNSUPPORTED, "text longer than 2^32-1 symbols");
+    if (n > 0x7fffffffull) throw Fail(EDSBWT_E_UNSUPPORTED, "text longer than 2^31-1 symbols (the suffix sort's hipcub passes count items in int)");
     if (b < 1 || b > 8) throw Fail(EDSBWT_E_ARG, "bits per code must be 1..8");
     if (!W || h_ends[W - 1] != n - 1) throw Fail(EDSBWT_E_ARG, "the text must end with a word's '#'");
     HIPCHK(hipSetDevice(device));
@@ -3536,18 +3543,18 @@ static void gsa_sort(const uint8_t* h_codes, uint64_t n, const uint64_t* h_ends,
     const int nbits = (int)std::max<uint32_t>(1, 64 - __builtin_clzll((unsigned long long)n));  // ranks < n
     auto sort = [&](int end_bit) {
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, sa1.p, sa2.p, (int)n, 0, end_bit, s));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, sa1.p, sa2.p, cub_n(n), 0, end_bit, s));
         tmp.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, sa1.p, sa2.p, (int)n, 0, end_bit, s));
+        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, sa1.p, sa2.p, cub_n(n), 0, end_bit, s));
         std::swap(k1.p, k2.p); std::swap(k1.cap, k2.cap);
         std::swap(sa1.p, sa2.p); std::swap(sa1.cap, sa2.cap);
     };
     auto ranks = [&]() {
         hipLaunchKernelGGL(k_gsa_heads, dim3(G), dim3(256), 0, s, (const uint64_t*)k1.p, n, sa2.p);
         size_t tb = 0;
-        HIPCHK(hipcub::DeviceScan::InclusiveScan(nullptr, tb, sa2.p, grp.p, MaxOp{}, (int)n, s));
+        HIPCHK(hipcub::DeviceScan::InclusiveScan(nullptr, tb, sa2.p, grp.p, MaxOp{}, cub_n(n), s));
         tmp.ensure(tb);
-        HIPCHK(hipcub::DeviceScan::InclusiveScan(tmp.p, tb, sa2.p, grp.p, MaxOp{}, (int)n, s));
+        HIPCHK(hipcub::DeviceScan::InclusiveScan(tmp.p, tb, sa2.p, grp.p, MaxOp{}, cub_n(n), s));
         hipLaunchKernelGGL(k_gsa_rank, dim3(G), dim3(256), 0, s, (const uint32_t*)sa1.p, (const uint32_t*)grp.p, n, rank.p);
         HIPCHK(hipGetLastError());
     };

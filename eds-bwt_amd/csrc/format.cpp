@@ -113,8 +113,10 @@ __attribute__((target("avx2"))) int pack_avx2(const uint8_t* s, uint64_t nb, uin
         const __m256i w = _mm256_shuffle_epi8(z, shuf);                                   // ... their low bytes
         const uint64_t codes = (((uint64_t)(uint32_t)_mm_cvtsi128_si32(_mm256_extracti128_si256(w, 1)) << 32) |
                                 (uint32_t)_mm_cvtsi128_si32(_mm256_castsi256_si128(w))) & cmask;
-        if (p + 1 < p1) std::memcpy(out + p * S, &codes, 8);  // the next line's bytes follow
-        else std::memcpy(out + p * S, &codes, S);             // the range's last line: its own bytes only
+        // an 8-byte store spills into the following lines' bytes: only while they are still in this
+        // range (another thread packs [p1, ...) concurrently), else the line's own S bytes
+        if ((p1 - p) * S >= 8) std::memcpy(out + p * S, &codes, 8);
+        else std::memcpy(out + p * S, &codes, S);
     }
     return 1;
 }

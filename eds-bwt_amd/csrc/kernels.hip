@@ -3099,7 +3099,9 @@ __global__ void __launch_bounds__(256) k_nl_count(const uint8_t* __restrict__ in
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t x = w[k] ^ 0x0A0A0A0Au;  // a zero byte where the byte is '\n'
-            c += __builtin_popcount((x - 0x01010101u) & ~x & 0x80808080u);
+            // exact per byte (no borrow between bytes): the high bit of t is 0 only for a zero byte
+            const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+            c += __builtin_popcount(~t & 0x80808080u);
         }
     } else {
         for (uint64_t i = b0; i < n && i < b0 + 16; i++) c += in[i] == '\n';

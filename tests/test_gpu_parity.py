@@ -754,3 +754,75 @@ def test_short_patterns_3bit_many_gpu(oracle, edsbwt, tmp_path):
         for kw in ({"direct": False}, {"ordered": True}, {"direct": False, "ktab": False}):
             gc, go = idx.search((buf, offs), **kw)
             assert np.array_equal(gc, oc) and np.array_equal(go, oo), kw
+
+
+def test_search_lines_vt_after_newline_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """Raw chunks are split on the device (k_nl_count, scan, k_nl_compact): a '\\v' byte right
+    after a '\\n' (the has-zero-byte trick double-counts that word's newline) must not shift
+    the line offsets of later blocks.  getline keeps '\\v' as a pattern byte."""
+    rng = random.Random(1313)
+    segs = _covid_like(rng, 300)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(3, 30)) or "ACGT" for _ in range(6000)]
+    for i in range(0, len(pats), 7):
+        pats[i] = "\v" + pats[i]          # '\n' then '\v' in the same 4-byte word
+    for i in range(3, len(pats), 11):
+        pats[i] = pats[i] + "\v"
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    text = ("\n".join(pats) + "\n").encode()
+    monkeypatch.setenv("EDSBWT_PACK_LINES", "0")
+    with edsbwt.Index(base) as idx:
+        gc, go = _lines_search(edsbwt, idx, text)
+    assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+
+
+def test_search_lines_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The host pipeline at its default chunk sizes over a batch of more chunks than slots
+    (ADVICE r2): ragged and packed chunks, patterns with thousands of records (the record
+    arena grows while chunks are in flight) and one chunk that fails a deferred check ('#' in a
+    pattern) and is searched again.  Equal to the device-resident search of the whole batch,
+    and to the oracle on a strided sample."""
+    torch = pytest.importorskip("torch")
+    for k in ("EDSBWT_CHUNK_MB", "EDSBWT_CHUNK_SINGLE_MB", "EDSBWT_PACK_LINES"):
+        monkeypatch.delenv(k, raising=False)
+    rng = random.Random(5150)
+    segs = _covid_like(rng, 400)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    uniq = [edsgen.planted(rng, segs, 31) or "ACGT" * 7 + "ACG" for _ in range(40000)]
+    uniq += ["".join(rng.choice("ACGT") for _ in range(rng.randint(20, 40))) for _ in range(10000)]
+    pats = uniq * 120                                   # 6M lines, ~190 MB
+    for i in range(777, len(pats), 20011):
+        pats[i] = rng.choice(["A", "C", "GT", "TA"])      # thousands of records each
+    pats[len(pats) // 2 + 5] = "ACGT#ACG"                 # '#': that chunk is searched again
+    text = ("\n".join(pats) + "\n").encode()
+    buf, offs = _pack(pats)
+    with edsbwt.Index(base) as idx:
+        d_bytes = torch.from_numpy(buf.copy()).cuda()
+        d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_counts = torch.zeros(len(pats), dtype=torch.int32, device="cuda")
+        ptr, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), len(pats), d_counts.data_ptr())
+        ref_counts = d_counts.cpu().numpy().view(np.uint32).copy()
+        ref_occ = torch.empty(n * 20, dtype=torch.uint8)
+        if n:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            assert hip.hipMemcpy(ctypes.c_void_p(ref_occ.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(n * 20), 2) == 0
+        ref_occ = ref_occ.numpy().view(edsbwt.OCC_DTYPE)
+        del d_bytes, d_offs, d_counts
+        gc, go = _lines_search(edsbwt, idx, text)
+        st = idx.stats()
+    assert st["chunks"] > 5 and st["redo_searches"] >= 1, st
+    assert np.array_equal(gc, ref_counts)
+    assert go.size == ref_occ.size and np.array_equal(go, ref_occ)
+    # the oracle on a strided sample of the batch (records of pattern i carry #Pat = i + 1)
+    sample = np.unique(np.concatenate([np.arange(0, len(pats), 997), np.arange(777, len(pats), 20011)[:20],
+                                       [len(pats) // 2 + 5]]))
+    sp = [pats[i] for i in sample]
+    sbuf, soffs = _pack(sp)
+    oc, oo, _ = oracle.Engine(base, 8).search(sbuf, soffs, threads=8)
+    assert np.array_equal(gc[sample], oc)
+    sel = np.isin(go["pat"], sample + 1)
+    got = go[sel].copy()
+    got["pat"] = np.searchsorted(sample, got["pat"] - 1) + 1
+    assert np.array_equal(got, oo)

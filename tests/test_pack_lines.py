@@ -30,8 +30,10 @@ def lib():
     return L
 
 
-def _pack(lib, text: bytes, parts=1):
-    """(P, L, packed bytes) or None when the packer refuses the chunk."""
+def _pack(lib, text: bytes, parts=1, reverse=False):
+    """(P, L, packed bytes) or None when the packer refuses the chunk.  reverse: pack the parts
+    last to first (the engine's pool threads finish in any order; a part must not write into
+    the bytes of the next part)."""
     src = np.frombuffer(text, np.uint8).copy() if text else np.zeros(1, np.uint8)
     Lo = ctypes.c_uint32(0)
     P = lib.edsbwt_lines_fixed(src.ctypes.data, len(text), ctypes.byref(Lo))
@@ -41,7 +43,8 @@ def _pack(lib, text: bytes, parts=1):
     S = (L + 3) // 4
     out = np.full(P * S + 16, 0xEE, np.uint8)
     end = src.ctypes.data + len(text)
-    for t in range(parts):  # the engine's pool splits the lines the same way
+    order = range(parts - 1, -1, -1) if reverse else range(parts)
+    for t in order:  # the engine's pool splits the lines the same way
         p0, p1 = P * t // parts, P * (t + 1) // parts
         if p0 < p1 and not lib.edsbwt_pack_lines(src.ctypes.data, len(text), L, p0, p1, end, out.ctypes.data):
             return None
@@ -99,3 +102,33 @@ def test_pack_refuses_other_forms(lib):
     assert _pack(lib, b"ACGT\r\nACGT\r\n", 1) is None           # '\r' kept by getline
     assert _pack(lib, b"ACGT\nACG", 1) is None                  # a short unterminated last line
     assert _pack(lib, b"ACGT", 1) is None                       # no '\n' at all: sent raw
+
+
+@pytest.mark.parametrize("L", list(range(1, 13)))
+def test_pack_parts_any_order(lib, L):
+    """Parts packed last-to-first, and on concurrent threads, over >= 32768 lines (the engine's
+    pool uses 2+ threads from there): every line keeps its bases (8-byte stores of a
+    part's last lines must not reach into the next part)."""
+    import threading
+    rng = np.random.default_rng(L)
+    P = 40000 + L
+    lines = ["".join("ACGT"[c] for c in row) for row in rng.integers(0, 4, (P, L))]
+    text = ("\n".join(lines) + "\n").encode()
+    want = _expect(lines, L)
+    for parts in (2, 7, 12):
+        r = _pack(lib, text, parts, reverse=True)
+        assert r is not None and np.array_equal(r[2], want), (L, parts)
+    src = np.frombuffer(text, np.uint8).copy()
+    S = (L + 3) // 4
+    out = np.full(P * S + 16, 0xEE, np.uint8)
+    end = src.ctypes.data + len(text)
+    parts = 12
+    ok = []
+    th = [threading.Thread(target=lambda t=t: ok.append(lib.edsbwt_pack_lines(
+        src.ctypes.data, len(text), L, P * t // parts, P * (t + 1) // parts, end, out.ctypes.data)))
+        for t in range(parts - 1, -1, -1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert all(ok) and np.array_equal(out[:P * S], want)
