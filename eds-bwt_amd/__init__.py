@@ -41,6 +41,12 @@ NO_DIRECT = 0x800
 NO_PAIRS = 0x1000
 NO_TEXT = 0x2000
 
+# edsbwt_last_paths bits (EDSBWT_PATH_TAGS=1): the kernels a pattern went through
+PATH_DEEP = 0x1
+PATH_WIDE = 0x2
+PATH_LEVELS = 0x4
+PATH_REDO = 0x8
+
 OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
 CSV_HEADER = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"  # MOVE_EDSBWTSearch.cpp:59 (note the trailing space)
 
@@ -125,6 +131,8 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_host_free.restype = None
     L.edsbwt_occ_free.argtypes = [vp]
     L.edsbwt_occ_free.restype = None
+    L.edsbwt_last_paths.argtypes = [vp, vp, u64]
+    L.edsbwt_last_paths.restype = i32
     L.edsbwt_last_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
     L.edsbwt_last_stats.restype = i32
     L.edsbwt_kernel_name.argtypes = [i32]
@@ -321,6 +329,14 @@ class Index:
         _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,
                                           ctypes.byref(occ_p), ctypes.byref(nocc), stream or None))
         return occ_p.value or 0, nocc.value
+
+    def path_tags(self, n: int) -> np.ndarray:
+        """PATH_* bits per pattern of the last search_device call (the process must run with
+        EDSBWT_PATH_TAGS=1 before the index is opened): which patterns took k_deep, the wide
+        lists, the level re-run, or a searched-again batch."""
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(lib().edsbwt_last_paths(self._h, out.ctypes.data, n))
+        return out[:n]
 
     def stats(self) -> dict:
         s = _Stats()

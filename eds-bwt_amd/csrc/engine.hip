@@ -286,6 +286,24 @@ struct Engine {
     DBuf<uint32_t> fu, fb, fe, fpre;  // the previous depth's item shards, read in place by k_lvl_items
     // run_grouped: group of each pattern, its members as a sub-batch
     DBuf<uint32_t> glen, gid, gflag, gscan, g_map;
+    // path tags (EDSBWT_PATH_TAGS=1, tests): per pattern of the last edsbwt_search_device call,
+    // the EDSBWT_PATH_* bits of the kernels it went through (edsbwt_last_paths)
+    bool tag_paths = env_double("EDSBWT_PATH_TAGS", 0) != 0, tag_now = false;
+    DBuf<uint8_t> ptag;
+    uint64_t ptag_n = 0;
+    const uint32_t* tag_map = nullptr;  // grouped search: group index -> batch index
+    void tag_queue(const uint4* q, const uint32_t* qcnt, uint32_t qcap, uint32_t bit) {
+        if (!tag_now) return;
+        hipLaunchKernelGGL(k_tag_queue, dim3((unsigned)std::min<uint64_t>(65535, ((uint64_t)qcap * NSHARD + 255) / 256)), dim3(256), 0,
+                           stream, q, qcnt, qcap, (const uint32_t*)perm.p, tag_map, ptag.p, bit);
+        HIPCHK(hipGetLastError());
+    }
+    void tag_list(const uint32_t* list, uint64_t cap, uint32_t bit) {
+        if (!tag_now || !cap) return;
+        hipLaunchKernelGGL(k_tag_list, dim3((unsigned)std::min<uint64_t>(65535, (cap + 255) / 256)), dim3(256), 0, stream, list, cap,
+                           (const uint32_t*)perm.p, tag_map, ptag.p, bit);
+        HIPCHK(hipGetLastError());
+    }
     DBuf<uint64_t> g_len, g_off;
     DBuf<uint8_t> g_bytes;
     DBuf<uint4> dq;                   // k_deep_fast -> k_deep queue (pattern, depth, b, e), sharded
@@ -1402,6 +1420,7 @@ struct Engine {
         launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
                pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr);
+        tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace)
@@ -1423,6 +1442,7 @@ struct Engine {
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
                        (const uint32_t*)ovf.p);
                 abase += (uint64_t)wcap * kDeepWide;
+                tag_list(ovf.p, wcap, EDSBWT_PATH_WIDE);
             }
             defer_ovf2 = no_wide ? ovf.p : ovf2.p;  // gathered by finish_deferred
             defer_wide_cap = no_wide ? 0 : wcap;
@@ -1444,7 +1464,9 @@ struct Engine {
             st.deep_overflow += nw;
             novf = read_u32(ovf2.p);
             list = ovf2.p + 1;
+            tag_list(ovf.p, nw, EDSBWT_PATH_WIDE);
         }
+        tag_list(list - 1, novf, EDSBWT_PATH_LEVELS);
         if (novf) {
             zero(ovf_orig, P * 4);
             launch(KC_DEEP, k_ovf_mark, novf, novf, list, (const uint32_t*)perm.p, ovf_orig);
@@ -1944,6 +1966,8 @@ struct Engine {
             launch(KC_TRIE, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)g_map.p, d_off, (const uint64_t*)g_off.p, d_bytes, g_bytes.p);
             g_res.ensure(n);
             zero(g_res.p, (size_t)n * sizeof(Res));
+            tag_map = g_map.p;
+            struct MapReset { const uint32_t*& m; ~MapReset() { m = nullptr; } } mr{tag_map};
             run_batch(g_bytes.p, g_off.p, n, allow_deep, ordered, g_res.p, abase);
             launch(KC_TRIE, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)g_map.p, (const Res*)g_res.p, res.p);
         }
@@ -2074,6 +2098,11 @@ struct Engine {
             recycle.done = true;
             const uint64_t m = search(d_bytes, d_off, P, first_id, flags | kFlagNoDefer, d_counts);
             st.redo_searches++;
+            if (tag_now) {
+                hipLaunchKernelGGL(k_tag_all, dim3((unsigned)std::min<uint64_t>(65535, (P + 255) / 256)), dim3(256), 0, stream, ptag.p, P,
+                                   (uint32_t)EDSBWT_PATH_REDO);
+                HIPCHK(hipGetLastError());
+            }
             return m;
         }
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
@@ -3628,6 +3657,13 @@ int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64
     HIPCHK(hipEventRecord(ev, (hipStream_t)stream));
     HIPCHK(hipStreamWaitEvent(E.stream, ev, 0));
     (void)hipEventDestroy(ev);
+    struct TagReset { bool& t; ~TagReset() { t = false; } } tr{E.tag_now};
+    if (E.tag_paths) {
+        E.ptag.ensure(npat + 1);
+        HIPCHK(hipMemsetAsync(E.ptag.p, 0, npat + 1, E.stream));
+        E.ptag_n = npat;
+        E.tag_now = true;
+    }
     uint64_t n = E.search(d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts);
     if (d_occ) *d_occ = n ? E.rec.p : nullptr;
     if (nocc) *nocc = n;
@@ -3684,6 +3720,18 @@ void edsbwt_host_free(void* p) {
 const char* edsbwt_build_id(void) { return EDSBWT_BUILD_ID; }
 
 void edsbwt_occ_free(edsbwt_occ* occ) { edsbwt::occ_free_any(occ); }
+
+int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n) {
+    if (!idx || (n && !out)) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    const Engine& E = *idx->eng;
+    if (!E.tag_paths || n > E.ptag_n) { edsbwt::g_err = "no path tags (EDSBWT_PATH_TAGS=1 and edsbwt_search_device first)"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    HIPCHK(hipSetDevice(E.device));
+    HIPCHK(hipStreamSynchronize(E.stream));
+    if (n) HIPCHK(hipMemcpy(out, E.ptag.p, n, hipMemcpyDeviceToHost));
+    return 0;
+    ABI_CATCH
+}
 
 int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st) {
     if (!idx || !st) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }

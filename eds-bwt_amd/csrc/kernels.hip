@@ -1705,6 +1705,32 @@ __global__ void __launch_bounds__(256) k_len_hist(const uint32_t* __restrict__ l
 
 // overflowed patterns → a compact sub-batch (original ids kept in `map`)
 // patterns the deep kernels could not hold (a flag_push list), flagged by input index
+// path tags (EDSBWT_PATH_TAGS, tests): the patterns a kernel's queue or list held.  Queue:
+// sharded (region s at s*qcap, count at qcnt[s*32]), entry .x = sorted pattern index.  List:
+// list[0] = count, then sorted indices.  perm maps sorted -> batch index, map (grouped
+// search) batch -> caller's index.
+__global__ void k_tag_queue(const uint4* __restrict__ q, const uint32_t* __restrict__ qcnt, uint32_t qcap, const uint32_t* __restrict__ perm,
+                            const uint32_t* __restrict__ map, uint8_t* __restrict__ tag, uint32_t bit) {
+    GRID_STRIDE(j, (uint64_t)qcap * NSHARD) {
+        const uint32_t sh = (uint32_t)(j / qcap), at = (uint32_t)(j % qcap);
+        if (at < min(qcnt[sh * 32], qcap)) {
+            uint32_t p = perm[q[j].x];
+            if (map) p = map[p];
+            tag[p] |= (uint8_t)bit;
+        }
+    }
+}
+__global__ void k_tag_list(const uint32_t* __restrict__ list, uint64_t cap, const uint32_t* __restrict__ perm,
+                           const uint32_t* __restrict__ map, uint8_t* __restrict__ tag, uint32_t bit) {
+    GRID_STRIDE(j, cap) {
+        if (j < list[0]) {
+            uint32_t p = perm[list[1 + j]];
+            if (map) p = map[p];
+            tag[p] |= (uint8_t)bit;
+        }
+    }
+}
+__global__ void k_tag_all(uint8_t* __restrict__ tag, uint64_t n, uint32_t bit) { GRID_STRIDE(i, n) tag[i] |= (uint8_t)bit; }
 __global__ void k_ovf_mark(uint32_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ perm, uint32_t* __restrict__ flag_orig) {
     GRID_STRIDE(j, n) flag_orig[perm[list[j]]] = 1;
 }

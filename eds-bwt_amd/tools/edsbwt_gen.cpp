@@ -8,7 +8,9 @@
 //     c5: c2 where 20% of the segments with k>=2 replace one string by the empty word
 //   edsbwt_gen patterns --eds file.eds --count P --seed S --out file.txt
 //                       [--len L | --lens 8,16,32,64] [--mode random|planted|mixed]
-//                       [--first I] [--threads T]
+//                       [--first I] [--threads T] [--planted-mask F]
+//     --planted-mask: one byte per pattern, 1 when the pattern was spelled along a path of
+//     the EDS (so it occurs), 0 when it is random (tests check that every planted one is found)
 //     pattern i of the stream is drawn from its own seeded generator: --first I --count P
 //     writes stream ids [I, I+P), identical to those lines of a single larger run
 //     planted: spelled along a random path (start segment, word and offset uniform,
@@ -72,7 +74,8 @@ static int gen_eds(const std::string& cfg, uint64_t chars, uint64_t seed, const 
 // shard [first, first + count) of the stream is reproducible on its own (one rank per GPU
 // generates its own shard of C4's 100M patterns) and the batch is generated in parallel.
 static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t first, uint64_t seed,
-                        const std::vector<uint64_t>& lens, const std::string& mode, const std::string& out, unsigned threads) {
+                        const std::vector<uint64_t>& lens, const std::string& mode, const std::string& out, unsigned threads,
+                        const std::string& mask_out) {
     Eds E;
     std::vector<uint64_t> seg_first;  // first word of each segment
     if (mode != "random") {
@@ -88,7 +91,7 @@ static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t fi
         if (l == 1 && E.text[E.wstart[w]] == 'Z') l = 0;  // the empty word
         return l;
     };
-    auto one = [&](uint64_t idx, std::string& p) {
+    auto one = [&](uint64_t idx, std::string& p) -> bool {
         Rng R(seed * 0x9E3779B97F4A7C15ull ^ (idx + 0x632BE59BD9B4E019ull));
         const uint64_t m = lens[R.below(lens.size())];
         const bool plant = (mode == "planted") || (mode == "mixed" && (R.next() & 1));
@@ -110,14 +113,17 @@ static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t fi
                 }
             }
         }
-        if (p.size() < m) {
+        const bool planted = p.size() >= m;
+        if (!planted) {
             p.clear();
             for (uint64_t t = 0; t < m; t++) p.push_back(ACGT[R.below(4)]);
         }
         p.push_back('\n');
+        return planted;
     };
     threads = std::max(1u, std::min<unsigned>(threads, (unsigned)std::max<uint64_t>(1, count / 4096)));
     std::vector<std::string> part(threads);
+    std::vector<uint8_t> mask(mask_out.empty() ? 0 : count);
     std::vector<std::thread> th;
     for (unsigned t = 0; t < threads; t++)
         th.emplace_back([&, t] {
@@ -125,13 +131,23 @@ static int gen_patterns(const std::string& eds_path, uint64_t count, uint64_t fi
             std::string& s = part[t];
             s.reserve((hi - lo) * (lens.back() + 1));
             std::string p;
-            for (uint64_t i = lo; i < hi; i++) { one(first + i, p); s += p; }
+            for (uint64_t i = lo; i < hi; i++) {
+                const bool pl = one(first + i, p);
+                if (!mask.empty()) mask[i] = pl ? 1 : 0;
+                s += p;
+            }
         });
     for (auto& x : th) x.join();
     FILE* f = std::fopen(out.c_str(), "wb");
     if (!f) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
     for (auto& s : part) std::fwrite(s.data(), 1, s.size(), f);
     std::fclose(f);
+    if (!mask.empty()) {
+        FILE* g = std::fopen(mask_out.c_str(), "wb");
+        if (!g) { std::fprintf(stderr, "cannot write %s\n", mask_out.c_str()); return 1; }
+        std::fwrite(mask.data(), 1, mask.size(), g);
+        std::fclose(g);
+    }
     std::fprintf(stderr, "edsbwt_gen: %llu patterns (%s, stream ids %llu..%llu) -> %s\n", (unsigned long long)count, mode.c_str(),
                  (unsigned long long)first, (unsigned long long)(first + count), out.c_str());
     return 0;
@@ -141,11 +157,11 @@ int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s eds --config c2|c3|c5 --chars N --seed S --out F\n"
                              "       %s patterns --eds F --count P --seed S --out F [--len L|--lens a,b,..] [--mode random|planted|mixed]\n"
-                             "                   [--first I (stream id of the first pattern)] [--threads T]\n",
+                             "                   [--first I (stream id of the first pattern)] [--threads T] [--planted-mask F]\n",
                      argv[0], argv[0]);
         return 1;
     }
-    std::string cmd = argv[1], cfg = "c2", out, eds, mode = "random";
+    std::string cmd = argv[1], cfg = "c2", out, eds, mode = "random", mask_out;
     uint64_t chars = 1000000, seed = 1, count = 1000, first = 0;
     unsigned threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<uint64_t> lens{20};
@@ -159,6 +175,7 @@ int main(int argc, char** argv) {
         else if (k == "--count") count = std::stoull(v);
         else if (k == "--first") first = std::stoull(v);
         else if (k == "--threads") threads = (unsigned)std::stoul(v);
+        else if (k == "--planted-mask") mask_out = v;
         else if (k == "--len") lens = {std::stoull(v)};
         else if (k == "--lens") {
             lens.clear();
@@ -174,7 +191,7 @@ int main(int argc, char** argv) {
     }
     try {
         if (cmd == "eds") return gen_eds(cfg, chars, seed, out);
-        if (cmd == "patterns") return gen_patterns(eds, count, first, seed, lens, mode, out, threads);
+        if (cmd == "patterns") return gen_patterns(eds, count, first, seed, lens, mode, out, threads, mask_out);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

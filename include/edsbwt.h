@@ -136,8 +136,9 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info);
  * With EDSBWT_LOCATE, *occ (library-owned, page-locked; give it back with
  * edsbwt_occ_free) receives *nocc records in reference order: pattern-major, then
  * interval order, rows ascending — the order of <patterns>output_M_LF.csv.
- * The batch is cut into chunks (EDSBWT_CHUNK_MB, default 64 MB of pattern bytes):
- * uploads, searches and downloads of consecutive chunks overlap on three streams.
+ * A batch of more than EDSBWT_CHUNK_SINGLE_MB (default 24 MB) of pattern bytes is cut into
+ * chunks (EDSBWT_CHUNK_MB, default 40 MB): uploads, searches and downloads of consecutive
+ * chunks overlap (two SDMA engines and the index's stream).
  * Host buffers from edsbwt_host_alloc (page-locked) are transferred directly;
  * pageable ones are staged through page-locked buffers. */
 int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_offsets,
@@ -169,6 +170,16 @@ const char* edsbwt_build_id(void);
 int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets,
                          uint64_t npat, uint32_t first_pattern_id, uint32_t flags,
                          uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc, void* stream);
+
+/* Tests: the kernels each pattern of the last edsbwt_search_device call went through, when the
+ * process runs with EDSBWT_PATH_TAGS=1 (else E_ARG): out[i] for pattern i, i < n (n <= that
+ * call's npat), bits EDSBWT_PATH_*.  Lets parity tests add every pattern of a rare path
+ * (register-list walk, wide lists, level re-run, a searched-again batch) to their oracle sample. */
+#define EDSBWT_PATH_DEEP   0x1u /* queued for k_deep (a list or a link, MOVE_EDSBWTSearch.cpp:258,512-563) */
+#define EDSBWT_PATH_WIDE   0x2u /* list outgrew k_deep's registers: k_deep_wide */
+#define EDSBWT_PATH_LEVELS 0x4u /* ... and the wide lists: re-run on the level-synchronous path */
+#define EDSBWT_PATH_REDO   0x8u /* the batch failed a deferred check and was searched again */
+int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n);
 
 /* Counters/timings of the last search on this index. */
 int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st);

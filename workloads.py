@@ -101,11 +101,19 @@ def shard(w: Workload, rank: int, world: int, patterns: int = 0) -> tuple[int, i
 
 
 def pattern_file(w: Workload, eds: str, workdir: str, lo: int, hi: int, tag: str = "") -> str:
-    """The pattern file of stream ids [lo, hi) (generated once, cached)."""
+    """The pattern file of stream ids [lo, hi) (generated once, cached), with its planted mask
+    (planted_mask(): one byte per pattern, 1 = spelled along a path of the EDS)."""
     path = os.path.join(workdir, f"{w.name}{tag}_pats_{w.pat_seed}_{lo}_{hi}.txt")
-    if not os.path.exists(path):
+    if not os.path.exists(path) or not os.path.exists(path + ".planted"):
         tmp = path + f".tmp{os.getpid()}"
         run([os.path.join(BUILD, "edsbwt_gen"), "patterns", "--eds", eds, "--count", hi - lo, "--first", lo, "--lens", w.lens,
-             "--mode", w.mode, "--seed", w.pat_seed, "--out", tmp])
+             "--mode", w.mode, "--seed", w.pat_seed, "--out", tmp, "--planted-mask", tmp + ".planted"])
+        os.replace(tmp + ".planted", path + ".planted")
         os.replace(tmp, path)
     return path
+
+
+def planted_mask(pattern_path: str):
+    """bool per pattern of a pattern_file(): True when it was planted (it must occur)."""
+    import numpy as np
+    return np.fromfile(pattern_path + ".planted", dtype=np.uint8).astype(bool)
