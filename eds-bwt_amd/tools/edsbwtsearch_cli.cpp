@@ -6,11 +6,19 @@
 // MOVE_EDSBWT::MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:23-176):
 //   * wrong argc → usage on stderr, exit 1 (:19-25); success also exits 1 (:61);
 //   * writes <pattern_file>output_M_LF.csv with header "#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n" (:55-64);
-//   * stdout: banner, index summary, per pattern "Pattern: <p> of length <n>" and
-//     "num occ <k>" (:113,:371), then "bs took:<secs>" without a newline (:145);
-//   * stderr: "OCCORRENZA DI: <p> TROVATA|NON TROVATA" per pattern (:124,:129), then
-//     "count_found = N" / "count_not_found = M" (:154-155) — the lines the
-//     reference's scripts grep (launch_COVID.sh:106-108).
+//   * stdout: banner (mainMove_EDSBWT.cpp:27-29), "DEBUG: 0" (:28), recoverInfo's index summary,
+//     "NUM OF EOF", TableOcc (:664-671,:725,:761-766), retrieve_MLF's "size= " (:191),
+//     "BitVector size: " (:86); per pattern "Pattern: <p> of length <n>" (:113) and — unless
+//     backwardSearch returned before its locate loop (:250-253,:295-297) — "num occ <k>" (:371);
+//     then "bs took:<secs>" without a newline (:145);
+//   * stderr: "Backward Search" (:25), "OCCORRENZA DI: <p> TROVATA|NON TROVATA" per pattern
+//     (:124,:129), then "count_found = N" / "count_not_found = M" (:154-155) — the lines the
+//     reference's scripts grep (launch_COVID.sh:106-108) — and main's closing lines (:50-59).
+//   Each pattern's stdout lines are flushed before its stderr line, as endl does, so the two
+//   streams interleave as the reference's do when they share a file.
+//   backwardSearch returns early exactly when the list after all but the first character is
+//   empty, i.e. when the pattern without its first character does not occur (its own final
+//   list is that list): the console stream asks the engine for those counts too.
 // --quiet drops the per-pattern lines (they dominate console time at 10^7 patterns).
 // --legacy writes <pattern_file>output.csv in the legacy EDSBWTsearch engine's record order
 // and header (EDSBWTsearch.cpp:180-186, findMultipleDollarsBackward :300-610) instead.
@@ -45,7 +53,9 @@ int main(int argc, char** argv) {
     }
     const std::string base = pos[0], pfile = pos[1];
     std::printf("BCR_eds: %s\nBCR_eds: The input ebwt file is %s\nBCR_eds: The pattern file is %s\n", argv[0], base.c_str(), pfile.c_str());
+    std::fflush(stdout);
     std::fprintf(stderr, "Backward Search\n");
+    std::printf("DEBUG: 0\n");
     edsbwt_index* idx = nullptr;
     int rc = edsbwt_index_open(base.c_str(), device, 8, &idx);
     if (rc) {
@@ -57,7 +67,24 @@ int main(int argc, char** argv) {
     std::printf("\nFrom %s_info.aux file:\n\tNumber of sequences: %llu\n\tTotal length (with $): %llu\n\tSize alpha: %u\n\tAlphabet: ",
                 base.c_str(), (unsigned long long)info.n_words, (unsigned long long)info.n_rows, info.sigma);
     for (uint32_t j = 0; j < info.sigma; j++) std::printf("%c\t", info.alphabet[j]);
-    std::printf("\nBitVector size: %llu\n", (unsigned long long)info.n_words);
+    std::printf("\nNUM OF EOF%llu\n", (unsigned long long)info.n_words);
+    {
+        // tableOcc (sigma x sigma u32 after the header and the EOF ids of <base>_info.aux,
+        // da_to_everything.cpp:249-254), printed as recoverInfo prints it
+        const std::string fn = base + "_info.aux";
+        std::printf("\nFrom %s file (TableOcc):\n", fn.c_str());
+        FILE* fi = std::fopen(fn.c_str(), "rb");
+        std::vector<uint32_t> tocc((size_t)info.sigma * info.sigma);
+        const long at = 9L + (long)info.sigma + 4L * (long)info.n_words;
+        if (fi && std::fseek(fi, at, SEEK_SET) == 0 && std::fread(tocc.data(), 4, tocc.size(), fi) == tocc.size()) {
+            for (uint32_t j = 0; j < info.sigma; j++) {
+                for (uint32_t h = 0; h < info.sigma; h++) std::printf("%u\t", tocc[(size_t)j * info.sigma + h]);
+                std::printf("\n");
+            }
+        }
+        if (fi) std::fclose(fi);
+    }
+    std::printf("size= %llu\nBitVector size: %llu\n", (unsigned long long)info.n_rows, (unsigned long long)info.n_words);
     // the pattern file, read into page-locked memory; the library splits its lines
     // (std::getline semantics, :111) on the device
     FILE* f = std::fopen(pfile.c_str(), "rb");
@@ -111,6 +138,39 @@ int main(int argc, char** argv) {
         std::fwrite(csv.data(), 1, sz, fo);
     }
     std::fclose(fo);
+    // the console stream: which patterns reach the locate loop (the pattern without its first
+    // character occurs, or the pattern is one character long) — one more count-only search
+    std::vector<uint8_t> reach;
+    if (!quiet && npat) {
+        char* suf = nullptr;
+        uint32_t* c2 = nullptr;
+        if (edsbwt_host_alloc(len + npat + 1, (void**)&suf) || edsbwt_host_alloc((npat + 1) * 4, (void**)&c2)) {
+            std::fprintf(stderr, "%s\n", edsbwt_last_error());
+            return 1;
+        }
+        uint64_t sl = 0;
+        std::vector<uint32_t> plen(npat);
+        const char* q = text;
+        for (uint64_t i = 0; i < npat; i++) {
+            const char* nl = (const char*)std::memchr(q, '\n', (size_t)(text + len - q));
+            const char* end = nl ? nl : text + len;
+            plen[i] = (uint32_t)(end - q);
+            if (end > q + 1) { std::memcpy(suf + sl, q + 1, (size_t)(end - q - 1)); sl += (uint64_t)(end - q - 1); }
+            suf[sl++] = '\n';
+            q = end + 1;
+        }
+        uint64_t n2 = 0, no2 = 0;
+        edsbwt_occ* o2 = nullptr;
+        if (edsbwt_search_lines(idx, suf, sl, 1, EDSBWT_COUNT_ONLY, c2, npat + 1, &n2, &o2, &no2) || n2 != npat) {
+            std::fprintf(stderr, "%s\n", edsbwt_last_error());
+            return 1;
+        }
+        edsbwt_occ_free(o2);
+        reach.resize(npat);
+        for (uint64_t i = 0; i < npat; i++) reach[i] = plen[i] == 1 || (plen[i] > 1 && c2[i] > 0);
+        edsbwt_host_free(c2);
+        edsbwt_host_free(suf);
+    }
     uint64_t found = 0;
     const char* line = text;
     for (uint64_t i = 0; i < npat; i++) {
@@ -119,9 +179,15 @@ int main(int argc, char** argv) {
         const bool ok = counts[i] > 0;
         found += ok;
         if (!quiet) {
-            const std::string p(line, end);
-            std::printf("Pattern: %s of length %zu\nnum occ %u\n", p.c_str(), p.size(), counts[i]);
-            std::fprintf(stderr, "OCCORRENZA DI: %s %s\n", p.c_str(), ok ? "TROVATA" : "NON TROVATA");
+            const size_t pl = (size_t)(end - line);
+            std::fputs("Pattern: ", stdout);
+            std::fwrite(line, 1, pl, stdout);
+            std::printf(" of length %zu\n", pl);
+            if (reach[i]) std::printf("num occ %u\n", counts[i]);
+            std::fflush(stdout);
+            std::fputs("OCCORRENZA DI: ", stderr);
+            std::fwrite(line, 1, pl, stderr);
+            std::fputs(ok ? " TROVATA\n" : " NON TROVATA\n", stderr);
         }
         line = end + 1;
     }

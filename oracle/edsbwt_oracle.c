@@ -657,6 +657,7 @@ typedef struct {
     uvec d;
     ovec out;
     orc_counters c;
+    int early; /* the last backward_search returned before locate (:250-253, :295-297) */
 } ctx_t;
 
 /* updateSingleInterval (MOVE_EDSBWTSearch.cpp:424-510) */
@@ -832,6 +833,7 @@ static int bs_level(const orc_engine* E, ctx_t* X, uint8_t sym) {
 
 /* backwardSearch (:228-374); occurrences appended to X->out */
 static uint32_t backward_search(const orc_engine* E, ctx_t* X, uint32_t n_kmer, const uint8_t* kmer, uint32_t len) {
+    X->early = 1;
     if (len == 0) return 0; /* kmer[len-1] is undefined behaviour in the reference (:239) */
     X->other.n = 0;
     X->dollar.n = 0;
@@ -840,6 +842,7 @@ static uint32_t backward_search(const orc_engine* E, ctx_t* X, uint32_t n_kmer, 
     if (!bs_step(E, X, kmer[len - 1], &X->other)) return 0;
     for (uint32_t pos = len - 1; pos > 0; pos--)
         if (!bs_level(E, X, kmer[pos - 1])) return 0;
+    X->early = 0;
     return locate_list(E, X, n_kmer, &X->other);
 }
 
@@ -850,6 +853,7 @@ typedef struct {
     uint64_t lo, hi;
     uint32_t first_id;
     uint32_t* counts;
+    uint8_t* early;
     ctx_t X;
 } job_t;
 
@@ -859,6 +863,7 @@ static void* job_run(void* arg) {
         uint32_t len = (uint32_t)(J->off[i + 1] - J->off[i]);
         uint32_t r = backward_search(J->E, &J->X, J->first_id + (uint32_t)i, J->bytes + J->off[i], len);
         J->counts[i] = r;
+        if (J->early) J->early[i] = (uint8_t)J->X.early;
         if (r > 0) J->X.c.found++; else J->X.c.not_found++;
     }
     return NULL;
@@ -874,9 +879,9 @@ static void add_ctr(orc_counters* a, const orc_counters* b) {
     a->found += b->found; a->not_found += b->not_found;
 }
 
-int orc_search_batch(orc_engine* E, const char* bytes, const uint64_t* offsets, uint64_t npat,
-                     uint32_t first_pattern_id, int threads, uint32_t* counts,
-                     orc_occ** occ, uint64_t* nocc, orc_counters* ctr) {
+static int search_batch(orc_engine* E, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                        uint32_t first_pattern_id, int threads, uint32_t* counts,
+                        orc_occ** occ, uint64_t* nocc, orc_counters* ctr, uint8_t* early) {
     if (threads < 1) threads = 1;
     if ((uint64_t)threads > npat) threads = npat ? (int)npat : 1;
     job_t* J = xcalloc((size_t)threads, sizeof(job_t));
@@ -885,7 +890,7 @@ int orc_search_batch(orc_engine* E, const char* bytes, const uint64_t* offsets, 
         J[t].E = E; J[t].bytes = (const uint8_t*)bytes; J[t].off = offsets;
         J[t].lo = npat * (uint64_t)t / (uint64_t)threads;
         J[t].hi = npat * (uint64_t)(t + 1) / (uint64_t)threads;
-        J[t].first_id = first_pattern_id; J[t].counts = counts;
+        J[t].first_id = first_pattern_id; J[t].counts = counts; J[t].early = early;
     }
     if (threads == 1) job_run(&J[0]);
     else {
@@ -904,6 +909,17 @@ int orc_search_batch(orc_engine* E, const char* bytes, const uint64_t* offsets, 
     for (int t = 0; t < threads; t++) { if (ctr) add_ctr(ctr, &J[t].X.c); ctx_free(&J[t].X); }
     free(J); free(th);
     return 0;
+}
+
+int orc_search_batch(orc_engine* E, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                     uint32_t first_pattern_id, int threads, uint32_t* counts,
+                     orc_occ** occ, uint64_t* nocc, orc_counters* ctr) {
+    return search_batch(E, bytes, offsets, npat, first_pattern_id, threads, counts, occ, nocc, ctr, NULL);
+}
+
+int orc_search_batch_console(orc_engine* E, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                             uint32_t first_pattern_id, int threads, uint32_t* counts, uint8_t* early) {
+    return search_batch(E, bytes, offsets, npat, first_pattern_id, threads, counts, NULL, NULL, NULL, early);
 }
 
 /* ---------------------------------------------------------- trie-sharing variant

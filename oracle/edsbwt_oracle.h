@@ -75,6 +75,12 @@ int orc_search_batch_trie(orc_engine*, const char* bytes, const uint64_t* offset
                           uint32_t first_pattern_id, int threads, uint32_t* counts,
                           orc_occ** occ, uint64_t* nocc, orc_counters* ctr);
 void orc_free(void* p);
+/* The literal loop (orc_search_batch, one thread per contiguous range) also reporting, per
+ * pattern, whether backwardSearch returned before its locate loop (early[i] = 1: the
+ * `return 0` of MOVE_EDSBWTSearch.cpp:250-253 / :295-297, so no "num occ" line, :371): the
+ * per-pattern console stream of the reference is a function of (pattern, count, early). */
+int orc_search_batch_console(orc_engine*, const char* bytes, const uint64_t* offsets, uint64_t npat,
+                             uint32_t first_pattern_id, int threads, uint32_t* counts, uint8_t* early);
 
 /* Same loop over a pattern file (getline semantics), writing <out_csv>
  * byte-for-byte as MOVE_EDSBWTSearch.cpp:55-64,365 does. limit=0 → all lines. */

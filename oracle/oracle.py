@@ -59,6 +59,8 @@ def lib():
         L.orc_search_batch.restype = i32
         L.orc_search_batch_trie.argtypes = L.orc_search_batch.argtypes
         L.orc_search_batch_trie.restype = i32
+        L.orc_search_batch_console.argtypes = [vp, vp, vp, u64, u32, i32, vp, vp]
+        L.orc_search_batch_console.restype = i32
         L.orc_free.argtypes = [vp]
         L.orc_search_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, u64, i32, ctypes.POINTER(Counters),
                                       ctypes.POINTER(ctypes.c_double)]
@@ -152,6 +154,20 @@ class Engine:
             ctypes.memmove(occ.ctypes.data, occ_p.value, nocc.value * OCC_DTYPE.itemsize)
         lib().orc_free(occ_p)
         return counts[:npat], occ, c.as_dict()
+
+    def console(self, buf: np.ndarray, offs: np.ndarray, threads: int = 1):
+        """(counts, early): early[i] when the reference's backwardSearch returns before its
+        locate loop for pattern i (no "num occ" line, MOVE_EDSBWTSearch.cpp:250-253,295-297,371)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        npat = offs.size - 1
+        counts = np.zeros(max(npat, 1), np.uint32)
+        early = np.zeros(max(npat, 1), np.uint8)
+        rc = lib().orc_search_batch_console(self._h, buf.ctypes.data if buf.size else None, offs.ctypes.data, npat, 1, threads,
+                                            counts.ctypes.data, early.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return counts[:npat], early[:npat].astype(bool)
 
     def search_file(self, patterns_path: str, out_csv: str | None, limit: int = 0, threads: int = 1):
         c = Counters()

@@ -135,7 +135,8 @@ def test_long_patterns_gpu(oracle, edsbwt, tmp_path, alphabet):
 
 def test_c5_style_gpu(oracle, edsbwt, tmp_path):
     """C5's shape at a size the oracle finishes in seconds: ~20% empty-word segments and
-    a mixed 8–64-mer batch (BASELINE.json configs[2] is 1 Gchar / 100M patterns)."""
+    a mixed 8–64-mer batch (BASELINE.json configs[4] is 1 Gchar; its production index and
+    batch are tests/test_production_gpu.py::test_c5_production_parity)."""
     rng = random.Random(55)
     segs = edsgen.random_eds(rng, 20000, kmax=4, lmax=12, p_empty=0.2)
     base = _build(oracle, tmp_path, edsgen.eds_text(segs))
@@ -786,15 +787,20 @@ def test_search_lines_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     torch = pytest.importorskip("torch")
     for k in ("EDSBWT_CHUNK_MB", "EDSBWT_CHUNK_SINGLE_MB", "EDSBWT_PACK_LINES"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")  # small tables hold long lists: direct start anyway
     rng = random.Random(5150)
     segs = _covid_like(rng, 400)
     base = _build(oracle, tmp_path, edsgen.eds_text(segs))
-    uniq = [edsgen.planted(rng, segs, 31) or "ACGT" * 7 + "ACG" for _ in range(40000)]
-    uniq += ["".join(rng.choice("ACGT") for _ in range(rng.randint(20, 40))) for _ in range(10000)]
-    pats = uniq * 120                                   # 6M lines, ~190 MB
-    for i in range(777, len(pats), 20011):
-        pats[i] = rng.choice(["A", "C", "GT", "TA"])      # thousands of records each
-    pats[len(pats) // 2 + 5] = "ACGT#ACG"                 # '#': that chunk is searched again
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    assert D0 >= 2
+    # lengths D0+1 .. D0+16: the packed direct start with its deferred checks
+    uniq = [edsgen.planted(rng, segs, D0 + 8) or ("ACGT" * 8)[:D0 + 8] for _ in range(40000)]
+    uniq += ["".join(rng.choice("ACGT") for _ in range(rng.randint(D0 + 1, D0 + 16))) for _ in range(10000)]
+    pats = uniq * 150                                   # 7.5M lines, ~150 MB
+    for i in range(777, len(pats) // 2, 20011):
+        pats[i] = rng.choice(["A", "C", "GT", "TA"])      # thousands of records each (checked-path chunks)
+    pats[3 * len(pats) // 4 + 5] = ("ACGT#ACG" * 8)[:D0 + 4]  # '#' in a direct-start chunk: searched again
     text = ("\n".join(pats) + "\n").encode()
     buf, offs = _pack(pats)
     with edsbwt.Index(base) as idx:
@@ -816,8 +822,8 @@ def test_search_lines_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     assert np.array_equal(gc, ref_counts)
     assert go.size == ref_occ.size and np.array_equal(go, ref_occ)
     # the oracle on a strided sample of the batch (records of pattern i carry #Pat = i + 1)
-    sample = np.unique(np.concatenate([np.arange(0, len(pats), 997), np.arange(777, len(pats), 20011)[:20],
-                                       [len(pats) // 2 + 5]]))
+    sample = np.unique(np.concatenate([np.arange(0, len(pats), 997), np.arange(777, len(pats) // 2, 20011)[:20],
+                                       [3 * len(pats) // 4 + 5]]))
     sp = [pats[i] for i in sample]
     sbuf, soffs = _pack(sp)
     oc, oo, _ = oracle.Engine(base, 8).search(sbuf, soffs, threads=8)
@@ -826,3 +832,59 @@ def test_search_lines_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     got = go[sel].copy()
     got["pat"] = np.searchsorted(sample, got["pat"] - 1) + 1
     assert np.array_equal(got, oo)
+
+
+def _expected_console(oracle, base, pfile, pats, argv0):
+    """The reference's stdout / stderr for `MOVE_EDSBWTSearch base pfile` (mainMove_EDSBWT.cpp:27-59,
+    MOVE_EDSBWTSearch.cpp:23-155,664-766), the per-pattern part from the oracle's literal loop
+    (orc_search_batch_console: count and early return per pattern); 'bs took:' left as a marker."""
+    raw = open(base + "_info.aux", "rb").read()
+    N, W = (int(x) for x in np.frombuffer(raw, np.uint32, 2))
+    sigma = raw[8]
+    alpha = raw[9:9 + sigma].decode("latin1")
+    tocc = np.frombuffer(raw, np.uint32, count=sigma * sigma, offset=9 + sigma + 4 * W).reshape(sigma, sigma)
+    buf, offs = _pack(pats)
+    counts, early = oracle.Engine(base, 8).console(buf, offs)
+    out = [f"BCR_eds: {argv0}\n", f"BCR_eds: The input ebwt file is {base}\n", f"BCR_eds: The pattern file is {pfile}\n", "DEBUG: 0\n",
+           f"\nFrom {base}_info.aux file:\n", f"\tNumber of sequences: {W}\n", f"\tTotal length (with $): {N}\n",
+           f"\tSize alpha: {sigma}\n", "\tAlphabet: " + "".join(c + "\t" for c in alpha) + "\n", f"NUM OF EOF{W}\n",
+           f"\nFrom {base}_info.aux file (TableOcc):\n"]
+    out += ["".join(f"{v}\t" for v in row) + "\n" for row in tocc]
+    out += [f"size= {N}\n", f"BitVector size: {W}\n"]
+    err = ["Backward Search\n"]
+    for p, c, e in zip(pats, counts, early):
+        out.append(f"Pattern: {p} of length {len(p)}\n")
+        if not e:
+            out.append(f"num occ {c}\n")
+        err.append(f"OCCORRENZA DI: {p} {'TROVATA' if c > 0 else 'NON TROVATA'}\n")
+    out.append("bs took:")
+    found = int((counts > 0).sum())
+    err += ["\n", f"count_found = {found}\n", f"count_not_found = {len(pats) - found}\n", "\nThe csv file is ready! \n", "The End!\n"]
+    return "".join(out), "".join(err), counts, early
+
+
+def test_cli_console_transcript(oracle, tmp_path):
+    """EDSBWTsearch without --quiet: stdout and stderr byte-identical to the reference's stream
+    (banner, index summary, TableOcc, per pattern 'Pattern: ... of length ...', 'num occ' only
+    when backwardSearch reaches its locate loop, 'OCCORRENZA DI ...'), from a transcript made by
+    the oracle's literal loop; 'bs took:<secs>' compared up to the number."""
+    import re
+    import subprocess
+    from conftest import ROOT
+    rng = random.Random(4711)
+    segs = edsgen.random_eds(rng, 400, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(2, 14)) or "ACGT" for _ in range(150)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(1, 12))) for _ in range(150)]  # many die early
+    pats += ["A", "N", "NA", "AN", "GATTACA"]
+    pfile = tmp_path / "p.txt"
+    pfile.write_text("\n".join(pats) + "\n")
+    cli = os.path.join(ROOT, "eds-bwt_amd", "_build", "EDSBWTsearch")
+    r = subprocess.run([cli, base, str(pfile)], capture_output=True, text=True)
+    assert r.returncode == 1, r.stderr
+    want_out, want_err, counts, early = _expected_console(oracle, base, str(pfile), pats, cli)
+    assert early.any() and (~early).any() and ((counts == 0) & ~early).any()  # all three console shapes occur
+    m = re.fullmatch(r"(.*bs took:)[0-9.e+-]+", r.stdout, re.S)
+    assert m, r.stdout[-200:]
+    assert m.group(1) == want_out
+    assert r.stderr == want_err

@@ -179,3 +179,32 @@ def test_trie_variant_equals_literal(oracle, tmp_path, seed):
         assert np.array_equal(tc, lc) and np.array_equal(to, lo)
         assert tctr["occurrences"] == lctr["occurrences"] and tctr["found"] == lctr["found"]
         assert tctr["interval_steps"] <= lctr["interval_steps"]
+
+
+def test_console_early_return_rule(oracle, tmp_path):
+    """The reference's backwardSearch returns before its locate loop (no 'num occ' line,
+    MOVE_EDSBWTSearch.cpp:250-253,295-297,371) exactly when the pattern without its first
+    character does not occur (its final list is the pattern's list after all but the first
+    character) — the rule the CLI's console stream uses; checked on the literal loop."""
+    import random
+    import edsgen
+    rng = random.Random(99)
+    for t in range(3):
+        segs = edsgen.random_eds(rng, 300, p_empty=0.25)
+        (tmp_path / f"e{t}.eds").write_text(edsgen.eds_text(segs))
+        base = str(tmp_path / f"e{t}")
+        oracle.transform(str(tmp_path / f"e{t}.eds"), base)
+        pats = [edsgen.planted(rng, segs, rng.randint(1, 12)) or "AC" for _ in range(200)]
+        pats += ["".join(rng.choice("ACGTN") for _ in range(rng.randint(0, 10))) for _ in range(200)]
+        buf = np.frombuffer("".join(pats).encode(), np.uint8)
+        offs = np.concatenate(([0], np.cumsum([len(p) for p in pats]))).astype(np.uint64)
+        eng = oracle.Engine(base, 8)
+        counts, early = eng.console(buf, offs)
+        c_ref, _, _ = eng.search(buf, offs)
+        assert np.array_equal(counts, c_ref)
+        sufs = [p[1:] for p in pats]
+        sb = np.frombuffer("".join(sufs).encode(), np.uint8)
+        so = np.concatenate(([0], np.cumsum([len(p) for p in sufs]))).astype(np.uint64)
+        cs, _, _ = eng.search(sb, so)
+        reach = np.array([len(p) == 1 or (len(p) > 1 and c > 0) for p, c in zip(pats, cs)])
+        assert np.array_equal(~early, reach)
