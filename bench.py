@@ -39,6 +39,9 @@ import workloads  # noqa: E402
 
 MI355X_HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
 MI355X_MALL_BYTES = 256 << 20  # Infinity Cache: index tables smaller than this are cache-resident
+# bench.py kernel class (engine.hip KClass) -> the kernels it times
+KERNELS_OF_CLASS = {"deep": "k_deep_fast", "deep_list": "k_deep", "deep_wide": "k_deep_wide",
+                    "step": "k_lvl_items + k_lvl_dollar + k_lvl_chunks", "locate": "k_locate_pp + k_locate_big (+ k_locate)"}
 # Practical ceilings of the deep kernels' access shape on MI355X (tools/calib_gather.hip,
 # profiles/r02_calib_gather.json): one random 16-B rank entry per lane per step from a
 # table of the C3 rank entries' size, issued as the kernel issues them.
@@ -64,6 +67,8 @@ def traffic_from_profile(cfg: str, kernel: str):
     path = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
     try:
         t = json.load(open(path))
+        if t.get("classes_version") != "r3":  # round-3 classes: deep = k_deep_fast alone
+            return None, None
         c = t["classes"][kernel]
         return int(c["pmc_hbm_bytes_per_launch"]), f"profiles/traffic_{cfg}.json ({t.get('source', '')})"
     except (OSError, KeyError, ValueError):
@@ -158,13 +163,21 @@ def main():
                          "trace of the whole run); the line's value is then the device-resident rate")
     ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
-    ap.add_argument("--gather", default="none", choices=("none", "counts"),
+    ap.add_argument("--gather", default="auto", choices=("auto", "none", "counts"),
                     help="N>1 exchange: the (patterns, records) sizes are all-gathered (each rank's output offsets: every "
-                         "rank keeps its counts and records as its slice of the output); 'counts' also gathers the "
-                         "per-pattern counts to rank 0 over RCCL inside the timed step")
+                         "rank keeps its counts and records as its slice of the output); 'counts' (the default when N>1) "
+                         "also gathers the per-pattern counts to rank 0 over RCCL inside the timed step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gather == "auto":
+        args.gather = "counts" if world > 1 else "none"
+    # the CPUs this process may use, before the NUMA pinning below; the CPU baseline uses them,
+    # capped by the job's CPU share when the launcher states one (OMP_NUM_THREADS: 16 per GPU
+    # on the GPU box, whose os.cpu_count() shows the whole machine)
+    cpus_usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cpu_share = int(os.environ.get("OMP_NUM_THREADS") or cpus_usable)
+    cpu_threads = max(1, min(cpus_usable, cpu_share))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # one process per GPU: start torchrun as a child (nothing has touched the GPU yet)
         port = free_port()
@@ -268,6 +281,7 @@ def main():
     held = (0, 0)
     total_occ = 0
     walls = []
+    redo_calls = 0
     for i in range(0 if args.no_e2e else args.steps):
         ta = time.perf_counter()
         last = i == args.steps - 1
@@ -278,7 +292,9 @@ def main():
         exchange(nocc)
         search_ms += 1e3 * (tb - ta)
         exch_ms += 1e3 * (time.perf_counter() - tb)
-        walls.append(idx.stats()["ms_wall"])
+        st_call = idx.stats()
+        walls.append(st_call["ms_wall"])
+        redo_calls += st_call["redo_searches"]
         total_occ += nocc
     torch.cuda.synchronize()
     barrier()
@@ -307,6 +323,28 @@ def main():
     occ_last = idx.occ_view(*held).copy() if held[1] else np.zeros(0, pkg.OCC_DTYPE)
     counts_last = counts[:npat].copy()
     idx.occ_free(held[0])
+
+    # ---- N > 1: every rank's first patterns against the oracle, outside the timed region
+    rank_parity = None
+    if world > 1 and not args.no_cpu:
+        n_par = min(16 if w.name == "c5" else 256, npat)
+        pbuf, poffs = pkg.read_pattern_file(pats_path)
+        ok = 0
+        try:
+            pr_ = cpu_baseline(base, pbuf, poffs, first_id, n_par, cpu_threads)
+            kk = int(pr_["counts"].astype(np.int64).sum())
+            ok = int(np.array_equal(pr_["counts"], counts_last[:n_par]) and (not locate or np.array_equal(pr_["occ"], occ_last[:kk])))
+        except Exception as e:  # noqa: BLE001 - reported as a mismatch
+            log(f"[bench] rank {rank} parity sample failed: {e!r}")
+        tt = torch.tensor([ok, n_par], dtype=torch.float64, device=gdev)
+        mn = tt.clone()
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        sm = tt.clone()
+        dist.all_reduce(sm)
+        rank_parity = {"n_per_rank": n_par, "ranks": world, "n": int(sm[1].item()), "match": bool(mn[0].item() == 1),
+                       "compared": "counts and records" if locate else "counts (count-only workload)",
+                       "what": "each rank's first n_per_rank patterns (its first_pattern_id offset) against the oracle "
+                               "(literal MOVE_EDSBWTSearch restatement), all-reduced (min)"}
 
     # ---- timed: device-resident (bytes + offsets in HBM, results left in HBM)
     dres = None
@@ -382,11 +420,14 @@ def main():
                                     + (" + counts gathered to rank 0 over RCCL" if args.gather == "counts" else "")),
                        "ktab_depth": idx.ktab_depth, "index_device_bytes": idx.device_bytes,
                        "host_numa_node": numa,
-                       "cache_resident": bool(rank_bytes <= MI355X_MALL_BYTES)},
+                       # every table the search reads (rank tables, k-mer table, samples) within the 256 MB MALL
+                       "cache_resident": bool(idx.device_bytes <= MI355X_MALL_BYTES), "rank_tables_bytes": int(rank_bytes)},
             "occurrences_per_step": int(total_occ / args.steps),
             "found_per_step": int(e2e_stats["found"]) if world == 1 else None,
             "e2e": {"ms_wall_per_call": round(float(np.mean(walls)), 3), "ms_wall_median": round(float(np.median(walls)), 3),
-                    "ms_wall_min": round(float(np.min(walls)), 3), "host_cores": round(host_cores, 2), "chunks": e2e_stats["chunks"],
+                    "ms_wall_min": round(float(np.min(walls)), 3), "ms_wall_p90": round(float(np.percentile(walls, 90)), 3),
+                    "ms_wall_max": round(float(np.max(walls)), 3), "ms_walls": [round(float(x), 3) for x in walls],
+                    "redo_searches": redo_calls, "host_cores": round(host_cores, 2), "chunks": e2e_stats["chunks"],
                     "bytes_h2d": e2e_stats["bytes_h2d"], "bytes_d2h": e2e_stats["bytes_d2h"],
                     "pcie_gbs": round((e2e_stats["bytes_h2d"] + e2e_stats["bytes_d2h"]) / max(1e-9, np.mean(walls) * 1e-3) / 1e9, 2),
                     "device_ms_per_call": round(e2e_stats["ms_total"], 3),
@@ -399,30 +440,45 @@ def main():
             kstats = dres["kstats"]
             dstat = dres["stats"]
             d_ms = 1000.0 * dres["elapsed"] / args.steps
-            dom = max((k for k in kstats if k != "scan"), key=lambda k: kstats[k]["ms"])
-            d = kstats[dom]
-            avg_ms = d["ms"] / max(1, d["launches"])
-            bpl = d["bytes"] / max(1, d["launches"])
-            lpl = d["lines"] / max(1, d["launches"])
-            achieved = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-            line_rate = lpl / (avg_ms * 1e-3) if avg_ms > 0 else 0.0
-            # SURVEY §8(d)'s per-step model: two 64-B lines per interval step (one per interval end)
-            steps_pl = dstat["intervals_stepped"] / max(1, kstats[dom]["launches"] / args.steps) if dom == "deep" else 0
-            survey_bpl = 2 * 64 * steps_pl
-            traffic, traffic_src = traffic_from_profile(w.name, dom)
             ceil, ceil_shape = gather_ceiling()
+
+            def kclass(name):
+                d = kstats.get(name)
+                if not d or not d["launches"] or d["ms"] <= 0:
+                    return None
+                avg_ms = d["ms"] / d["launches"]
+                bpl = d["bytes"] / d["launches"]
+                lpl = d["lines"] / d["launches"]
+                ach = bpl / (avg_ms * 1e-3) / 1e9
+                rate = lpl / (avg_ms * 1e-3)
+                traffic, tsrc = traffic_from_profile(w.name, name)
+                return {"kernels": KERNELS_OF_CLASS.get(name, name), "ms_per_step": round(d["ms"] / args.steps, 4),
+                        "launches_per_step": round(d["launches"] / args.steps, 2), "avg_launch_ms": round(avg_ms, 4),
+                        "bytes_per_launch": int(bpl), "lines_per_launch": int(lpl),
+                        "achieved": round(ach, 1), "frac": round(ach / MI355X_HBM_PEAK_GBS, 4) if bpl else None,
+                        "lines_per_s": round(rate, 1), "frac_of_gather_ceiling": round(rate / ceil, 4) if (ceil and lpl) else None,
+                        "traffic": traffic, "traffic_source": tsrc}
+
+            per_class = {k: v for k in ("deep", "deep_list", "deep_wide", "step", "locate") if (v := kclass(k))}
+            dom = max((k for k in kstats if k != "scan"), key=lambda k: kstats[k]["ms"])
+            dk = per_class.get(dom) or kclass(dom)
+            # SURVEY §8(d)'s per-step model over the deep family: two 64-B lines per interval step
+            fam_ms = sum(kstats[k]["ms"] for k in ("deep", "deep_list", "deep_wide") if k in kstats) / args.steps
+            survey_b = 2 * 64 * dstat["intervals_stepped"]
             out["roofline"] = {
-                "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": MI355X_HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / MI355X_HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "avg_launch_ms": round(avg_ms, 4), "launches": d["launches"],
-                "bytes_model": "line model: the 64-B lines the class gathers (a narrow interval's two ends in one line count "
-                               "once; one 16-B two-step rank entry per end) + '#'-row reads (DESIGN.md §6)",
-                "bytes_per_launch": int(bpl),
-                "survey_model_bytes_per_launch": int(survey_bpl),
-                "survey_model_frac": round(survey_bpl / (avg_ms * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4) if avg_ms > 0 else None,
-                "lines_per_launch": int(lpl), "lines_per_s": round(line_rate, 1),
+                "bound": "hbm", "kernel": dom, "kernels": dk["kernels"], "achieved": dk["achieved"], "peak": MI355X_HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": dk["frac"], "traffic": dk["traffic"], "traffic_source": dk["traffic_source"],
+                "avg_launch_ms": dk["avg_launch_ms"], "launches": kstats[dom]["launches"],
+                "bytes_model": "line model: the 64-B lines the kernel gathers as it counts them (a narrow interval's two ends in "
+                               "one line count once; one 16-B two-step rank entry per end; the single-row text compare's sample, "
+                               "text-position and text lines) + 24 B of per-pattern streams (DESIGN.md §6)",
+                "bytes_per_launch": dk["bytes_per_launch"], "lines_per_launch": dk["lines_per_launch"], "lines_per_s": dk["lines_per_s"],
                 "gather_ceiling_lines_per_s": ceil, "gather_ceiling_shape": ceil_shape,
-                "frac_of_gather_ceiling": round(line_rate / ceil, 4) if ceil else None,
+                "frac_of_gather_ceiling": dk["frac_of_gather_ceiling"],
+                "per_kernel": per_class,
+                "survey_model_deep_family": {"interval_steps_per_step": int(dstat["intervals_stepped"]),
+                                             "bytes_per_step": int(survey_b), "deep_family_ms_per_step": round(fam_ms, 4),
+                                             "frac": round(survey_b / (fam_ms * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4) if fam_ms > 0 else None},
                 "from": "device_resident leg (HIP events on the library stream, EDSBWT_PROFILE_LIGHT)",
             }
             out["device_resident"] = {
@@ -433,19 +489,24 @@ def main():
                                        for k, v in sorted(kstats.items()) if v["lines"]},
                 "engine": {k: dstat[k] for k in ("depths", "deep_from_depth", "deep_overflow", "deep_level_rerun", "search_groups",
                                                  "trie_nodes", "intervals_stepped", "link_hash_rows", "start_depth",
-                                                 "locate_lf_steps")},
+                                                 "locate_lf_steps", "redo_searches", "text_rows", "text_chars")},
                 # LF steps the device executed: 2 per interval step (one per end) + locate walk moves
                 "device_lf_steps_per_sec": round((2 * dstat["intervals_stepped"] + dstat["locate_lf_steps"]) * args.steps
                                                  / dres["elapsed"], 1),
                 "reference_locate_lf_steps_per_sec": round(dstat["locate_offsets"] * args.steps / dres["elapsed"], 1),
             }
+        if rank_parity is not None:
+            out["parity_sample"] = rank_parity
         if world == 1 and not args.no_cpu:
             buf, offs = pkg.read_pattern_file(pats_path)
-            threads = max(1, min(16, os.cpu_count() or 1))
+            threads = cpu_threads
             try:
-                samp_n = min(args.cpu_sample or (64 * threads if w.name != "c2" else 512 * threads), npat)
+                # a fixed prefix of the batch on every usable CPU, and the reference's
+                # single thread; C5's literal loop runs ~1.9 patterns/s on 16 threads, so its
+                # samples are scaled to ~30 s
+                samp_n = min(args.cpu_sample or (48 if w.name == "c5" else 4096), npat)
+                samp1 = min(4 if w.name == "c5" else 128, npat)
                 cb = cpu_baseline(base, buf, offs, first_id, samp_n, threads)
-                samp1 = max(8, samp_n // (4 * threads))
                 c1 = cpu_baseline(base, buf, offs, first_id, samp1, 1)
                 # parity of the sample: the oracle's counts and records vs the GPU's (end-to-end run)
                 k = int(cb["counts"].astype(np.int64).sum())
@@ -454,7 +515,7 @@ def main():
                              and (not locate or np.array_equal(cb["occ"], occ_last[:k])))
                 ctr = cb["ctr"]
                 lf_ref = (ctr["step_moves"] + ctr["locate_moves"]) / samp_n  # reference-literal M_LF moves per pattern
-                out["parity_sample"] = {"n": samp_n, "records": k if locate else None, "occurrences": k,
+                out["parity_sample"] = {"n": samp_n, "ranks": 1, "records": k if locate else None, "occurrences": k,
                                         "compared": "counts and records" if locate else "counts (count-only workload)",
                                         "match": match,
                                         "what": "oracle (literal MOVE_EDSBWTSearch restatement) vs GPU end-to-end results "
@@ -467,7 +528,10 @@ def main():
                     "seconds": round(cb["seconds"], 3),
                     "single_thread": {"value": round(c1["value"], 3), "cores": 1, "sample": f"first {samp1} patterns",
                                       "seconds": round(c1["seconds"], 3)},
-                    "host_cpus_visible": os.cpu_count(),
+                    "cpus_usable": cpus_usable, "cpu_share": cpu_share, "host_cpus_visible": os.cpu_count(),
+                    "cores_note": ("threads = the CPUs this process may use (sched_getaffinity, before NUMA pinning), capped by "
+                                   "the job's CPU share OMP_NUM_THREADS when set (16 per GPU on the GPU box, whose "
+                                   "os.cpu_count() shows the whole machine)"),
                     "lf_steps_per_pattern": round(lf_ref, 1), "interval_steps_per_pattern": round(ctr["interval_steps"] / samp_n, 1),
                 }
                 # SURVEY §8(d) LF-steps: the reference-literal M_LF moves (oracle-counted on the sample)
@@ -477,13 +541,9 @@ def main():
                                         "sample x value (SURVEY §8(d)); the device executes far fewer (device_resident."
                                         "device_lf_steps_per_sec)")
                 out["cpu_baseline"]["lf_steps_per_sec"] = round(lf_ref * cb["value"], 1)
-                # the trie-sharing CPU variant on the same sample, and §8(d)'s
-                # algorithmic bytes from its deduplicated counters
+                # the trie-sharing CPU variant on the same sample
                 ct = cpu_baseline(base, buf, offs, first_id, samp_n, threads, trie=True)
                 tc = ct["ctr"]
-                plen = int(offs[samp_n] - offs[0])
-                B = (64 * (2 * tc["interval_steps"] + 2 * tc["pdf_calls"] + tc["locate_moves"] + 3 * tc["occurrences"])
-                     + 4 * tc["eof_reads"] + plen + samp_n + 4 * samp_n + 20 * tc["occurrences"])
                 out["cpu_baseline"]["trie_sharing"] = {
                     "value": round(ct["value"], 3), "cores": threads, "seconds": round(ct["seconds"], 3),
                     "sample": f"first {samp_n} patterns, sorted by reversed pattern, each thread a contiguous range of "
@@ -491,11 +551,6 @@ def main():
                     "match_literal": bool(np.array_equal(ct["counts"], cb["counts"]) and np.array_equal(ct["occ"], cb["occ"])),
                     "interval_steps_per_pattern": round(tc["interval_steps"] / samp_n, 1),
                 }
-                out.setdefault("roofline", {})["survey_oracle_bytes_per_pattern"] = round(B / samp_n, 1)
-                out["roofline"]["survey_oracle_note"] = (
-                    "SURVEY §8(d) B = 64(2 S_steps + 2 K_pdf + W_lf + 3 O) + 4 D_eof + sum(|P|+1) + 4 N_pat + 20 O from the "
-                    "trie-sharing oracle's deduplicated counters on the cpu_baseline sample; a sample shares far fewer "
-                    "suffixes than the full batch, so this overstates the batch's per-pattern bytes")
                 if not match:
                     diff = np.nonzero(cb["counts"] != counts_last[:samp_n])[0]
                     log("[bench] PARITY SAMPLE MISMATCH", "counts differ at", diff[:8].tolist(),

@@ -134,10 +134,12 @@ struct DBuf {
     }
 };
 
+// KC_DEEP: k_deep_fast (and the deep stage's small helpers); KC_DEEPQ: k_deep (queued patterns,
+// register lists); KC_DEEPW: k_deep_wide
 enum KClass { KC_TRIE = 0, KC_NODES, KC_EXPAND, KC_LINK, KC_LINKSORT, KC_STEP, KC_MERGE, KC_FINISH, KC_DEEP, KC_LOCPREP, KC_LOCATE, KC_SCAN,
-              KC_TABLE, KC_COUNT };
+              KC_TABLE, KC_DEEPQ, KC_DEEPW, KC_COUNT };
 static const char* kKNames[KC_COUNT] = {"trie_sort", "trie_nodes", "expand", "link", "link_sort", "step", "merge", "finish",
-                                        "deep", "locate_prep", "locate", "scan", "table"};
+                                        "deep", "locate_prep", "locate", "scan", "table", "deep_list", "deep_wide"};
 // k_deep keeps at most kDeepK intervals per list in registers (C3 sweep, 1x MI355X: K=2 1.08e9,
 // K=3 1.20e9, K=4 1.21e9, K=8 1.15e9 patterns/s; longer lists retry in k_deep_wide)
 constexpr int kDeepK = 4;
@@ -1417,7 +1419,7 @@ struct Engine {
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? k_deep<4, 3> : k_deep<4, 4>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
-        launch(KC_DEEP, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
+        launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
                pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr);
         tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
@@ -1438,7 +1440,7 @@ struct Engine {
             if (!no_wide) {
                 ab.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
                 ae.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
-                launch(KC_DEEP, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
+                launch(KC_DEEPW, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
                        (const uint32_t*)ovf.p);
                 abase += (uint64_t)wcap * kDeepWide;
@@ -1457,7 +1459,7 @@ struct Engine {
             zero(ovf2.p, 4);
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
-            launch(KC_DEEP, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
+            launch(KC_DEEPW, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                    d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
                    (const uint32_t*)nullptr);
             abase += (uint64_t)nw * kDeepWide;
@@ -1469,7 +1471,7 @@ struct Engine {
         tag_list(list - 1, novf, EDSBWT_PATH_LEVELS);
         if (novf) {
             zero(ovf_orig, P * 4);
-            launch(KC_DEEP, k_ovf_mark, novf, novf, list, (const uint32_t*)perm.p, ovf_orig);
+            launch(KC_MERGE, k_ovf_mark, novf, novf, list, (const uint32_t*)perm.p, ovf_orig);
         }
         if (no_wide) st.deep_overflow += nw;
         st.deep_level_rerun += novf;
@@ -1703,7 +1705,7 @@ struct Engine {
                 gend.ensure(Mcur);
                 if (d0 && d == d0) {
                     // the table's items are already grouped by node: [kt_pos[u], + kt_cnt[u])
-                    launch(KC_DEEP, k_group_end, Mcur, Mcur, (const uint32_t*)kt_pos.p, (const uint32_t*)kt_cnt.p, gend.p);
+                    launch(KC_MERGE, k_group_end, Mcur, Mcur, (const uint32_t*)kt_pos.p, (const uint32_t*)kt_cnt.p, gend.p);
                     novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, kt_pos.p, gend.p, ib[cur].p, ie[cur].p, r, abase,
                                     ovf_orig);
                     break;
@@ -1711,14 +1713,14 @@ struct Engine {
                 if (in_sharded) pack_items(cur);
                 // group the unordered items by node, then finish patterns one per thread
                 gcnt.ensure(Mcur); gfill.ensure(Mcur); goff.ensure(Mcur);
-                launch(KC_DEEP, k_zero4, 2 * (size_t)Mcur, gcnt.p, (uint64_t)Mcur, gfill.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0,
+                launch(KC_MERGE, k_zero4, 2 * (size_t)Mcur, gcnt.p, (uint64_t)Mcur, gfill.p, (uint64_t)Mcur, (uint32_t*)nullptr, (uint64_t)0,
                        (uint32_t*)nullptr, (uint64_t)0);
-                launch(KC_DEEP, k_group_count, ncur, ncur, (const uint32_t*)iu[cur].p, gcnt.p);
+                launch(KC_MERGE, k_group_count, ncur, ncur, (const uint32_t*)iu[cur].p, gcnt.p);
                 exclusive_scan(gcnt.p, goff.p, Mcur);
                 gb.ensure(ncur); gee.ensure(ncur);
-                launch(KC_DEEP, k_group_scatter, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p,
+                launch(KC_MERGE, k_group_scatter, ncur, ncur, (const uint32_t*)iu[cur].p, (const uint32_t*)ib[cur].p, (const uint32_t*)ie[cur].p,
                        (const uint32_t*)goff.p, gfill.p, gb.p, gee.p);
-                launch(KC_DEEP, k_group_end, Mcur, Mcur, (const uint32_t*)goff.p, (const uint32_t*)gcnt.p, gend.p);
+                launch(KC_MERGE, k_group_end, Mcur, Mcur, (const uint32_t*)goff.p, (const uint32_t*)gcnt.p, gend.p);
                 novf = run_deep(d, M, P, ge[D], d_bytes, d_off, nid[cur].p, goff.p, gend.p, gb.p, gee.p, r, abase, ovf_orig);
                 break;
             }
@@ -1930,15 +1932,15 @@ struct Engine {
         const uint32_t n = scan_u32(ovf_orig.p, ovf_scan, P);
         sub_map.ensure(n);
         sub_len.ensure(n + 1);
-        launch(KC_DEEP, k_sub_build, P, P, (const uint32_t*)ovf_orig.p, (const uint32_t*)ovf_scan.p, (const uint32_t*)len.p, sub_map.p, sub_len.p);
+        launch(KC_MERGE, k_sub_build, P, P, (const uint32_t*)ovf_orig.p, (const uint32_t*)ovf_scan.p, (const uint32_t*)len.p, sub_map.p, sub_len.p);
         const uint64_t nbytes = scan_u64(sub_len.p, sub_off, n);
         sub_bytes.ensure(nbytes + 1);
-        launch(KC_DEEP, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)sub_map.p, d_off, (const uint64_t*)sub_off.p, d_bytes, sub_bytes.p);
+        launch(KC_MERGE, k_sub_bytes, n, (uint64_t)n, (const uint32_t*)sub_map.p, d_off, (const uint64_t*)sub_off.p, d_bytes, sub_bytes.p);
         sub_res.ensure(n);
         zero(sub_res.p, (size_t)n * sizeof(Res));
         if (ordered) levels(sub_bytes.p, sub_off.p, n, false, sub_res.p, abase, ovf_orig.p);
         else levels2(sub_bytes.p, sub_off.p, n, false, sub_res.p, abase, ovf_orig.p);
-        launch(KC_DEEP, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const Res*)sub_res.p, r);
+        launch(KC_MERGE, k_sub_scatter, n, (uint64_t)n, (const uint32_t*)sub_map.p, (const Res*)sub_res.p, r);
     }
 
     // The batch as separate trie subtrees: patterns grouped by their last k characters
@@ -2006,7 +2008,9 @@ struct Engine {
         st = edsbwt_stats{};
         guessed_len = false;
         prof = (flags & (EDSBWT_PROFILE | EDSBWT_PROFILE_LIGHT)) != 0;
-        prof_mask = (flags & EDSBWT_PROFILE) ? ~0u : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_LOCATE) | (1u << KC_LINKSORT));
+        prof_mask = (flags & EDSBWT_PROFILE) ? ~0u
+                                             : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_DEEPQ) | (1u << KC_DEEPW) | (1u << KC_LOCATE) |
+                                                (1u << KC_LINKSORT));
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
         const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
         count_only = !locate;
@@ -2158,13 +2162,15 @@ struct Engine {
         (void)P;
         {
             const std::vector<uint64_t> sv = fold_pinned_stats();
-            st.intervals_stepped += sv[ST_DEEP_STEPS];
+            st.intervals_stepped += sv[ST_DEEP_STEPS] + sv[ST_DEEPQ_STEPS];
             st.link_hash_rows += sv[ST_DEEP_HASH];
             // the 64-B lines the deep kernels gather (occ blocks or the 16-B rank entries' lines; a
             // narrow interval's two ends in one block count once) and the '#'-row reads; + P * 24
-            // record bytes above
-            st.bytes_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS] * 64 + sv[ST_DEEP_HASH] * 4;
+            // record bytes above (k_deep_fast).  k_deep_wide's lines are not counted.
+            st.bytes_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS] * 64;
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
+            st.bytes_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS] * 64 + sv[ST_DEEP_HASH] * 4;
+            st.lines_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];
             st.text_chars = sv[ST_TEXT_CHARS];

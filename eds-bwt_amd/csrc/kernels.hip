@@ -290,7 +290,8 @@ constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards 
 enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5,
                   ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10,
                   ST_DEEP_PAIR_LINES = 11,  // of ST_DEEP_BLOCKS, the rank-entry lines
-                  ST_TEXT_CHARS = 12, ST_TEXT_ROWS = 13 };  // characters decided / single rows met by the text compare
+                  ST_TEXT_CHARS = 12, ST_TEXT_ROWS = 13,  // characters decided / single rows met by the text compare
+                  ST_DEEPQ_STEPS = 14, ST_DEEPQ_BLOCKS = 15 };  // k_deep's own (ST_DEEP_*: k_deep_fast's)
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -1578,9 +1579,9 @@ __global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const
         put_res(res, o, at, cn, occ);
     }
     __shared__ unsigned long long sh[4];
-    stat_add(ctr, ST_DEEP_STEPS, n_steps, sh);
+    stat_add(ctr, ST_DEEPQ_STEPS, n_steps, sh);
     stat_add(ctr, ST_DEEP_HASH, n_hash, sh);
-    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, sh);
+    stat_add(ctr, ST_DEEPQ_BLOCKS, n_blk, sh);
     stat_add(ctr, ST_TEXT_CHARS, n_text, sh);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, sh);
 #ifdef EDSBWT_DEEP_CLOCKS

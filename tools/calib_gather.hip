@@ -3,7 +3,10 @@
 //
 //   calib_gather [table_MB ...]          prints one JSON line per (shape, table size)
 //
-// Shapes: "gather64"   — one random 64-B block per lane (4 × 16-B loads, the rank query);
+// Shapes: "gather16"   — one random 16-B load per lane and iteration (a rank entry, rent1/rent2:
+//                        the deep kernels' load; FETCH_SIZE / TCC_EA0_RDREQ_DRAM_32B per load
+//                        under --pmc calibrate the counters for this shape);
+//         "gather64"   — one random 64-B block per lane (4 × 16-B loads, the rank query);
 //         "gather128"  — one random 128-B line per lane (8 × 16-B loads);
 //         "stream16"   — coalesced 16-B-per-lane streaming read of the whole table (the
 //                        shape MI355X_MICROARCH.md calibrates FETCH_SIZE on);
@@ -158,7 +161,7 @@ int main(int argc, char** argv) {
         uint4* t;
         CK(hipMalloc(&t, bytes));
         CK(hipMemset(t, 1, bytes));
-        for (int shape = 0; shape < 4; shape++) {
+        for (int shape = 0; shape < 5; shape++) {
             float best = 1e30f;
             double alg = 0;
             for (int rep = 0; rep < 5; rep++) {
@@ -172,6 +175,9 @@ int main(int argc, char** argv) {
                 } else if (shape == 2) {
                     hipLaunchKernelGGL(k_stream, dim3(grid), dim3(block), 0, 0, t, bytes / 16, sink);
                     alg = (double)bytes;
+                } else if (shape == 4) {
+                    hipLaunchKernelGGL(k_gather<1>, dim3(grid), dim3(block), 0, 0, t, (uint32_t)(bytes / 16), iters, 17u + rep, sink);
+                    alg = (double)grid * block * iters * 16;
                 } else {
                     hipLaunchKernelGGL(k_stream4, dim3(grid), dim3(block), 0, 0, reinterpret_cast<const uint32_t*>(t), bytes / 4, sink);
                     alg = (double)bytes;
@@ -183,9 +189,10 @@ int main(int argc, char** argv) {
                 CK(hipEventElapsedTime(&ms, a, b));
                 if (rep > 0 && ms < best) best = ms;
             }
-            const char* nm = shape == 0 ? "gather64" : shape == 1 ? "gather128" : shape == 2 ? "stream16" : "stream4";
-            std::printf("{\"shape\": \"%s\", \"table_MB\": %zu, \"bytes_per_launch\": %.0f, \"best_ms\": %.4f, \"GBps\": %.1f}\n", nm, mb, alg,
-                        best, alg / best / 1e6);
+            const char* nm = shape == 0 ? "gather64" : shape == 1 ? "gather128" : shape == 2 ? "stream16" : shape == 3 ? "stream4" : "gather16";
+            std::printf("{\"shape\": \"%s\", \"table_MB\": %zu, \"bytes_per_launch\": %.0f, \"best_ms\": %.4f, \"GBps\": %.1f, "
+                        "\"accesses_per_launch\": %.0f, \"launches\": 5}\n", nm, mb, alg, best, alg / best / 1e6,
+                        shape == 0 ? alg / 64 : shape == 1 ? alg / 128 : shape == 4 ? alg / 16 : alg / (shape == 2 ? 16 : 4));
             std::fflush(stdout);
         }
         CK(hipFree(t));

@@ -23,12 +23,13 @@ import json
 import os
 
 # bench.py kernel class -> kernels (engine.hip KClass)
+# (round 3: the deep stage's three kernels are classes of their own, KC_DEEP / KC_DEEPQ /
+# KC_DEEPW, so each has its own rocprof average and PMC bytes per launch)
 CLASSES = {
-    "step": ("k_lvl_items", "k_lvl_dollar"),
-    # every kernel the engine launches under KC_DEEP (engine.hip), so the rocprof
-    # average per launch is comparable with bench.py's event-timed class average
-    "deep": ("k_deep_fast", "k_deep", "k_deep_wide", "k_list_flagged", "k_ovf_lens",
-             "k_group_end", "k_group_count", "k_group_scatter", "k_sub_build", "k_sub_bytes", "k_sub_scatter"),
+    "step": ("k_lvl_items", "k_lvl_dollar", "k_lvl_chunks"),
+    "deep": ("k_deep_fast",),
+    "deep_list": ("k_deep",),
+    "deep_wide": ("k_deep_wide",),
     "locate": ("k_locate", "k_locate_pp", "k_locate_big"),
 }
 FETCH_FACTOR_GATHER64 = 1.0
@@ -106,7 +107,8 @@ def main():
              "kernels": {k: {**per[k], **pmc.get(k, {}), **res.get(k, {})} for k in sorted(per, key=lambda k: -per[k]["total_ms"])}}
     json.dump(out_d, open(a.out, "w"), indent=1)
     if a.traffic:
-        json.dump({"source": a.source, "fetch_factor": FETCH_FACTOR_GATHER64, "classes": classes}, open(a.traffic, "w"), indent=1)
+        json.dump({"source": a.source, "classes_version": "r3", "fetch_factor": FETCH_FACTOR_GATHER64, "classes": classes},
+                  open(a.traffic, "w"), indent=1)
     print(json.dumps(classes, indent=1))
 
 
