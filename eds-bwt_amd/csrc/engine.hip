@@ -324,6 +324,7 @@ struct Engine {
     DBuf<unsigned long long> stats;  // kStatSlots sharded statistics counters (stat_add)
     unsigned long long* pinned_stats = nullptr;
     // sum of the kStatShards shards of each statistic, from pinned_stats (already copied)
+    uint64_t trace_single = 0, trace_lines = 0;  // EDSBWT_TRACE: stats at the previous depth's print
     std::vector<uint64_t> fold_pinned_stats() const {
         std::vector<uint64_t> v(kStatStride, 0);
         for (uint32_t s = 0; s < kStatShards; s++)
@@ -1840,8 +1841,17 @@ struct Engine {
             // two 64-B lines per interval step, plus the item streams
             // (the lines actually read are counted by the kernels: lines_kernel)
             st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * sizeof(OccBlock)) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
-            if (trace) std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u, link keys %u, link ranges %u, next items %u\n", D, M,
-                                    ncur, nkeys, nkeys ? hsh[NSHARD * 32] : 0u, nnext);
+            if (trace) {
+                // single-row items and lines read by this depth's step (stats so far, less the last depth's)
+                small_copy(pinned_stats, stats.p, kStatSlots * 8);
+                HIPCHK(hipStreamSynchronize(stream));
+                const std::vector<uint64_t> sv = fold_pinned_stats();
+                std::fprintf(stderr, "[edsbwt] depth %u: nodes %u, items %u (single-row %llu), link keys %u, link ranges %u, next items %u, "
+                                     "step lines %llu\n", D, M, ncur, (unsigned long long)(sv[ST_LVL_SINGLE] - trace_single),
+                             nkeys, nkeys ? hsh[NSHARD * 32] : 0u, nnext, (unsigned long long)(sv[ST_STEP_BLOCKS] - trace_lines));
+                trace_single = sv[ST_LVL_SINGLE];
+                trace_lines = sv[ST_STEP_BLOCKS];
+            }
             // hand the item shards to the next depth as they are (k_lvl_items reads them in
             // place); they are packed only for the finishers below or the deep cutover
             {
@@ -2006,6 +2016,7 @@ struct Engine {
     uint64_t search(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, uint32_t first_id, uint32_t flags, uint32_t* d_counts) {
         t_search0 = std::chrono::steady_clock::now();
         st = edsbwt_stats{};
+        trace_single = trace_lines = 0;
         guessed_len = false;
         prof = (flags & (EDSBWT_PROFILE | EDSBWT_PROFILE_LIGHT)) != 0;
         prof_mask = (flags & EDSBWT_PROFILE) ? ~0u
@@ -2078,6 +2089,7 @@ struct Engine {
                     discard_attempt();
                     defer_call = defer = false;
                     st = edsbwt_stats{};
+                    trace_single = trace_lines = 0;
                     st.patterns = P;
                     zero(res.p, P * sizeof(Res));
                     zero(stats.p, kStatSlots * 8);

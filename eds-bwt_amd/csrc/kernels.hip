@@ -285,13 +285,14 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long x, un
 // statistics counters: block-reduced, then one atomic per block into one of kStatShards
 // 128-B lines (the host folds the shards), so no address takes every block's add.
 // Every thread of the block must call it.
-constexpr uint32_t kStatShards = 32, kStatStride = 16, kStatSlots = kStatShards * kStatStride;
+constexpr uint32_t kStatShards = 32, kStatStride = 32, kStatSlots = kStatShards * kStatStride;
 // statistic slots (zeroed once per search, folded at its end)
 enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP_BLOCKS = 3, ST_DEEP_BLOCKS = 4, ST_LOC_OFFSETS = 5,
                   ST_CLK_RANK = 6, ST_CLK_RUNS = 7, ST_CLK_REST = 8, ST_CLK_STEPS = 9, ST_CLK_HASH_STEPS = 10,
                   ST_DEEP_PAIR_LINES = 11,  // of ST_DEEP_BLOCKS, the rank-entry lines
                   ST_TEXT_CHARS = 12, ST_TEXT_ROWS = 13,  // characters decided / single rows met by the text compare
-                  ST_DEEPQ_STEPS = 14, ST_DEEPQ_BLOCKS = 15 };  // k_deep's own (ST_DEEP_*: k_deep_fast's)
+                  ST_DEEPQ_STEPS = 14, ST_DEEPQ_BLOCKS = 15,  // k_deep's own (ST_DEEP_*: k_deep_fast's)
+                  ST_LVL_SINGLE = 16 };  // k_lvl_items input items of one row (b == e)
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -1820,7 +1821,7 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
         __syncthreads();
     }
     const uint32_t sh = blockIdx.x % NSHARD;
-    unsigned long long n_blk = 0;  // occ blocks read
+    unsigned long long n_blk = 0, n_single = 0;  // occ blocks read, single-row items
     uint32_t* cnt = cnt_all + sh * 32;
     nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
     keys += (size_t)sh * cap_keys;
@@ -1841,7 +1842,9 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
                 src = (size_t)lo * icap + ((uint32_t)i - spre[lo]);
             }
             u = iu[src];
-            LVL_STEP_LOAD(u, ib[src], ie[src] + 1)
+            const uint32_t b0 = ib[src], e0 = ie[src];
+            n_single += b0 == e0;
+            LVL_STEP_LOAD(u, b0, e0 + 1)
         }
         // backward step of every child symbol (updateSingleInterval, :424-510)
         uint32_t emit = 0;
@@ -1895,6 +1898,7 @@ __global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* _
     }
     __shared__ unsigned long long ssum[4];
     stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
+    stat_add(stats, ST_LVL_SINGLE, n_single, ssum);
 }
 
 // long '#'-row ranges: one wave per chunk (<= 256 rows, clipped to the item's end);
