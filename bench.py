@@ -70,7 +70,10 @@ def traffic_from_profile(cfg: str, kernel: str):
         if t.get("classes_version") != "r3":  # round-3 classes: deep = k_deep_fast alone
             return None, None
         c = t["classes"][kernel]
-        return int(c["pmc_hbm_bytes_per_launch"]), f"profiles/traffic_{cfg}.json ({t.get('source', '')})"
+        # calibrated DRAM bytes (TCC_EA0_RDREQ_DRAM_32B x 32 + WRITE_SIZE; profiles/r03_calib_counters.json)
+        # when the TCC pass was taken, else FETCH_SIZE + WRITE_SIZE
+        f = t.get("traffic_field", "pmc_hbm_bytes_per_launch")
+        return int(c[f]), f"profiles/traffic_{cfg}.json: {f} ({t.get('source', '')})"
     except (OSError, KeyError, ValueError):
         return None, None
 
@@ -453,6 +456,7 @@ def main():
                 rate = lpl / (avg_ms * 1e-3)
                 traffic, tsrc = traffic_from_profile(w.name, name)
                 return {"kernels": KERNELS_OF_CLASS.get(name, name), "ms_per_step": round(d["ms"] / args.steps, 4),
+                        "traffic_frac": round(traffic / (avg_ms * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4) if traffic else None,
                         "launches_per_step": round(d["launches"] / args.steps, 2), "avg_launch_ms": round(avg_ms, 4),
                         "bytes_per_launch": int(bpl), "lines_per_launch": int(lpl),
                         "achieved": round(ach, 1), "frac": round(ach / MI355X_HBM_PEAK_GBS, 4) if bpl else None,
@@ -468,6 +472,10 @@ def main():
             out["roofline"] = {
                 "bound": "hbm", "kernel": dom, "kernels": dk["kernels"], "achieved": dk["achieved"], "peak": MI355X_HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": dk["frac"], "traffic": dk["traffic"], "traffic_source": dk["traffic_source"],
+                "traffic_frac": dk["traffic_frac"],
+                "traffic_note": ("DRAM bytes per launch from the PMC (calibrated: a random 16-B load moves one 128-B line, "
+                                 "profiles/r03_calib_counters.json), over this line's event-timed launch; the line model counts "
+                                 "64 B per line, so traffic ~ 2x bytes_per_launch is the DRAM line size, not re-reads"),
                 "avg_launch_ms": dk["avg_launch_ms"], "launches": kstats[dom]["launches"],
                 "bytes_model": "line model: the 64-B lines the kernel gathers as it counts them (a narrow interval's two ends in "
                                "one line count once; one 16-B two-step rank entry per end; the single-row text compare's sample, "

@@ -2122,6 +2122,7 @@ struct Engine {
             return m;
         }
         // ---- D. counts (backwardSearch's return value) and locate; one read-back for the sizes
+        last_locate_pp = false;
         zero(counters.p + 1, 8);
         zero(counters.p + 12, 16);
         if (locate) occ64.ensure(P);
@@ -2170,8 +2171,8 @@ struct Engine {
     }
 
     // the end of search(): device statistics (already copied to pinned_stats), timings
+    bool last_locate_pp = false;  // finish_deferred took the per-pattern locate (bytes model in finish_stats)
     uint64_t finish_stats(uint64_t P, bool locate, bool use_table, int loc_mode, uint64_t OCC, hipEvent_t e0, hipEvent_t e1) {
-        (void)P;
         {
             const std::vector<uint64_t> sv = fold_pinned_stats();
             st.intervals_stepped += sv[ST_DEEP_STEPS] + sv[ST_DEEPQ_STEPS];
@@ -2194,9 +2195,14 @@ struct Engine {
                              (double)sv[ST_CLK_RANK] / sv[ST_CLK_STEPS], (double)sv[ST_CLK_RUNS] / sv[ST_CLK_STEPS],
                              (double)sv[ST_CLK_REST] / sv[ST_CLK_STEPS]);
             // one line per walk position, plus the sample read
-            if (locate && !use_table) st.lines_kernel[KC_LOCATE] += st.locate_lf_steps + OCC + (loc_mode == 2 ? OCC : 0);
+            if (locate && !use_table && !last_locate_pp) st.lines_kernel[KC_LOCATE] += st.locate_lf_steps + OCC + (loc_mode == 2 ? OCC : 0);
+            // per-pattern locate (k_locate_pp / k_locate_big): at most one sample line per record
+            // (none for a text-compare result), the 20-B record stores, the pattern's result and offset
+            if (locate && last_locate_pp) st.lines_kernel[KC_LOCATE] += OCC;
         }
-        if (locate && OCC) {
+        if (locate && OCC && last_locate_pp) {
+            st.bytes_kernel[KC_LOCATE] += OCC * (64 + sizeof(edsbwt_occ)) + P * (sizeof(Res) + 4);
+        } else if (locate && OCC) {
             st.bytes_kernel[KC_LOCATE] += st.locate_lf_steps * sizeof(OccBlock) + OCC * (sizeof(OccBlock) + 8 + 8 + 4 + 4 + 4 + sizeof(edsbwt_occ)) +
                                           (loc_mode != 0 ? OCC * 8 : 0);
         }
@@ -2245,6 +2251,7 @@ struct Engine {
         // dense samples: records straight from each pattern's result (k_locate_pp / k_locate_big),
         // no tasks (EDSBWT_LOCATE_TASKS=1: the task path as for every other search)
         const bool per_pattern = locate && loc_mode == 2 && X.samp_dense && locate_pp;
+        last_locate_pp = per_pattern;
         if (locate && !per_pattern) occ64.ensure(P);
         launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                       locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);

@@ -13,6 +13,13 @@
   shape of every rank query, which dominates the step / deep / locate classes — and
   2.0 for 16-B-per-lane streaming reads (the guide's gfx950 correction).  The classes
   below use the gather factor; WRITE_SIZE × 1024 as is.
+* --tcc <dir>: a third PMC pass of TCC_EA0_RDREQ_sum, TCC_BUBBLE_sum, TCC_EA0_RDREQ_32B_sum and
+  TCC_EA0_RDREQ_DRAM_32B_sum.  Round 3 calibration on MI355X (tools/calib_gather.hip, 4 GB table,
+  profiles/r03_calib_counters.json): TCC_EA0_RDREQ_DRAM_32B x 32 equals the bytes of a 16-B-per-lane
+  streaming read exactly (FETCH_SIZE shows half of them, as the guide says), and a random 16-, 64-
+  or 128-B access is ONE 128-B request (RDREQ = accesses, DRAM_32B = 4 per access) while
+  FETCH_SIZE tallies it at 64 B.  So DRAM read bytes = TCC_EA0_RDREQ_DRAM_32B x 32 for every
+  shape, and = 2 x FETCH_SIZE for the random gathers; with --tcc the classes' HBM traffic uses it.
 * --traffic writes the per-class HBM bytes per launch that bench.py reports as
   `roofline.traffic`.
 """
@@ -49,6 +56,7 @@ def main():
     ap.add_argument("bench_json")
     ap.add_argument("out")
     ap.add_argument("--traffic")
+    ap.add_argument("--tcc")
     ap.add_argument("--source", default="")
     a = ap.parse_args()
 
@@ -74,6 +82,12 @@ def main():
             pmc[k][key] += FETCH_FACTOR_GATHER64 * v if key == "fetch_bytes" else v
             if key == "fetch_bytes":
                 pmc[k]["dispatches"] += 1
+    tcc = collections.defaultdict(lambda: collections.defaultdict(float))
+    if a.tcc:
+        for r in csv.DictReader(open(first_csv(a.tcc, "counter_collection.csv"))):
+            tcc[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+            if r["Counter_Name"] == "TCC_EA0_RDREQ_sum":
+                tcc[short(r["Kernel_Name"])]["dispatches"] += 1
     # registers, LDS and the occupancy they allow, per kernel (kernel trace columns).  gfx950:
     # 512 VGPRs per lane per SIMD shared by the arch and accumulation registers (granule 8),
     # at most 8 waves per SIMD, 160 KB of LDS per CU (4 SIMDs)
@@ -101,14 +115,21 @@ def main():
         classes[c] = {"rocprof_calls": calls, "rocprof_avg_launch_ms": tot / max(1, calls),
                       "pmc_hbm_bytes_per_launch": (fb + wb) / max(1, disp),
                       "pmc_fetch_bytes_per_launch": fb / max(1, disp), "pmc_write_bytes_per_launch": wb / max(1, disp)}
+        if a.tcc:
+            td = sum(tcc[k]["dispatches"] for k in ks if k in tcc)
+            dram = 32.0 * sum(tcc[k]["TCC_EA0_RDREQ_DRAM_32B_sum"] for k in ks if k in tcc)
+            req = sum(tcc[k]["TCC_EA0_RDREQ_sum"] for k in ks if k in tcc)
+            classes[c].update({"pmc_dram_read_bytes_per_launch": dram / max(1, td), "pmc_read_requests_per_launch": req / max(1, td),
+                               "pmc_dram_bytes_per_launch": dram / max(1, td) + wb / max(1, disp)})
     out_d = {"bench": {k: bench.get(k) for k in ("value", "ms_per_step", "roofline", "kernel_ms_per_step")},
              "fetch_factor": FETCH_FACTOR_GATHER64,
              "classes": classes,
              "kernels": {k: {**per[k], **pmc.get(k, {}), **res.get(k, {})} for k in sorted(per, key=lambda k: -per[k]["total_ms"])}}
     json.dump(out_d, open(a.out, "w"), indent=1)
     if a.traffic:
-        json.dump({"source": a.source, "classes_version": "r3", "fetch_factor": FETCH_FACTOR_GATHER64, "classes": classes},
-                  open(a.traffic, "w"), indent=1)
+        json.dump({"source": a.source, "classes_version": "r3", "fetch_factor": FETCH_FACTOR_GATHER64,
+                   "traffic_field": "pmc_dram_bytes_per_launch" if a.tcc else "pmc_hbm_bytes_per_launch",
+                   "classes": classes}, open(a.traffic, "w"), indent=1)
     print(json.dumps(classes, indent=1))
 
 
