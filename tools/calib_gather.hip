@@ -17,6 +17,8 @@
 //                        previous step's values; W = waves per SIMD the launch is held to
 //                        (dynamic LDS), so the ceiling is measured at a kernel's occupancy.
 //   calib_gather --chain [table_MB ...]   runs only the chain shapes
+//   calib_gather --window [table_MB ...]  one 16-B load per random 64-B block within a window that
+//                        slides over the table (row-bucketed items): accesses/s per window size
 // Algorithmic bytes are known exactly, so running this under
 // `rocprofv3 --pmc FETCH_SIZE` gives the FETCH_SIZE → bytes factor for each shape, and the
 // timed rate is the practical ceiling of the rank-block gathers (vs HBM peak 8 TB/s).
@@ -86,6 +88,23 @@ __global__ void __launch_bounds__(256) k_chain(const uint4* __restrict__ t, uint
     if (acc == 0x12345678u) { sink[g] = acc; hold[threadIdx.x] = acc; }
 }
 
+// bucketed gathers: access i (grid-stride order, so the lanes in flight hold neighbouring i)
+// reads one random 64-B block (one 16-B load of it: the rank query's first half) within a
+// window of `wblk` blocks that slides over the table as i grows — items partitioned by row
+// bucket and stepped bucket after bucket.  wblk = nblk: fully random.
+__global__ void __launch_bounds__(256) k_gather_win(const uint4* __restrict__ t, uint32_t nblk, uint64_t n, uint32_t wblk, uint32_t seed,
+                                                    uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    const uint32_t nwin = nblk / wblk;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t w = (uint32_t)(i * nwin / n);
+        const uint32_t h = mix((uint32_t)i ^ seed);
+        const uint4 v = t[((size_t)w * wblk + h % wblk) * 4];
+        acc ^= v.x + v.w;
+    }
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
 __global__ void __launch_bounds__(256) k_stream4(const uint32_t* __restrict__ t, size_t n4, uint32_t* __restrict__ sink) {
     uint32_t acc = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) acc ^= t[i];
@@ -140,12 +159,49 @@ static void chains(const std::vector<size_t>& mbs, uint32_t* sink, hipEvent_t a,
     }
 }
 
+static void windows(size_t mb, uint32_t* sink, hipEvent_t a, hipEvent_t b) {
+    const size_t bytes = mb << 20;
+    uint4* t;
+    CK(hipMalloc(&t, bytes));
+    CK(hipMemset(t, 5, bytes));
+    const uint32_t nblk = (uint32_t)(bytes / 64);
+    const uint64_t n = 1ull << 30;  // accesses per launch
+    for (size_t wkb : {(size_t)256, (size_t)512, (size_t)1024, (size_t)2048, (size_t)4096, (size_t)8192, (size_t)16384, (size_t)65536,
+                       (size_t)262144, (size_t)0}) {
+        const uint32_t wblk = wkb ? (uint32_t)std::min<size_t>(nblk, wkb * 1024 / 64) : nblk;
+        float best = 1e30f;
+        for (int rep = 0; rep < 4; rep++) {
+            CK(hipEventRecord(a));
+            hipLaunchKernelGGL(k_gather_win, dim3(256 * 64), dim3(256), 0, 0, t, nblk, n, wblk, 11u + rep, sink);
+            CK(hipGetLastError());
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            if (rep > 0 && ms < best) best = ms;
+        }
+        std::printf("{\"shape\": \"gather_window\", \"table_MB\": %zu, \"window_KB\": %zu, \"accesses\": %llu, \"best_ms\": %.4f, "
+                    "\"accesses_per_s\": %.4g}\n", mb, (size_t)wblk * 64 / 1024, (unsigned long long)n, best, n / (best * 1e-3));
+        std::fflush(stdout);
+    }
+    CK(hipFree(t));
+}
+
 int main(int argc, char** argv) {
     std::vector<size_t> mbs;
-    bool chain_only = false;
+    bool chain_only = false, window_only = false;
     for (int i = 1; i < argc; i++) {
         if (std::string(argv[i]) == "--chain") chain_only = true;
-        else mbs.push_back(std::strtoull(argv[i], nullptr, 10));
+        else if (std::string(argv[i]) == "--window") window_only = true;
+        else {
+            char* end = nullptr;
+            const unsigned long long v = std::strtoull(argv[i], &end, 10);
+            if (!end || *end || v < 16) {  // a table under 16 MB (or not a number) is refused, not launched
+                std::fprintf(stderr, "calib_gather: bad table size '%s' (MB, >= 16)\n", argv[i]);
+                return 2;
+            }
+            mbs.push_back(v);
+        }
     }
     if (mbs.empty()) mbs = {16, 100, 200, 1024, 4096};
     uint32_t* sink;
@@ -154,6 +210,10 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    if (window_only) {
+        for (size_t mb : mbs) windows(mb, sink, a, b);
+        return 0;
+    }
     chains(mbs, sink, a, b);
     if (chain_only) return 0;
     for (size_t mb : mbs) {
