@@ -2664,20 +2664,25 @@ struct Engine {
             sizes = {len};
         } else {
             const bool ramp = env_double("EDSBWT_CHUNK_RAMP", 1) != 0;
-            const uint64_t steps[3] = {std::max<uint64_t>(1, target / 8), std::max<uint64_t>(1, target / 4), std::max<uint64_t>(1, target / 2)};
-            const uint64_t rsum = steps[0] + steps[1] + steps[2];
+            // ramp chunks target/2^R .. target/2 (R = EDSBWT_RAMP_STEPS, default 3): the first
+            // chunk's search ends early, so the downloads (the call's bound) start early
+            const int R = (int)std::max(1.0, std::min(8.0, env_double("EDSBWT_RAMP_STEPS", 3)));
+            std::vector<uint64_t> steps;
+            for (int i = R; i >= 1; i--) steps.push_back(std::max<uint64_t>(1, target >> i));
+            uint64_t rsum = 0;
+            for (uint64_t x : steps) rsum += x;
             if (ramp && len > 2 * rsum) {
                 // ramp up, uniform middle chunks of at most `target`, ramp down: the last
                 // chunk's search and download (the drain) stay short
                 const uint64_t mid = len - 2 * rsum, nm = (mid + target - 1) / target;
-                sizes = {steps[0], steps[1], steps[2]};
+                sizes = steps;
                 for (uint64_t q = 0; q < nm; q++) sizes.push_back(mid * (q + 1) / nm - mid * q / nm);
-                sizes.insert(sizes.end(), {steps[2], steps[1], steps[0]});
+                sizes.insert(sizes.end(), steps.rbegin(), steps.rend());
             } else {
                 std::vector<uint64_t> front, back;
                 uint64_t covered = 0;
                 for (int i = 0; covered < len; i++) {
-                    const uint64_t a = std::max<uint64_t>(1, ramp && i < 3 ? steps[i] : target);
+                    const uint64_t a = std::max<uint64_t>(1, ramp && i < (int)steps.size() ? steps[i] : target);
                     front.push_back(a);
                     covered += a;
                     if (covered >= len) break;
