@@ -241,6 +241,8 @@ struct Engine {
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
     DBuf<uint4> rent1, rent2, rent3;
+    DBuf<uint4> rk16, rk16sup;  // all-symbol rank entries (sigma <= 5; kernels.h): the level step's ranks
+    bool use_rk16 = env_double("EDSBWT_NO_RANK16", 0) == 0;
     DBuf<uint32_t> pc3;
     uint32_t r2stride = 0, r3stride = 0;
     bool use_triples = env_double("EDSBWT_NO_TRIPLES", 0) == 0;
@@ -488,6 +490,8 @@ struct Engine {
         X.wrow = wrow.p;
         X.text_deep = text_deep ? 1u : 0u;
         X.kt1_pos = kt1_pos ? 1u : 0u;
+        X.rk16 = use_rk16 ? rk16.p : nullptr;
+        X.rk16sup = use_rk16 ? rk16sup.p : nullptr;
         return X;
     }
 
@@ -889,6 +893,15 @@ struct Engine {
         if (sigma > 5 || sigma < 2) {
             HIPCHK(hipStreamSynchronize(stream));
             return;
+        }
+        {
+            // all-symbol rank entries: 16 B per 16 rows + 16 B per 65536 rows
+            const uint64_t n16 = (uint64_t)N / 16 + 1, nsup = (uint64_t)N / 65536 + 1;
+            rk16.ensure(n16);
+            rk16sup.ensure(nsup);
+            launch(KC_TABLE, k_rk16, n16, n16, X, rk16.p);
+            launch(KC_TABLE, k_rk16_sup, nsup, nsup, X, rk16sup.p);
+            device_bytes += (n16 + nsup) * 16;
         }
         const uint32_t nc = 1 + (sigma - 1) * sigma;
         const uint64_t nblk = (uint64_t)N / 64 + 1, nrows = nblk * 64;

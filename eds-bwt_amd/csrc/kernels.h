@@ -96,6 +96,16 @@ struct KIdx {
     uint32_t text_deep;        // k_deep compares single rows too (EDSBWT_TEXT_DEEP, A/B)
     uint32_t kt1_pos;          // the direct start's inline D-mer entries of ONE row hold that row's
                                // text position too (k_ktab_one): bit 62 set, gpos in bits [31, 62)
+    // All-symbol rank entries (sigma <= 5; nullptr: not built or not used): the rank of every
+    // symbol at a row from ONE 16-B load (the 64-B occ block takes four: the level step's
+    // gathers are bound by load requests).
+    //   rk16[k]    = {cnt_1 | cnt_2 << 16, cnt_3 | cnt_4 << 16, plane_0 | plane_1 << 16, plane_2}
+    //                cnt_c: rows of symbol c in [65536 * (k >> 12), 16 k); planes: the 3 code bits
+    //                of rows 16k .. 16k+15 (bit j = row 16k + j)
+    //   rk16sup[s] = {rank_1 .. rank_4 at row 65536 s}
+    // rank_'#'(x) = x - (rank_1 + rank_2 + rank_3 + rank_4).
+    const uint4* rk16;
+    const uint4* rk16sup;
 };
 
 }  // namespace edsbwt

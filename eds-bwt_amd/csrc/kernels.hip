@@ -215,6 +215,35 @@ __device__ __forceinline__ uint32_t rank2_pair(const OccBlock* __restrict__ occ,
 }
 #endif
 
+// every symbol's rank at x from the all-symbol rank entries (kernels.h rk16; sigma <= 5)
+__device__ __forceinline__ void rk16_rank_v(uint4 v, uint4 s, uint32_t x, uint32_t* out) {
+    const uint32_t m = (1u << (x & 15u)) - 1u;
+    const uint32_t p0 = v.z & 0xFFFFu, p1 = v.z >> 16, p2 = v.w & 0xFFFFu;
+    const uint32_t r1 = s.x + (v.x & 0xFFFFu) + (uint32_t)__popc(p0 & ~p1 & ~p2 & m);
+    const uint32_t r2 = s.y + (v.x >> 16) + (uint32_t)__popc(~p0 & p1 & ~p2 & m);
+    const uint32_t r3 = s.z + (v.y & 0xFFFFu) + (uint32_t)__popc(p0 & p1 & ~p2 & m);
+    const uint32_t r4 = s.w + (v.y >> 16) + (uint32_t)__popc(~p0 & ~p1 & p2 & m);
+    out[0] = x - (r1 + r2 + r3 + r4);
+    out[1] = r1; out[2] = r2; out[3] = r3; out[4] = r4;
+    out[5] = out[6] = out[7] = 0u;
+}
+// ranks of every symbol at both interval ends x0 <= x1: one 16-B entry per end (one when both
+// fall in the same 16 rows), else the 64-B occ blocks.  Returns 1 when one load served both.
+__device__ __forceinline__ uint32_t rank_all_pair_any(const KIdx& X, uint32_t x0, uint32_t x1, uint32_t* o0, uint32_t* o1) {
+    if (X.rk16) {
+        const bool same = (x0 >> 4) == (x1 >> 4);
+        const uint4 v0 = X.rk16[x0 >> 4], s0 = X.rk16sup[x0 >> 16];
+        rk16_rank_v(v0, s0, x0, o0);
+        if (same) {
+            rk16_rank_v(v0, s0, x1, o1);
+        } else {
+            rk16_rank_v(X.rk16[x1 >> 4], X.rk16sup[x1 >> 16], x1, o1);
+        }
+        return same;
+    }
+    return rank_all_pair(X.occ, x0, x1, X.sigma, o0, o1);
+}
+
 // one 16-B rank entry (kernels.h): rank of its code and of its '#' (or '#'-or-(c1,'#')) rows at x
 __device__ __forceinline__ void rent_rank(uint4 v, uint32_t x, uint32_t& r, uint32_t& h) {
     const uint32_t m = (1u << (x & 31u)) - 1u;
@@ -865,7 +894,7 @@ __global__ void __launch_bounds__(256) k_expand(const uint32_t* __restrict__ ib,
                                                 uint32_t* __restrict__ ocb, uint32_t* __restrict__ oce) {
     GRID_STRIDE(j, n) {
         uint32_t rb[8], re[8];
-        rank_all_pair(X.occ, ib[j], ie[j] + 1, X.sigma, rb, re);
+        rank_all_pair_any(X, ib[j], ie[j] + 1, rb, re);
         uint4* pb = reinterpret_cast<uint4*>(ocb + j * 8);
         uint4* pe = reinterpret_cast<uint4*>(oce + j * 8);
         pb[0] = make_uint4(rb[0], rb[1], rb[2], rb[3]);
@@ -1785,7 +1814,7 @@ __global__ void k_child_info(uint32_t M, const uint32_t* __restrict__ node_paren
 #define LVL_STEP_LOAD(u, b, e1)                                                         \
     {                                                                                   \
         const uint64_t ci = child_info[u];                                              \
-        n_blk += 2 - rank_all_pair(X.occ, b, e1, X.sigma, rb, re);                     \
+        n_blk += 2 - rank_all_pair_any(X, b, e1, rb, re);                               \
         cf = (uint32_t)ci;                                                              \
         mask = (uint32_t)(ci >> 32);                                                    \
     }
@@ -2688,6 +2717,32 @@ __global__ void k_rent3(uint64_t nb32, uint64_t nblk, const uint8_t* __restrict_
 // (position 0): rows visited get DA = w and their distance from the word end.
 // segment link table (index open): for s >= 2 the c-ranks at both ends of the words of
 // segments [seg_lo[s], s-1] (the range link() adds for a word of s, :533-561, :620)
+// all-symbol rank entries (kernels.h rk16), from the 64-row occ blocks: entry k = rows 16k..16k+15
+// of block k >> 2; its counts relative to the superblock start (block (k >> 12) << 10)
+__device__ __forceinline__ uint64_t occ_match(const OccV& v, uint32_t c) {
+    return ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
+}
+__global__ void k_rk16(uint64_t n16, KIdx X, uint4* __restrict__ out) {
+    GRID_STRIDE(k, n16) {
+        const OccV v = load_block(X.occ, (uint32_t)(k >> 2));
+        const OccV s = load_block(X.occ, (uint32_t)((k >> 12) << 10));
+        const uint32_t sh = (uint32_t)(k & 3) * 16u;
+        const uint64_t below = sh ? (1ull << sh) - 1ull : 0ull;
+        uint32_t c[5];
+#pragma unroll
+        for (uint32_t q = 1; q <= 4; q++) c[q] = v.cnt[q] + (uint32_t)__popcll(occ_match(v, q) & below) - s.cnt[q];
+        out[k] = make_uint4(c[1] | (c[2] << 16), c[3] | (c[4] << 16),
+                            (uint32_t)((v.p0 >> sh) & 0xFFFFu) | ((uint32_t)((v.p1 >> sh) & 0xFFFFu) << 16),
+                            (uint32_t)((v.p2 >> sh) & 0xFFFFu));
+    }
+}
+__global__ void k_rk16_sup(uint64_t nsup, KIdx X, uint4* __restrict__ out) {
+    GRID_STRIDE(s, nsup) {
+        const OccV v = load_block(X.occ, (uint32_t)(s << 10));
+        out[s] = make_uint4(v.cnt[1], v.cnt[2], v.cnt[3], v.cnt[4]);
+    }
+}
+
 __global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
     GRID_STRIDE(s, (size_t)S + 2) {
         uint32_t* e = tab + s * X.seg_stride;

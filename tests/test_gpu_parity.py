@@ -888,3 +888,23 @@ def test_cli_console_transcript(oracle, tmp_path):
     assert m, r.stdout[-200:]
     assert m.group(1) == want_out
     assert r.stderr == want_err
+
+
+@pytest.mark.parametrize("alphabet", ["ACGT", "ACG", "AC"])
+def test_rank16_level_step_gpu(oracle, edsbwt, tmp_path, monkeypatch, alphabet):
+    """The level step's ranks from the all-symbol 16-B rank entries (rk16, sigma <= 5) against the
+    64-B occ blocks (EDSBWT_NO_RANK16=1) and the oracle: trie levels at every depth (deep=False),
+    the ordered path, and the k-mer start table built with each."""
+    rng = random.Random(1616 + len(alphabet))
+    segs = edsgen.random_eds(rng, 3000, alphabet=alphabet, lmax=9, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 40)) or alphabet * 3 for _ in range(2500)]
+    pats += ["".join(rng.choice(alphabet + "T") for _ in range(rng.randint(1, 30))) for _ in range(1500)]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    for off in ("0", "1"):
+        monkeypatch.setenv("EDSBWT_NO_RANK16", off)
+        with edsbwt.Index(base) as idx:
+            for kw in ({}, {"deep": False}, {"direct": False, "deep": False}, {"ordered": True, "deep": False}, {"ktab": False}):
+                gc, go = idx.search((buf, offs), **kw)
+                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (off, kw)
