@@ -259,6 +259,11 @@ def main():
         assert n == npat, (n, npat)
         return ptr, nocc
 
+    if world > 1 and args.gather == "counts" and args.dist_backend == "nccl":
+        # the engine leaves each call's u32 counts in d_counts_x too (a device-to-device copy per
+        # chunk): RCCL gathers them from HBM, no second upload of the counts
+        idx.set_counts_mirror(d_counts_x.data_ptr(), npat)
+
     def exchange(nocc):
         # the path's exchange step: every rank's (patterns, records) all-gathered — its offsets in
         # the output (each rank writes its slice); --gather counts also gathers the
@@ -268,8 +273,6 @@ def main():
         sizes = shard.exchange_sizes(npat, nocc, gdev)
         if args.gather == "counts":
             src = d_counts_x if args.dist_backend == "nccl" else torch.from_numpy(counts[:npat].view(np.int32))
-            if args.dist_backend == "nccl":
-                d_counts_x.copy_(torch.from_numpy(counts[:npat].view(np.int32)), non_blocking=True)
             shard.gather_counts(src, [int(x) for x in sizes[:, 0]])
 
     # ---- timed: end-to-end (host memory -> host memory)

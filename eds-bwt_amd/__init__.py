@@ -131,6 +131,8 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_host_free.restype = None
     L.edsbwt_occ_free.argtypes = [vp]
     L.edsbwt_occ_free.restype = None
+    L.edsbwt_set_counts_mirror.argtypes = [vp, vp, u64]
+    L.edsbwt_set_counts_mirror.restype = i32
     L.edsbwt_last_paths.argtypes = [vp, vp, u64]
     L.edsbwt_last_paths.restype = i32
     L.edsbwt_last_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
@@ -329,6 +331,11 @@ class Index:
         _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,
                                           ctypes.byref(occ_p), ctypes.byref(nocc), stream or None))
         return occ_p.value or 0, nocc.value
+
+    def set_counts_mirror(self, d_counts: int, cap: int) -> None:
+        """Host-pipeline calls also leave the u32 counts in device array d_counts[cap] (the
+        multi-GPU exchange gathers them over RCCL); 0 turns it off."""
+        _check(lib().edsbwt_set_counts_mirror(self._h, d_counts or None, int(cap) if d_counts else 0))
 
     def path_tags(self, n: int) -> np.ndarray:
         """PATH_* bits per pattern of the last search_device call (the process must run with

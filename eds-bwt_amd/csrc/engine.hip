@@ -241,6 +241,10 @@ struct Engine {
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
     DBuf<uint4> rent1, rent2, rent3;
+    // host-pipeline calls also leave every pattern's u32 count in this device array (the
+    // multi-GPU exchange gathers them over RCCL without copying them back up; nullptr: off)
+    uint32_t* counts_mirror = nullptr;
+    uint64_t counts_mirror_cap = 0;
     DBuf<uint4> rk16, rk16sup;  // all-symbol rank entries (sigma <= 5; kernels.h): the level step's ranks
     bool use_rk16 = env_double("EDSBWT_NO_RANK16", 0) == 0;
     DBuf<uint32_t> pc3;
@@ -3087,6 +3091,10 @@ struct Engine {
                 known_len = false;
                 c8_out = C8Out{};
                 std::swap(rec, hrec[sl]);
+                if (counts_mirror && P) {
+                    if (pats + P > counts_mirror_cap) throw Fail(EDSBWT_E_ARG, "device counts mirror smaller than the batch");
+                    HIPCHK(hipMemcpyAsync(counts_mirror + pats, hcounts[sl].p, P * 4, hipMemcpyDeviceToDevice, stream));
+                }
                 mark("searched", k);
                 accumulate(agg, st);
                 if (locate && n && total + n > arena_cap) {
@@ -3124,6 +3132,7 @@ struct Engine {
         td.join();
         if (tc.joinable()) tc.join();
         (void)hipStreamSynchronize(up);
+        if (counts_mirror) (void)hipStreamSynchronize(stream);  // the mirror is complete when the call returns
         if (err) {
             (void)hipStreamSynchronize(stream);  // no kernel may still touch the slots
             std::rethrow_exception(err);
@@ -3763,6 +3772,13 @@ void edsbwt_host_free(void* p) {
 const char* edsbwt_build_id(void) { return EDSBWT_BUILD_ID; }
 
 void edsbwt_occ_free(edsbwt_occ* occ) { edsbwt::occ_free_any(occ); }
+
+int edsbwt_set_counts_mirror(edsbwt_index* idx, uint32_t* d_counts, uint64_t cap) {
+    if (!idx) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    idx->eng->counts_mirror = cap ? d_counts : nullptr;
+    idx->eng->counts_mirror_cap = d_counts ? cap : 0;
+    return 0;
+}
 
 int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n) {
     if (!idx || (n && !out)) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }

@@ -181,6 +181,13 @@ int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64
 #define EDSBWT_PATH_REDO   0x8u /* the batch failed a deferred check and was searched again */
 int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n);
 
+/* Multi-GPU exchange: later edsbwt_search / edsbwt_search_lines calls on this
+ * index also write every pattern's count (u32, pattern i at d_counts[i]) into d_counts, a device
+ * array of cap entries on the index's device, complete when the call returns — the counts RCCL
+ * gathers to rank 0 without a second upload.  cap = 0 or d_counts = NULL turns it off.  A batch
+ * larger than cap fails with E_ARG. */
+int edsbwt_set_counts_mirror(edsbwt_index* idx, uint32_t* d_counts, uint64_t cap);
+
 /* Counters/timings of the last search on this index. */
 int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st);
 const char* edsbwt_kernel_name(int k);

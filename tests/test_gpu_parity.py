@@ -908,3 +908,32 @@ def test_rank16_level_step_gpu(oracle, edsbwt, tmp_path, monkeypatch, alphabet):
             for kw in ({}, {"deep": False}, {"direct": False, "deep": False}, {"ordered": True, "deep": False}, {"ktab": False}):
                 gc, go = idx.search((buf, offs), **kw)
                 assert np.array_equal(gc, oc) and np.array_equal(go, oo), (off, kw)
+
+
+def test_counts_mirror_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """edsbwt_set_counts_mirror: the host pipeline also leaves every pattern's u32 count in a
+    device array (what bench.py's ranks gather over RCCL), over several chunks; a batch larger
+    than the mirror fails with E_ARG; cap 0 turns it off."""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(6060)
+    segs = _covid_like(rng, 300)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 40)) or "ACGT" for _ in range(6000)] + ["", "N"]
+    buf, offs = _pack(pats)
+    oc, _, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=9)
+    text = ("\n".join(pats) + "\n").encode()
+    monkeypatch.setenv("EDSBWT_CHUNK_MB", "0.01")
+    monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+    with edsbwt.Index(base) as idx:
+        mirror = torch.full((len(pats),), -1, dtype=torch.int32, device="cuda")
+        idx.set_counts_mirror(mirror.data_ptr(), len(pats))
+        gc, _ = _lines_search(edsbwt, idx, text, first_id=9)
+        assert idx.stats()["chunks"] > 5
+        assert np.array_equal(gc, oc) and np.array_equal(mirror.cpu().numpy().view(np.uint32), oc)
+        small = torch.zeros(10, dtype=torch.int32, device="cuda")
+        idx.set_counts_mirror(small.data_ptr(), 10)
+        with pytest.raises(edsbwt.EdsBwtError):
+            _lines_search(edsbwt, idx, text, first_id=9)
+        idx.set_counts_mirror(0, 0)
+        gc2, _ = _lines_search(edsbwt, idx, text, first_id=9)
+        assert np.array_equal(gc2, oc)
