@@ -2206,6 +2206,10 @@ struct Engine {
             st.text_chars = sv[ST_TEXT_CHARS];
             st.text_rows = sv[ST_TEXT_ROWS];
             st.locate_offsets = sv[ST_LOC_OFFSETS];
+            if (trace && sv[ST_DF_WAVE_ROUNDS])
+                std::fprintf(stderr, "[edsbwt] k_deep_fast: %llu dependent load rounds over the lanes' patterns, %llu lane slots: lane utilisation %.3f\n",
+                             (unsigned long long)sv[ST_DF_LANE_ROUNDS], (unsigned long long)sv[ST_DF_WAVE_ROUNDS],
+                             (double)sv[ST_DF_LANE_ROUNDS] / (double)sv[ST_DF_WAVE_ROUNDS]);
             if (trace && sv[ST_CLK_STEPS])
                 std::fprintf(stderr, "[edsbwt] k_deep lane-steps %llu (with '#' rows %llu): cycles/step rank+link %.0f, runs %.0f, rest %.0f\n",
                              (unsigned long long)sv[ST_CLK_STEPS], (unsigned long long)sv[ST_CLK_HASH_STEPS],

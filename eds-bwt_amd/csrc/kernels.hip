@@ -321,7 +321,9 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_DEEP_PAIR_LINES = 11,  // of ST_DEEP_BLOCKS, the rank-entry lines
                   ST_TEXT_CHARS = 12, ST_TEXT_ROWS = 13,  // characters decided / single rows met by the text compare
                   ST_DEEPQ_STEPS = 14, ST_DEEPQ_BLOCKS = 15,  // k_deep's own (ST_DEEP_*: k_deep_fast's)
-                  ST_LVL_SINGLE = 16 };  // k_lvl_items input items of one row (b == e)
+                  ST_LVL_SINGLE = 16,  // k_lvl_items input items of one row (b == e)
+                  ST_DF_LANE_ROUNDS = 17, ST_DF_WAVE_ROUNDS = 18 };  // k_deep_fast: dependent load rounds of the
+                  // lanes' patterns, and 64 x the slowest lane's per pattern slot (lane utilisation)
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -1145,12 +1147,13 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
                                                    uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1,
                                                    uint64_t* __restrict__ q2) {
-    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
+    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0, n_lane = 0, n_wave = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     if (q2) q2 += (size_t)sh * qcap;
     UNIFORM_STRIDE(i, valid, P) {
         uint32_t want = 0;
+        uint32_t rounds = valid ? 1u : 0u;  // dependent load rounds of this lane's pattern
         uint4 w = make_uint4(0, 0, 0, 0);
         // ind: slen and the key chunks are in input order, pattern i (sorted) is input perm[i].
         // pv (packed direct start): input index and remaining symbols sorted along with the
@@ -1204,6 +1207,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                 // each backward step keeps one row and succeeds iff the text character before it
                 // equals the pattern's, so the next k = min(o, m) characters are decided by comparing
                 // them with the text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row)
+                rounds++;
                 const uint4 s = X.samples[b];
                 const uint32_t g = first && g1 != ~0u ? g1 : X.gpos[b];
                 n_blk += first && g1 != ~0u ? 2 : 3;
@@ -1276,6 +1280,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             for (; d < L; d++) {
                 const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
+                rounds++;
                 // three characters from one rank entry per end (rent3), as the pair below
                 if (X.rent3 && d >= tri_from && d + 2 < L && c != 0) {
                     const uint32_t c2 = code_at(d + 1), c3 = code_at(d + 2);
@@ -1350,8 +1355,15 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             q[at] = w;
             if (pv) q2[at] = pvv;  // k_deep reads the packed start instead of perm, slen and the key chunks
         }
+        uint32_t wmax = rounds;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor(wmax, o, 64));
+        n_lane += rounds;
+        n_wave += wmax;
     }
     __shared__ unsigned long long ssum[4];
+    stat_add(ctr, ST_DF_LANE_ROUNDS, n_lane, ssum);
+    stat_add(ctr, ST_DF_WAVE_ROUNDS, n_wave, ssum);
     stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
     stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
     stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
