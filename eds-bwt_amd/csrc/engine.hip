@@ -444,7 +444,9 @@ struct Engine {
     static constexpr uint32_t kFlagNoDefer = 0x80000000u;    // internal flag: the checked path
     uint32_t defer_wide_cap = 0;
     const uint32_t* defer_ovf2 = nullptr;
-    static constexpr uint32_t kWideCap = 16384;  // k_deep_wide lanes launched without a count read-back
+    static constexpr uint32_t kWideCap = 16384;
+    // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
+    bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;  // k_deep_wide lanes launched without a count read-back
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -1458,9 +1460,14 @@ struct Engine {
             if (!no_wide) {
                 ab.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
                 ae.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
-                launch(KC_DEEPW, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
-                       d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
-                       (const uint32_t*)ovf.p);
+                if (deep_wave)
+                    launch(KC_DEEPW, k_deep_wave, (size_t)wcap * 64, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
+                           d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
+                           (const uint32_t*)ovf.p, stats.p);
+                else
+                    launch(KC_DEEPW, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
+                           d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
+                           (const uint32_t*)ovf.p);
                 abase += (uint64_t)wcap * kDeepWide;
                 tag_list(ovf.p, wcap, EDSBWT_PATH_WIDE);
             }
@@ -1477,9 +1484,14 @@ struct Engine {
             zero(ovf2.p, 4);
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
-            launch(KC_DEEPW, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
-                   d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
-                   (const uint32_t*)nullptr);
+            if (deep_wave)
+                launch(KC_DEEPW, k_deep_wave, (size_t)nw * 64, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
+                       d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
+                       (const uint32_t*)nullptr, stats.p);
+            else
+                launch(KC_DEEPW, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
+                       d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
+                       (const uint32_t*)nullptr);
             abase += (uint64_t)nw * kDeepWide;
             st.deep_overflow += nw;
             novf = read_u32(ovf2.p);
@@ -2201,6 +2213,9 @@ struct Engine {
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
             st.bytes_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS] * 64 + sv[ST_DEEP_HASH] * 4;
             st.lines_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS];
+            st.bytes_kernel[KC_DEEPW] += sv[ST_DW_BLOCKS] * 64;  // k_deep_wave (k_deep_wide counts none)
+            st.lines_kernel[KC_DEEPW] += sv[ST_DW_BLOCKS];
+            st.intervals_stepped += sv[ST_DW_STEPS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
             st.locate_lf_steps = sv[ST_LOC_STEPS];
             st.text_chars = sv[ST_TEXT_CHARS];

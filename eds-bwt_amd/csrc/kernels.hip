@@ -322,8 +322,9 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_TEXT_CHARS = 12, ST_TEXT_ROWS = 13,  // characters decided / single rows met by the text compare
                   ST_DEEPQ_STEPS = 14, ST_DEEPQ_BLOCKS = 15,  // k_deep's own (ST_DEEP_*: k_deep_fast's)
                   ST_LVL_SINGLE = 16,  // k_lvl_items input items of one row (b == e)
-                  ST_DF_LANE_ROUNDS = 17, ST_DF_WAVE_ROUNDS = 18 };  // k_deep_fast: dependent load rounds of the
+                  ST_DF_LANE_ROUNDS = 17, ST_DF_WAVE_ROUNDS = 18,  // k_deep_fast: dependent load rounds of the
                   // lanes' patterns, and 64 x the slowest lane's per pattern slot (lane utilisation)
+                  ST_DW_BLOCKS = 19, ST_DW_STEPS = 20 };  // k_deep_wave's lines and interval steps
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -1723,6 +1724,193 @@ __global__ void __launch_bounds__(256) k_deep_wide(uint64_t P, uint32_t D0, cons
         for (uint32_t t = 0; t < cn; t++) { ab[at + t] = cb[t]; ae[at + t] = ce[t]; occ += ce[t] - cb[t] + 1; }
         put_res(res, o, at, cn, occ);
     }
+}
+
+// Wide lists, one wavefront per pattern (the patterns whose list outgrew k_deep's registers):
+// lane t holds interval t of the list (at most 64) and steps it by the pattern's next character
+// with one rank-entry load per end (updateSingleInterval, MOVE_EDSBWTSearch.cpp:424-510).  The
+// link (:512-563): the '#' rows of every lane's interval are gathered in LDS, their segments
+// sorted and deduplicated by the wave, cut into maximal runs of [seg_lo[s], s-1] ranges (a lane
+// per run) and stepped from the occ blocks; the new list (runs and stepped intervals) is sorted
+// by row and adjacent intervals merged (:309-324), so lists stay short and end sorted, as the
+// finished list must be.  A list or a '#'-row set beyond the wave's LDS goes to the level path
+// (ovf2), as it did for the lane-per-pattern k_deep_wide.
+constexpr uint32_t kWaveHash = 512;  // '#' rows one step may gather
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, uint32_t& total) {
+    uint32_t v = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64);
+        if ((int)lane >= o) v += y;
+    }
+    total = __shfl(v, 63, 64);
+    return v - x;
+}
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t lane) { return (uint32_t)__popcll(m & ((1ull << lane) - 1ull)); }
+// the n (<= 128) intervals in lb/le, sorted by row into tb/te and adjacent ones merged; lane r
+// receives the r-th merged interval.  Returns the merged count (> 64: the caller overflows).
+__device__ __forceinline__ uint32_t wave_sort_merge(uint32_t n, uint32_t* lb, uint32_t* le, uint32_t* tb, uint32_t* te, uint32_t lane,
+                                                    uint32_t& cb, uint32_t& ce) {
+    for (uint32_t k = lane; k < n; k += 64) {  // rank sort: the rows of disjoint intervals are distinct
+        const uint32_t v = lb[k];
+        uint32_t r = 0;
+        for (uint32_t q = 0; q < n; q++) r += lb[q] < v;
+        tb[r] = v;
+        te[r] = le[k];
+    }
+    __threadfence_block();
+    uint32_t m = 0;
+    cb = ce = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t k = base + lane;
+        const bool start = k < n && (k == 0 || tb[k] != te[k - 1] + 1u);
+        const uint64_t sm = __ballot(start);
+        // a run's end: one before the next start (or the list's end)
+        if (start) {
+            uint32_t e = k + 1;
+            while (e < n && tb[e] == te[e - 1] + 1u) e++;
+            const uint32_t r = m + lane_rank(sm, lane);
+            if (r < 64) {  // park the merged interval at slot r of lb/le (read back below)
+                lb[128 + r] = tb[k];
+                le[128 + r] = te[e - 1];
+            }
+        }
+        m += (uint32_t)__popcll(sm);
+    }
+    __threadfence_block();
+    if (lane < m && m <= 64) { cb = lb[128 + lane]; ce = le[128 + lane]; }
+    return m;
+}
+__global__ void __launch_bounds__(256) k_deep_wave(uint64_t P, uint32_t D0, const uint32_t* __restrict__ todo, uint32_t ntodo,
+                                                  const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm, uint32_t ind,
+                                                  const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                                                  const uint8_t* __restrict__ code_of, const uint32_t* __restrict__ nid,
+                                                  const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
+                                                  const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
+                                                  uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
+                                                  uint32_t* __restrict__ ovf2, const uint32_t* __restrict__ ntodo_dev,
+                                                  unsigned long long* __restrict__ ctr) {
+    (void)P;
+    __shared__ uint32_t s_seg[4][kWaveHash], s_tmp[4][kWaveHash];
+    __shared__ uint32_t s_b[4][192], s_e[4][192];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* seg = s_seg[wv];
+    uint32_t* tmp = s_tmp[wv];
+    uint32_t* lb = s_b[wv];
+    uint32_t* le = s_e[wv];
+    // ntodo_dev (deferred checks): the list's length lives on the device; ntodo is the grid's
+    // capacity, and a longer list is caught by the caller's final check
+    if (ntodo_dev) ntodo = min(ntodo, *ntodo_dev);
+    unsigned long long n_blk = 0, n_steps = 0;
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t j = blockIdx.x * (blockDim.x >> 6) + wv; j < ntodo; j += nwaves) {  // wave-uniform
+        const uint32_t i = todo[j];
+        const uint32_t L = slen[ind ? perm[i] : i];
+        const uint32_t u = nid[i];
+        const uint32_t o0 = ioff[u];
+        uint32_t cn = iend[u] - o0;
+        if (cn > 64) {
+            if (lane == 0) flag_push(ovf2, i);
+            continue;
+        }
+        if (lane < cn) { lb[lane] = ib[o0 + lane]; le[lane] = ie[o0 + lane]; }
+        __threadfence_block();
+        uint32_t cb, ce;
+        cn = wave_sort_merge(cn, lb, le, tmp, tmp + 256, lane, cb, ce);
+        const uint8_t* pat = bytes + off[perm[i]];
+        bool over = false;
+        for (uint32_t d = D0; d < L && cn && !over; d++) {
+            const uint32_t c = code_of[pat[L - 1 - d]];
+            if (c >= X.sigma) { cn = 0; break; }
+            // every interval stepped by c, and its '#' rows [h0, h1)
+            uint32_t h0 = 0, h1 = 0, sb = 0, se = 0;
+            if (lane < cn) {
+                n_blk += 2 - rank2_any(X, cb, ce + 1, c, h0, sb, h1, se);
+                n_steps++;
+            }
+            uint32_t H;
+            const uint32_t hpre = wave_excl_scan(h1 - h0, lane, H);
+            if (H > kWaveHash) { over = true; break; }
+            for (uint32_t k = h0; k < h1; k++) seg[hpre + k - h0] = X.eof_seg[k];
+            __threadfence_block();
+            // keep the segments of words outside segment 1 (eof_seg 0: no previous segment)
+            uint32_t R0 = 0;
+            for (uint32_t base = 0; base < H; base += 64) {
+                const uint32_t v = base + lane < H ? seg[base + lane] : 0u;
+                const uint64_t km = __ballot(v != 0);
+                __threadfence_block();
+                if (v) tmp[R0 + lane_rank(km, lane)] = v;
+                R0 += (uint32_t)__popcll(km);
+            }
+            __threadfence_block();
+            // sorted (rank with ties broken by position) into seg, then the distinct ones into tmp
+            for (uint32_t k = lane; k < R0; k += 64) {
+                const uint32_t v = tmp[k];
+                uint32_t r = 0;
+                for (uint32_t q = 0; q < R0; q++) {
+                    const uint32_t w = tmp[q];
+                    r += (w < v) || (w == v && q < k);
+                }
+                seg[r] = v;
+            }
+            __threadfence_block();
+            uint32_t R = 0;
+            for (uint32_t base = 0; base < R0; base += 64) {
+                const uint32_t k = base + lane;
+                const bool f = k < R0 && (k == 0 || seg[k] != seg[k - 1]);
+                const uint64_t fm = __ballot(f);
+                if (f) tmp[R + lane_rank(fm, lane)] = seg[k];
+                R += (uint32_t)__popcll(fm);
+            }
+            __threadfence_block();
+            if (R > 64) { over = true; break; }
+            // maximal runs (link(), :533-561): a run starts where seg_lo of the segment passes the
+            // previous segment; lane r handles the run starting at distinct segment r
+            const uint32_t sr = lane < R ? tmp[lane] : 0u;
+            const uint32_t lor = lane < R ? X.seg_lo[sr] : 0u;
+            const uint32_t prev = __shfl_up(sr, 1, 64);
+            const bool rstart = lane < R && (lane == 0 || lor > prev);
+            const uint64_t rm = __ballot(rstart);
+            uint32_t nb_ = 0, ne_ = 0;
+            bool rv = false;
+            if (rstart) {
+                const uint64_t later = lane == 63 ? 0ull : rm & ~((2ull << lane) - 1ull);  // starts after this lane
+                const uint32_t end = later ? (uint32_t)(__ffsll((unsigned long long)later) - 1) - 1u : R - 1u;
+                const uint32_t hi = tmp[end];
+                uint32_t x0, x1, y0, y1;
+                rank2_pair(X.occ, X.seg_start[lor], X.seg_start[hi], c, x0, x1, y0, y1);  // hi: one past the last word of segment hi-1
+                n_blk += 2;
+                if (y1 > x1) { rv = true; nb_ = X.C[c] + x1; ne_ = X.C[c] + y1 - 1; }
+            }
+            // the new list: runs, then stepped intervals, into lb/le; sorted and merged
+            const uint64_t vm = __ballot(rv), sm = __ballot(lane < cn && se > sb);
+            const uint32_t nr = (uint32_t)__popcll(vm), ns = (uint32_t)__popcll(sm);
+            __threadfence_block();
+            if (rv) { const uint32_t r = lane_rank(vm, lane); lb[r] = nb_; le[r] = ne_; }
+            if (lane < cn && se > sb) { const uint32_t r = nr + lane_rank(sm, lane); lb[r] = X.C[c] + sb; le[r] = X.C[c] + se - 1; }
+            __threadfence_block();
+            cn = wave_sort_merge(nr + ns, lb, le, tmp, tmp + 256, lane, cb, ce);
+            if (cn > 64) over = true;
+        }
+        if (over) {
+            if (lane == 0) flag_push(ovf2, i);
+            continue;
+        }
+        const uint32_t o = perm[i];
+        const uint64_t at = abase + (uint64_t)j * 64;
+        if (cn == 1) {
+            if (lane == 0) put_res(res, o, cb, 1u | kResRow, ce - cb + 1);
+            continue;
+        }
+        uint32_t occ = lane < cn ? ce - cb + 1 : 0u;
+#pragma unroll
+        for (int q = 32; q >= 1; q >>= 1) occ += __shfl_xor(occ, q, 64);
+        if (lane < cn) { ab[at + lane] = cb; ae[at + lane] = ce; }
+        if (lane == 0) put_res(res, o, at, cn, occ);
+    }
+    __shared__ unsigned long long ssum[4];
+    stat_add(ctr, ST_DW_BLOCKS, n_blk, ssum);
+    stat_add(ctr, ST_DW_STEPS, n_steps, ssum);
 }
 
 __global__ void k_list_flagged(uint64_t P, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ fscan, uint32_t* __restrict__ out) {
