@@ -446,7 +446,10 @@ struct Engine {
     const uint32_t* defer_ovf2 = nullptr;
     static constexpr uint32_t kWideCap = 16384;
     // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
-    bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;  // k_deep_wide lanes launched without a count read-back
+    bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;
+    // packed direct start: k_deep_refill (lane refill) instead of k_deep_fast; EDSBWT_DEEP_REFILL=0: k_deep_fast (A/B)
+    bool deep_refill = env_double("EDSBWT_DEEP_REFILL", 1) != 0;
+    DBuf<unsigned long long> rf_next;  // k_deep_refill's pattern counter  // k_deep_wide lanes launched without a count read-back
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -1123,7 +1126,7 @@ struct Engine {
             launch(KC_TABLE, k_u32_of_u64, W, (const uint64_t*)ws64.p, (uint64_t)W, ws.p);
             wsp = ws.p;
         }
-        const uint64_t nw = tlen / 32 + 2;
+        const uint64_t nw = tlen / 32 + 5;  // k_deep_refill reads the 16-B pair holding rt[q], rt[q+1] and the next pair
         rtext.ensure(nw);
         zero(rtext.p, nw * 8);
         gpos.ensure(N);
@@ -1430,9 +1433,24 @@ struct Engine {
             krest = skey.p;
             lens = slen.p;
         }
-        launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
-               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p,
-               goff == ktab_off.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr, pv ? dq2.p : (uint64_t*)nullptr);
+        const uint64_t* kt1 = goff == ktab_off.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr;
+        if (deep_refill && pv && kt1 && X.rent1 && !X.rent3) {
+            // packed direct start: the lane-refill walk (same results, counters and queue)
+            rf_next.ensure(1);
+            HIPCHK(hipMemsetAsync(rf_next.p, 0, 8, stream));
+            const unsigned G = (unsigned)std::min<uint64_t>((P + 255) / 256, 4096);
+            timed(KC_DEEP, [&] {
+                hipLaunchKernelGGL(k_deep_refill, dim3(G), dim3(256), 0, stream, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p,
+                                   stats.p, pv, perm.p, kt1, dq2.p, rf_next.p);
+            });
+            HIPCHK(hipGetLastError());
+            sync_check((const void*)k_deep_refill);
+            st.launches_kernel[KC_DEEP]++;
+        } else {
+            launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
+                   nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
+                   pv ? dq2.p : (uint64_t*)nullptr);
+        }
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)

@@ -1356,15 +1356,315 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             q[at] = w;
             if (pv) q2[at] = pvv;  // k_deep reads the packed start instead of perm, slen and the key chunks
         }
+#ifdef EDSBWT_DEEP_CLOCKS
         uint32_t wmax = rounds;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor(wmax, o, 64));
         n_lane += rounds;
         n_wave += wmax;
+#else
+        (void)rounds;
+#endif
     }
     __shared__ unsigned long long ssum[4];
     stat_add(ctr, ST_DF_LANE_ROUNDS, n_lane, ssum);
     stat_add(ctr, ST_DF_WAVE_ROUNDS, n_wave, ssum);
+    stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
+    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
+    stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
+    stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
+    stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
+}
+
+// rank of `lane` among the set lanes of mask m
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t lane) { return (uint32_t)__popcll(m & ((1ull << lane) - 1ull)); }
+
+// k_deep_fast for the packed direct start, with lane refill.  k_deep_fast gives each lane one
+// pattern per grid-stride slot, so a wave waits for its slowest pattern: on C3 its lanes do useful
+// dependent load rounds 29% of the time (an average pattern needs 2.7 rounds, the slowest of 64
+// 9.5).  Here every lane is a small state machine that takes the next pattern (one atomic per
+// wave, in order, keeping the D-mer sort's locality) as soon as its own is done, and each loop
+// iteration is ONE round for every lane: the lane uses the 16-B words it loaded in the previous
+// iteration, decides what comes next, and issues that step's loads (at most two 16-B loads: an
+// entry, or the aligned 16 B holding a narrower value), so one wait covers all lanes whatever
+// step they are at.  Walk, counters, results and queue entries are k_deep_fast's for the packed
+// mode with rank entries (and no rent3): the same walk, cut into rounds.
+enum : uint32_t { RF_IDLE = 0, RF_PV, RF_ENT, RF_SAMPLE, RF_TEXT, RF_SEG, RF_PAIR, RF_SINGLE };
+__device__ __forceinline__ uint32_t rf_u32(uint4 v, uint32_t part) {
+    return part == 0 ? v.x : part == 1 ? v.y : part == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ uint64_t rf_u64(uint4 v, uint32_t part) {
+    return part == 0 ? ((uint64_t)v.y << 32 | v.x) : ((uint64_t)v.w << 32 | v.z);
+}
+template <typename T>
+__device__ __forceinline__ const uint4* rf_line(const T* p) {  // the aligned 16 B holding *p
+    return reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15);
+}
+template <typename T>
+__device__ __forceinline__ uint32_t rf_part(const T* p) {  // which 4-B word of it
+    return (uint32_t)((reinterpret_cast<uintptr_t>(p) >> 2) & 3);
+}
+__global__ void __launch_bounds__(256) k_deep_refill(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
+                                                    uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
+                                                    uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
+                                                    const uint64_t* __restrict__ pv, uint32_t* __restrict__ perm_out,
+                                                    const uint64_t* __restrict__ kt1, uint64_t* __restrict__ q2,
+                                                    unsigned long long* __restrict__ next) {
+    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
+    const uint32_t sh = blockIdx.x % NSHARD;
+    q += (size_t)sh * qcap;
+    q2 += (size_t)sh * qcap;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t phase = RF_IDLE;
+    bool exhausted = false;
+    uint64_t i = 0, pvv = 0, rem = 0;
+    uint32_t pi = 0, L = 0, d = 0, b = 0, e = 0, g = 0, c = 0, p = 0, pa = 0, pb = 0;
+    uint32_t sx = 0, sy = 0, sz = 0, sw = 0;  // the row's sample (word, offset, segment, word in segment)
+    bool gknown = false, pair_skip = false;
+    uint4 la = make_uint4(0, 0, 0, 0), lb = make_uint4(0, 0, 0, 0);  // what the previous round loaded
+    for (;;) {
+        // ---- refill: idle lanes take the next patterns (one atomic per wave)
+        const uint64_t idle = __ballot(phase == RF_IDLE && !exhausted);
+        if (idle) {
+            const int l0 = __ffsll((unsigned long long)idle) - 1;
+            unsigned long long base = 0;
+            if ((int)lane == l0) base = atomicAdd(next, (unsigned long long)__popcll(idle));
+            base = __shfl(base, l0, 64);
+            if (phase == RF_IDLE && !exhausted) {
+                i = base + lane_rank(idle, lane);
+                if (i < P) phase = RF_PV;
+                else exhausted = true;
+            }
+        }
+        if (!__ballot(phase != RF_IDLE)) break;  // every lane exhausted: the grid drains
+        const uint4* ra = nullptr;
+        const uint4* rb = nullptr;
+        bool done = false, alive = true, res_written = false;
+        uint32_t want = 0;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        bool issue_sample = false, issue_step = false;
+        // ---- use what the last round loaded
+        switch (phase) {
+        case RF_PV:  // first round: nothing loaded yet; the packed start and the D-mer id
+            ra = rf_line(pv + i);
+            rb = rf_line(nid + i);
+            pa = (uint32_t)(i & 1);
+            pb = rf_part(nid + i);
+            phase = RF_ENT;
+            break;
+        case RF_ENT: {
+            pvv = rf_u64(la, pa);
+            pi = (uint32_t)(pvv & 0x7fffffffu);
+            rem = pvv >> 31;
+            L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
+            perm_out[i] = pi;
+            if (L <= D0) {  // nothing after the D-mer: no list walked, count 0 (k_deep_fast writes none either)
+                done = true;
+                res_written = true;
+                break;
+            }
+            const uint32_t u = rf_u32(lb, pb);
+            ra = rf_line(kt1 + u);
+            pa = u & 1u;
+            phase = RF_SAMPLE;  // next round: the table entry (handled at RF_SAMPLE with gknown unset)
+            d = D0;
+            pair_skip = false;
+            gknown = false;
+            b = ~0u;  // the entry is pending
+            break;
+        }
+        case RF_SAMPLE:
+            if (b == ~0u) {
+                // the D-mer's table entry: one interval inline, or the list's length
+                const uint64_t ent = rf_u64(la, pa);
+                const uint32_t n0 = (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
+                if (n0 > 1) {
+                    want = 1;
+                    w = make_uint4((uint32_t)i, D0, ~0u, 0u);
+                    done = true;
+                } else if (n0 == 0) {
+                    done = true;
+                    res_written = true;  // (no result: count 0)
+                } else {
+                    if (X.kt1_pos && ((ent >> 62) & 1)) {
+                        b = e = (uint32_t)ent & 0x7fffffffu;
+                        g = (uint32_t)(ent >> 31) & 0x7fffffffu;
+                        gknown = true;
+                    } else {
+                        b = (uint32_t)ent;
+                        e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+                    }
+                    if (X.rtext && b == e && d < L) issue_sample = true;
+                    else issue_step = true;
+                }
+            } else {
+                // the row's sample (and text position): compare the next k = min(o, m) characters
+                sx = la.x; sy = la.y; sz = la.z; sw = la.w;
+                if (!gknown) g = rf_u32(lb, pb);
+                const uint32_t m = L - d, k = min(sy, m);
+                if (k) {
+                    const uint64_t qq = ((X.tlen - g) >> 5) & ~1ull;
+                    ra = reinterpret_cast<const uint4*>(X.rtext + qq);
+                    rb = reinterpret_cast<const uint4*>(X.rtext + qq + 2);
+                    phase = RF_TEXT;
+                } else {
+                    phase = RF_TEXT;
+                    la = lb = make_uint4(0, 0, 0, 0);  // nothing to compare: RF_TEXT below, this round
+                }
+            }
+            break;
+        default:
+            break;
+        }
+        if (phase == RF_TEXT && ra == nullptr) {
+            // the text window arrived (or k = 0): MOVE_EDSBWTSearch.cpp:424-510 stepping one row
+            const uint32_t m = L - d, k = min(sy, m);
+            bool eq = true;
+            if (k) {
+                const uint64_t r0 = X.tlen - g;
+                const uint32_t shf = (uint32_t)(r0 & 31u) * 2u;
+                const bool odd = ((r0 >> 5) & 1) != 0;
+                const uint64_t a0 = odd ? ((uint64_t)la.w << 32 | la.z) : ((uint64_t)la.y << 32 | la.x);
+                const uint64_t a1 = odd ? ((uint64_t)lb.y << 32 | lb.x) : ((uint64_t)la.w << 32 | la.z);
+                const uint64_t win = shf ? (a0 >> shf) | (a1 << (64 - shf)) : a0;
+                const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1ull);
+                eq = ((win ^ (rem >> (2 * (d - D0)))) & mask) == 0;
+            }
+            if (!eq) {
+                alive = false;
+                done = true;
+            } else if (sy >= m && sw <= kResCnt) {
+                n_text += m;
+                put_res(res, pi, (uint64_t)(sy - m) << 32 | sx, kResRow | kResPos | sw, sz);
+                res_written = true;
+                done = true;
+            } else if (sy >= m) {
+                issue_step = true;  // a segment of 2^30 words: the rank walk decides
+            } else {
+                // the word's first o characters matched: the link from its '#' row, one segment
+                n_text += sy;
+                d += sy;
+                c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
+                if (sz < 2) {
+                    alive = false;
+                    done = true;
+                } else {
+                    const uint32_t* et = X.segtab + (size_t)sz * X.seg_stride;
+                    ra = rf_line(et + 1 + c);
+                    rb = rf_line(et + X.seg_hi + c);
+                    pa = rf_part(et + 1 + c);
+                    pb = rf_part(et + X.seg_hi + c);
+                    n_blk++;
+                    n_steps++;
+                    phase = RF_SEG;
+                }
+            }
+        } else if (phase == RF_TEXT) {
+            // (the window is being loaded this round)
+        } else if (phase == RF_SEG && ra == nullptr) {
+            const uint32_t rx = rf_u32(la, pa), ry = rf_u32(lb, pb);
+            if (ry <= rx) {
+                alive = false;
+                done = true;
+            } else {
+                b = X.C[c] + rx;
+                e = X.C[c] + ry - 1;
+                d++;
+                gknown = false;
+                if (d >= L) done = true;
+                else if (X.rtext && b == e) issue_sample = true;
+                else issue_step = true;
+            }
+        } else if (phase == RF_PAIR) {
+            // a two-step rank entry per end
+            uint32_t p0, x0, p1, x1;
+            rent_rank(la, b, p0, x0);
+            rent_rank(lb, e + 1, p1, x1);
+            if (x1 == x0 && p1 > p0) {
+                n_steps += 2;
+                b = X.PC[p] + p0;
+                e = X.PC[p] + p1 - 1;
+                d += 2;
+                if (d >= L) done = true;
+                else issue_step = true;
+            } else {
+                pair_skip = true;
+                c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
+                ra = X.rent1 + (size_t)(b >> 5) * X.sigma + c;
+                rb = X.rent1 + (size_t)((e + 1) >> 5) * X.sigma + c;
+                const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
+                n_blk += nl;
+                n_pl += nl;
+                phase = RF_SINGLE;
+            }
+        } else if (phase == RF_SINGLE) {
+            // a one-step rank entry per end (rank of c and of '#')
+            uint32_t h0, sb, h1, se;
+            rent_rank(la, b, sb, h0);
+            rent_rank(lb, e + 1, se, h1);
+            if (h1 > h0) {  // '#' rows: the link needs k_deep
+                want = 1;
+                w = make_uint4((uint32_t)i, d, b, e);
+                done = true;
+            } else {
+                n_steps++;
+                if (se <= sb) {
+                    alive = false;
+                    done = true;
+                } else {
+                    b = X.C[c] + sb;
+                    e = X.C[c] + se - 1;
+                    d++;
+                    if (d >= L) done = true;
+                    else issue_step = true;
+                }
+            }
+        }
+        // ---- the next step's loads
+        if (issue_sample) {
+            // one row = one text position: its sample, and its text position unless known
+            ra = reinterpret_cast<const uint4*>(X.samples + b);
+            if (!gknown) { rb = rf_line(X.gpos + b); pb = rf_part(X.gpos + b); }
+            n_blk += gknown ? 2 : 3;
+            n_trow++;
+            phase = RF_SAMPLE;
+        } else if (issue_step) {
+            c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
+            if (X.rent2 && !pair_skip && d + 1 < L) {
+                const uint32_t c2 = 1u + (uint32_t)((rem >> (2 * (d + 1 - D0))) & 3u);
+                p = 1 + (c - 1) * X.sigma + c2;
+                ra = X.rent2 + (size_t)(b >> 5) * X.r2stride + p - 1;
+                rb = X.rent2 + (size_t)((e + 1) >> 5) * X.r2stride + p - 1;
+                phase = RF_PAIR;
+            } else {
+                pair_skip = false;
+                ra = X.rent1 + (size_t)(b >> 5) * X.sigma + c;
+                rb = X.rent1 + (size_t)((e + 1) >> 5) * X.sigma + c;
+                phase = RF_SINGLE;
+            }
+            const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
+            n_blk += nl;
+            n_pl += nl;
+        }
+        // ---- a finished pattern: its result, or its queue entry
+        if (done) {
+            if (!want && !res_written) {
+                if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
+                else put_res(res, pi, abase + i * K, 0u, 0u);
+            }
+            phase = RF_IDLE;
+            ra = rb = nullptr;
+        }
+        const uint32_t at = wave_append(qcnt + sh * 32, want);
+        if (want && at < qcap) {
+            q[at] = w;
+            q2[at] = pvv;
+        }
+        // ---- this round's loads (a lane without a pending step loads nothing)
+        if (ra) la = *ra;
+        if (rb) lb = *rb;
+    }
+    __shared__ unsigned long long ssum[4];
     stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
     stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
     stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
@@ -1746,7 +2046,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, uint32_t lane, ui
     total = __shfl(v, 63, 64);
     return v - x;
 }
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t lane) { return (uint32_t)__popcll(m & ((1ull << lane) - 1ull)); }
 // the n (<= 128) intervals in lb/le, sorted by row into tb/te and adjacent ones merged; lane r
 // receives the r-th merged interval.  Returns the merged count (> 64: the caller overflows).
 __device__ __forceinline__ uint32_t wave_sort_merge(uint32_t n, uint32_t* lb, uint32_t* le, uint32_t* tb, uint32_t* te, uint32_t lane,
