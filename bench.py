@@ -7,18 +7,19 @@ A *step* is one pass of the hot path — MOVE_EDSBWTSearch's pattern loop with p
 recovery (MOVE_EDSBWTSearch.cpp:97-155, 228-374) — over one batch of synthetic patterns:
 the pattern file's bytes in (page-locked) host memory go through edsbwt_search_lines,
 the library's pipelined host path (H2D of chunk k+1 overlaps the search of chunk k and the
-D2H of chunk k-1), until every count and occurrence record is back in host memory.
-`value` is therefore SURVEY.md §8(d)'s patterns/s: first H2D of the patterns to the last
-D2H of the results.  The same batch with its bytes and offsets already in HBM and the
-results left there is timed next and reported as `device_resident` (the kernel roofline
-comes from that run).
+D2H of chunk k-1), until every count and occurrence record is back in host memory: SURVEY.md
+§8(d)'s PCIe-inclusive clock, reported as `e2e` (value, ms_per_step, per-call walls).  The same
+batch with its bytes and offsets already in HBM and the counts and records left there
+(edsbwt_search_device) is timed next: that leg is `value` / `ms_per_step` (the task's
+contract: inputs resident in HBM when the timed region starts; the PCIe-inclusive rate is
+never `value`) and `device_resident`, and the kernel roofline comes from it.
 
 Default workload = C3 (BASELINE.json configs[2]): ~100 Mchar COVID-like synthetic EDS,
 10M planted 31-mers per GPU, full locate.  C4 = the C3 index with 100M patterns in total,
 sharded over the ranks.  N>1: one process per GPU (torchrun; `--gpus N` without torchrun
 starts it), each rank searches its contiguous shard against a replicated index; the
 exchange step — sizes all-gathered, per-pattern counts gathered to rank 0 over RCCL — is
-inside the timed step.  rank 0 prints one JSON line.
+inside both timed legs' steps.  rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -264,15 +265,18 @@ def main():
         # chunk): RCCL gathers them from HBM, no second upload of the counts
         idx.set_counts_mirror(d_counts_x.data_ptr(), npat)
 
-    def exchange(nocc):
+    def exchange(nocc, d_src=None):
         # the path's exchange step: every rank's (patterns, records) all-gathered — its offsets in
         # the output (each rank writes its slice); --gather counts also gathers the
-        # per-pattern counts to rank 0 (RCCL/xGMI)
+        # per-pattern counts to rank 0 (RCCL/xGMI).  d_src: the device-resident leg's counts.
         if world == 1:
             return
         sizes = shard.exchange_sizes(npat, nocc, gdev)
         if args.gather == "counts":
-            src = d_counts_x if args.dist_backend == "nccl" else torch.from_numpy(counts[:npat].view(np.int32))
+            if d_src is not None:
+                src = d_src if args.dist_backend == "nccl" else d_src.cpu()
+            else:
+                src = d_counts_x if args.dist_backend == "nccl" else torch.from_numpy(counts[:npat].view(np.int32))
             shard.gather_counts(src, [int(x) for x in sizes[:, 0]])
 
     # ---- timed: end-to-end (host memory -> host memory)
@@ -365,13 +369,15 @@ def main():
                                      locate=locate, profile=profile, stream=stream, **flags_kw)
 
         for _ in range(max(1, args.warmup)):
-            dev_step()
+            _, dn = dev_step()
+            exchange(dn, d_counts)
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         kstats = {}
         for _ in range(args.steps):
-            dev_step(profile="light")
+            _, dn = dev_step(profile="light")
+            exchange(dn, d_counts)
             st = idx.stats()
             for k, v in st["kernels"].items():
                 a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
@@ -389,12 +395,14 @@ def main():
             raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")
 
     if rank == 0:
-        ms_step = 1000.0 * elapsed / args.steps
         total_pats = npat * world if w.per_gpu else (args.patterns or w.patterns)  # every rank's shard
-        if args.no_e2e:  # profiling run: the device-resident rate stands in (labelled below)
-            elapsed = dres["elapsed"] if dres else 1.0
-            ms_step = 1000.0 * elapsed / args.steps
-        value = total_pats * args.steps / elapsed
+        e2e_value = None if args.no_e2e else total_pats * args.steps / elapsed
+        e2e_ms = None if args.no_e2e else 1000.0 * elapsed / args.steps
+        # value: the device-resident leg (inputs in HBM); --no-device runs (host-pipeline studies)
+        # fall back to the end-to-end rate, labelled in timed_region
+        v_elapsed = dres["elapsed"] if dres else elapsed
+        value = total_pats * args.steps / v_elapsed
+        ms_step = 1000.0 * v_elapsed / args.steps
         rows = idx.n_rows
         # tables the deep kernels gather from: occ blocks (1 B/row), rent1 (sigma/2 B/row), rent2 (10 B/row)
         rank_bytes = rows * (1 + idx.sigma / 2 + (10 if idx.pair_blocks else 0))
@@ -418,9 +426,11 @@ def main():
                                    "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
                                   if locate else "count-only"),
                        "parallelism": f"pattern-shard x{world}",
-                       "timed_region": ("device-resident leg only (--no-e2e profiling run)" if args.no_e2e else
-                                        "edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> counts + records D2H "
-                                        "(SURVEY §8(d)), plus the exchange step when N>1"),
+                       "timed_region": ("edsbwt_search_device: pattern bytes + offsets resident in HBM -> counts + records "
+                                        "in HBM, plus the exchange step when N>1; the PCIe-inclusive rate is `e2e`"
+                                        if dres else
+                                        "(--no-device) edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> "
+                                        "counts + records D2H (SURVEY §8(d)), plus the exchange step when N>1"),
                        "exchange": ("none (one GPU)" if world == 1 else
                                     "sizes all-gathered (each rank keeps its counts + records as its output slice)"
                                     + (" + counts gathered to rank 0 over RCCL" if args.gather == "counts" else "")),
@@ -429,8 +439,11 @@ def main():
                        # every table the search reads (rank tables, k-mer table, samples) within the 256 MB MALL
                        "cache_resident": bool(idx.device_bytes <= MI355X_MALL_BYTES), "rank_tables_bytes": int(rank_bytes)},
             "occurrences_per_step": int(total_occ / args.steps),
-            "found_per_step": int(e2e_stats["found"]) if world == 1 else None,
-            "e2e": {"ms_wall_per_call": round(float(np.mean(walls)), 3), "ms_wall_median": round(float(np.median(walls)), 3),
+            "found_per_step": int((dres["stats"] if dres else e2e_stats)["found"]) if world == 1 else None,
+            "e2e": {"value": round(e2e_value, 1) if e2e_value else None, "ms_per_step": round(e2e_ms, 3) if e2e_ms else None,
+                    "what": "SURVEY §8(d)'s clock: page-locked pattern-file bytes H2D -> search -> every count and 20-B "
+                            "record D2H (edsbwt_search_lines), plus the exchange step when N>1",
+                    "ms_wall_per_call": round(float(np.mean(walls)), 3), "ms_wall_median": round(float(np.median(walls)), 3),
                     "ms_wall_min": round(float(np.min(walls)), 3), "ms_wall_p90": round(float(np.percentile(walls, 90)), 3),
                     "ms_wall_max": round(float(np.max(walls)), 3), "ms_walls": [round(float(x), 3) for x in walls],
                     "redo_searches": redo_calls, "host_cores": round(host_cores, 2), "chunks": e2e_stats["chunks"],
@@ -438,7 +451,7 @@ def main():
                     "pcie_gbs": round((e2e_stats["bytes_h2d"] + e2e_stats["bytes_d2h"]) / max(1e-9, np.mean(walls) * 1e-3) / 1e9, 2),
                     "device_ms_per_call": round(e2e_stats["ms_total"], 3),
                     "per_rank_search_exchange_ms": per_rank_all},
-            "bs_took": round(elapsed / args.steps, 6),
+            "bs_took": round(elapsed / args.steps, 6) if not args.no_e2e else None,
             "index_open_s": round(t_open, 2),
             "inputs_prepare_s": round(t_prep, 1),
         }
@@ -494,7 +507,8 @@ def main():
             }
             out["device_resident"] = {
                 "value": round(total_pats * args.steps / dres["elapsed"], 1), "ms_per_step": round(d_ms, 3),
-                "what": "pattern bytes + u64 offsets resident in HBM before the timed region; counts + records left in HBM",
+                "what": "pattern bytes + u64 offsets resident in HBM before the timed region; counts + records left in HBM"
+                        + ("; the exchange step (sizes all-gathered, counts gathered to rank 0) in every step" if world > 1 else ""),
                 "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items()) if v["ms"]},
                 "kernel_lines_per_s": {k: round((v["lines"] / (v["ms"] * 1e-3)) if v["ms"] > 0 else 0.0, 1)
                                        for k, v in sorted(kstats.items()) if v["lines"]},

@@ -161,6 +161,7 @@ constexpr double kKtabItems = 268435456.0;  // at least 2^28 intervals (2 GiB) .
 constexpr double kKtabHbmShare = 0.15;      // ... or as many as kKtabHbmShare of the free HBM holds at
 constexpr double kKtabBuildBytes = 40.0;    // the build's transient bytes per interval (capture + sort)
 constexpr uint32_t kKtabMinDepth = 2;
+constexpr double kKt1WideHbmShare = 2.5;  // the wide k-mer entries are built when free HBM > 2.5x their bytes
 // ... and no deeper than B^(K-1) <= kKtabOver * N: most longer D-mers do not occur (an
 // entry is 12 B; C2, 12.5M rows: depth 15 = 12.9 GB of the 288 GB, searches 4.6x faster
 // than at depth 11)
@@ -237,6 +238,7 @@ struct Engine {
     bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     DBuf<uint64_t> ktab_one;  // per D-mer: its one interval inline, else list length and offset (k_ktab_one)
+    DBuf<uint4> ktab_wide;    // ... or the wide form, 32 B per D-mer (k_ktab_wide; replaces ktab_one)
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
@@ -447,9 +449,9 @@ struct Engine {
     static constexpr uint32_t kWideCap = 16384;
     // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
     bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;
-    // packed direct start: k_deep_refill (lane refill) instead of k_deep_fast; EDSBWT_DEEP_REFILL=0: k_deep_fast (A/B)
+    // packed direct start: k_deep_refill (lane refill, coalesced intake); EDSBWT_DEEP_REFILL=0: k_deep_fast
     bool deep_refill = env_double("EDSBWT_DEEP_REFILL", 1) != 0;
-    DBuf<unsigned long long> rf_next;  // k_deep_refill's pattern counter  // k_deep_wide lanes launched without a count read-back
+    unsigned refill_blocks = 0;  // its resident grid (occupancy x CUs)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -542,6 +544,15 @@ struct Engine {
     void launch(int k, K kern, size_t n, A... a) {
         if (!n) return;
         timed(k, [&] { hipLaunchKernelGGL(kern, dim3(grid_for(n)), dim3(256), 0, stream, a...); });
+        HIPCHK(hipGetLastError());
+        hmark_kern((const void*)kern);
+        sync_check((const void*)kern);
+        st.launches_kernel[k]++;
+    }
+    template <typename K, typename... A>
+    void launch_grid(int k, K kern, unsigned blocks, A... a) {  // an explicit grid (a kernel that strides itself)
+        if (!blocks) return;
+        timed(k, [&] { hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream, a...); });
         HIPCHK(hipGetLastError());
         hmark_kern((const void*)kern);
         sync_check((const void*)kern);
@@ -1048,11 +1059,27 @@ struct Engine {
         launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, ktab_b.p);
         HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
         if (N < 0x80000000u) {  // inline single intervals need bit 63 free
-            ktab_one.ensure(E + 1);
             kt1_pos = have_text && gpos.p && N < 0x40000000u && tlen < 0x80000000ull && env_double("EDSBWT_KT1_POS", 1) != 0;
-            launch(KC_TABLE, k_ktab_one, E + 1, E, (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p, (const uint32_t*)ktab_e.p,
-                   ktab_one.p, kt1_pos ? (const uint32_t*)gpos.p : (const uint32_t*)nullptr);
-            device_bytes += (E + 1) * 8;
+            // the wide form when a one-row entry can carry its sample and text window (dense
+            // samples, the text) and HBM holds 32 B per D-mer with room to spare (C3: 4^15 D-mers,
+            // 34 GB); EDSBWT_KT1_WIDE=0: the 8-B entries
+            size_t fb = 0, tb_ = 0;
+            if (hipMemGetInfo(&fb, &tb_) != hipSuccess) { (void)hipGetLastError(); fb = 0; }
+            const uint64_t wide_b = (E + 1) * 32;
+            const bool wide = kt1_pos && have_samples && samp_shift == 0 && samples.p && rtext.p &&
+                              (double)fb > kKt1WideHbmShare * (double)wide_b && env_double("EDSBWT_KT1_WIDE", 1) != 0;
+            if (wide) {
+                ktab_wide.ensure(2 * (E + 1));
+                launch(KC_TABLE, k_ktab_wide, E + 1, E, (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p,
+                       (const uint32_t*)ktab_e.p, (const uint32_t*)gpos.p, (const uint4*)samples.p, (const uint64_t*)rtext.p,
+                       (uint64_t)tlen, ktab_wide.p);
+                device_bytes += wide_b;
+            } else {
+                ktab_one.ensure(E + 1);
+                launch(KC_TABLE, k_ktab_one, E + 1, E, (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p,
+                       (const uint32_t*)ktab_e.p, ktab_one.p, kt1_pos ? (const uint32_t*)gpos.p : (const uint32_t*)nullptr);
+                device_bytes += (E + 1) * 8;
+            }
         }
         HIPCHK(hipStreamSynchronize(stream));
         ktab_depth = c.depth;
@@ -1126,7 +1153,7 @@ struct Engine {
             launch(KC_TABLE, k_u32_of_u64, W, (const uint64_t*)ws64.p, (uint64_t)W, ws.p);
             wsp = ws.p;
         }
-        const uint64_t nw = tlen / 32 + 5;  // k_deep_refill reads the 16-B pair holding rt[q], rt[q+1] and the next pair
+        const uint64_t nw = tlen / 32 + 5;  // rtext_window(tlen) reads word tlen/32 + 1
         rtext.ensure(nw);
         zero(rtext.p, nw * 8);
         gpos.ensure(N);
@@ -1433,23 +1460,28 @@ struct Engine {
             krest = skey.p;
             lens = slen.p;
         }
-        const uint64_t* kt1 = goff == ktab_off.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr;
-        if (deep_refill && pv && kt1 && X.rent1 && !X.rent3) {
-            // packed direct start: the lane-refill walk (same results, counters and queue)
-            rf_next.ensure(1);
-            HIPCHK(hipMemsetAsync(rf_next.p, 0, 8, stream));
-            const unsigned G = (unsigned)std::min<uint64_t>((P + 255) / 256, 4096);
-            timed(KC_DEEP, [&] {
-                hipLaunchKernelGGL(k_deep_refill, dim3(G), dim3(256), 0, stream, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p,
-                                   stats.p, pv, perm.p, kt1, dq2.p, rf_next.p);
-            });
-            HIPCHK(hipGetLastError());
-            sync_check((const void*)k_deep_refill);
-            st.launches_kernel[KC_DEEP]++;
+        // direct start from the k-mer table: its 8-B entries, or the wide ones (entry + a one-row
+        // entry's sample and text window)
+        const bool dstart = goff == ktab_off.p;
+        const uint64_t* kt1 = dstart && ktab_one.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr;
+        const uint4* kt1w = dstart && ktab_wide.p ? (const uint4*)ktab_wide.p : (const uint4*)nullptr;
+        if (deep_refill && pv && (kt1 || kt1w) && X.rent1 && !X.rent3) {
+            // packed direct start: the lane-refill walk (same results, counters and queue); waves
+            // take stages of 64 patterns, this wave's t-th is stage (wave + t * waves)
+            // (no more blocks than stay resident: a late wave would run its whole share after the rest)
+            if (!refill_blocks) {
+                int per_cu = 0, cus = 0;
+                HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_deep_refill, 256, 0));
+                HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+                refill_blocks = (unsigned)std::max(1, per_cu * cus);
+            }
+            const unsigned G = (unsigned)std::min<uint64_t>((P + 255) / 256, refill_blocks);
+            launch_grid(KC_DEEP, k_deep_refill, G, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p,
+                        kt1, kt1w, dq2.p);
         } else {
             launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
                    nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
-                   pv ? dq2.p : (uint64_t*)nullptr);
+                   pv ? dq2.p : (uint64_t*)nullptr, kt1w);
         }
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());

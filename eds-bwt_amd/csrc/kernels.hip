@@ -1147,7 +1147,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                                                    uint4* __restrict__ q, uint32_t qcap, uint32_t* __restrict__ qcnt,
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
                                                    uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1,
-                                                   uint64_t* __restrict__ q2) {
+                                                   uint64_t* __restrict__ q2, const uint4* __restrict__ kt1w) {
     unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0, n_lane = 0, n_wave = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
@@ -1173,16 +1173,27 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
             L = valid ? slen[pi] : 0u;
         }
         const uint32_t u = L > D0 ? nid[i] : 0u;
-        // kt1 (direct start): the D-mer's one interval inline, or its list's length
-        const uint64_t ent = kt1 && L > D0 ? kt1[u] : 0ull;
-        const uint32_t n0 = L <= D0 ? 0u : kt1 ? ((ent >> 63) ? 1u : (uint32_t)(ent >> 32)) : iend[u] - ioff[u];
+        // kt1 (direct start): the D-mer's one interval inline, or its list's length; kt1w (the
+        // wide form) also holds a one-row entry's sample and the 32 text characters before it
+        const bool dtab = kt1 || kt1w;
+        uint64_t ent = 0, win1 = 0;
+        uint4 s1 = make_uint4(0, 0, 0, 0);
+        if (L > D0 && kt1w) {
+            const uint4 w0 = kt1w[2 * (size_t)u];
+            s1 = kt1w[2 * (size_t)u + 1];
+            ent = (uint64_t)w0.y << 32 | w0.x;
+            win1 = (uint64_t)w0.w << 32 | w0.z;
+        } else if (L > D0 && kt1) {
+            ent = kt1[u];
+        }
+        const uint32_t n0 = L <= D0 ? 0u : dtab ? ((ent >> 63) ? 1u : (uint32_t)(ent >> 32)) : iend[u] - ioff[u];
         if (n0 > 1) {
             want = 1;
             w = make_uint4((uint32_t)i, D0, ~0u, 0u);
         } else if (n0 == 1) {
             uint32_t b, e;
             uint32_t g1 = ~0u;  // the row's text position when the table entry holds it
-            if (kt1) {
+            if (dtab) {
                 if (X.kt1_pos && ((ent >> 62) & 1)) {
                     b = e = (uint32_t)ent & 0x7fffffffu;
                     g1 = (uint32_t)(ent >> 31) & 0x7fffffffu;
@@ -1209,9 +1220,11 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                 // equals the pattern's, so the next k = min(o, m) characters are decided by comparing
                 // them with the text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row)
                 rounds++;
-                const uint4 s = X.samples[b];
+                // the wide entry brought the first row's sample and text window with it (one line)
+                const bool wide = first && g1 != ~0u && kt1w;
+                const uint4 s = wide ? s1 : X.samples[b];
                 const uint32_t g = first && g1 != ~0u ? g1 : X.gpos[b];
-                n_blk += first && g1 != ~0u ? 2 : 3;
+                n_blk += wide ? 1 : first && g1 != ~0u ? 2 : 3;
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 bool eq = true, valid_codes = true;
@@ -1231,7 +1244,7 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
                         }
                         if (!valid_codes || !eq) break;
                     }
-                    eq = ((rtext_window(X.rtext, r0 + j) ^ want) & mask) == 0;
+                    eq = (((wide && j == 0 ? win1 : rtext_window(X.rtext, r0 + j)) ^ want) & mask) == 0;
                 }
                 if (!valid_codes) break;  // '#' in the pattern: the walk below takes it
                 if (!eq) {
@@ -1379,17 +1392,20 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
 // rank of `lane` among the set lanes of mask m
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t lane) { return (uint32_t)__popcll(m & ((1ull << lane) - 1ull)); }
 
-// k_deep_fast for the packed direct start, with lane refill.  k_deep_fast gives each lane one
-// pattern per grid-stride slot, so a wave waits for its slowest pattern: on C3 its lanes do useful
-// dependent load rounds 29% of the time (an average pattern needs 2.7 rounds, the slowest of 64
-// 9.5).  Here every lane is a small state machine that takes the next pattern (one atomic per
-// wave, in order, keeping the D-mer sort's locality) as soon as its own is done, and each loop
-// iteration is ONE round for every lane: the lane uses the 16-B words it loaded in the previous
-// iteration, decides what comes next, and issues that step's loads (at most two 16-B loads: an
-// entry, or the aligned 16 B holding a narrower value), so one wait covers all lanes whatever
-// step they are at.  Walk, counters, results and queue entries are k_deep_fast's for the packed
-// mode with rank entries (and no rent3): the same walk, cut into rounds.
-enum : uint32_t { RF_IDLE = 0, RF_PV, RF_ENT, RF_SAMPLE, RF_TEXT, RF_SEG, RF_PAIR, RF_SINGLE };
+// k_deep_fast for the packed direct start with lane refill and coalesced intake.  k_deep_fast
+// gives each lane one pattern per grid-stride slot, so a wave lasts as long as its slowest
+// pattern (C3: 2.7 dependent rounds on average, 9.5 for the slowest of 64).  Here a lane that
+// finishes takes the next pattern at once: each wave reads its patterns in stages of 64 (the
+// packed starts and D-mer ids in one coalesced load, perm written back coalesced), idle lanes
+// take staged patterns by lane shuffle and issue their table entry in the same round, and every
+// loop iteration is ONE round for every lane: it uses the 16-B words the lane loaded in the
+// previous iteration, decides, and issues the next step's loads (at most two), so one wait
+// covers all lanes whatever step they are at.  With the wide table (kt1w) a one-row D-mer's
+// sample and text window come with its entry: a pattern decided there costs one load round.
+// Walk, counters, results and queue entries are k_deep_fast's for the packed start with rank
+// entries and no rent3 (every pattern has at most 16 symbols after its D-mer, so one 32-symbol
+// window decides each text compare).  EDSBWT_DEEP_REFILL=0: k_deep_fast.
+enum : uint32_t { RF_IDLE = 0, RF_ENT, RF_SAMPLE, RF_TEXT, RF_SEG, RF_PAIR, RF_SINGLE };
 __device__ __forceinline__ uint32_t rf_u32(uint4 v, uint32_t part) {
     return part == 0 ? v.x : part == 1 ? v.y : part == 2 ? v.z : v.w;
 }
@@ -1408,160 +1424,138 @@ __global__ void __launch_bounds__(256) k_deep_refill(uint64_t P, uint32_t D0, co
                                                     uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
                                                     uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
                                                     const uint64_t* __restrict__ pv, uint32_t* __restrict__ perm_out,
-                                                    const uint64_t* __restrict__ kt1, uint64_t* __restrict__ q2,
-                                                    unsigned long long* __restrict__ next) {
+                                                    const uint64_t* __restrict__ kt1, const uint4* __restrict__ kt1w,
+                                                    uint64_t* __restrict__ q2) {
     unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
     const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    // the wave's stage: patterns [st_base, st_base + st_cnt), pattern st_base + l held by lane l
+    uint64_t st_pv = 0, st_base = 0, st_t = 0;
+    uint32_t st_nid = 0, st_cnt = 0, st_taken = 0;
+    bool st_ready = false, st_fresh = false, st_end = false;
     uint32_t phase = RF_IDLE;
-    bool exhausted = false;
     uint64_t i = 0, pvv = 0, rem = 0;
     uint32_t pi = 0, L = 0, d = 0, b = 0, e = 0, g = 0, c = 0, p = 0, pa = 0, pb = 0;
     uint32_t sx = 0, sy = 0, sz = 0, sw = 0;  // the row's sample (word, offset, segment, word in segment)
     bool gknown = false, pair_skip = false;
     uint4 la = make_uint4(0, 0, 0, 0), lb = make_uint4(0, 0, 0, 0);  // what the previous round loaded
     for (;;) {
-        // ---- refill: idle lanes take the next patterns (one atomic per wave)
-        const uint64_t idle = __ballot(phase == RF_IDLE && !exhausted);
-        if (idle) {
-            const int l0 = __ffsll((unsigned long long)idle) - 1;
-            unsigned long long base = 0;
-            if ((int)lane == l0) base = atomicAdd(next, (unsigned long long)__popcll(idle));
-            base = __shfl(base, l0, 64);
-            if (phase == RF_IDLE && !exhausted) {
-                i = base + lane_rank(idle, lane);
-                if (i < P) phase = RF_PV;
-                else exhausted = true;
-            }
-        }
-        if (!__ballot(phase != RF_IDLE)) break;  // every lane exhausted: the grid drains
         const uint4* ra = nullptr;
         const uint4* rb = nullptr;
         bool done = false, alive = true, res_written = false;
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
-        bool issue_sample = false, issue_step = false;
+        bool issue_sample = false, issue_step = false, text_now = false;
+        uint64_t win = 0;
+        // ---- intake: the stage loaded last round (perm written back), idle lanes take from it
+        if (st_fresh) {
+            if (lane < st_cnt) perm_out[st_base + lane] = (uint32_t)(st_pv & 0x7fffffffu);
+            st_fresh = false;
+        }
+        if (st_ready) {
+            const uint64_t idle = __ballot(phase == RF_IDLE);
+            const uint32_t r = lane_rank(idle, lane);
+            const uint32_t take = min((uint32_t)__popcll(idle), st_cnt - st_taken);
+            const uint32_t src = min(st_taken + r, 63u);
+            const uint64_t v = __shfl(st_pv, (int)src, 64);
+            const uint32_t u = __shfl(st_nid, (int)src, 64);
+            if (phase == RF_IDLE && r < take) {
+                i = st_base + st_taken + r;
+                pvv = v;
+                pi = (uint32_t)(v & 0x7fffffffu);
+                rem = v >> 31;
+                L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
+                d = D0;
+                pair_skip = false;
+                gknown = false;
+                if (L <= D0) {  // nothing after the D-mer: no list walked (k_deep_fast writes nothing either)
+                    done = true;
+                    res_written = true;
+                } else if (kt1w) {
+                    ra = kt1w + 2 * (size_t)u;
+                    rb = ra + 1;
+                    phase = RF_ENT;
+                } else {
+                    ra = rf_line(kt1 + u);
+                    pa = u & 1u;
+                    phase = RF_ENT;
+                }
+            }
+            st_taken += take;
+            if (st_taken == st_cnt) st_ready = false;
+        }
+        bool stage_load = false;
+        if (!st_ready && !st_end) {  // the next stage: this wave's t-th (wave + t * waves)
+            st_base = (wave + st_t * nwaves) * 64;
+            st_t++;
+            if (st_base >= P) {
+                st_end = true;
+            } else {
+                st_cnt = (uint32_t)min<uint64_t>(64, P - st_base);
+                st_taken = 0;
+                st_ready = st_fresh = stage_load = true;
+            }
+        }
+        if (st_end && !__ballot(phase != RF_IDLE || done)) break;  // the grid drains
         // ---- use what the last round loaded
-        switch (phase) {
-        case RF_PV:  // first round: nothing loaded yet; the packed start and the D-mer id
-            ra = rf_line(pv + i);
-            rb = rf_line(nid + i);
-            pa = (uint32_t)(i & 1);
-            pb = rf_part(nid + i);
-            phase = RF_ENT;
-            break;
-        case RF_ENT: {
-            pvv = rf_u64(la, pa);
-            pi = (uint32_t)(pvv & 0x7fffffffu);
-            rem = pvv >> 31;
-            L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
-            perm_out[i] = pi;
-            if (L <= D0) {  // nothing after the D-mer: no list walked, count 0 (k_deep_fast writes none either)
+        if (phase == RF_ENT && ra == nullptr) {
+            const uint64_t ent = kt1w ? ((uint64_t)la.y << 32 | la.x) : rf_u64(la, pa);
+            const uint32_t n0 = (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
+            if (n0 > 1) {
+                want = 1;
+                w = make_uint4((uint32_t)i, D0, ~0u, 0u);
                 done = true;
-                res_written = true;
-                break;
-            }
-            const uint32_t u = rf_u32(lb, pb);
-            ra = rf_line(kt1 + u);
-            pa = u & 1u;
-            phase = RF_SAMPLE;  // next round: the table entry (handled at RF_SAMPLE with gknown unset)
-            d = D0;
-            pair_skip = false;
-            gknown = false;
-            b = ~0u;  // the entry is pending
-            break;
-        }
-        case RF_SAMPLE:
-            if (b == ~0u) {
-                // the D-mer's table entry: one interval inline, or the list's length
-                const uint64_t ent = rf_u64(la, pa);
-                const uint32_t n0 = (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
-                if (n0 > 1) {
-                    want = 1;
-                    w = make_uint4((uint32_t)i, D0, ~0u, 0u);
-                    done = true;
-                } else if (n0 == 0) {
-                    done = true;
-                    res_written = true;  // (no result: count 0)
+            } else if (n0 == 0) {
+                done = true;
+                res_written = true;  // (no result: count 0)
+            } else {
+                if (X.kt1_pos && ((ent >> 62) & 1)) {
+                    b = e = (uint32_t)ent & 0x7fffffffu;
+                    g = (uint32_t)(ent >> 31) & 0x7fffffffu;
+                    gknown = true;
                 } else {
-                    if (X.kt1_pos && ((ent >> 62) & 1)) {
-                        b = e = (uint32_t)ent & 0x7fffffffu;
-                        g = (uint32_t)(ent >> 31) & 0x7fffffffu;
-                        gknown = true;
+                    b = (uint32_t)ent;
+                    e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+                }
+                if (X.rtext && b == e && d < L) {
+                    if (kt1w && gknown) {  // the entry brought the sample and the text window
+                        sx = lb.x; sy = lb.y; sz = lb.z; sw = lb.w;
+                        win = (uint64_t)la.w << 32 | la.z;
+                        n_blk++;
+                        n_trow++;
+                        text_now = true;
                     } else {
-                        b = (uint32_t)ent;
-                        e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+                        issue_sample = true;
                     }
-                    if (X.rtext && b == e && d < L) issue_sample = true;
-                    else issue_step = true;
-                }
-            } else {
-                // the row's sample (and text position): compare the next k = min(o, m) characters
-                sx = la.x; sy = la.y; sz = la.z; sw = la.w;
-                if (!gknown) g = rf_u32(lb, pb);
-                const uint32_t m = L - d, k = min(sy, m);
-                if (k) {
-                    const uint64_t qq = ((X.tlen - g) >> 5) & ~1ull;
-                    ra = reinterpret_cast<const uint4*>(X.rtext + qq);
-                    rb = reinterpret_cast<const uint4*>(X.rtext + qq + 2);
-                    phase = RF_TEXT;
                 } else {
-                    phase = RF_TEXT;
-                    la = lb = make_uint4(0, 0, 0, 0);  // nothing to compare: RF_TEXT below, this round
+                    issue_step = true;
                 }
             }
-            break;
-        default:
-            break;
-        }
-        if (phase == RF_TEXT && ra == nullptr) {
-            // the text window arrived (or k = 0): MOVE_EDSBWTSearch.cpp:424-510 stepping one row
-            const uint32_t m = L - d, k = min(sy, m);
-            bool eq = true;
-            if (k) {
-                const uint64_t r0 = X.tlen - g;
-                const uint32_t shf = (uint32_t)(r0 & 31u) * 2u;
-                const bool odd = ((r0 >> 5) & 1) != 0;
-                const uint64_t a0 = odd ? ((uint64_t)la.w << 32 | la.z) : ((uint64_t)la.y << 32 | la.x);
-                const uint64_t a1 = odd ? ((uint64_t)lb.y << 32 | lb.x) : ((uint64_t)la.w << 32 | la.z);
-                const uint64_t win = shf ? (a0 >> shf) | (a1 << (64 - shf)) : a0;
-                const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1ull);
-                eq = ((win ^ (rem >> (2 * (d - D0)))) & mask) == 0;
-            }
-            if (!eq) {
-                alive = false;
-                done = true;
-            } else if (sy >= m && sw <= kResCnt) {
-                n_text += m;
-                put_res(res, pi, (uint64_t)(sy - m) << 32 | sx, kResRow | kResPos | sw, sz);
-                res_written = true;
-                done = true;
-            } else if (sy >= m) {
-                issue_step = true;  // a segment of 2^30 words: the rank walk decides
+        } else if (phase == RF_SAMPLE) {
+            // the row's sample (and text position): compare the next k = min(o, m) characters
+            sx = la.x; sy = la.y; sz = la.z; sw = la.w;
+            if (!gknown) g = rf_u32(lb, pb);
+            if (min(sy, L - d)) {
+                const uint64_t qq = ((X.tlen - g) >> 5) & ~1ull;
+                ra = reinterpret_cast<const uint4*>(X.rtext + qq);
+                rb = reinterpret_cast<const uint4*>(X.rtext + qq + 2);
+                phase = RF_TEXT;
             } else {
-                // the word's first o characters matched: the link from its '#' row, one segment
-                n_text += sy;
-                d += sy;
-                c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
-                if (sz < 2) {
-                    alive = false;
-                    done = true;
-                } else {
-                    const uint32_t* et = X.segtab + (size_t)sz * X.seg_stride;
-                    ra = rf_line(et + 1 + c);
-                    rb = rf_line(et + X.seg_hi + c);
-                    pa = rf_part(et + 1 + c);
-                    pb = rf_part(et + X.seg_hi + c);
-                    n_blk++;
-                    n_steps++;
-                    phase = RF_SEG;
-                }
+                text_now = true;  // nothing to compare
             }
         } else if (phase == RF_TEXT) {
-            // (the window is being loaded this round)
-        } else if (phase == RF_SEG && ra == nullptr) {
+            const uint64_t r0 = X.tlen - g;
+            const uint32_t shf = (uint32_t)(r0 & 31u) * 2u;
+            const bool odd = ((r0 >> 5) & 1) != 0;
+            const uint64_t a0 = odd ? ((uint64_t)la.w << 32 | la.z) : ((uint64_t)la.y << 32 | la.x);
+            const uint64_t a1 = odd ? ((uint64_t)lb.y << 32 | lb.x) : ((uint64_t)la.w << 32 | la.z);
+            win = shf ? (a0 >> shf) | (a1 << (64 - shf)) : a0;
+            text_now = true;
+        } else if (phase == RF_SEG) {
             const uint32_t rx = rf_u32(la, pa), ry = rf_u32(lb, pb);
             if (ry <= rx) {
                 alive = false;
@@ -1588,8 +1582,8 @@ __global__ void __launch_bounds__(256) k_deep_refill(uint64_t P, uint32_t D0, co
                 if (d >= L) done = true;
                 else issue_step = true;
             } else {
+                // k_deep_fast's order: one step from this rank entry, then one more before the next pair
                 pair_skip = true;
-                c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
                 ra = X.rent1 + (size_t)(b >> 5) * X.sigma + c;
                 rb = X.rent1 + (size_t)((e + 1) >> 5) * X.sigma + c;
                 const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
@@ -1617,6 +1611,40 @@ __global__ void __launch_bounds__(256) k_deep_refill(uint64_t P, uint32_t D0, co
                     d++;
                     if (d >= L) done = true;
                     else issue_step = true;
+                }
+            }
+        }
+        if (text_now) {
+            // MOVE_EDSBWTSearch.cpp:424-510 stepping one row: the next k characters against the text
+            const uint32_t m = L - d, k = min(sy, m);  // m <= 16
+            const uint64_t mask = (1ull << (2 * k)) - 1ull;
+            if (k && ((win ^ (rem >> (2 * (d - D0)))) & mask) != 0) {
+                alive = false;
+                done = true;
+            } else if (sy >= m && sw <= kResCnt) {
+                n_text += m;
+                put_res(res, pi, (uint64_t)(sy - m) << 32 | sx, kResRow | kResPos | sw, sz);
+                res_written = true;
+                done = true;
+            } else if (sy >= m) {
+                issue_step = true;  // a segment of 2^30 words: the rank walk decides
+            } else {
+                // the word's first o characters matched: the link from its '#' row, one segment
+                n_text += sy;
+                d += sy;
+                c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
+                if (sz < 2) {
+                    alive = false;
+                    done = true;
+                } else {
+                    const uint32_t* et = X.segtab + (size_t)sz * X.seg_stride;
+                    ra = rf_line(et + 1 + c);
+                    rb = rf_line(et + X.seg_hi + c);
+                    pa = rf_part(et + 1 + c);
+                    pb = rf_part(et + X.seg_hi + c);
+                    n_blk++;
+                    n_steps++;
+                    phase = RF_SEG;
                 }
             }
         }
@@ -1661,6 +1689,10 @@ __global__ void __launch_bounds__(256) k_deep_refill(uint64_t P, uint32_t D0, co
             q2[at] = pvv;
         }
         // ---- this round's loads (a lane without a pending step loads nothing)
+        if (stage_load && lane < st_cnt) {
+            st_pv = pv[st_base + lane];
+            st_nid = nid[st_base + lane];
+        }
         if (ra) la = *ra;
         if (rb) lb = *rb;
     }
@@ -3436,6 +3468,29 @@ __global__ void k_ktab_one(uint64_t E, const uint32_t* __restrict__ off, const u
             one[u] = 3ull << 62 | (uint64_t)(gpos[b[o]] & 0x7fffffffu) << 31 | (b[o] & 0x7fffffffu);
         else
             one[u] = n == 1 ? (1ull << 63 | (uint64_t)e[o] << 32 | b[o]) : ((uint64_t)n << 32 | o);
+    }
+}
+
+// the wide form (k_deep_fast's direct start, one line per pattern): 32 B per D-mer — k_ktab_one's
+// entry and, for a one-row entry with its text position, the 32 characters of the reversed text
+// before the row's suffix (rtext_window at tlen - g) and the row's sample
+__global__ void k_ktab_wide(uint64_t E, const uint32_t* __restrict__ off, const uint32_t* __restrict__ b, const uint32_t* __restrict__ e,
+                            const uint32_t* __restrict__ gpos, const uint4* __restrict__ samples, const uint64_t* __restrict__ rtext,
+                            uint64_t tlen, uint4* __restrict__ w) {
+    GRID_STRIDE(u, E + 1) {
+        const uint32_t o = off[u], n = off[u + 1] - o;
+        uint64_t ent, win = 0;
+        uint4 s = make_uint4(0, 0, 0, 0);
+        if (n == 1 && b[o] == e[o]) {
+            const uint32_t g = gpos[b[o]];
+            ent = 3ull << 62 | (uint64_t)(g & 0x7fffffffu) << 31 | (b[o] & 0x7fffffffu);
+            win = rtext_window(rtext, tlen - g);
+            s = samples[b[o]];
+        } else {
+            ent = n == 1 ? (1ull << 63 | (uint64_t)e[o] << 32 | b[o]) : ((uint64_t)n << 32 | o);
+        }
+        w[2 * u] = make_uint4((uint32_t)ent, (uint32_t)(ent >> 32), (uint32_t)win, (uint32_t)(win >> 32));
+        w[2 * u + 1] = s;
     }
 }
 

@@ -411,6 +411,52 @@ def test_packed_direct_start_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             assert np.array_equal(gp, oc) and np.array_equal(gop, oo)
 
 
+def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The wide k-mer table (k_ktab_wide: 32 B per D-mer, a one-row entry carries the row's
+    sample and the 32 text characters before it, so k_deep_fast compares them with no further
+    load) against the 8-B entries (EDSBWT_KT1_WIDE=0), each with k_deep_refill and k_deep_fast
+    (EDSBWT_DEEP_REFILL), and the oracle: patterns finished inside
+    the window, ones longer than it (D0 + 33 .. D0 + 60: the compare goes on from the text),
+    crossing into earlier segments, mismatching at either end, with bytes outside the alphabet;
+    packed and unpacked direct starts, located and count-only, the text compare on and off."""
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
+    rng = random.Random(3232)
+    segs = _covid_like(rng, 700)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    assert D0 >= 2
+    short = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(2500)]
+    short = [p[: D0 + 16] if len(p) > D0 + 16 else p for p in short]
+    short += [p[:-2] + rng.choice("ACGT") + p[-1:] for p in short[:300]]   # a mismatch near the end
+    short += [rng.choice("ACGT") + p[1:] for p in short[300:600]]          # ... at the start
+    long_ = [edsgen.planted(rng, segs, rng.randint(D0 + 17, D0 + 60)) or "ACGT" * 20 for _ in range(1200)]
+    long_ += [p[:4] + "N" + p[5:] for p in long_[:100]]                       # outside the alphabet
+    sizes = {}
+    for pats, packed in ((short, "1"), (short + long_, "0")):
+        buf, offs = _pack(pats)
+        oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+        monkeypatch.setenv("EDSBWT_DIRECT_PACKED", packed)
+        for wide, refill in (("1", "1"), ("1", "0"), ("0", "1"), ("0", "0")):
+            monkeypatch.setenv("EDSBWT_KT1_WIDE", wide)
+            monkeypatch.setenv("EDSBWT_DEEP_REFILL", refill)  # k_deep_refill (packed start) or k_deep_fast
+            with edsbwt.Index(base) as idx:
+                sizes[wide] = idx.device_bytes
+                for kw in ({}, {"locate": False}, {"text": False}):
+                    gc, go = idx.search((buf, offs), **kw)
+                    st = idx.stats()
+                    assert st["start_depth"] == D0, (wide, refill, packed, kw)
+                    assert np.array_equal(gc, oc), (wide, refill, packed, kw)
+                    if kw.get("locate", True):
+                        assert np.array_equal(go, oo), (wide, refill, packed, kw)
+                    if not kw:
+                        assert st["text_rows"] > 1000, st
+    E = (4 ** D0) + 1
+    assert sizes["1"] - sizes["0"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
+
+
 @pytest.mark.parametrize("direct", [True, False])
 def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, direct):
     """Single-row intervals decided by comparing the pattern with the words' text: patterns

@@ -4,10 +4,10 @@
 export TMPDIR=/tmp
 TAG=${1:-r3n}
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -k "direct or pair or single_row or deferred or production or many_chunks or kmer_start or grouped or smoke or console" > gpurun_out/${TAG}_pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -k "${TESTS:-direct or pair or single_row or deferred or production or many_chunks or kmer_start or grouped or smoke or console}" > gpurun_out/${TAG}_pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
 tail -1 gpurun_out/${TAG}_pytest.log
 w() { python -c "import json,sys; d=json.loads(sys.stdin.readline()); print(d['value'], d['ms_per_step'], d['device_resident']['kernel_ms_per_step'])"; }
-for spec in "X=1" "EDSBWT_DEEP_REFILL=0" "X=2"; do
+for spec in ${SPECS:-X=1 EDSBWT_DEEP_REFILL=0 X=2}; do
   echo "== c3 $spec" >> gpurun_out/${TAG}_ab.txt
   env $spec timeout -k 10 200 python bench.py --no-cpu --no-e2e --steps 20 --warmup 3 2>/dev/null | w >> gpurun_out/${TAG}_ab.txt || exit 1
   echo "== c2 $spec" >> gpurun_out/${TAG}_ab.txt
