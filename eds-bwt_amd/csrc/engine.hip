@@ -218,7 +218,12 @@ struct Engine {
     bool use_direct = true;     // direct start from the table (EDSBWT_NO_DIRECT turns it off)
     bool direct_sort = env_double("EDSBWT_DIRECT_SORT", 1) != 0;  // direct start: patterns sorted by D-mer
     bool use_packed = env_double("EDSBWT_DIRECT_PACKED", 1) != 0;  // ... carrying index + remaining symbols
-    int direct_sort_bits = (int)env_double("EDSBWT_DIRECT_SORT_BITS", 16);  // ... by the D-mer's leading bits (C3 A/B, round 1: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9; round 2: 16 bits 3.115 ms against 20 bits 3.145)
+    // (default -1: 16 bits, or input order with the wide k-mer table — C3, round 3: 1.96 ms
+    // against 2.22 sorted, the deep walk equal: a wide entry brings what the order shared)
+    // ... by the D-mer's leading bits (C3 A/B, round 1: 20 bits 2.67e9, 30 2.52e9, 12 2.43e9; round 2:
+    // 16 bits 3.115 ms against 20 bits 3.145)
+    int direct_sort_bits_env = (int)env_double("EDSBWT_DIRECT_SORT_BITS", -1);
+    int sort_bits() const { return direct_sort_bits_env >= 0 ? direct_sort_bits_env : ktab_wide.p ? 0 : 16; }
     // ... for batches of at least this many patterns (C3 pipeline chunks: 7.84 ms per call against
     // 7.92-8.06 sorting every chunk)
     uint64_t direct_sort_min = (uint64_t)env_double("EDSBWT_DIRECT_SORT_MIN", 2000000);
@@ -449,9 +454,6 @@ struct Engine {
     static constexpr uint32_t kWideCap = 16384;
     // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
     bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;
-    // packed direct start: k_deep_refill (lane refill, coalesced intake); EDSBWT_DEEP_REFILL=0: k_deep_fast
-    bool deep_refill = env_double("EDSBWT_DEEP_REFILL", 1) != 0;
-    unsigned refill_blocks = 0;  // its resident grid (occupancy x CUs)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -1465,24 +1467,9 @@ struct Engine {
         const bool dstart = goff == ktab_off.p;
         const uint64_t* kt1 = dstart && ktab_one.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr;
         const uint4* kt1w = dstart && ktab_wide.p ? (const uint4*)ktab_wide.p : (const uint4*)nullptr;
-        if (deep_refill && pv && (kt1 || kt1w) && X.rent1 && !X.rent3) {
-            // packed direct start: the lane-refill walk (same results, counters and queue); waves
-            // take stages of 64 patterns, this wave's t-th is stage (wave + t * waves)
-            // (no more blocks than stay resident: a late wave would run its whole share after the rest)
-            if (!refill_blocks) {
-                int per_cu = 0, cus = 0;
-                HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_deep_refill, 256, 0));
-                HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-                refill_blocks = (unsigned)std::max(1, per_cu * cus);
-            }
-            const unsigned G = (unsigned)std::min<uint64_t>((P + 255) / 256, refill_blocks);
-            launch_grid(KC_DEEP, k_deep_refill, G, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p,
-                        kt1, kt1w, dq2.p);
-        } else {
-            launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
-                   nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
-                   pv ? dq2.p : (uint64_t*)nullptr, kt1w);
-        }
+        launch(KC_DEEP, bps == 3 ? k_deep_fast<3> : k_deep_fast<4>, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
+               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
+               pv ? dq2.p : (uint64_t*)nullptr, kt1w);
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
@@ -1568,9 +1555,9 @@ struct Engine {
     static constexpr uint32_t kNotDirect = 0xFFFFFFFEu;
     // buckets of the direct start's grouping (0: the radix sort path or no direct start)
     uint64_t direct_buckets() const {
-        if (!ktab_depth || !use_buckets || direct_sort_bits <= 0) return 0;
+        if (!ktab_depth || !use_buckets || sort_bits() <= 0) return 0;
         const uint64_t E = ktab_entries;
-        const int shift = std::max(0, (int)bits_for(E) - direct_sort_bits);
+        const int shift = std::max(0, (int)bits_for(E) - sort_bits());
         const uint64_t nb = (E >> shift) + 1;
         return nb <= (1u << 22) ? nb : 0;
     }
@@ -1625,6 +1612,7 @@ struct Engine {
         // the packed start's grouping by the D-mer's leading bits: a bucket histogram from k_keys,
         // a scan, one scatter (EDSBWT_BUCKETS=0: hipcub radix sort over those bits instead)
         const int endbit_e = (int)bits_for(E);
+        const int direct_sort_bits = sort_bits();
         const uint32_t hshift = (uint32_t)std::max(0, endbit_e - direct_sort_bits);
         const uint64_t nbkt = direct_buckets();
         const bool buckets = packed && nbkt;

@@ -1392,318 +1392,6 @@ __global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, cons
 // rank of `lane` among the set lanes of mask m
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t lane) { return (uint32_t)__popcll(m & ((1ull << lane) - 1ull)); }
 
-// k_deep_fast for the packed direct start with lane refill and coalesced intake.  k_deep_fast
-// gives each lane one pattern per grid-stride slot, so a wave lasts as long as its slowest
-// pattern (C3: 2.7 dependent rounds on average, 9.5 for the slowest of 64).  Here a lane that
-// finishes takes the next pattern at once: each wave reads its patterns in stages of 64 (the
-// packed starts and D-mer ids in one coalesced load, perm written back coalesced), idle lanes
-// take staged patterns by lane shuffle and issue their table entry in the same round, and every
-// loop iteration is ONE round for every lane: it uses the 16-B words the lane loaded in the
-// previous iteration, decides, and issues the next step's loads (at most two), so one wait
-// covers all lanes whatever step they are at.  With the wide table (kt1w) a one-row D-mer's
-// sample and text window come with its entry: a pattern decided there costs one load round.
-// Walk, counters, results and queue entries are k_deep_fast's for the packed start with rank
-// entries and no rent3 (every pattern has at most 16 symbols after its D-mer, so one 32-symbol
-// window decides each text compare).  EDSBWT_DEEP_REFILL=0: k_deep_fast.
-enum : uint32_t { RF_IDLE = 0, RF_ENT, RF_SAMPLE, RF_TEXT, RF_SEG, RF_PAIR, RF_SINGLE };
-__device__ __forceinline__ uint32_t rf_u32(uint4 v, uint32_t part) {
-    return part == 0 ? v.x : part == 1 ? v.y : part == 2 ? v.z : v.w;
-}
-__device__ __forceinline__ uint64_t rf_u64(uint4 v, uint32_t part) {
-    return part == 0 ? ((uint64_t)v.y << 32 | v.x) : ((uint64_t)v.w << 32 | v.z);
-}
-template <typename T>
-__device__ __forceinline__ const uint4* rf_line(const T* p) {  // the aligned 16 B holding *p
-    return reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)15);
-}
-template <typename T>
-__device__ __forceinline__ uint32_t rf_part(const T* p) {  // which 4-B word of it
-    return (uint32_t)((reinterpret_cast<uintptr_t>(p) >> 2) & 3);
-}
-__global__ void __launch_bounds__(256) k_deep_refill(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
-                                                    uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
-                                                    uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
-                                                    const uint64_t* __restrict__ pv, uint32_t* __restrict__ perm_out,
-                                                    const uint64_t* __restrict__ kt1, const uint4* __restrict__ kt1w,
-                                                    uint64_t* __restrict__ q2) {
-    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
-    const uint32_t sh = blockIdx.x % NSHARD;
-    q += (size_t)sh * qcap;
-    q2 += (size_t)sh * qcap;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    // the wave's stage: patterns [st_base, st_base + st_cnt), pattern st_base + l held by lane l
-    uint64_t st_pv = 0, st_base = 0, st_t = 0;
-    uint32_t st_nid = 0, st_cnt = 0, st_taken = 0;
-    bool st_ready = false, st_fresh = false, st_end = false;
-    uint32_t phase = RF_IDLE;
-    uint64_t i = 0, pvv = 0, rem = 0;
-    uint32_t pi = 0, L = 0, d = 0, b = 0, e = 0, g = 0, c = 0, p = 0, pa = 0, pb = 0;
-    uint32_t sx = 0, sy = 0, sz = 0, sw = 0;  // the row's sample (word, offset, segment, word in segment)
-    bool gknown = false, pair_skip = false;
-    uint4 la = make_uint4(0, 0, 0, 0), lb = make_uint4(0, 0, 0, 0);  // what the previous round loaded
-    for (;;) {
-        const uint4* ra = nullptr;
-        const uint4* rb = nullptr;
-        bool done = false, alive = true, res_written = false;
-        uint32_t want = 0;
-        uint4 w = make_uint4(0, 0, 0, 0);
-        bool issue_sample = false, issue_step = false, text_now = false;
-        uint64_t win = 0;
-        // ---- intake: the stage loaded last round (perm written back), idle lanes take from it
-        if (st_fresh) {
-            if (lane < st_cnt) perm_out[st_base + lane] = (uint32_t)(st_pv & 0x7fffffffu);
-            st_fresh = false;
-        }
-        if (st_ready) {
-            const uint64_t idle = __ballot(phase == RF_IDLE);
-            const uint32_t r = lane_rank(idle, lane);
-            const uint32_t take = min((uint32_t)__popcll(idle), st_cnt - st_taken);
-            const uint32_t src = min(st_taken + r, 63u);
-            const uint64_t v = __shfl(st_pv, (int)src, 64);
-            const uint32_t u = __shfl(st_nid, (int)src, 64);
-            if (phase == RF_IDLE && r < take) {
-                i = st_base + st_taken + r;
-                pvv = v;
-                pi = (uint32_t)(v & 0x7fffffffu);
-                rem = v >> 31;
-                L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
-                d = D0;
-                pair_skip = false;
-                gknown = false;
-                if (L <= D0) {  // nothing after the D-mer: no list walked (k_deep_fast writes nothing either)
-                    done = true;
-                    res_written = true;
-                } else if (kt1w) {
-                    ra = kt1w + 2 * (size_t)u;
-                    rb = ra + 1;
-                    phase = RF_ENT;
-                } else {
-                    ra = rf_line(kt1 + u);
-                    pa = u & 1u;
-                    phase = RF_ENT;
-                }
-            }
-            st_taken += take;
-            if (st_taken == st_cnt) st_ready = false;
-        }
-        bool stage_load = false;
-        if (!st_ready && !st_end) {  // the next stage: this wave's t-th (wave + t * waves)
-            st_base = (wave + st_t * nwaves) * 64;
-            st_t++;
-            if (st_base >= P) {
-                st_end = true;
-            } else {
-                st_cnt = (uint32_t)min<uint64_t>(64, P - st_base);
-                st_taken = 0;
-                st_ready = st_fresh = stage_load = true;
-            }
-        }
-        if (st_end && !__ballot(phase != RF_IDLE || done)) break;  // the grid drains
-        // ---- use what the last round loaded
-        if (phase == RF_ENT && ra == nullptr) {
-            const uint64_t ent = kt1w ? ((uint64_t)la.y << 32 | la.x) : rf_u64(la, pa);
-            const uint32_t n0 = (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
-            if (n0 > 1) {
-                want = 1;
-                w = make_uint4((uint32_t)i, D0, ~0u, 0u);
-                done = true;
-            } else if (n0 == 0) {
-                done = true;
-                res_written = true;  // (no result: count 0)
-            } else {
-                if (X.kt1_pos && ((ent >> 62) & 1)) {
-                    b = e = (uint32_t)ent & 0x7fffffffu;
-                    g = (uint32_t)(ent >> 31) & 0x7fffffffu;
-                    gknown = true;
-                } else {
-                    b = (uint32_t)ent;
-                    e = (uint32_t)(ent >> 32) & 0x7fffffffu;
-                }
-                if (X.rtext && b == e && d < L) {
-                    if (kt1w && gknown) {  // the entry brought the sample and the text window
-                        sx = lb.x; sy = lb.y; sz = lb.z; sw = lb.w;
-                        win = (uint64_t)la.w << 32 | la.z;
-                        n_blk++;
-                        n_trow++;
-                        text_now = true;
-                    } else {
-                        issue_sample = true;
-                    }
-                } else {
-                    issue_step = true;
-                }
-            }
-        } else if (phase == RF_SAMPLE) {
-            // the row's sample (and text position): compare the next k = min(o, m) characters
-            sx = la.x; sy = la.y; sz = la.z; sw = la.w;
-            if (!gknown) g = rf_u32(lb, pb);
-            if (min(sy, L - d)) {
-                const uint64_t qq = ((X.tlen - g) >> 5) & ~1ull;
-                ra = reinterpret_cast<const uint4*>(X.rtext + qq);
-                rb = reinterpret_cast<const uint4*>(X.rtext + qq + 2);
-                phase = RF_TEXT;
-            } else {
-                text_now = true;  // nothing to compare
-            }
-        } else if (phase == RF_TEXT) {
-            const uint64_t r0 = X.tlen - g;
-            const uint32_t shf = (uint32_t)(r0 & 31u) * 2u;
-            const bool odd = ((r0 >> 5) & 1) != 0;
-            const uint64_t a0 = odd ? ((uint64_t)la.w << 32 | la.z) : ((uint64_t)la.y << 32 | la.x);
-            const uint64_t a1 = odd ? ((uint64_t)lb.y << 32 | lb.x) : ((uint64_t)la.w << 32 | la.z);
-            win = shf ? (a0 >> shf) | (a1 << (64 - shf)) : a0;
-            text_now = true;
-        } else if (phase == RF_SEG) {
-            const uint32_t rx = rf_u32(la, pa), ry = rf_u32(lb, pb);
-            if (ry <= rx) {
-                alive = false;
-                done = true;
-            } else {
-                b = X.C[c] + rx;
-                e = X.C[c] + ry - 1;
-                d++;
-                gknown = false;
-                if (d >= L) done = true;
-                else if (X.rtext && b == e) issue_sample = true;
-                else issue_step = true;
-            }
-        } else if (phase == RF_PAIR) {
-            // a two-step rank entry per end
-            uint32_t p0, x0, p1, x1;
-            rent_rank(la, b, p0, x0);
-            rent_rank(lb, e + 1, p1, x1);
-            if (x1 == x0 && p1 > p0) {
-                n_steps += 2;
-                b = X.PC[p] + p0;
-                e = X.PC[p] + p1 - 1;
-                d += 2;
-                if (d >= L) done = true;
-                else issue_step = true;
-            } else {
-                // k_deep_fast's order: one step from this rank entry, then one more before the next pair
-                pair_skip = true;
-                ra = X.rent1 + (size_t)(b >> 5) * X.sigma + c;
-                rb = X.rent1 + (size_t)((e + 1) >> 5) * X.sigma + c;
-                const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
-                n_blk += nl;
-                n_pl += nl;
-                phase = RF_SINGLE;
-            }
-        } else if (phase == RF_SINGLE) {
-            // a one-step rank entry per end (rank of c and of '#')
-            uint32_t h0, sb, h1, se;
-            rent_rank(la, b, sb, h0);
-            rent_rank(lb, e + 1, se, h1);
-            if (h1 > h0) {  // '#' rows: the link needs k_deep
-                want = 1;
-                w = make_uint4((uint32_t)i, d, b, e);
-                done = true;
-            } else {
-                n_steps++;
-                if (se <= sb) {
-                    alive = false;
-                    done = true;
-                } else {
-                    b = X.C[c] + sb;
-                    e = X.C[c] + se - 1;
-                    d++;
-                    if (d >= L) done = true;
-                    else issue_step = true;
-                }
-            }
-        }
-        if (text_now) {
-            // MOVE_EDSBWTSearch.cpp:424-510 stepping one row: the next k characters against the text
-            const uint32_t m = L - d, k = min(sy, m);  // m <= 16
-            const uint64_t mask = (1ull << (2 * k)) - 1ull;
-            if (k && ((win ^ (rem >> (2 * (d - D0)))) & mask) != 0) {
-                alive = false;
-                done = true;
-            } else if (sy >= m && sw <= kResCnt) {
-                n_text += m;
-                put_res(res, pi, (uint64_t)(sy - m) << 32 | sx, kResRow | kResPos | sw, sz);
-                res_written = true;
-                done = true;
-            } else if (sy >= m) {
-                issue_step = true;  // a segment of 2^30 words: the rank walk decides
-            } else {
-                // the word's first o characters matched: the link from its '#' row, one segment
-                n_text += sy;
-                d += sy;
-                c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
-                if (sz < 2) {
-                    alive = false;
-                    done = true;
-                } else {
-                    const uint32_t* et = X.segtab + (size_t)sz * X.seg_stride;
-                    ra = rf_line(et + 1 + c);
-                    rb = rf_line(et + X.seg_hi + c);
-                    pa = rf_part(et + 1 + c);
-                    pb = rf_part(et + X.seg_hi + c);
-                    n_blk++;
-                    n_steps++;
-                    phase = RF_SEG;
-                }
-            }
-        }
-        // ---- the next step's loads
-        if (issue_sample) {
-            // one row = one text position: its sample, and its text position unless known
-            ra = reinterpret_cast<const uint4*>(X.samples + b);
-            if (!gknown) { rb = rf_line(X.gpos + b); pb = rf_part(X.gpos + b); }
-            n_blk += gknown ? 2 : 3;
-            n_trow++;
-            phase = RF_SAMPLE;
-        } else if (issue_step) {
-            c = 1u + (uint32_t)((rem >> (2 * (d - D0))) & 3u);
-            if (X.rent2 && !pair_skip && d + 1 < L) {
-                const uint32_t c2 = 1u + (uint32_t)((rem >> (2 * (d + 1 - D0))) & 3u);
-                p = 1 + (c - 1) * X.sigma + c2;
-                ra = X.rent2 + (size_t)(b >> 5) * X.r2stride + p - 1;
-                rb = X.rent2 + (size_t)((e + 1) >> 5) * X.r2stride + p - 1;
-                phase = RF_PAIR;
-            } else {
-                pair_skip = false;
-                ra = X.rent1 + (size_t)(b >> 5) * X.sigma + c;
-                rb = X.rent1 + (size_t)((e + 1) >> 5) * X.sigma + c;
-                phase = RF_SINGLE;
-            }
-            const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
-            n_blk += nl;
-            n_pl += nl;
-        }
-        // ---- a finished pattern: its result, or its queue entry
-        if (done) {
-            if (!want && !res_written) {
-                if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
-                else put_res(res, pi, abase + i * K, 0u, 0u);
-            }
-            phase = RF_IDLE;
-            ra = rb = nullptr;
-        }
-        const uint32_t at = wave_append(qcnt + sh * 32, want);
-        if (want && at < qcap) {
-            q[at] = w;
-            q2[at] = pvv;
-        }
-        // ---- this round's loads (a lane without a pending step loads nothing)
-        if (stage_load && lane < st_cnt) {
-            st_pv = pv[st_base + lane];
-            st_nid = nid[st_base + lane];
-        }
-        if (ra) la = *ra;
-        if (rb) lb = *rb;
-    }
-    __shared__ unsigned long long ssum[4];
-    stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
-    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
-    stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
-    stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
-    stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
-}
-
 // shard prefix sums of k_deep_fast's queue counters (one block)
 __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __restrict__ qpre) {
     if (threadIdx.x == 0) {

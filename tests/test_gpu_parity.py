@@ -414,11 +414,11 @@ def test_packed_direct_start_gpu(oracle, edsbwt, tmp_path, monkeypatch):
 def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     """The wide k-mer table (k_ktab_wide: 32 B per D-mer, a one-row entry carries the row's
     sample and the 32 text characters before it, so k_deep_fast compares them with no further
-    load) against the 8-B entries (EDSBWT_KT1_WIDE=0), each with k_deep_refill and k_deep_fast
-    (EDSBWT_DEEP_REFILL), and the oracle: patterns finished inside
+    load) against the 8-B entries (EDSBWT_KT1_WIDE=0) and the oracle: patterns finished inside
     the window, ones longer than it (D0 + 33 .. D0 + 60: the compare goes on from the text),
     crossing into earlier segments, mismatching at either end, with bytes outside the alphabet;
-    packed and unpacked direct starts, located and count-only, the text compare on and off."""
+    packed and unpacked direct starts, in input order (the default with the wide table) and
+    sorted by D-mer, located and count-only, the text compare on and off."""
     monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
     rng = random.Random(3232)
     segs = _covid_like(rng, 700)
@@ -439,18 +439,19 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         buf, offs = _pack(pats)
         oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
         monkeypatch.setenv("EDSBWT_DIRECT_PACKED", packed)
-        for wide, refill in (("1", "1"), ("1", "0"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("EDSBWT_DIRECT_SORT_MIN", "0")  # the D-mer sort even for this small batch, when on
+        for wide, sort_bits in (("1", "-1"), ("1", "16"), ("0", "-1")):  # -1: the default (input order when wide)
             monkeypatch.setenv("EDSBWT_KT1_WIDE", wide)
-            monkeypatch.setenv("EDSBWT_DEEP_REFILL", refill)  # k_deep_refill (packed start) or k_deep_fast
+            monkeypatch.setenv("EDSBWT_DIRECT_SORT_BITS", sort_bits)
             with edsbwt.Index(base) as idx:
                 sizes[wide] = idx.device_bytes
                 for kw in ({}, {"locate": False}, {"text": False}):
                     gc, go = idx.search((buf, offs), **kw)
                     st = idx.stats()
-                    assert st["start_depth"] == D0, (wide, refill, packed, kw)
-                    assert np.array_equal(gc, oc), (wide, refill, packed, kw)
+                    assert st["start_depth"] == D0, (wide, sort_bits, packed, kw)
+                    assert np.array_equal(gc, oc), (wide, sort_bits, packed, kw)
                     if kw.get("locate", True):
-                        assert np.array_equal(go, oo), (wide, refill, packed, kw)
+                        assert np.array_equal(go, oo), (wide, sort_bits, packed, kw)
                     if not kw:
                         assert st["text_rows"] > 1000, st
     E = (4 ** D0) + 1

@@ -17,6 +17,9 @@
 //                        previous step's values; W = waves per SIMD the launch is held to
 //                        (dynamic LDS), so the ceiling is measured at a kernel's occupancy.
 //   calib_gather --chain [table_MB ...]   runs only the chain shapes
+//   calib_gather --tlb [table_MB ...]     gather16 with 64-bit indices over tables up to 128 GB: the
+//                        rate of random 16-B loads as the table outgrows the GPU's address translation
+//                        caches (the wide k-mer table is 34 GB at C3)
 //   calib_gather --window [table_MB ...]  one 16-B load per random 64-B block within a window that
 //                        slides over the table (row-bucketed items): accesses/s per window size
 // Algorithmic bytes are known exactly, so running this under
@@ -60,6 +63,44 @@ __global__ void __launch_bounds__(256) k_gather(const uint4* __restrict__ t, uin
         for (int k = 0; k < LINES16; k++) acc ^= v[k].x + v[k].y + v[k].z + v[k].w;
     }
     if (acc == 0x12345678u) sink[g] = acc;  // keeps the loads alive; never true in practice
+}
+
+// gather16 over a table of n16 16-B entries (n16 may exceed 2^32)
+__global__ void __launch_bounds__(256) k_gather16w(const uint4* __restrict__ t, uint64_t n16, uint32_t iters, uint32_t seed,
+                                                   uint32_t* __restrict__ sink) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t h = mix(g ^ seed), acc = 0;
+    for (uint32_t i = 0; i < iters; i++) {
+        h = mix(h + i);
+        const uint64_t x = ((uint64_t)mix(h ^ 0x9e3779b9u) << 32 | h) % n16;
+        const uint4 v = t[x];
+        acc ^= v.x + v.y + v.z + v.w;
+    }
+    if (acc == 0x12345678u) sink[g] = acc;
+}
+
+static void tlb(size_t mb, uint32_t* sink, hipEvent_t a, hipEvent_t b) {
+    const size_t bytes = mb << 20;
+    uint4* t;
+    CK(hipMalloc(&t, bytes));
+    CK(hipMemset(t, 7, bytes));
+    const uint32_t grid = 256 * 32, block = 256, iters = 64;
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; rep++) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_gather16w, dim3(grid), dim3(block), 0, 0, t, (uint64_t)(bytes / 16), iters, 23u + rep, sink);
+        CK(hipGetLastError());
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (rep > 0 && ms < best) best = ms;
+    }
+    const double loads = (double)grid * block * iters;
+    std::printf("{\"shape\": \"gather16_tlb\", \"table_MB\": %zu, \"loads\": %.0f, \"best_ms\": %.4f, \"loads_per_s\": %.4g}\n", mb,
+                loads, best, loads / (best * 1e-3));
+    std::fflush(stdout);
+    CK(hipFree(t));
 }
 
 // the deep walk's access shape: per lane, patterns of `steps` dependent steps; each step
@@ -189,15 +230,20 @@ static void windows(size_t mb, uint32_t* sink, hipEvent_t a, hipEvent_t b) {
 
 int main(int argc, char** argv) {
     std::vector<size_t> mbs;
-    bool chain_only = false, window_only = false;
+    bool chain_only = false, window_only = false, tlb_only = false;
     for (int i = 1; i < argc; i++) {
         if (std::string(argv[i]) == "--chain") chain_only = true;
         else if (std::string(argv[i]) == "--window") window_only = true;
+        else if (std::string(argv[i]) == "--tlb") tlb_only = true;
         else {
             char* end = nullptr;
             const unsigned long long v = std::strtoull(argv[i], &end, 10);
             if (!end || *end || v < 16) {  // a table under 16 MB (or not a number) is refused, not launched
                 std::fprintf(stderr, "calib_gather: bad table size '%s' (MB, >= 16)\n", argv[i]);
+                return 2;
+            }
+            if (v > 131072) {  // 128 GB at most
+                std::fprintf(stderr, "calib_gather: table size '%s' MB too large\n", argv[i]);
                 return 2;
             }
             mbs.push_back(v);
@@ -210,6 +256,15 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
+    if (tlb_only) {
+        for (size_t mb : mbs) tlb(mb, sink, a, b);
+        return 0;
+    }
+    for (size_t mb : mbs)
+        if (mb > 16384) {  // the other shapes index with 32 bits
+            std::fprintf(stderr, "calib_gather: tables over 16384 MB only with --tlb\n");
+            return 2;
+        }
     if (window_only) {
         for (size_t mb : mbs) windows(mb, sink, a, b);
         return 0;
