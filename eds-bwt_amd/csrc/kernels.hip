@@ -1136,8 +1136,8 @@ struct SymReader {
 // a list or a link is queued as (pattern, depth, b, e) — b = ~0u: "from its node's
 // items" — and k_deep finishes the queued ones with register lists.  The queue is
 // sharded like the item appends (region s at s*qcap, counter s at qcnt[s*32]).
-template <int BPS>
-__global__ void __launch_bounds__(256) k_deep_fast(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
+template <int BPS, int MINW = 1>  // MINW: waves per SIMD the register budget is held to (1: no bound)
+__global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0, const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
                                                    const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind,
                                                    const uint32_t* __restrict__ nid,
                                                    const uint32_t* __restrict__ ioff, const uint32_t* __restrict__ iend,
@@ -1401,8 +1401,8 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
     }
 }
 
-template <int K, int BPS>
-__global__ void __launch_bounds__(256) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
+template <int K, int BPS, int MINW = 1>  // MINW: waves per SIMD the register budget is held to (1: no bound)
+__global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
                                               const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind, uint64_t P,
                                               const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
