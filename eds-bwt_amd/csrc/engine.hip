@@ -455,7 +455,11 @@ struct Engine {
     // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
     bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;
     // k_deep_fast's register budget: waves per SIMD (5 unbounded; 6 without scratch; 8 spills)
-    int deep_waves = (int)env_double("EDSBWT_DEEP_WAVES", 5);
+    int deep_waves = (int)env_double("EDSBWT_DEEP_WAVES", 6);
+    // the packed start with the wide table: k_deep_direct (EDSBWT_DEEP_DIRECT=0: k_deep_fast), held
+    // to EDSBWT_DIRECT_WAVES waves per SIMD
+    bool deep_direct = env_double("EDSBWT_DEEP_DIRECT", 1) != 0;
+    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 1);
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 4);  // k_deep<4, 3> likewise (4 unbounded)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
@@ -1470,10 +1474,16 @@ struct Engine {
         const bool dstart = goff == ktab_off.p;
         const uint64_t* kt1 = dstart && ktab_one.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr;
         const uint4* kt1w = dstart && ktab_wide.p ? (const uint4*)ktab_wide.p : (const uint4*)nullptr;
-        auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
-        launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
-               nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
-               pv ? dq2.p : (uint64_t*)nullptr, kt1w);
+        if (pv && kt1w && !X.rent3 && deep_direct) {
+            auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
+                                                                                                        : k_deep_direct<1>;
+            launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p);
+        } else {
+            auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
+            launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
+                   nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
+                   pv ? dq2.p : (uint64_t*)nullptr, kt1w);
+        }
         hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)

@@ -1389,6 +1389,169 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
     stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
 }
 
+// k_deep_fast specialised to the path C3 takes: the packed direct start (pv: input index and
+// <= 16 remaining symbols as 2-bit digits) with the wide k-mer table (kt1w) and no three-step
+// entries.  Same walk, results, queue entries and counters as k_deep_fast there; without the
+// generic key-chunk reader, list offsets and rent3 it needs fewer registers, and the walk is
+// latency-bound (C3: 6 waves per SIMD instead of 5 took k_deep_fast from 1.02 to 0.92 ms).
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
+                                                           uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
+                                                           uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
+                                                           const uint64_t* __restrict__ pv, uint32_t* __restrict__ perm_out,
+                                                           const uint4* __restrict__ kt1w, uint64_t* __restrict__ q2) {
+    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
+    const uint32_t sh = blockIdx.x % NSHARD;
+    q += (size_t)sh * qcap;
+    q2 += (size_t)sh * qcap;
+    UNIFORM_STRIDE(i, valid, P) {
+        uint32_t want = 0;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        const uint64_t v = valid ? pv[i] : 0ull;
+        const uint32_t pi = (uint32_t)(v & 0x7fffffffu);
+        const uint64_t rem = v >> 31;
+        const uint32_t L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
+        if (valid) perm_out[i] = pi;
+        // the D-mer's wide entry: its one interval inline (or its list's length), and for one
+        // row with its text position, the row's sample and the 32 text characters before it
+        uint64_t ent = 0, win1 = 0;
+        uint4 s1 = make_uint4(0, 0, 0, 0);
+        if (L > D0) {
+            const size_t u = nid[i];
+            const uint4 w0 = kt1w[2 * u];
+            s1 = kt1w[2 * u + 1];
+            ent = (uint64_t)w0.y << 32 | w0.x;
+            win1 = (uint64_t)w0.w << 32 | w0.z;
+        }
+        const uint32_t n0 = L <= D0 ? 0u : (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
+        if (n0 > 1) {
+            want = 1;
+            w = make_uint4((uint32_t)i, D0, ~0u, 0u);
+        } else if (n0 == 1) {
+            uint32_t b, e, g1 = ~0u;
+            if (X.kt1_pos && ((ent >> 62) & 1)) {
+                b = e = (uint32_t)ent & 0x7fffffffu;
+                g1 = (uint32_t)(ent >> 31) & 0x7fffffffu;
+            } else {
+                b = (uint32_t)ent;
+                e = (uint32_t)(ent >> 32) & 0x7fffffffu;
+            }
+            auto code_at = [&](uint32_t dd) -> uint32_t { return 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u); };
+            bool alive = true, pair_skip = false, posres = false;
+            uint32_t d = D0;
+            for (bool first = true; X.rtext && b == e && d < L; first = false) {
+                // one row = one text position: the next k = min(o, m) <= 16 characters against the
+                // text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row), as in k_deep_fast
+                const bool wide = first && g1 != ~0u;
+                const uint4 s = wide ? s1 : X.samples[b];
+                const uint32_t g = wide ? g1 : X.gpos[b];
+                n_blk += wide ? 1 : 3;
+                n_trow++;
+                const uint32_t m = L - d, k = min(s.y, m);
+                if (k) {
+                    const uint64_t mask = (1ull << (2 * k)) - 1ull;
+                    const uint64_t tw = wide ? win1 : rtext_window(X.rtext, X.tlen - g);
+                    if (((tw ^ (rem >> (2 * (d - D0)))) & mask) != 0) {
+                        alive = false;
+                        d = L;
+                        break;
+                    }
+                }
+                if (s.y >= m) {
+                    if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
+                        posres = true;
+                        n_text += m;
+                        d = L;
+                        put_res(res, pi, (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                    }
+                    break;
+                }
+                // the word matched to its start: the link from its '#' row, one segment (:512-563)
+                n_text += s.y;
+                d += s.y;
+                const uint32_t c = code_at(d);
+                if (c >= X.sigma) {
+                    b = e = X.wrow[s.x];
+                    n_blk++;
+                    break;
+                }
+                if (s.z < 2) {
+                    alive = false;
+                    d = L;
+                    break;
+                }
+                const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
+                const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
+                n_blk++;
+                n_steps++;
+                if (ry <= rx) {
+                    alive = false;
+                    d = L;
+                    break;
+                }
+                b = X.C[c] + rx;
+                e = X.C[c] + ry - 1;
+                d++;
+            }
+            for (; d < L; d++) {
+                const uint32_t c = code_at(d);
+                if (c >= X.sigma) { alive = false; break; }
+                // two characters from one rank entry per interval end (rent2), else one step
+                if (X.rent2 && !pair_skip && d + 1 < L) {
+                    const uint32_t c2 = code_at(d + 1);
+                    if (c2 < X.sigma) {
+                        const uint32_t p = 1 + (c - 1) * X.sigma + c2;
+                        const uint4 v0 = X.rent2[(size_t)(b >> 5) * X.r2stride + p - 1];
+                        const uint4 v1 = X.rent2[(size_t)((e + 1) >> 5) * X.r2stride + p - 1];
+                        uint32_t p0, x0, p1, x1;
+                        rent_rank(v0, b, p0, x0);
+                        rent_rank(v1, e + 1, p1, x1);
+                        const uint32_t nl = (b >> 5) == ((e + 1) >> 5) ? 1 : 2;
+                        n_blk += nl;
+                        n_pl += nl;
+                        if (x1 == x0 && p1 > p0) {
+                            n_steps += 2;
+                            b = X.PC[p] + p0;
+                            e = X.PC[p] + p1 - 1;
+                            d++;
+                            continue;
+                        }
+                        pair_skip = true;
+                    }
+                } else {
+                    pair_skip = false;
+                }
+                uint32_t h0, h1, sb, se;
+                const uint32_t nl = 2 - rank2_any(X, b, e + 1, c, h0, sb, h1, se);
+                n_blk += nl;
+                if (X.rent1) n_pl += nl;
+                if (h1 > h0) { want = 1; break; }  // '#' rows: the link needs k_deep
+                n_steps++;
+                if (se <= sb) { alive = false; break; }
+                b = X.C[c] + sb;
+                e = X.C[c] + se - 1;
+            }
+            if (want) {
+                w = make_uint4((uint32_t)i, d, b, e);
+            } else if (!posres) {
+                if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
+                else put_res(res, pi, abase + i * K, 0u, 0u);
+            }
+        }
+        const uint32_t at = wave_append(qcnt + sh * 32, want);
+        if (want && at < qcap) {
+            q[at] = w;
+            q2[at] = v;  // k_deep reads the packed start instead of perm, slen and the key chunks
+        }
+    }
+    __shared__ unsigned long long ssum[4];
+    stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
+    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
+    stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
+    stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
+    stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
+}
+
 // rank of `lane` among the set lanes of mask m
 __device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t lane) { return (uint32_t)__popcll(m & ((1ull << lane) - 1ull)); }
 
