@@ -459,7 +459,10 @@ struct Engine {
     // the packed start with the wide table: k_deep_direct (EDSBWT_DEEP_DIRECT=0: k_deep_fast), held
     // to EDSBWT_DIRECT_WAVES waves per SIMD
     bool deep_direct = env_double("EDSBWT_DEEP_DIRECT", 1) != 0;
-    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 1);
+    // the level step (k_lvl_items, k_lvl_dollar): 7 waves per SIMD (SGPR-bound) or 8 (arguments
+    // spilled to VGPR lanes)
+    int lvl_waves = (int)env_double("EDSBWT_LVL_WAVES", 7);
+    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 7);
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 4);  // k_deep<4, 3> likewise (4 unbounded)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
@@ -1837,12 +1840,12 @@ struct Engine {
                 eck_u.ensure(cap_chunks * NSHARD); eck_k.ensure(cap_chunks * NSHARD); eck_e.ensure(cap_chunks * NSHARD);
                 if (!first) zero(lcnt.p, NSHARD * 32 * 4);
                 if (d > 0)
-                    launch(KC_STEP, k_lvl_items<true>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
+                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<true, 8> : k_lvl_items<true>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
                            (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
                            eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap);
                 else  // no link before the first step (:246-258)
-                    launch(KC_STEP, k_lvl_items<false>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
+                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<false, 8> : k_lvl_items<false>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
                            (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
                            eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap);
@@ -1900,7 +1903,7 @@ struct Engine {
                        (const uint32_t*)rscan.p, X.segbits, rb.p, re.p, ru.p, d_runs);
                 const std::vector<uint32_t> keep_items = shard_counts(0);
                 for (;;) {
-                    launch(KC_STEP, k_lvl_dollar, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
+                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_dollar<8> : k_lvl_dollar<1>, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p,
                            (uint32_t)cap_next, lcnt.p, stats.p);
                     fetch_shards();  // sync B

@@ -1148,7 +1148,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
                                                    unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ pv,
                                                    uint32_t* __restrict__ perm_out, const uint64_t* __restrict__ kt1,
                                                    uint64_t* __restrict__ q2, const uint4* __restrict__ kt1w) {
-    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0, n_lane = 0, n_wave = 0;
+    uint32_t n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0, n_lane = 0, n_wave = 0;  // per lane (widened at the end)
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     if (q2) q2 += (size_t)sh * qcap;
@@ -1400,7 +1400,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                                                            uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
                                                            const uint64_t* __restrict__ pv, uint32_t* __restrict__ perm_out,
                                                            const uint4* __restrict__ kt1w, uint64_t* __restrict__ q2) {
-    unsigned long long n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;
+    uint32_t n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;  // per lane: < 2^32 (widened at the end)
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
@@ -1439,24 +1439,32 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             auto code_at = [&](uint32_t dd) -> uint32_t { return 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u); };
             bool alive = true, pair_skip = false, posres = false;
             uint32_t d = D0;
-            for (bool first = true; X.rtext && b == e && d < L; first = false) {
+            // the row's sample and text window: the wide entry's for the first row (have), loaded
+            // for rows reached through a link
+            uint4 s = s1;
+            uint64_t tw = win1;
+            bool have = g1 != ~0u;
+            while (X.rtext && b == e && d < L) {
                 // one row = one text position: the next k = min(o, m) <= 16 characters against the
                 // text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row), as in k_deep_fast
-                const bool wide = first && g1 != ~0u;
-                const uint4 s = wide ? s1 : X.samples[b];
-                const uint32_t g = wide ? g1 : X.gpos[b];
-                n_blk += wide ? 1 : 3;
+                uint32_t g = 0;
+                if (!have) {
+                    s = X.samples[b];
+                    g = X.gpos[b];
+                }
+                n_blk += have ? 1 : 3;
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 if (k) {
                     const uint64_t mask = (1ull << (2 * k)) - 1ull;
-                    const uint64_t tw = wide ? win1 : rtext_window(X.rtext, X.tlen - g);
+                    if (!have) tw = rtext_window(X.rtext, X.tlen - g);
                     if (((tw ^ (rem >> (2 * (d - D0)))) & mask) != 0) {
                         alive = false;
                         d = L;
                         break;
                     }
                 }
+                have = false;
                 if (s.y >= m) {
                     if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
                         posres = true;
@@ -1541,7 +1549,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         const uint32_t at = wave_append(qcnt + sh * 32, want);
         if (want && at < qcap) {
             q[at] = w;
-            q2[at] = v;  // k_deep reads the packed start instead of perm, slen and the key chunks
+            q2[at] = rem << 31 | pi;  // the packed start: k_deep reads it instead of perm, slen and the key chunks
         }
     }
     __shared__ unsigned long long ssum[4];
@@ -1573,7 +1581,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2) {
-    unsigned long long n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0;  // n_blk: occ blocks read
+    uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0;  // n_blk: occ blocks read (per lane, widened at the end)
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
@@ -2216,8 +2224,8 @@ __device__ __forceinline__ void lvl_emit(uint32_t mask, uint32_t emit, uint32_t 
         }
 }
 
-template <bool LINK>
-__global__ void __launch_bounds__(256) k_lvl_items(uint32_t n, const uint32_t* __restrict__ iu, const uint32_t* __restrict__ ib,
+template <bool LINK, int MINW = 1>  // MINW 8: 8 waves per SIMD (the kernel arguments then spill to VGPR lanes)
+__global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint32_t* __restrict__ iu, const uint32_t* __restrict__ ib,
                                                    const uint32_t* __restrict__ ie, const uint64_t* __restrict__ child_info, KIdx X,
                                                    uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
@@ -2341,7 +2349,8 @@ __global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* 
 }
 
 // dollar items (previous-segment word ranges of a node) stepped by each child
-__global__ void __launch_bounds__(256) k_lvl_dollar(const uint32_t* __restrict__ dn, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
+template <int MINW = 1>
+__global__ void __launch_bounds__(256, MINW) k_lvl_dollar(const uint32_t* __restrict__ dn, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
                                                     const uint32_t* __restrict__ de, const uint64_t* __restrict__ child_info, KIdx X,
                                                     uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                     uint32_t cap_next, uint32_t* __restrict__ cnt_all, unsigned long long* __restrict__ stats) {
