@@ -462,7 +462,7 @@ struct Engine {
     // the level step (k_lvl_items, k_lvl_dollar): 7 waves per SIMD (SGPR-bound) or 8 (arguments
     // spilled to VGPR lanes)
     int lvl_waves = (int)env_double("EDSBWT_LVL_WAVES", 7);
-    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 7);
+    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 8);
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 4);  // k_deep<4, 3> likewise (4 unbounded)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
