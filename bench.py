@@ -41,7 +41,8 @@ import workloads  # noqa: E402
 MI355X_HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
 MI355X_MALL_BYTES = 256 << 20  # Infinity Cache: index tables smaller than this are cache-resident
 # bench.py kernel class (engine.hip KClass) -> the kernels it times
-KERNELS_OF_CLASS = {"deep": "k_deep_fast", "deep_list": "k_deep", "deep_wide": "k_deep_wide",
+KERNELS_OF_CLASS = {"deep": "k_deep_direct (packed start, wide k-mer entries; else k_deep_fast)", "deep_list": "k_deep",
+                    "deep_wide": "k_deep_wave",
                     "step": "k_lvl_items + k_lvl_dollar + k_lvl_chunks", "locate": "k_locate_pp + k_locate_big (+ k_locate)"}
 # Practical ceilings of the deep kernels' access shape on MI355X (tools/calib_gather.hip,
 # profiles/r02_calib_gather.json): one random 16-B rank entry per lane per step from a
@@ -68,7 +69,7 @@ def traffic_from_profile(cfg: str, kernel: str):
     path = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
     try:
         t = json.load(open(path))
-        if t.get("classes_version") != "r3":  # round-3 classes: deep = k_deep_fast alone
+        if t.get("classes_version") != "r3b":  # the current classes: deep = k_deep_direct / k_deep_fast
             return None, None
         c = t["classes"][kernel]
         # calibrated DRAM bytes (TCC_EA0_RDREQ_DRAM_32B x 32 + WRITE_SIZE; profiles/r03_calib_counters.json)

@@ -31,12 +31,13 @@ import os
 
 # bench.py kernel class -> kernels (engine.hip KClass)
 # (round 3: the deep stage's three kernels are classes of their own, KC_DEEP / KC_DEEPQ /
-# KC_DEEPW, so each has its own rocprof average and PMC bytes per launch)
+# KC_DEEPW, so each has its own rocprof average and PMC bytes per launch; "r3b": deep is
+# k_deep_direct on the packed start with the wide k-mer table, deep_wide k_deep_wave)
 CLASSES = {
     "step": ("k_lvl_items", "k_lvl_dollar", "k_lvl_chunks"),
-    "deep": ("k_deep_fast",),
+    "deep": ("k_deep_direct", "k_deep_fast"),
     "deep_list": ("k_deep",),
-    "deep_wide": ("k_deep_wide",),
+    "deep_wide": ("k_deep_wave", "k_deep_wide"),
     "locate": ("k_locate", "k_locate_pp", "k_locate_big"),
 }
 FETCH_FACTOR_GATHER64 = 1.0
@@ -127,7 +128,7 @@ def main():
              "kernels": {k: {**per[k], **pmc.get(k, {}), **res.get(k, {})} for k in sorted(per, key=lambda k: -per[k]["total_ms"])}}
     json.dump(out_d, open(a.out, "w"), indent=1)
     if a.traffic:
-        json.dump({"source": a.source, "classes_version": "r3", "fetch_factor": FETCH_FACTOR_GATHER64,
+        json.dump({"source": a.source, "classes_version": "r3b", "fetch_factor": FETCH_FACTOR_GATHER64,
                    "traffic_field": "pmc_dram_bytes_per_launch" if a.tcc else "pmc_hbm_bytes_per_launch",
                    "classes": classes}, open(a.traffic, "w"), indent=1)
     print(json.dumps(classes, indent=1))
