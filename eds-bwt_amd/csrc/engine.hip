@@ -244,6 +244,7 @@ struct Engine {
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     DBuf<uint64_t> ktab_one;  // per D-mer: its one interval inline, else list length and offset (k_ktab_one)
     DBuf<uint4> ktab_wide;    // ... or the wide form, 32 B per D-mer (k_ktab_wide; replaces ktab_one)
+    DBuf<uint4> srow;         // per-row text-compare entries, 32 B per row (k_srow; KIdx::srow)
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
@@ -511,6 +512,7 @@ struct Engine {
         X.tlen = tlen;
         X.gpos = gpos.p;
         X.wrow = wrow.p;
+        X.srow = txt && srow.p ? (const uint4*)srow.p : nullptr;
         X.text_deep = text_deep ? 1u : 0u;
         X.kt1_pos = kt1_pos ? 1u : 0u;
         X.rk16 = use_rk16 ? rk16.p : nullptr;
@@ -908,8 +910,25 @@ struct Engine {
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
+        build_srow();
         build_rank_entries();
         build_ktab();
+    }
+
+    // Per-row text-compare entries (KIdx::srow, 32 B per row: C3 3.3 GB): with dense samples and
+    // the text, a single row reached through a link is compared with the text from one line
+    // instead of three (sample, text position, text window).  EDSBWT_SROW=0: off.
+    void build_srow() {
+        if (!have_text || !have_samples || samp_shift != 0 || !samples.p || !gpos.p || !rtext.p) return;
+        if (env_double("EDSBWT_SROW", 1) == 0) return;
+        size_t fb = 0, tb_ = 0;
+        if (hipMemGetInfo(&fb, &tb_) != hipSuccess) { (void)hipGetLastError(); fb = 0; }
+        if ((double)fb < 4.0 * (double)N * 32) return;
+        srow.ensure(2 * (size_t)N);
+        launch(KC_TABLE, k_srow, N, (uint64_t)N, (const uint4*)samples.p, (const uint32_t*)gpos.p, (const uint64_t*)rtext.p,
+               (uint64_t)tlen, srow.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        device_bytes += (size_t)N * 32;
     }
 
     // Rank entries (kernels.h): rent1 for every alphabet, rent2 (the pair codes of every row,

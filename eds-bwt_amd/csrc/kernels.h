@@ -93,6 +93,9 @@ struct KIdx {
     uint64_t tlen;             // characters in the text
     const uint32_t* gpos;      // [N] text position of row x's suffix (word start + offset)
     const uint32_t* wrow;      // [W] row of each word's whole-word suffix (offset 0)
+    const uint4* srow;         // nullptr, or [2N]: row x's sample (srow[2x]) and {gpos[x], 0, the 32
+                               // reversed-text characters before its suffix} (srow[2x+1]): a single
+                               // row's text compare from ONE line (k_srow; dense samples + text)
     uint32_t text_deep;        // k_deep compares single rows too (EDSBWT_TEXT_DEEP, A/B)
     uint32_t kt1_pos;          // the direct start's inline D-mer entries of ONE row hold that row's
                                // text position too (k_ktab_one): bit 62 set, gpos in bits [31, 62)

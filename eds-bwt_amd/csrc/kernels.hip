@@ -1221,10 +1221,24 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
                 // them with the text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row)
                 rounds++;
                 // the wide entry brought the first row's sample and text window with it (one line)
-                const bool wide = first && g1 != ~0u && kt1w;
-                const uint4 s = wide ? s1 : X.samples[b];
-                const uint32_t g = first && g1 != ~0u ? g1 : X.gpos[b];
-                n_blk += wide ? 1 : first && g1 != ~0u ? 2 : 3;
+                // (or the per-row entry: sample, text position and window in one line)
+                const bool wide = first && g1 != ~0u && kt1w, sr = !wide && X.srow;
+                uint4 s;
+                uint32_t g;
+                uint64_t w0 = win1;
+                if (wide) {
+                    s = s1;
+                    g = g1;
+                } else if (sr) {
+                    s = X.srow[2 * (size_t)b];
+                    const uint4 t2 = X.srow[2 * (size_t)b + 1];
+                    g = t2.x;
+                    w0 = (uint64_t)t2.w << 32 | t2.z;
+                } else {
+                    s = X.samples[b];
+                    g = first && g1 != ~0u ? g1 : X.gpos[b];
+                }
+                n_blk += wide || sr ? 1 : first && g1 != ~0u ? 2 : 3;
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 bool eq = true, valid_codes = true;
@@ -1244,7 +1258,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
                         }
                         if (!valid_codes || !eq) break;
                     }
-                    eq = (((wide && j == 0 ? win1 : rtext_window(X.rtext, r0 + j)) ^ want) & mask) == 0;
+                    eq = ((((wide || sr) && j == 0 ? w0 : rtext_window(X.rtext, r0 + j)) ^ want) & mask) == 0;
                 }
                 if (!valid_codes) break;  // '#' in the pattern: the walk below takes it
                 if (!eq) {
@@ -1448,11 +1462,19 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 // one row = one text position: the next k = min(o, m) <= 16 characters against the
                 // text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row), as in k_deep_fast
                 uint32_t g = 0;
-                if (!have) {
+                if (!have && X.srow) {  // the row's sample, text position and window in one line
+                    s = X.srow[2 * (size_t)b];
+                    const uint4 t2 = X.srow[2 * (size_t)b + 1];
+                    tw = (uint64_t)t2.w << 32 | t2.z;
+                    have = true;
+                    n_blk += 1;
+                } else if (!have) {
                     s = X.samples[b];
                     g = X.gpos[b];
+                    n_blk += 3;
+                } else {
+                    n_blk += 1;
                 }
-                n_blk += have ? 1 : 3;
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 if (k) {
@@ -1636,9 +1658,20 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             if (X.rtext && X.text_deep && cn == 1 && cb[0] == ce[0]) {
                 // a single row: compare with the text as k_deep_fast does
                 const uint32_t x0 = cb[0];
-                const uint4 s = X.samples[x0];
-                const uint32_t g = X.gpos[x0];
-                n_blk += 3;
+                uint4 s;
+                uint32_t g;
+                uint64_t w0 = 0;
+                if (X.srow) {  // sample, text position and window in one line
+                    s = X.srow[2 * (size_t)x0];
+                    const uint4 t2 = X.srow[2 * (size_t)x0 + 1];
+                    g = t2.x;
+                    w0 = (uint64_t)t2.w << 32 | t2.z;
+                    n_blk += 1;
+                } else {
+                    s = X.samples[x0];
+                    g = X.gpos[x0];
+                    n_blk += 3;
+                }
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 bool eq = true, valid_codes = true;
@@ -1653,7 +1686,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                         if (c >= X.sigma) { eq = false; break; }
                         want |= (uint64_t)(c - 1) << (2 * t);
                     }
-                    if (valid_codes && eq) eq = ((rtext_window(X.rtext, r0 + j) ^ want) & mask) == 0;
+                    if (valid_codes && eq) eq = (((X.srow && j == 0 ? w0 : rtext_window(X.rtext, r0 + j)) ^ want) & mask) == 0;
                 }
                 if (valid_codes) {
                     if (!eq) { cn = 0; break; }
@@ -3351,6 +3384,18 @@ __global__ void k_ktab_wide(uint64_t E, const uint32_t* __restrict__ off, const 
         }
         w[2 * u] = make_uint4((uint32_t)ent, (uint32_t)(ent >> 32), (uint32_t)win, (uint32_t)(win >> 32));
         w[2 * u + 1] = s;
+    }
+}
+
+// per-row text-compare entries (KIdx::srow): the row's sample, its text position and the 32
+// characters of the reversed text before its suffix
+__global__ void k_srow(uint64_t N, const uint4* __restrict__ samples, const uint32_t* __restrict__ gpos, const uint64_t* __restrict__ rtext,
+                       uint64_t tlen, uint4* __restrict__ out) {
+    GRID_STRIDE(x, N) {
+        const uint32_t g = gpos[x];
+        const uint64_t win = rtext_window(rtext, tlen - g);
+        out[2 * x] = samples[x];
+        out[2 * x + 1] = make_uint4(g, 0u, (uint32_t)win, (uint32_t)(win >> 32));
     }
 }
 

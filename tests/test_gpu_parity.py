@@ -418,7 +418,8 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     the window, ones longer than it (D0 + 33 .. D0 + 60: the compare goes on from the text),
     crossing into earlier segments, mismatching at either end, with bytes outside the alphabet;
     packed and unpacked direct starts, in input order (the default with the wide table) and
-    sorted by D-mer, located and count-only, the text compare on and off."""
+    sorted by D-mer, with and without the per-row text-compare entries (EDSBWT_SROW), located and
+    count-only, the text compare on and off."""
     monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
     rng = random.Random(3232)
     segs = _covid_like(rng, 700)
@@ -440,22 +441,25 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
         monkeypatch.setenv("EDSBWT_DIRECT_PACKED", packed)
         monkeypatch.setenv("EDSBWT_DIRECT_SORT_MIN", "0")  # the D-mer sort even for this small batch, when on
-        for wide, sort_bits in (("1", "-1"), ("1", "16"), ("0", "-1")):  # -1: the default (input order when wide)
+        # -1: the default sort (input order when wide); srow: the per-row text-compare entries
+        for wide, sort_bits, srow in (("1", "-1", "1"), ("1", "16", "1"), ("0", "-1", "1"), ("1", "-1", "0"), ("0", "-1", "0")):
             monkeypatch.setenv("EDSBWT_KT1_WIDE", wide)
             monkeypatch.setenv("EDSBWT_DIRECT_SORT_BITS", sort_bits)
+            monkeypatch.setenv("EDSBWT_SROW", srow)
             with edsbwt.Index(base) as idx:
-                sizes[wide] = idx.device_bytes
+                sizes[wide + srow] = idx.device_bytes
                 for kw in ({}, {"locate": False}, {"text": False}):
                     gc, go = idx.search((buf, offs), **kw)
                     st = idx.stats()
-                    assert st["start_depth"] == D0, (wide, sort_bits, packed, kw)
-                    assert np.array_equal(gc, oc), (wide, sort_bits, packed, kw)
+                    assert st["start_depth"] == D0, (wide, sort_bits, srow, packed, kw)
+                    assert np.array_equal(gc, oc), (wide, sort_bits, srow, packed, kw)
                     if kw.get("locate", True):
-                        assert np.array_equal(go, oo), (wide, sort_bits, packed, kw)
+                        assert np.array_equal(go, oo), (wide, sort_bits, srow, packed, kw)
                     if not kw:
                         assert st["text_rows"] > 1000, st
     E = (4 ** D0) + 1
-    assert sizes["1"] - sizes["0"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
+    assert sizes["11"] - sizes["01"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
+    assert sizes["11"] > sizes["10"]  # ... and the per-row entries
 
 
 @pytest.mark.parametrize("direct", [True, False])
