@@ -453,6 +453,7 @@ struct Engine {
     uint32_t defer_wide_cap = 0;
     const uint32_t* defer_ovf2 = nullptr;
     static constexpr uint32_t kWideCap = 16384;
+    static constexpr uint32_t kWaveGrid = 2048;  // k_deep_wave's waves (each strides over the wide list)
     // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
     bool deep_wave = env_double("EDSBWT_DEEP_WAVE", 1) != 0;
     // k_deep_fast's register budget: waves per SIMD (5 unbounded; 6 without scratch; 8 spills)
@@ -594,6 +595,14 @@ struct Engine {
         uint64_t v;
         std::memcpy(&v, pinned, 8);
         return v;
+    }
+    // the deferred search's result array before a walk that leaves results unwritten (k_deep_direct
+    // writes every one: its search skips the 160 MB zeroing at C3)
+    bool res_unzeroed = false;
+    void settle_res(const Res* r) {
+        if (!res_unzeroed || r != res.p) return;  // (a group's or a subset's results have their own zeroing)
+        zero(res.p, st.patterns * sizeof(Res));
+        res_unzeroed = false;
     }
     // zeroing by our own kernel: hipMemsetAsync's fill kernel ran at PCIe-like rates beside the
     // host pipeline's download blits (0.4-0.7 ms for a 32 MB result array)
@@ -1496,7 +1505,9 @@ struct Engine {
         const bool dstart = goff == ktab_off.p;
         const uint64_t* kt1 = dstart && ktab_one.p ? (const uint64_t*)ktab_one.p : (const uint64_t*)nullptr;
         const uint4* kt1w = dstart && ktab_wide.p ? (const uint4*)ktab_wide.p : (const uint4*)nullptr;
-        if (pv && kt1w && !X.rent3 && deep_direct) {
+        const bool kdd = pv && kt1w && !X.rent3 && deep_direct;
+        if (!kdd) settle_res(r);  // (k_deep_direct writes every result; the other walks need zeros)
+        if (kdd) {
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
                                                                                                         : k_deep_direct<1>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p);
@@ -1534,8 +1545,9 @@ struct Engine {
             if (!no_wide) {
                 ab.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
                 ae.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
+                // (the waves stride over the list: 2048 of them, not one per possible pattern)
                 if (deep_wave)
-                    launch(KC_DEEPW, k_deep_wave, (size_t)wcap * 64, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
+                    launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(wcap, kWaveGrid) * 64, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
                            d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
                            (const uint32_t*)ovf.p, stats.p);
                 else
@@ -1559,7 +1571,7 @@ struct Engine {
             ab.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             ae.grow_keep(abase + (uint64_t)nw * kDeepWide, stream);
             if (deep_wave)
-                launch(KC_DEEPW, k_deep_wave, (size_t)nw * 64, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
+                launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(nw, kWaveGrid) * 64, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
                        (const uint32_t*)nullptr, stats.p);
             else
@@ -2035,6 +2047,7 @@ struct Engine {
     void run_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, Res* r, uint64_t& abase) {
         uint32_t novf = kNotDirect;
         if (!ordered && allow_deep) novf = direct(d_off, d_bytes, P, r, abase, ovf_orig.p);
+        if (novf == kNotDirect || novf == kNeedOrdered) settle_res(r);
         if (novf == kNeedOrdered) ordered = true;
         if (!ordered && novf == kNotDirect) {
             novf = levels2(d_bytes, d_off, P, allow_deep, r, abase, ovf_orig.p);
@@ -2063,6 +2076,7 @@ struct Engine {
     void run_grouped(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, uint32_t k, uint64_t& abase) {
         abase = 0;
         zero(res.p, P * sizeof(Res));
+        res_unzeroed = false;
         glen.ensure(P);
         gid.ensure(P);
         gflag.ensure(P);
@@ -2170,11 +2184,15 @@ struct Engine {
             oscan.ensure(P + 1);
             const uint64_t nb = direct_buckets();
             if (nb) bhist.ensure(nb + 1);
-            zero_many({{res.p, P * sizeof(Res)}, {stats.p, kStatSlots * 8}, {counters.p, 24 * 8}, {tflag.p, 4}, {hcnt.p, 4},
+            // (the result array only when the search does not turn out to be k_deep_direct's, which
+            // writes every result: res_unzeroed, settled by run_batch / run_deep)
+            zero_many({{stats.p, kStatSlots * 8}, {counters.p, 24 * 8}, {tflag.p, 4}, {hcnt.p, 4},
                        {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}});
+            res_unzeroed = true;
         } else {
             zero(res.p, P * sizeof(Res));
             zero(stats.p, kStatSlots * 8);
+            res_unzeroed = false;
         }
         uint64_t abase = 0;
         // patterns holding '#' make the reference's lists overlap: they take the ordered path
@@ -2196,6 +2214,7 @@ struct Engine {
                     trace_single = trace_lines = 0;
                     st.patterns = P;
                     zero(res.p, P * sizeof(Res));
+                    res_unzeroed = false;
                     zero(stats.p, kStatSlots * 8);
                     abase = 0;
                     run_grouped(d_bytes, d_off, P, allow_deep, ordered, k, abase);

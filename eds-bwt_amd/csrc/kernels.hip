@@ -1408,6 +1408,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
 // entries.  Same walk, results, queue entries and counters as k_deep_fast there; without the
 // generic key-chunk reader, list offsets and rent3 it needs fewer registers, and the walk is
 // latency-bound (C3: 6 waves per SIMD instead of 5 took k_deep_fast from 1.02 to 0.92 ms).
+// It writes every pattern's result (an empty list's too), so the result array needs no zeroing.
 template <int MINW>
 __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
                                                            uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
@@ -1441,7 +1442,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         if (n0 > 1) {
             want = 1;
             w = make_uint4((uint32_t)i, D0, ~0u, 0u);
-        } else if (n0 == 1) {
+        } else if (n0 == 0) {
+            if (valid) put_res(res, pi, 0, 0u, 0u);  // no list: count 0 (every result is written here or by k_deep)
+        } else {
             uint32_t b, e, g1 = ~0u;
             if (X.kt1_pos && ((ent >> 62) & 1)) {
                 b = e = (uint32_t)ent & 0x7fffffffu;
