@@ -1571,6 +1571,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 else put_res(res, pi, abase + i * K, 0u, 0u);
             }
         }
+        if (want) put_res(res, pi, 0, 0u, 0u);  // the zeroed result the later walks expect
         const uint32_t at = wave_append(qcnt + sh * 32, want);
         if (want && at < qcap) {
             q[at] = w;
