@@ -193,6 +193,7 @@ struct Engine {
     uint64_t device_bytes = 0;
     DBuf<OccBlock> occ;
     DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt, segtab;
+    DBuf<uint32_t> seg_chain;  // bit s: seg_lo[s] != s - 1 (k_run_flags gathers seg_lo only there)
     DBuf<uint32_t> kpos;  // '#'-row rank of each word (inverse of eof_word): legacy output order
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
@@ -411,6 +412,8 @@ struct Engine {
     bool prof = false;
     bool no_wide = false;
     bool count_only = false;  // current search returns counts only (no interval archive at finishing depths)
+    // count only: the level step sums finishing nodes' occurrences itself (EDSBWT_FUSE_FINISH=0: k_fin_emit, A/B)
+    bool fuse_finish = env_double("EDSBWT_FUSE_FINISH", 1) != 0;
     // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
@@ -908,6 +911,12 @@ struct Engine {
         h_seg_of_word = sow;  // the host pipeline's record expansion (search_host)
         h_seg_start = sst;
         up(seg_lo, slo);
+        {
+            std::vector<uint32_t> chain(((size_t)S + 2 + 31) / 32, 0u);
+            for (uint32_t t = 2; t <= S; t++)
+                if (slo[t] != t - 1) chain[t >> 5] |= 1u << (t & 31);
+            up(seg_chain, chain);
+        }
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
         counters.ensure(32);
@@ -1398,7 +1407,8 @@ struct Engine {
                         timed(KC_LINKSORT, [&] { HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, lkeys.p, lkeys2.p, cub_n(Hn), 0, 64, stream)); });
                         sync_check(nullptr, "hipcub call at engine.hip:862");
                         rflag.ensure(V);
-                        launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, 32u, rflag.p);
+                        launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, 32u, rflag.p,
+                               (const uint32_t*)seg_chain.p);
                         R = scan_u32(rflag.p, rscan, V);
                         rb.ensure(R); re.ensure(R); ru.ensure(R);
                         launch(KC_LINK, k_run_build, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
@@ -1844,6 +1854,9 @@ struct Engine {
             st.depths++;
             st.trie_nodes += M;
             const bool finishing = hist[D] != 0;
+            // count only: the step itself sums the finishing children's occurrences (child_info
+            // marks them), so no finisher pass reads this depth's items again
+            const bool fuse_fin = finishing && count_only && !cap && fuse_finish;
             // one zeroing launch: shard counters, child links of the parents, finisher tables
             child_info.ensure(Mcur);
             if (finishing) { node_occ.ensure(M); foff.ensure(M); fend.ensure(M); fin.ensure(M); }
@@ -1856,7 +1869,8 @@ struct Engine {
             node_scan(D, P);
             launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, D, (const uint32_t*)slen.p, sorted_chunk(D, P), sigma, (const uint32_t*)lcp.p,
                    (const uint32_t*)scan.p, (const uint32_t*)nid[cur].p, nid[nxt].p, node_first.p, node_parent.p, node_char.p);
-            launch(KC_NODES, k_child_info, M, M, (const uint32_t*)node_parent.p, (const uint8_t*)node_char.p, child_info.p);
+            launch(KC_NODES, k_child_info, M, M, (const uint32_t*)node_parent.p, (const uint8_t*)node_char.p, child_info.p, D,
+                   fuse_fin ? (const uint32_t*)node_first.p : (const uint32_t*)nullptr, (const uint32_t*)slen.p);
             // fused step + '#'-row emission over the current items (sharded appends)
             size_t cap_next = std::max<size_t>(shard_bound(ncur, 2), 4096);
             size_t cap_keys = std::max<size_t>(shard_bound(ncur, 1), 4096);
@@ -1874,12 +1888,14 @@ struct Engine {
                     launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<true, 8> : k_lvl_items<true>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
                            (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
-                           eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap);
+                           eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap,
+                           fuse_fin && first ? node_occ.p : (uint32_t*)nullptr);
                 else  // no link before the first step (:246-258)
                     launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<false, 8> : k_lvl_items<false>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
                            (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
-                           eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap);
+                           eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap,
+                           fuse_fin && first ? node_occ.p : (uint32_t*)nullptr);
                 fetch_shards();  // sync A
                 const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
                 if (m0 <= cap_next && m1 <= cap_keys && m2 <= cap_chunks) break;
@@ -1927,16 +1943,18 @@ struct Engine {
                 sort_link_keys(lkeys.p, lkeys2.p, nkeys, endbit);
                 rflag.ensure(nkeys);
                 rscan.ensure(nkeys);
-                launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, X.segbits, rflag.p);
+                launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, X.segbits, rflag.p,
+                       (const uint32_t*)seg_chain.p);
                 exclusive_scan(rflag.p, rscan.p, nkeys);
                 rb.ensure(nkeys); re.ensure(nkeys); ru.ensure(nkeys);
                 launch(KC_LINK, k_run_build_seg, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p,
                        (const uint32_t*)rscan.p, X.segbits, rb.p, re.p, ru.p, d_runs);
                 const std::vector<uint32_t> keep_items = shard_counts(0);
-                for (;;) {
+                for (bool dfirst = true;; dfirst = false) {
+                    // (a redo after a regrow adds no counts: the first launch counted every item)
                     launch(KC_STEP, lvl_waves >= 8 ? k_lvl_dollar<8> : k_lvl_dollar<1>, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p,
-                           (uint32_t)cap_next, lcnt.p, stats.p);
+                           (uint32_t)cap_next, lcnt.p, stats.p, fuse_fin && dfirst ? node_occ.p : (uint32_t*)nullptr);
                     fetch_shards();  // sync B
                     const uint32_t m0 = shard_max(0);
                     if (m0 <= cap_next) break;
@@ -2002,12 +2020,12 @@ struct Engine {
             if (finishing) {
                 // the items stay in their shards (k_fin_emit reads them in place, as the next
                 // depth's k_lvl_items does)
-                launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
                 const size_t cap_fin = count_only ? 0 : shard_bound(nnext, 1);
                 if (!count_only) { efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD); }
+                if (!fuse_fin) launch(KC_FINISH, k_fin_flags, M, M, D, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
                 // count only: per-node occurrence sums, no interval archive (C5-scale batches
-                // finish billions of intervals)
-                launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)fu.p, (const uint32_t*)fb.p, (const uint32_t*)fe.p,
+                // finish billions of intervals); fused into the step unless EDSBWT_FUSE_FINISH=0
+                if (!fuse_fin) launch(KC_FINISH, k_fin_emit, nnext, nnext, (const uint32_t*)fu.p, (const uint32_t*)fb.p, (const uint32_t*)fe.p,
                        (const uint8_t*)fin.p, lcnt.p, count_only ? (uint64_t*)nullptr : efk.p, count_only ? (uint32_t*)nullptr : efv.p,
                        (uint32_t)cap_fin, node_occ.p, X.rowbits, (const uint32_t*)fpre.p, (uint32_t)fcap);
                 uint32_t F = 0;

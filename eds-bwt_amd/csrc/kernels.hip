@@ -939,8 +939,11 @@ __global__ void k_link_emit(uint64_t H, const uint32_t* __restrict__ hoff, uint6
 // LINK step 3: union of previous-segment ranges [seg_lo[s], s-1] per owner
 // (the deque walk of link(), :533-561, yields exactly these maximal runs, ascending)
 // keys: node << sb | segment
+// seg_chain (optional): bit s set when seg_lo[s] != s - 1 (segment s - 1 holds an empty word); a
+// clear bit settles a key that does not touch its predecessor without the seg_lo gather (an
+// 11 MB bitmap at C5 stays in the caches, seg_lo's 352 MB does not)
 __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ seg_lo, uint32_t sb,
-                            uint32_t* __restrict__ flag) {
+                            uint32_t* __restrict__ flag, const uint32_t* __restrict__ seg_chain) {
     const uint64_t sm = (1ull << sb) - 1;
     // four keys per lane, a grid stride apart: their seg_lo gathers (random, L2-missing) are
     // independent and in flight together
@@ -962,7 +965,7 @@ __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const
                     // seg_lo[s] <= s - 1: a key one segment after (or equal to) its
                     // predecessor continues the run without the gather
                     if (sp[q] + 1 >= s[q]) f[q] = 0;
-                    else need[q] = true;
+                    else need[q] = !seg_chain || ((seg_chain[s[q] >> 5] >> (s[q] & 31)) & 1);
                 }
             }
         }
@@ -2220,20 +2223,51 @@ __global__ void k_sub_scatter(uint64_t n, const uint32_t* __restrict__ map, cons
 // Children of node u, packed by k_child_info: child_info[u] = first child | symbol
 // mask << 32.  Children are in trie order (ascending symbol code, a child for bytes
 // outside the alphabet last), so the child with symbol c is first + popcount of the
-// mask bits below c.
+// mask bits below c.  Mask bit 8 + c (node_first given): that child finishes a pattern
+// (its first pattern, the shortest in trie order, has length D) — the count-only step
+// sums its occurrences.
 __global__ void k_child_info(uint32_t M, const uint32_t* __restrict__ node_parent, const uint8_t* __restrict__ node_char,
-                             uint64_t* __restrict__ info) {
+                             uint64_t* __restrict__ info, uint32_t D, const uint32_t* __restrict__ node_first,
+                             const uint32_t* __restrict__ slen) {
     GRID_STRIDE(u, M) {
         const uint32_t p = node_parent[u];
         if (u == 0 || node_parent[u - 1] != p) {
             uint32_t mask = 0;
             for (size_t v = u; v < M && node_parent[v] == p; v++) {
                 const uint32_t c = node_char[v];
-                if (c < 8) mask |= 1u << c;
+                if (c < 8) {
+                    mask |= 1u << c;
+                    if (node_first && slen[node_first[v]] == D) mask |= 1u << (8 + c);
+                }
             }
             info[p] = ((uint64_t)mask << 32) | (uint32_t)u;
         }
     }
+}
+
+// Count-only finishing fused into the level step: a finishing child's occurrences
+// (e - b + 1 of each interval it receives, as k_fin_emit sums them) go to a block-wide
+// LDS table (open addressing; a full probe run adds to memory directly), which goes to
+// node_occ once at the end of the block.
+constexpr uint32_t kFinH = 1024;
+__device__ __forceinline__ void fin_add(uint32_t* hk, uint32_t* hv, uint32_t* __restrict__ node_occ, uint32_t key, uint32_t v) {
+    uint32_t slot = (key * 2654435761u) >> 22;
+    for (uint32_t q = 0; q < 16; q++, slot = (slot + 1) & (kFinH - 1)) {
+        const uint32_t seen = hk[slot];
+        if (seen == key) { atomicAdd(&hv[slot], v); return; }
+        if (seen == 0xffffffffu) {
+            const uint32_t old = atomicCAS(&hk[slot], 0xffffffffu, key);
+            if (old == 0xffffffffu || old == key) { atomicAdd(&hv[slot], v); return; }
+        }
+    }
+    atomicAdd(node_occ + key, v);
+}
+__device__ __forceinline__ void fin_init(uint32_t* hk, uint32_t* hv) {
+    for (uint32_t t = threadIdx.x; t < kFinH; t += blockDim.x) { hk[t] = 0xffffffffu; hv[t] = 0; }
+}
+__device__ __forceinline__ void fin_flush(const uint32_t* hk, const uint32_t* hv, uint32_t* __restrict__ node_occ) {
+    for (uint32_t t = threadIdx.x; t < kFinH; t += blockDim.x)
+        if (hv[t]) atomicAdd(node_occ + hk[t], hv[t]);
 }
 
 // one interval (node u, rows b..e1-1) stepped by every live child symbol: appends the
@@ -2248,16 +2282,19 @@ __global__ void k_child_info(uint32_t M, const uint32_t* __restrict__ node_paren
 
 __device__ __forceinline__ void lvl_emit(uint32_t mask, uint32_t emit, uint32_t cf, const uint32_t* rb, const uint32_t* re, const KIdx& X,
                                          uint32_t at, uint32_t cap, uint32_t* __restrict__ nu, uint32_t* __restrict__ nb,
-                                         uint32_t* __restrict__ ne) {
+                                         uint32_t* __restrict__ ne, uint32_t* hk, uint32_t* hv, uint32_t* __restrict__ node_occ) {
 #pragma unroll
     for (uint32_t c = 0; c < 8; c++)
         if ((emit >> c) & 1) {
+            const uint32_t child = cf + (uint32_t)__popc(mask & ((1u << c) - 1u));
             if (at < cap) {
-                nu[at] = cf + (uint32_t)__popc(mask & ((1u << c) - 1u));
+                nu[at] = child;
                 nb[at] = X.C[c] + rb[c];
                 ne[at] = X.C[c] + re[c] - 1;
             }
             at++;
+            // (counted whether or not the append fits: a relaunch after a regrow passes no node_occ)
+            if (node_occ && ((mask >> (8 + c)) & 1)) fin_add(hk, hv, node_occ, child, re[c] - rb[c]);
         }
 }
 
@@ -2268,14 +2305,16 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
                                                    uint32_t cap_keys, uint32_t* __restrict__ ck_u, uint32_t* __restrict__ ck_k,
                                                    uint32_t* __restrict__ ck_e, uint32_t cap_chunks, unsigned long long* __restrict__ stats,
-                                                   const uint32_t* __restrict__ ipre, uint32_t icap) {
+                                                   const uint32_t* __restrict__ ipre, uint32_t icap, uint32_t* __restrict__ node_occ) {
     // ipre != nullptr: the input items are still in the previous depth's NSHARD regions
-    // (region s at s*icap, ipre = their prefix sums), read in place instead of packed
+    // (region s at s*icap, ipre = their prefix sums), read in place instead of packed;
+    // node_occ != nullptr (count only): finishing children's occurrences are summed here
     __shared__ uint32_t spre[NSHARD + 1];
-    if (ipre) {
+    __shared__ uint32_t hk[kFinH], hv[kFinH];
+    if (node_occ) fin_init(hk, hv);
+    if (ipre)
         for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) spre[t] = ipre[t];
-        __syncthreads();
-    }
+    if (ipre || node_occ) __syncthreads();
     const uint32_t sh = blockIdx.x % NSHARD;
     unsigned long long n_blk = 0, n_single = 0;  // occ blocks read, single-row items
     uint32_t* cnt = cnt_all + sh * 32;
@@ -2317,7 +2356,7 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
             for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
         uint32_t at, kat, cat;
         wave_append3(cnt, nk, nz, nc, at, kat, cat);  // one atomic round trip for the three lists
-        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne);
+        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne, hk, hv, node_occ);
         if (LINK) {
             if (nz)
                 for (uint32_t k = rb[0]; k < re[0]; k++) {
@@ -2351,6 +2390,10 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
                     }
             }
         }
+    }
+    if (node_occ) {
+        __syncthreads();
+        fin_flush(hk, hv, node_occ);
     }
     __shared__ unsigned long long ssum[4];
     stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);
@@ -2390,9 +2433,16 @@ template <int MINW = 1>
 __global__ void __launch_bounds__(256, MINW) k_lvl_dollar(const uint32_t* __restrict__ dn, const uint32_t* __restrict__ du, const uint32_t* __restrict__ db,
                                                     const uint32_t* __restrict__ de, const uint64_t* __restrict__ child_info, KIdx X,
                                                     uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
-                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, unsigned long long* __restrict__ stats) {
+                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, unsigned long long* __restrict__ stats,
+                                                    uint32_t* __restrict__ node_occ) {
     const uint32_t n = *dn;  // link runs, counted on the device by k_run_build
     unsigned long long n_blk = 0;  // occ blocks read
+    // node_occ != nullptr (count only): finishing children's occurrences are summed here
+    __shared__ uint32_t hk[kFinH], hv[kFinH];
+    if (node_occ) {
+        fin_init(hk, hv);
+        __syncthreads();
+    }
     const uint32_t sh = blockIdx.x % NSHARD;
     uint32_t* cnt = cnt_all + sh * 32;
     nu += (size_t)sh * cap_next; nb += (size_t)sh * cap_next; ne += (size_t)sh * cap_next;
@@ -2425,7 +2475,11 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_dollar(const uint32_t* __rest
         for (uint32_t c = 0; c < 8; c++)
             if (((mask >> c) & 1) && re[c] > rb[c]) emit |= 1u << c;
         const uint32_t at = wave_append(cnt + 0, (uint32_t)__popc(emit));
-        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne);
+        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne, hk, hv, node_occ);
+    }
+    if (node_occ) {
+        __syncthreads();
+        fin_flush(hk, hv, node_occ);
     }
     __shared__ unsigned long long ssum[4];
     stat_add(stats, ST_STEP_BLOCKS, n_blk, ssum);

@@ -50,6 +50,11 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         assert idx.stats()["locate_lf_steps"] == int(oo["offset"].astype(np.uint64).sum())
         gc4, go4 = idx.search((buf, offs), deep=False)   # level-synchronous path only
         assert np.array_equal(gc4, oc) and np.array_equal(go4, oo)
+        # count only on the level path: finishing counts summed inside the step (fused finish),
+        # from the table's depth and from depth 0
+        for ktab in (True, False):
+            gcf, gof = idx.search((buf, offs), locate=False, deep=False, ktab=ktab)
+            assert np.array_equal(gcf, oc) and gof.size == 0
         gk, gok = idx.search((buf, offs), ktab=False)     # walk from depth 0, no k-mer start table
         assert np.array_equal(gk, oc) and np.array_equal(gok, oo)
         assert idx.stats()["start_depth"] == 0
