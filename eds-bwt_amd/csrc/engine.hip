@@ -414,6 +414,8 @@ struct Engine {
     bool count_only = false;  // current search returns counts only (no interval archive at finishing depths)
     // count only: the level step sums finishing nodes' occurrences itself (EDSBWT_FUSE_FINISH=0: k_fin_emit, A/B)
     bool fuse_finish = env_double("EDSBWT_FUSE_FINISH", 1) != 0;
+    // ... and walks single rows as text items (kernels.hip kTextItem; EDSBWT_TEXT_ITEMS=0: off, A/B)
+    bool text_items = env_double("EDSBWT_TEXT_ITEMS", 1) != 0;
     // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
@@ -928,9 +930,11 @@ struct Engine {
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
-        build_srow();
         build_rank_entries();
         build_ktab();
+        // last: the k-mer table's interval budget is a share of the free HBM, which the 32-B
+        // per-row entries would take first (C5: 40 GB, the table then one depth shallower)
+        build_srow();
     }
 
     // Per-row text-compare entries (KIdx::srow, 32 B per row: C3 3.3 GB): with dense samples and
@@ -1781,6 +1785,11 @@ struct Engine {
             small_copy(iu[0].p, &h[2], 4);
         }
         uint32_t novf = 0;
+        // text items (count-only walks with the per-row text entries): no new ones once a deep
+        // cutover may come, and no cutover while any is alive (they carry no row)
+        const bool titems = text_items && count_only && fuse_finish && !cap && X.srow && N < 0x80000000u && (uint64_t)S + 2 < kTextSeg;
+        bool text_stop = false;
+        uint32_t text_alive = 0;
         bool in_sharded = false;  // current items in fu/fb/fe shards (prefix fpre, capacity fcap)
         size_t fcap = 0;
         auto pack_items = [&](int dst) {  // shards -> iu/ib/ie[dst]
@@ -1828,7 +1837,9 @@ struct Engine {
             const int nxt = cur ^ 1;
             const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
-            if (!cap && allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D] && (double)ncur <= deep_items * (double)Mcur) {
+            const bool cut_static = !cap && allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D];
+            if (cut_static) text_stop = true;
+            if (cut_static && text_alive == 0 && (double)ncur <= deep_items * (double)Mcur) {
                 gend.ensure(Mcur);
                 if (d0 && d == d0) {
                     // the table's items are already grouped by node: [kt_pos[u], + kt_cnt[u])
@@ -1885,17 +1896,17 @@ struct Engine {
                 eck_u.ensure(cap_chunks * NSHARD); eck_k.ensure(cap_chunks * NSHARD); eck_e.ensure(cap_chunks * NSHARD);
                 if (!first) zero(lcnt.p, NSHARD * 32 * 4);
                 if (d > 0)
-                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<true, 8> : k_lvl_items<true>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
+                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<true, 8> : lvl_waves >= 7 ? k_lvl_items<true, 7> : k_lvl_items<true>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
                            (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
                            eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap,
-                           fuse_fin && first ? node_occ.p : (uint32_t*)nullptr);
+                           fuse_fin && first ? node_occ.p : (uint32_t*)nullptr, titems ? (text_stop ? 1u : 3u) : 0u);
                 else  // no link before the first step (:246-258)
-                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<false, 8> : k_lvl_items<false>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
+                    launch(KC_STEP, lvl_waves >= 8 ? k_lvl_items<false, 8> : lvl_waves >= 7 ? k_lvl_items<false, 7> : k_lvl_items<false>, ncur, ncur, (const uint32_t*)(in_sharded ? fu.p : iu[cur].p),
                            (const uint32_t*)(in_sharded ? fb.p : ib[cur].p), (const uint32_t*)(in_sharded ? fe.p : ie[cur].p),
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p, (uint32_t)cap_next, lcnt.p, ekeys.p, (uint32_t)cap_keys, eck_u.p,
                            eck_k.p, eck_e.p, (uint32_t)cap_chunks, stats.p, (const uint32_t*)(in_sharded ? fpre.p : nullptr), (uint32_t)fcap,
-                           fuse_fin && first ? node_occ.p : (uint32_t*)nullptr);
+                           fuse_fin && first ? node_occ.p : (uint32_t*)nullptr, titems ? (text_stop ? 1u : 3u) : 0u);
                 fetch_shards();  // sync A
                 const uint32_t m0 = shard_max(0), m1 = shard_max(1), m2 = shard_max(2);
                 if (m0 <= cap_next && m1 <= cap_keys && m2 <= cap_chunks) break;
@@ -1903,6 +1914,7 @@ struct Engine {
                 cap_keys = std::max<size_t>(cap_keys, m1 + m1 / 4 + 1024);
                 cap_chunks = std::max<size_t>(cap_chunks, m2 + m2 / 4 + 256);
             }
+            text_alive = titems ? shard_total(5) : 0u;
             const uint32_t nchunks = shard_total(2);
             st.intervals_stepped += ncur;
             const std::vector<uint32_t> keep_keys = shard_counts(1);

@@ -2298,6 +2298,16 @@ __device__ __forceinline__ void lvl_emit(uint32_t mask, uint32_t emit, uint32_t 
         }
 }
 
+// Text items (count-only level walk): a single row whose suffix starts r <= 16
+// characters after its word's start is one text position, so its next r backward steps are the
+// r text characters before it and its '#' comes right after them.  Its first step reads the row's
+// srow line (sample + text window) instead of a rank entry, and its child becomes a text item
+// (node, kTextItem | r << 27 | segment, the next 16 characters, 2 bits each): every further step
+// takes its character from the item itself and needs only the node's child word; at r = 0 it
+// leaves the link key of its word's segment, as the row's '#' would.  Items carry no row, so
+// they exist only when the walk counts (fused finish) and never reach the deep cutover.
+constexpr uint32_t kTextItem = 0x80000000u, kTextSeg = 0x07ffffffu;
+
 template <bool LINK, int MINW = 1>  // MINW 8: 8 waves per SIMD (the kernel arguments then spill to VGPR lanes)
 __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint32_t* __restrict__ iu, const uint32_t* __restrict__ ib,
                                                    const uint32_t* __restrict__ ie, const uint64_t* __restrict__ child_info, KIdx X,
@@ -2305,10 +2315,12 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
                                                    uint32_t cap_next, uint32_t* __restrict__ cnt_all, uint64_t* __restrict__ keys,
                                                    uint32_t cap_keys, uint32_t* __restrict__ ck_u, uint32_t* __restrict__ ck_k,
                                                    uint32_t* __restrict__ ck_e, uint32_t cap_chunks, unsigned long long* __restrict__ stats,
-                                                   const uint32_t* __restrict__ ipre, uint32_t icap, uint32_t* __restrict__ node_occ) {
+                                                   const uint32_t* __restrict__ ipre, uint32_t icap, uint32_t* __restrict__ node_occ,
+                                                   uint32_t text_mode) {
     // ipre != nullptr: the input items are still in the previous depth's NSHARD regions
     // (region s at s*icap, ipre = their prefix sums), read in place instead of packed;
-    // node_occ != nullptr (count only): finishing children's occurrences are summed here
+    // node_occ != nullptr (count only): finishing children's occurrences are summed here;
+    // text_mode bit 0: step text items (rows < 2^31), bit 1: also turn single rows into them
     __shared__ uint32_t spre[NSHARD + 1];
     __shared__ uint32_t hk[kFinH], hv[kFinH];
     if (node_occ) fin_init(hk, hv);
@@ -2326,6 +2338,8 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
         uint32_t rb[8], re[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
+        bool tx = false;  // a text item (or a single row turned into one): r, segment, window
+        uint32_t t_r = 0, t_seg = 0, t_win = 0;
         if (valid) {
             size_t src = i;
             if (ipre) {
@@ -2339,25 +2353,78 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
             u = iu[src];
             const uint32_t b0 = ib[src], e0 = ie[src];
             n_single += b0 == e0;
-            LVL_STEP_LOAD(u, b0, e0 + 1)
+            if (text_mode && (b0 & kTextItem)) {
+                const uint64_t ci = child_info[u];
+                cf = (uint32_t)ci;
+                mask = (uint32_t)(ci >> 32);
+                tx = true;
+                t_r = (b0 >> 27) & 15u;
+                t_seg = b0 & kTextSeg;
+                t_win = e0;
+            } else if ((text_mode & 2u) && b0 == e0) {
+                const uint64_t ci = child_info[u];
+                const uint4 s0 = X.srow[2 * (size_t)b0];  // (word, offset, segment, word in segment)
+                const uint4 s1 = X.srow[2 * (size_t)b0 + 1];  // {text position, 0, window}
+                n_blk += 1;
+                cf = (uint32_t)ci;
+                mask = (uint32_t)(ci >> 32);
+                if (s0.y <= 16) {
+                    tx = true;
+                    t_r = s0.y;
+                    t_seg = s0.z;
+                    t_win = s1.z;
+                } else {  // a suffix deeper in a long word: the rank step
+                    n_blk += 2 - rank_all_pair_any(X, b0, e0 + 1, rb, re);
+                }
+            } else {
+                LVL_STEP_LOAD(u, b0, e0 + 1)
+            }
         }
         // backward step of every child symbol (updateSingleInterval, :424-510)
         uint32_t emit = 0;
 #pragma unroll
         for (uint32_t c = 0; c < 8; c++)
             if (((mask >> c) & 1) && re[c] > rb[c]) emit |= 1u << c;
-        const uint32_t nk = (uint32_t)__popc(emit);
+        // a text item steps by its next character only (r > 0), or meets its word's '#' (r = 0)
+        uint32_t t_c = 0;
+        bool t_child = false, t_key = false;
+        if (tx) {
+            if (t_r == 0) {
+                t_key = LINK && (mask & 0xffu) && t_seg >= 2;
+            } else {
+                t_c = 1u + (t_win & 3u);
+                t_child = (mask >> t_c) & 1u;
+            }
+        }
+        const uint32_t nk = (uint32_t)__popc(emit) + (t_child ? 1u : 0u);
         // '#' rows of the item (dollars_in_interval, :607-625): short ranges inline,
         // long ones as chunks of 256 rows for k_lvl_chunks
         const uint32_t h = (LINK && mask) ? re[0] - rb[0] : 0u;
         const uint32_t nc = h > 16 ? (h + 255) / 256 : 0u;
-        uint32_t nz = 0;
+        uint32_t nz = t_key ? 1u : 0u;
         if (LINK && h && h <= 16)
             for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
         uint32_t at, kat, cat;
         wave_append3(cnt, nk, nz, nc, at, kat, cat);  // one atomic round trip for the three lists
         lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne, hk, hv, node_occ);
+        if (text_mode) {
+            if (t_child) {
+                const uint32_t child = cf + (uint32_t)__popc(mask & ((1u << t_c) - 1u));
+                if (at < cap_next) {
+                    nu[at] = child;
+                    nb[at] = kTextItem | ((t_r - 1u) << 27) | t_seg;
+                    ne[at] = t_win >> 2;
+                }
+                if (node_occ && ((mask >> (8 + t_c)) & 1u)) fin_add(hk, hv, node_occ, child, 1u);
+            }
+            const uint64_t tb = __ballot(t_child);  // text items handed to the next depth (the deep cutover waits for none)
+            if ((threadIdx.x & 63) == 0 && tb) atomicAdd(cnt + 5, (uint32_t)__popcll(tb));
+        }
         if (LINK) {
+            if (t_key) {
+                if (kat < cap_keys) keys[kat] = ((uint64_t)u << X.segbits) | t_seg;
+                kat++;
+            }
             if (nz)
                 for (uint32_t k = rb[0]; k < re[0]; k++) {
                     const uint32_t s = X.eof_seg[k];
