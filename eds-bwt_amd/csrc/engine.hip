@@ -194,6 +194,7 @@ struct Engine {
     DBuf<OccBlock> occ;
     DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt, segtab;
     DBuf<uint32_t> seg_chain;  // bit s: seg_lo[s] != s - 1 (k_run_flags gathers seg_lo only there)
+    DBuf<uint32_t> eof_key;    // [W] eof_seg[k] << 1 | chain bit of that segment (0: segment 1): KIdx::link_seg
     DBuf<uint32_t> kpos;  // '#'-row rank of each word (inverse of eof_word): legacy output order
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
@@ -416,6 +417,8 @@ struct Engine {
     bool fuse_finish = env_double("EDSBWT_FUSE_FINISH", 1) != 0;
     // ... and walks single rows as text items (kernels.hip kTextItem; EDSBWT_TEXT_ITEMS=0: off, A/B)
     bool text_items = env_double("EDSBWT_TEXT_ITEMS", 1) != 0;
+    // link keys carry their segment's chain bit (KIdx::link_cb; EDSBWT_LINK_CB=0: eof_seg keys, A/B)
+    bool link_cb_on = env_double("EDSBWT_LINK_CB", 1) != 0;
     // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
@@ -491,6 +494,9 @@ struct Engine {
         KIdx X;
         X.occ = occ.p;
         X.eof_seg = eof_seg.p;
+        // (segment ids below 2^31: the chain bit fits beside them)
+        X.link_cb = link_cb_on && eof_key.p && S < 0x7fffffffu ? 1u : 0u;
+        X.link_seg = X.link_cb ? eof_key.p : eof_seg.p;
         X.eof_word = eof_word.p;
         X.seg_of_word = seg_of_word.p;
         X.seg_start = seg_start.p;
@@ -918,6 +924,9 @@ struct Engine {
             for (uint32_t t = 2; t <= S; t++)
                 if (slo[t] != t - 1) chain[t >> 5] |= 1u << (t & 31);
             up(seg_chain, chain);
+            std::vector<uint32_t> ek(W);
+            for (uint32_t k = 0; k < W; k++) ek[k] = eseg[k] ? eseg[k] << 1 | (slo[eseg[k]] != eseg[k] - 1 ? 1u : 0u) : 0u;
+            up(eof_key, ek);
         }
         std::vector<uint8_t> co(H.code_of, H.code_of + 256);
         up(code_of, co);
@@ -948,7 +957,7 @@ struct Engine {
         if ((double)fb < 4.0 * (double)N * 32) return;
         srow.ensure(2 * (size_t)N);
         launch(KC_TABLE, k_srow, N, (uint64_t)N, (const uint4*)samples.p, (const uint32_t*)gpos.p, (const uint64_t*)rtext.p,
-               (uint64_t)tlen, srow.p);
+               (uint64_t)tlen, srow.p, (const uint32_t*)seg_lo.p);
         HIPCHK(hipStreamSynchronize(stream));
         device_bytes += (size_t)N * 32;
     }
@@ -1412,7 +1421,7 @@ struct Engine {
                         sync_check(nullptr, "hipcub call at engine.hip:862");
                         rflag.ensure(V);
                         launch(KC_LINK, k_run_flags, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)seg_lo.p, 32u, rflag.p,
-                               (const uint32_t*)seg_chain.p);
+                               (const uint32_t*)seg_chain.p, 0u);
                         R = scan_u32(rflag.p, rscan, V);
                         rb.ensure(R); re.ensure(R); ru.ensure(R);
                         launch(KC_LINK, k_run_build, V, (const uint64_t*)lkeys2.p, (uint64_t)V, (const uint32_t*)rflag.p, (const uint32_t*)rscan.p,
@@ -1951,16 +1960,16 @@ struct Engine {
                 lkeys.ensure(nkeys);
                 lkeys2.ensure(nkeys);
                 unshard1(1, cap_keys, ekeys.p, lkeys.p, nkeys);
-                const int endbit = (int)std::min<uint32_t>(64, X.segbits + bits_for(Mcur));
+                const int endbit = (int)std::min<uint32_t>(64, X.segbits + X.link_cb + bits_for(Mcur));
                 sort_link_keys(lkeys.p, lkeys2.p, nkeys, endbit);
                 rflag.ensure(nkeys);
                 rscan.ensure(nkeys);
                 launch(KC_LINK, k_run_flags, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)seg_lo.p, X.segbits, rflag.p,
-                       (const uint32_t*)seg_chain.p);
+                       (const uint32_t*)seg_chain.p, X.link_cb);
                 exclusive_scan(rflag.p, rscan.p, nkeys);
                 rb.ensure(nkeys); re.ensure(nkeys); ru.ensure(nkeys);
                 launch(KC_LINK, k_run_build_seg, nkeys, (const uint64_t*)lkeys2.p, (uint64_t)nkeys, (const uint32_t*)rflag.p,
-                       (const uint32_t*)rscan.p, X.segbits, rb.p, re.p, ru.p, d_runs);
+                       (const uint32_t*)rscan.p, X.segbits, rb.p, re.p, ru.p, d_runs, X.link_cb);
                 const std::vector<uint32_t> keep_items = shard_counts(0);
                 for (bool dfirst = true;; dfirst = false) {
                     // (a redo after a regrow adds no counts: the first launch counted every item)

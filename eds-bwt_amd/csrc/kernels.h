@@ -109,6 +109,12 @@ struct KIdx {
     // rank_'#'(x) = x - (rank_1 + rank_2 + rank_3 + rank_4).
     const uint4* rk16;
     const uint4* rk16sup;
+    // link keys of the order-free level walk (k_lvl_items, k_lvl_chunks): link_seg[k] for the
+    // k-th '#' row; link_cb = 1: link_seg holds segment << 1 | chain bit (seg_lo[s] != s - 1,
+    // 0 for segment 1) and the keys are node << (segbits + 1) | link_seg, so k_run_flags needs
+    // no seg_lo or bitmap read for a key without a chain; link_cb = 0: link_seg = eof_seg
+    const uint32_t* link_seg;
+    uint32_t link_cb;
 };
 
 }  // namespace edsbwt

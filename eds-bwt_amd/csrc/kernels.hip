@@ -942,9 +942,12 @@ __global__ void k_link_emit(uint64_t H, const uint32_t* __restrict__ hoff, uint6
 // seg_chain (optional): bit s set when seg_lo[s] != s - 1 (segment s - 1 holds an empty word); a
 // clear bit settles a key that does not touch its predecessor without the seg_lo gather (an
 // 11 MB bitmap at C5 stays in the caches, seg_lo's 352 MB does not)
+// cb = 1: the keys are node << (sb + 1) | segment << 1 | chain bit (KIdx::link_cb), and a clear
+// chain bit settles the key with no read at all
 __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ seg_lo, uint32_t sb,
-                            uint32_t* __restrict__ flag, const uint32_t* __restrict__ seg_chain) {
+                            uint32_t* __restrict__ flag, const uint32_t* __restrict__ seg_chain, uint32_t cb) {
     const uint64_t sm = (1ull << sb) - 1;
+    const uint32_t ns = sb + cb;
     // four keys per lane, a grid stride apart: their seg_lo gathers (random, L2-missing) are
     // independent and in flight together
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -959,13 +962,13 @@ __global__ void k_run_flags(const uint64_t* __restrict__ keys, uint64_t V, const
             s[q] = sp[q] = 0;
             if (t < V && t) {
                 const uint64_t k = keys[t], kp = keys[t - 1];
-                s[q] = (uint32_t)(k & sm);
-                sp[q] = (uint32_t)(kp & sm);
-                if ((kp >> sb) == (k >> sb)) {
+                s[q] = (uint32_t)((k >> cb) & sm);
+                sp[q] = (uint32_t)((kp >> cb) & sm);
+                if ((kp >> ns) == (k >> ns)) {
                     // seg_lo[s] <= s - 1: a key one segment after (or equal to) its
                     // predecessor continues the run without the gather
                     if (sp[q] + 1 >= s[q]) f[q] = 0;
-                    else need[q] = !seg_chain || ((seg_chain[s[q] >> 5] >> (s[q] & 31)) & 1);
+                    else need[q] = cb ? (k & 1) != 0 : !seg_chain || ((seg_chain[s[q] >> 5] >> (s[q] & 31)) & 1);
                 }
             }
         }
@@ -1003,15 +1006,15 @@ __global__ void k_run_build(const uint64_t* __restrict__ keys, uint64_t V, const
 // ends the segment table holds — no row lookups here, no occ lines in k_lvl_dollar
 __global__ void k_run_build_seg(const uint64_t* __restrict__ keys, uint64_t V, const uint32_t* __restrict__ flag,
                                 const uint32_t* __restrict__ rscan, uint32_t sb, uint32_t* __restrict__ rs0, uint32_t* __restrict__ rs1,
-                                uint32_t* __restrict__ rown, uint32_t* __restrict__ nruns) {
+                                uint32_t* __restrict__ rown, uint32_t* __restrict__ nruns, uint32_t cb) {
     GRID_STRIDE(t, V) {
         if (nruns && t + 1 == V) *nruns = rscan[t] + flag[t];
         const uint64_t k = keys[t];
-        const uint32_t s = (uint32_t)(k & ((1ull << sb) - 1));
+        const uint32_t s = (uint32_t)((k >> cb) & ((1ull << sb) - 1));
         const uint32_t r = rscan[t] + flag[t] - 1;
         if (flag[t]) {
             rs0[r] = s;
-            rown[r] = (uint32_t)(k >> sb);
+            rown[r] = (uint32_t)(k >> (sb + cb));
         }
         if (t + 1 == V || flag[t + 1]) rs1[r] = s;
     }
@@ -2338,8 +2341,8 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
         uint32_t rb[8], re[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
-        bool tx = false;  // a text item (or a single row turned into one): r, segment, window
-        uint32_t t_r = 0, t_seg = 0, t_win = 0;
+        bool tx = false;  // a text item (or a single row turned into one): r, segment, window,
+        uint32_t t_r = 0, t_seg = 0, t_win = 0, t_ch = 0;  // and the segment's chain bit (seg_lo != s - 1)
         if (valid) {
             size_t src = i;
             if (ipre) {
@@ -2360,7 +2363,8 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
                 tx = true;
                 t_r = (b0 >> 27) & 15u;
                 t_seg = b0 & kTextSeg;
-                t_win = e0;
+                t_win = e0 & 0x7fffffffu;
+                t_ch = e0 >> 31;
             } else if ((text_mode & 2u) && b0 == e0) {
                 const uint64_t ci = child_info[u];
                 const uint4 s0 = X.srow[2 * (size_t)b0];  // (word, offset, segment, word in segment)
@@ -2373,6 +2377,7 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
                     t_r = s0.y;
                     t_seg = s0.z;
                     t_win = s1.z;
+                    t_ch = s1.y & 1u;
                 } else {  // a suffix deeper in a long word: the rank step
                     n_blk += 2 - rank_all_pair_any(X, b0, e0 + 1, rb, re);
                 }
@@ -2403,7 +2408,7 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
         const uint32_t nc = h > 16 ? (h + 255) / 256 : 0u;
         uint32_t nz = t_key ? 1u : 0u;
         if (LINK && h && h <= 16)
-            for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.eof_seg[k] != 0;
+            for (uint32_t k = rb[0]; k < re[0]; k++) nz += X.link_seg[k] != 0;
         uint32_t at, kat, cat;
         wave_append3(cnt, nk, nz, nc, at, kat, cat);  // one atomic round trip for the three lists
         lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne, hk, hv, node_occ);
@@ -2413,7 +2418,7 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
                 if (at < cap_next) {
                     nu[at] = child;
                     nb[at] = kTextItem | ((t_r - 1u) << 27) | t_seg;
-                    ne[at] = t_win >> 2;
+                    ne[at] = (t_win >> 2) | (t_ch << 31);
                 }
                 if (node_occ && ((mask >> (8 + t_c)) & 1u)) fin_add(hk, hv, node_occ, child, 1u);
             }
@@ -2422,14 +2427,14 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_items(uint32_t n, const uint3
         }
         if (LINK) {
             if (t_key) {
-                if (kat < cap_keys) keys[kat] = ((uint64_t)u << X.segbits) | t_seg;
+                if (kat < cap_keys) keys[kat] = ((uint64_t)u << (X.segbits + X.link_cb)) | (X.link_cb ? t_seg << 1 | t_ch : t_seg);
                 kat++;
             }
             if (nz)
                 for (uint32_t k = rb[0]; k < re[0]; k++) {
-                    const uint32_t s = X.eof_seg[k];
+                    const uint32_t s = X.link_seg[k];
                     if (s) {
-                        if (kat < cap_keys) keys[kat] = ((uint64_t)u << X.segbits) | s;
+                        if (kat < cap_keys) keys[kat] = ((uint64_t)u << (X.segbits + X.link_cb)) | s;
                         kat++;
                     }
                 }
@@ -2482,14 +2487,14 @@ __global__ void __launch_bounds__(256) k_lvl_chunks(uint32_t n, const uint32_t* 
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t k = k0 + lane + 64 * q;
-            s[q] = k < k1 ? X.eof_seg[k] : 0u;
+            s[q] = k < k1 ? X.link_seg[k] : 0u;
             nz += s[q] != 0;
         }
         uint32_t at = wave_append(cnt + 1, nz);
 #pragma unroll
         for (int q = 0; q < 4; q++)
             if (s[q]) {
-                if (at < cap_keys) keys[at] = ((uint64_t)u << X.segbits) | s[q];
+                if (at < cap_keys) keys[at] = ((uint64_t)u << (X.segbits + X.link_cb)) | s[q];
                 at++;
             }
     }
@@ -3515,12 +3520,16 @@ __global__ void k_ktab_wide(uint64_t E, const uint32_t* __restrict__ off, const 
 // per-row text-compare entries (KIdx::srow): the row's sample, its text position and the 32
 // characters of the reversed text before its suffix
 __global__ void k_srow(uint64_t N, const uint4* __restrict__ samples, const uint32_t* __restrict__ gpos, const uint64_t* __restrict__ rtext,
-                       uint64_t tlen, uint4* __restrict__ out) {
+                       uint64_t tlen, uint4* __restrict__ out, const uint32_t* __restrict__ seg_lo) {
     GRID_STRIDE(x, N) {
         const uint32_t g = gpos[x];
         const uint64_t win = rtext_window(rtext, tlen - g);
-        out[2 * x] = samples[x];
-        out[2 * x + 1] = make_uint4(g, 0u, (uint32_t)win, (uint32_t)(win >> 32));
+        const uint4 s = samples[x];
+        out[2 * x] = s;
+        // .y: the chain bit of the row's word segment (seg_lo[s] != s - 1), carried by text items
+        // into their link keys
+        const uint32_t ch = s.z >= 2 && seg_lo[s.z] != s.z - 1 ? 1u : 0u;
+        out[2 * x + 1] = make_uint4(g, ch, (uint32_t)win, (uint32_t)(win >> 32));
     }
 }
 
