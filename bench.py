@@ -150,6 +150,54 @@ def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int,
     return {"value": sample / dt, "seconds": dt, "open_s": t_open, "counts": counts, "occ": occ, "ctr": ctr}
 
 
+def located_leg(idx, buf, offs, counts, dev, stream, first_id: int, budget: float, torch) -> dict:
+    """C5's located leg: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
+    and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so
+    the batch is searched WITH locate in contiguous pattern-id ranges (chunks) whose records
+    fit `budget`; each chunk's counts + records are left in HBM (device-resident, as the timed
+    leg) and the next chunk reuses the record buffer.  Per chunk: its records == Σ its counts
+    from the count-only leg, and its counts equal them.  Outside the timed legs, one pass."""
+    npat = offs.size - 1
+    c64 = counts.astype(np.int64)
+    cuts = [0]
+    acc = 0
+    for i in range(npat):  # greedy contiguous ranges of at most `budget` records
+        if acc + c64[i] > budget and i > cuts[-1]:
+            cuts.append(i)
+            acc = 0
+        acc += int(c64[i])
+    cuts.append(npat)
+    lens = np.diff(offs.astype(np.int64))
+    chunks = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        o = offs[a:b + 1].astype(np.int64) - int(offs[a])
+        chunks.append((a, b, torch.from_numpy(buf[int(offs[a]):int(offs[b])].copy()).to(dev), torch.from_numpy(o).to(dev),
+                       torch.zeros(max(1, b - a), dtype=torch.int32, device=dev)))
+    torch.cuda.synchronize()
+    per, recs, ok, t_all = [], 0, True, 0.0
+    for a, b, db, do, dc in chunks:
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        _, n = idx.search_device(db.data_ptr(), do.data_ptr(), b - a, dc.data_ptr(), first_pattern_id=first_id + a, locate=True,
+                                 stream=stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        t_all += dt
+        want = int(c64[a:b].sum())
+        cm = bool(np.array_equal(dc.cpu().numpy().view(np.uint32)[:b - a], counts[a:b]))
+        ok = ok and cm and n == want
+        recs += n
+        per.append({"patterns": [a, b], "records": int(n), "records_expected": want, "counts_match": cm, "s": round(dt, 3)})
+        log(f"[bench] located chunk [{a}, {b}): {n} records in {dt:.2f}s")
+    by_len = {str(L): {"patterns": int((lens == L).sum()), "records": int(c64[lens == L].sum())} for L in np.unique(lens)}
+    return {"patterns": npat, "records": int(recs), "chunks": len(chunks), "records_budget_per_chunk": int(budget),
+            "seconds": round(t_all, 3), "patterns_per_sec": round(npat / t_all, 1), "records_per_sec": round(recs / t_all, 1),
+            "records_equal_counts": ok, "lengths": by_len, "per_chunk": per,
+            "what": "every pattern of the batch searched WITH locate (counts + 20-B records left in HBM, device-resident), "
+                    "in contiguous pattern-id chunks whose records fit the budget; records == the count-only leg's counts per "
+                    "chunk; one pass outside the timed legs"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,6 +214,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true",
                     help="profiling runs: only the device-resident leg (its kernel averages then match a rocprofv3 "
                          "trace of the whole run); the line's value is then the device-resident rate")
+    ap.add_argument("--no-located", action="store_true", help="C5: skip the located leg")
+    ap.add_argument("--located-budget", type=float, default=1.0e9,
+                    help="C5 located leg: most records per pattern-range chunk (20 B each, left in HBM)")
     ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
     ap.add_argument("--gather", default="auto", choices=("auto", "none", "counts"),
@@ -394,33 +445,9 @@ def main():
         dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": idx.stats(), "d_counts": d_counts}
         if not args.no_e2e and not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
             raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")
-        if w.name == "c5" and rank == 0:
-            # C5 is count-only as BASELINE names it; its >= 32-mers are also searched WITH locate
-            # (device-resident, outside the timed legs): the 8/16-mers' tens of thousands of
-            # occurrences each are what makes locating the whole batch an output-volume problem
-            lens = np.diff(offs)
-            sel = np.flatnonzero(lens >= 32)
-            sub = np.concatenate([buf[offs[i]:offs[i + 1]] for i in sel]) if sel.size else np.zeros(0, np.uint8)
-            soff = np.concatenate(([0], np.cumsum(lens[sel]))).astype(np.int64)
-            ds_b, ds_o = torch.from_numpy(sub).to(dev), torch.from_numpy(soff).to(dev)
-            ds_c = torch.zeros(max(1, sel.size), dtype=torch.int32, device=dev)
-            loc_step = lambda: idx.search_device(ds_b.data_ptr(), ds_o.data_ptr(), int(sel.size), ds_c.data_ptr(),  # noqa: E731
-                                                 first_pattern_id=1, locate=True, stream=stream)
-            loc_step()
-            torch.cuda.synchronize()
-            reps = 3
-            tl = time.perf_counter()
-            nrec = 0
-            for _ in range(reps):
-                _, nrec = loc_step()
-            torch.cuda.synchronize()
-            tl = (time.perf_counter() - tl) / reps
-            sub_counts = ds_c.cpu().numpy().view(np.uint32)[:sel.size]
-            dres["located_long"] = {"patterns": int(sel.size), "lengths": sorted({int(x) for x in lens[sel]}), "records": int(nrec),
-                                    "ms_per_call": round(1e3 * tl, 2), "patterns_per_sec": round(sel.size / tl, 1),
-                                    "counts_match_count_only": bool(np.array_equal(sub_counts, counts_last[sel])) if not args.no_e2e else None,
-                                    "what": "the batch's >= 32-mers searched with locate (device-resident: counts + 20-B records "
-                                            "left in HBM), mean of 3 calls outside the timed legs"}
+        if w.name == "c5" and rank == 0 and not args.no_located:
+            dres["located"] = located_leg(idx, buf, offs, d_counts.cpu().numpy().view(np.uint32)[:npat].copy(), dev, stream,
+                                          first_id, args.located_budget, torch)
 
     if rank == 0:
         total_pats = npat * world if w.per_gpu else (args.patterns or w.patterns)  # every rank's shard
@@ -442,6 +469,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
+            "value_kind": ("device_resident: pattern bytes + offsets in HBM -> counts + records left in HBM (since round 3; "
+                           "rounds 1-2 reported the PCIe-inclusive rate, now e2e.value)" if dres else
+                           "end_to_end (--no-device): host memory -> host memory"),
             "higher_is_better": True,
             "scaling": "weak" if w.per_gpu else "strong",
             "vs_baseline": None,
@@ -461,7 +491,11 @@ def main():
                                         "counts + records D2H (SURVEY §8(d)), plus the exchange step when N>1"),
                        "exchange": ("none (one GPU)" if world == 1 else
                                     "sizes all-gathered (each rank keeps its counts + records as its output slice)"
-                                    + (" + counts gathered to rank 0 over RCCL" if args.gather == "counts" else "")),
+                                    + ((" + counts gathered to rank 0 over RCCL (device counts mirror, xGMI)"
+                                        if args.dist_backend == "nccl" else
+                                        f" + counts gathered to rank 0 over {args.dist_backend} (rehearsal: counts staged "
+                                        "through host memory)") if args.gather == "counts" else "")),
+                       "dist_backend": args.dist_backend if world > 1 else None,
                        "ktab_depth": idx.ktab_depth, "index_device_bytes": idx.device_bytes,
                        "host_numa_node": numa,
                        # every table the search reads (rank tables, k-mer table, samples) within the 256 MB MALL
@@ -510,8 +544,8 @@ def main():
             per_class = {k: v for k in ("deep", "deep_list", "deep_wide", "step", "locate") if (v := kclass(k))}
             dom = max((k for k in kstats if k != "scan"), key=lambda k: kstats[k]["ms"])
             dk = per_class.get(dom) or kclass(dom)
-            # SURVEY §8(d)'s per-step model over the deep family: two 64-B lines per interval step
-            fam_ms = sum(kstats[k]["ms"] for k in ("deep", "deep_list", "deep_wide") if k in kstats) / args.steps
+            # SURVEY §8(d)'s per-step model: two 64-B lines per interval step, whichever kernel
+            # takes it (level step, dollar step, deep walk), over the whole device-resident step
             survey_b = 2 * 64 * dstat["intervals_stepped"]
             out["roofline"] = {
                 "bound": "hbm", "kernel": dom, "kernels": dk["kernels"], "achieved": dk["achieved"], "peak": MI355X_HBM_PEAK_GBS,
@@ -528,9 +562,12 @@ def main():
                 "gather_ceiling_lines_per_s": ceil, "gather_ceiling_shape": ceil_shape,
                 "frac_of_gather_ceiling": dk["frac_of_gather_ceiling"],
                 "per_kernel": per_class,
-                "survey_model_deep_family": {"interval_steps_per_step": int(dstat["intervals_stepped"]),
-                                             "bytes_per_step": int(survey_b), "deep_family_ms_per_step": round(fam_ms, 4),
-                                             "frac": round(survey_b / (fam_ms * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4) if fam_ms > 0 else None},
+                "survey_model_whole_step": {"interval_steps_per_step": int(dstat["intervals_stepped"]),
+                                            "bytes_per_step": int(survey_b), "device_ms_per_step": round(d_ms, 4),
+                                            "frac": round(survey_b / (d_ms * 1e-3) / 1e9 / MI355X_HBM_PEAK_GBS, 4) if d_ms > 0 else None,
+                                            "what": "SURVEY §8(d): 2 x 64 B per interval step (every kernel that steps "
+                                                    "intervals) over the whole device-resident step; omits the text "
+                                                    "compares, table entries, link sorts and stores"},
                 "from": "device_resident leg (HIP events on the library stream, EDSBWT_PROFILE_LIGHT)",
             }
             out["device_resident"] = {
@@ -548,8 +585,13 @@ def main():
                                                  / dres["elapsed"], 1),
                 "reference_locate_lf_steps_per_sec": round(dstat["locate_offsets"] * args.steps / dres["elapsed"], 1),
             }
-            if "located_long" in dres:
-                out["device_resident"]["located_long"] = dres["located_long"]
+            if "located" in dres:
+                out["located"] = dres["located"]
+            # the LF steps the device executed (measured: 2 rank queries per interval step + locate moves)
+            out["lf_steps_per_sec"] = out["device_resident"]["device_lf_steps_per_sec"]
+            out["lf_steps_note"] = ("lf_steps_per_sec: LF steps the device executed (2 per interval step + locate walk moves), "
+                                    "measured over the device-resident leg; lf_steps_per_sec_reference_equivalent_modelled: "
+                                    "oracle-counted reference M_LF moves per pattern x value (SURVEY §8(d)), not executed")
         if rank_parity is not None:
             out["parity_sample"] = rank_parity
         if world == 1 and not args.no_cpu:
@@ -589,12 +631,10 @@ def main():
                                    "os.cpu_count() shows the whole machine)"),
                     "lf_steps_per_pattern": round(lf_ref, 1), "interval_steps_per_pattern": round(ctr["interval_steps"] / samp_n, 1),
                 }
-                # SURVEY §8(d) LF-steps: the reference-literal M_LF moves (oracle-counted on the sample)
-                # per pattern, times the measured patterns/s
-                out["lf_steps_per_sec"] = round(lf_ref * value, 1)
-                out["lf_steps_note"] = ("reference-equivalent: oracle-counted M_LF moves per pattern on the cpu_baseline "
-                                        "sample x value (SURVEY §8(d)); the device executes far fewer (device_resident."
-                                        "device_lf_steps_per_sec)")
+                # SURVEY §8(d) LF-steps, reference-equivalent: the reference-literal M_LF moves
+                # (oracle-counted on the sample) per pattern, times the measured patterns/s — a
+                # MODELLED rate (the device does not execute those moves)
+                out["lf_steps_per_sec_reference_equivalent_modelled"] = round(lf_ref * value, 1)
                 out["cpu_baseline"]["lf_steps_per_sec"] = round(lf_ref * cb["value"], 1)
                 # the trie-sharing CPU variant on the same sample
                 ct = cpu_baseline(base, buf, offs, first_id, samp_n, threads, trie=True)

@@ -3224,6 +3224,7 @@ struct Engine {
                 known_lmin = ~(uint32_t)pm[2];
                 HIPCHK(hipStreamWaitEvent(stream, prep_done[sl], 0));
                 if (pats + P > counts_cap) throw Fail(EDSBWT_E_ARG, "counts buffer holds " + std::to_string(counts_cap) + " patterns, the batch has more");
+                if (counts_mirror && pats + P > counts_mirror_cap) throw Fail(EDSBWT_E_ARG, "device counts mirror smaller than the batch");
                 hcounts[sl].ensure(P + 1);
                 std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
                 uint64_t n = 0;
@@ -3243,10 +3244,7 @@ struct Engine {
                 known_len = false;
                 c8_out = C8Out{};
                 std::swap(rec, hrec[sl]);
-                if (counts_mirror && P) {
-                    if (pats + P > counts_mirror_cap) throw Fail(EDSBWT_E_ARG, "device counts mirror smaller than the batch");
-                    HIPCHK(hipMemcpyAsync(counts_mirror + pats, hcounts[sl].p, P * 4, hipMemcpyDeviceToDevice, stream));
-                }
+                mirror_counts(pats, P, hcounts[sl].p);
                 mark("searched", k);
                 accumulate(agg, st);
                 if (locate && n && total + n > arena_cap) {
@@ -3326,6 +3324,9 @@ struct Engine {
         // measured slower on MI355X: their PCIe stores slow the search kernels running beside them)
         const bool sdma_down = env_double("EDSBWT_D2H_KERNEL", 0) == 0;
         uint32_t* counts_dev = pin_cnt ? static_cast<uint32_t*>(host_dev_ptr(counts)) : nullptr;
+        // a packed batch's size is known up front: refuse it before any chunk is searched (a lines
+        // batch is counted chunk by chunk, each checked before its search)
+        if (!lines && counts_mirror && npat > counts_mirror_cap) throw Fail(EDSBWT_E_ARG, "device counts mirror smaller than the batch");
         std::vector<Chunk> ch = cut_chunks(text, len, offs, npat, lines);
         {
             const bool eager_req = !lines && pin_in && pin_off && env_double("EDSBWT_EAGER_UP", 0) != 0;
@@ -3487,6 +3488,7 @@ struct Engine {
             }
             HIPCHK(hipStreamWaitEvent(stream, down_done[sl], 0));  // chunk k-3's results have left the slot
             if (pats + P > counts_cap) throw Fail(EDSBWT_E_ARG, "counts buffer holds " + std::to_string(counts_cap) + " patterns, the batch has more");
+            if (counts_mirror && pats + P > counts_mirror_cap) throw Fail(EDSBWT_E_ARG, "device counts mirror smaller than the batch");
             hcounts[sl].ensure(P + 1);
             std::swap(rec, hrec[sl]);  // this chunk's records land in slot sl
             uint64_t n = 0;
@@ -3499,6 +3501,7 @@ struct Engine {
             }
             known_len = false;
             std::swap(rec, hrec[sl]);
+            mirror_counts(pats, P, hcounts[sl].p);
             if (compact && locate && n) {  // (word, offset) per record for the download
                 hrec8[sl].ensure(n);
                 launch(KC_LOCATE, k_rec_compact, n, (const edsbwt_occ*)hrec[sl].p, n, hrec8[sl].p);
@@ -3548,6 +3551,7 @@ struct Engine {
             pats += P;
         }
         xfinish();
+        if (counts_mirror) HIPCHK(hipStreamSynchronize(stream));  // the mirror is complete when the call returns
         HIPCHK(hipStreamSynchronize(down));
         HIPCHK(hipStreamSynchronize(up));
         mark("drained", ch.size());
@@ -3575,6 +3579,13 @@ struct Engine {
             }
         }
         return total;
+    }
+    // edsbwt_set_counts_mirror: a chunk's u32 counts also go to the caller's device array (every
+    // host-pipeline path; the capacity was checked before the chunk's search)
+    void mirror_counts(uint64_t pats, uint64_t P, const uint32_t* d_counts) {
+        if (!counts_mirror || !P) return;
+        if (pats + P > counts_mirror_cap) throw Fail(EDSBWT_E_ARG, "device counts mirror smaller than the batch");
+        HIPCHK(hipMemcpyAsync(counts_mirror + pats, d_counts, P * 4, hipMemcpyDeviceToDevice, stream));
     }
     uint64_t* pinned_u64() { return reinterpret_cast<uint64_t*>(pinned + 8); }
     template <typename K, typename... A>

@@ -71,18 +71,30 @@ int main(int argc, char** argv) {
     {
         // tableOcc (sigma x sigma u32 after the header and the EOF ids of <base>_info.aux,
         // da_to_everything.cpp:249-254), printed as recoverInfo prints it
+        // (header: u32 N, u32 W, u8 sigma, sigma alphabet bytes — 4-byte dataTypeNChar and
+        // dataTypeNSeq, Parameters.h:65-71 — then W u32 EOF ids).  A short or unreadable file ends
+        // the run as recoverInfo's failed fread does (MOVE_EDSBWTSearch.cpp:751-755: message, exit
+        // EXIT_FAILURE, before the table is printed)
         const std::string fn = base + "_info.aux";
-        std::printf("\nFrom %s file (TableOcc):\n", fn.c_str());
         FILE* fi = std::fopen(fn.c_str(), "rb");
         std::vector<uint32_t> tocc((size_t)info.sigma * info.sigma);
         const long at = 9L + (long)info.sigma + 4L * (long)info.n_words;
-        if (fi && std::fseek(fi, at, SEEK_SET) == 0 && std::fread(tocc.data(), 4, tocc.size(), fi) == tocc.size()) {
-            for (uint32_t j = 0; j < info.sigma; j++) {
-                for (uint32_t h = 0; h < info.sigma; h++) std::printf("%u\t", tocc[(size_t)j * info.sigma + h]);
-                std::printf("\n");
-            }
-        }
+        long fsz = -1;
+        if (fi && std::fseek(fi, 0, SEEK_END) == 0) fsz = std::ftell(fi);
+        const bool ok = fi && fsz >= at + 4L * (long)tocc.size() && std::fseek(fi, at, SEEK_SET) == 0 &&
+                        std::fread(tocc.data(), 4, tocc.size(), fi) == tocc.size();
         if (fi) std::fclose(fi);
+        if (!ok) {
+            std::fflush(stdout);
+            std::fprintf(stderr, "Error reading tableOcc%s.\n", fn.c_str());
+            edsbwt_index_close(idx);
+            return EXIT_FAILURE;
+        }
+        std::printf("\nFrom %s file (TableOcc):\n", fn.c_str());
+        for (uint32_t j = 0; j < info.sigma; j++) {
+            for (uint32_t h = 0; h < info.sigma; h++) std::printf("%u\t", tocc[(size_t)j * info.sigma + h]);
+            std::printf("\n");
+        }
     }
     std::printf("size= %llu\nBitVector size: %llu\n", (unsigned long long)info.n_rows, (unsigned long long)info.n_words);
     // the pattern file, read into page-locked memory; the library splits its lines

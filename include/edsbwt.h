@@ -184,8 +184,11 @@ int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n);
 /* Multi-GPU exchange: later edsbwt_search / edsbwt_search_lines calls on this
  * index also write every pattern's count (u32, pattern i at d_counts[i]) into d_counts, a device
  * array of cap entries on the index's device, complete when the call returns — the counts RCCL
- * gathers to rank 0 without a second upload.  cap = 0 or d_counts = NULL turns it off.  A batch
- * larger than cap fails with E_ARG. */
+ * gathers to rank 0 without a second upload; every host-pipeline path fills it.  cap = 0 or
+ * d_counts = NULL turns it off.  A batch larger than cap fails with E_ARG: an edsbwt_search batch
+ * before any chunk is searched (the mirror is untouched); an edsbwt_search_lines batch, whose
+ * line count is known chunk by chunk, before the first chunk that would overflow it (the
+ * mirror then holds the earlier chunks' counts). */
 int edsbwt_set_counts_mirror(edsbwt_index* idx, uint32_t* d_counts, uint64_t cap);
 
 /* Counters/timings of the last search on this index. */

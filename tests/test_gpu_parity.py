@@ -67,6 +67,24 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
         for deep in (True, False):                       # reference-ordered lists at every depth
             gc5, go5 = idx.search((buf, offs), ordered=True, deep=deep)
             assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
+    # the defaults' A/B fallbacks (read when an index opens): the finisher pass instead of the
+    # fused count (k_fin_flags / k_fin_emit), no text items, eof_seg link keys without the chain
+    # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide)
+    for var in ("EDSBWT_FUSE_FINISH", "EDSBWT_TEXT_ITEMS", "EDSBWT_LINK_CB", "EDSBWT_DEEP_WAVE"):
+        old = os.environ.get(var)
+        os.environ[var] = "0"
+        try:
+            with edsbwt.Index(base) as idx:
+                for kw in ({}, {"locate": False}, {"locate": False, "deep": False}, {"locate": False, "deep": False, "ktab": False}):
+                    gv, gov = idx.search((buf, offs), **kw)
+                    assert np.array_equal(gv, oc), (var, kw)
+                    if kw.get("locate", True):
+                        assert np.array_equal(gov, oo), (var, kw)
+        finally:
+            if old is None:
+                os.environ.pop(var)
+            else:
+                os.environ[var] = old
     return oc, oo
 
 
@@ -993,3 +1011,21 @@ def test_counts_mirror_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         idx.set_counts_mirror(0, 0)
         gc2, _ = _lines_search(edsbwt, idx, text, first_id=9)
         assert np.array_equal(gc2, oc)
+        # the stream pipeline (the fallback when the SDMA path is not taken: here kernel-store
+        # downloads, EDSBWT_D2H_KERNEL=1) fills the mirror too
+        monkeypatch.setenv("EDSBWT_D2H_KERNEL", "1")
+        mirror.fill_(-1)
+        idx.set_counts_mirror(mirror.data_ptr(), len(pats))
+        gc3, _ = _lines_search(edsbwt, idx, text, first_id=9)
+        assert idx.stats()["chunks"] > 5
+        assert np.array_equal(gc3, oc) and np.array_equal(mirror.cpu().numpy().view(np.uint32), oc)
+        idx.set_counts_mirror(small.data_ptr(), 10)
+        with pytest.raises(edsbwt.EdsBwtError):
+            _lines_search(edsbwt, idx, text, first_id=9)
+        # a packed batch larger than the mirror is refused before any chunk runs: the mirror is untouched
+        monkeypatch.delenv("EDSBWT_D2H_KERNEL")
+        small.fill_(-7)
+        with pytest.raises(edsbwt.EdsBwtError):
+            idx.search((buf, offs), first_pattern_id=9)
+        assert (small.cpu().numpy() == -7).all()
+        idx.set_counts_mirror(0, 0)

@@ -221,12 +221,43 @@ def test_c4_rank_shard_parity(oracle, edsbwt):
                    "literal_sample": int(idx_s.size), "literal_s": round(t_lit, 1), "sample_records": k, "match": True})
 
 
-def test_c5_production_parity(oracle, edsbwt):
+def _group_ends(buf, offs, alphabet, G):
+    """First and last batch position of every trie-subtree search group (engine.hip run_grouped,
+    kernels.hip k_pattern_group: patterns grouped by their last k characters' codes, G =
+    (sigma + 2)^k groups; alphabet = the index's symbols, '#' first: code_of[byte] = its position)."""
+    sigma = len(alphabet)
+    if G <= 1:
+        return np.zeros(0, np.int64)
+    k = int(round(np.log(G) / np.log(sigma + 2)))
+    assert (sigma + 2) ** k == G, (G, sigma)
+    code = np.full(256, sigma + 1, np.int64)
+    for j, ch in enumerate(alphabet):
+        code[ch] = j + 1  # k_pattern_group: v = code_of + 1, sigma + 1 outside the alphabet
+    ends = offs[1:].astype(np.int64)
+    lens = np.diff(offs.astype(np.int64))
+    gid = np.zeros(lens.size, np.int64)
+    for t in range(k):
+        v = np.where(t < lens, code[buf[np.maximum(ends - 1 - t, 0)]], 0)
+        gid = gid * (sigma + 2) + v
+    out = []
+    for g in np.unique(gid):
+        m = np.flatnonzero(gid == g)
+        out += [m[0], m[-1]]
+    return np.unique(np.array(out, np.int64))
+
+
+def test_c5_production_parity(oracle, edsbwt, monkeypatch):
     """C5 (BASELINE configs[4]): the 1 Gchar EDS with 20% empty-word segments and the 200K
-    mixed 8/16/32/64-mer batch of bench.py's C5 line (count-only there).  Counts of the whole
-    batch (every planted pattern found); the >= 32-mers located (Σ records == their counts,
-    every record spells its pattern in the .eds); and the oracle's counts and records for a
-    sample of every length class, planted and random."""
+    mixed 8/16/32/64-mer batch of bench.py's C5 line.
+    * Counts of the whole batch (count-only, bench.py's timed C5 leg), from the host path and
+      the device-resident path with path tags (EDSBWT_PATH_TAGS): equal, every planted pattern found.
+    * Located (the reference always locates, MOVE_EDSBWTSearch.cpp:328-369): every >= 32-mer, and
+      512 8-mers + 512 16-mers (tens of millions of records): Σ records == counts, records
+      pattern-major, every record spells its pattern in the .eds (orc_check_records).
+    * The oracle's counts and records, in order, for: 8 patterns per length x planted class;
+      up to 64 of the patterns the device walk sent to the wide lists / level re-run
+      (deep_overflow); the first and last pattern of every trie-subtree search group."""
+    monkeypatch.setenv("EDSBWT_PATH_TAGS", "1")
     w = workloads.CONFIGS["c5"]
     wd = workloads.default_workdir()
     workloads.ensure_built()
@@ -240,37 +271,55 @@ def test_c5_production_parity(oracle, edsbwt):
     npat = offs.size - 1
     lens = (offs[1:] - offs[:-1]).astype(np.int64)
     assert npat == w.patterns and set(np.unique(lens).tolist()) == {8, 16, 32, 64}
-    long_ = np.flatnonzero(lens >= 32)
     rng = np.random.default_rng(5)
     samp = []
     for L in (8, 16, 32, 64):
         for pl in (True, False):
             cand = np.flatnonzero((lens == L) & (planted == pl))
             samp.append(rng.choice(cand, size=min(8, cand.size), replace=False))
-    idx_s = np.unique(np.concatenate(samp))
+    short_loc = np.sort(np.concatenate([rng.choice(np.flatnonzero(lens == L), size=512, replace=False) for L in (8, 16)]))
+    loc = np.union1d(np.flatnonzero(lens >= 32), short_loc)
     with edsbwt.Index(base) as idx:
         t = time.time()
         counts, _ = idx.search((buf, offs), first_pattern_id=lo + 1, locate=False)
         t_count = time.time() - t
         st = idx.stats()
-        sb, so = _subset(buf, offs, long_)
+        dc, _, tags, dst = _device_tags(edsbwt, idx, buf, offs, lo + 1, locate=False)
+        assert np.array_equal(dc, counts)
+        sb, so = _subset(buf, offs, loc)
+        t = time.time()
         cl, ol = idx.search((sb, so), first_pattern_id=1, locate=True)
-        ss, soo = _subset(buf, offs, idx_s)
-        cs, os_ = idx.search((ss, soo), first_pattern_id=1, locate=True)
+        t_loc = time.time() - t
+        alphabet = idx.alphabet
     assert (counts[planted] > 0).all()
-    assert np.array_equal(cl, counts[long_]) and int(cl.astype(np.uint64).sum()) == ol.size
+    assert np.array_equal(cl, counts[loc]) and int(cl.astype(np.uint64).sum()) == ol.size
+    pat0 = ol["pat"].astype(np.int64) - 1
+    assert (np.diff(pat0) >= 0).all() and np.array_equal(np.bincount(pat0, minlength=loc.size), cl.astype(np.int64))
     bad, first = oracle.check_records(eds, sb, so, ol, 1, threads=THREADS)
     assert bad == 0, (bad, ol[first])
+    # the targeted oracle sample
+    ovf = np.flatnonzero(tags & (edsbwt.PATH_WIDE | edsbwt.PATH_LEVELS))
+    assert ovf.size == dst["deep_overflow"], (ovf.size, dst["deep_overflow"])
+    ovf_s = ovf[np.linspace(0, ovf.size - 1, min(64, ovf.size)).astype(np.int64)] if ovf.size else ovf
+    gends = _group_ends(buf, offs, alphabet, st["search_groups"])
+    idx_s = np.unique(np.concatenate(samp + [ovf_s, gends]))
+    with edsbwt.Index(base) as idx:
+        ss, soo = _subset(buf, offs, idx_s)
+        cs, os_ = idx.search((ss, soo), first_pattern_id=1, locate=True)
     assert np.array_equal(cs, counts[idx_s])
     eng = oracle.Engine(base, 8)
     t = time.time()
-    oc, oo, _ = eng.search(ss, soo, first_pattern_id=1, threads=THREADS)
+    oc, oo, _ = eng.search(ss, soo, first_pattern_id=1, threads=THREADS, trie=True)
     t_orc = time.time() - t
     eng.close()
     assert np.array_equal(oc, cs), (idx_s[oc != cs][:8].tolist(), oc[oc != cs][:8].tolist(), cs[oc != cs][:8].tolist())
     assert np.array_equal(oo, os_)
     _report("c5", {"config": "c5", "patterns": int(npat), "planted": int(planted.sum()), "index_s": round(t_index, 1),
                    "count_only_s": round(t_count, 2), "search_groups": st["search_groups"], "occurrences": int(counts.astype(np.uint64).sum()),
-                   "located_long_patterns": int(long_.size), "located_long_records": int(ol.size), "check_records_bad": bad,
-                   "oracle_sample": int(idx_s.size), "oracle_sample_records": int(oo.size), "oracle_s": round(t_orc, 1),
+                   "located_patterns": int(loc.size), "located_records": int(ol.size), "located_s": round(t_loc, 2),
+                   "located_by_length": {str(L): int((lens[loc] == L).sum()) for L in (8, 16, 32, 64)}, "check_records_bad": bad,
+                   "deep_overflow": int(dst["deep_overflow"]), "deep_overflow_in_sample": int(ovf_s.size),
+                   "group_ends_in_sample": int(gends.size), "oracle_sample": int(idx_s.size), "oracle_sample_records": int(oo.size),
+                   "oracle": "trie-sharing restatement (orc_search_batch_trie, pinned to the literal loop by tests/test_oracle.py)",
+                   "oracle_s": round(t_orc, 1),
                    "sample_lengths": {str(L): int((lens[idx_s] == L).sum()) for L in (8, 16, 32, 64)}, "match": True})

@@ -1,0 +1,67 @@
+#!/bin/bash
+# One GPU-box pass, parameterised (replaces round 1-3's one-off gpu_r*.sh scripts).
+#
+#   bash tools/gpu.sh <tag> <task> [<task> ...]
+#
+# tasks (each under its own time limit; the first failure ends the pass):
+#   suite                   the whole `pytest -m gpu` suite in one process, then smoke()
+#   test:<pytest -k expr>   selected GPU tests
+#   bench:<cfg>[:<steps>[:<warmup>]]     one bench.py line (CPU baseline included)
+#   quick:<cfg>[:<steps>]   a bench line without the CPU leg
+#   trace:<cfg>             rocprofv3 --kernel-trace --stats of the device-resident leg
+#   pmc:<cfg>               separate PMC passes of the same command: FETCH_SIZE, WRITE_SIZE, the TCC
+#                           DRAM request counters, SQ stall + L2 counters (tools/profile_summary.py)
+#   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
+#   cli:<cfg>               the EDSBWTsearch CLI timed on the config's index and pattern file
+#   ab:<cfg>:<VAR=a,VAR2=b>[:<VAR=c>...] A/B bench lines (no CPU leg) under env settings
+# Outputs: gpurun_out/<tag>_<task>*.{json,log}.
+export TMPDIR=/tmp
+TAG=$1; shift
+mkdir -p gpurun_out
+B0="python3 bench.py --no-cpu --no-e2e --no-located --steps 3 --warmup 1"
+fail() { echo "FAIL $1"; tail -30 "$2"; exit 1; }
+for task in "$@"; do
+  IFS=: read -r kind a b c d <<< "$task"
+  out=gpurun_out/${TAG}_${kind}${a:+_$a}
+  echo "[gpu.sh] $task -> $out ($(date +%T))"
+  case $kind in
+    suite)
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > ${out}_pytest.log 2>&1 || fail suite ${out}_pytest.log
+      tail -2 ${out}_pytest.log
+      timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > ${out}_smoke.log 2>&1 || fail smoke ${out}_smoke.log ;;
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "$a" > ${out}.log 2>&1 || fail test ${out}.log
+      tail -2 ${out}.log ;;
+    bench)
+      timeout -k 10 900 python bench.py --config ${a:-c3} --steps ${b:-20} --warmup ${c:-3} > ${out}.json 2> ${out}.log || fail bench ${out}.log
+      head -c 400 ${out}.json; echo ;;
+    quick)
+      timeout -k 10 600 python bench.py --no-cpu --config ${a:-c3} --steps ${b:-10} --warmup 2 > ${out}.json 2> ${out}.log || fail quick ${out}.log
+      head -c 400 ${out}.json; echo ;;
+    trace)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- $B0 --config ${a:-c3} > ${out}.json 2> ${out}.log || fail trace ${out}.log ;;
+    pmc)
+      cfg=${a:-c3}
+      timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d ${out}_fetch -o pmc --output-format csv -- $B0 --config $cfg > ${out}_fetch.json 2> ${out}_fetch.log || fail pmc_fetch ${out}_fetch.log
+      timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d ${out}_write -o pmc --output-format csv -- $B0 --config $cfg > ${out}_write.json 2> ${out}_write.log || fail pmc_write ${out}_write.log
+      timeout -s KILL 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_tccreq -o pmc --output-format csv -- $B0 --config $cfg > ${out}_tccreq.json 2> ${out}_tccreq.log || fail pmc_tcc ${out}_tccreq.log
+      timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY TCC_HIT_sum TCC_MISS_sum -d ${out}_sq -o pmc --output-format csv -- $B0 --config $cfg > ${out}_sq.json 2> ${out}_sq.log || fail pmc_sq ${out}_sq.log ;;
+    rehearse)
+      n=${a:-2}; cfg=${b:-c4}
+      timeout -k 10 1100 python bench.py --gpus $n --config $cfg --steps 3 --warmup 1 --dist-backend gloo ${c:+--patterns $c} > ${out}_${b}.json 2> ${out}_${b}.log || fail rehearse ${out}_${b}.log
+      head -c 400 ${out}_${b}.json; echo ;;
+    cli)
+      timeout -k 10 900 python tools/cli_timing.py --config ${a:-c3} > ${out}.json 2> ${out}.log || fail cli ${out}.log
+      cat ${out}.json ;;
+    ab)
+      cfg=${a:-c3}; i=0
+      for spec in "$b" "$c" "$d"; do
+        [ -z "$spec" ] && continue
+        i=$((i+1))
+        env ${spec//,/ } timeout -k 10 600 python bench.py --no-cpu --no-located --config $cfg --steps 5 --warmup 2 > ${out}_$i.json 2> ${out}_$i.log || fail ab ${out}_$i.log
+        python3 -c "import json;d=json.load(open('${out}_$i.json'));r=d.get('device_resident',{});print('$spec', d['value'], d['ms_per_step'], r.get('kernel_ms_per_step'))"
+      done ;;
+    *) echo "unknown task $task"; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] EXIT 0 ($(date +%T))"

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timeline of the last end-to-end call in a rocprofv3 kernel + memory-copy trace
-(tools/gpu_copytrace.sh): every kernel and copy with start/end relative to the call's first
+(a kernel + copy trace: rocprofv3 --kernel-trace --memory-copy-trace of bench.py): every kernel and copy with start/end relative to the call's first
 upload, its stream, and the idle gap of the engine stream before it.
     python tools/timeline.py <trace_dir> [min_ms]"""
 import csv

@@ -5,7 +5,10 @@ and the production-scale parity tests.
     C2  10 Mchar EDS (seed 1, ~3 strings/segment), 1M random 20-mers per GPU (seed 2), count-only
     C3  ~100 Mchar COVID-like EDS (seed 3), 10M planted 31-mers per GPU (seed 4), full locate
     C4  the C3 index, 100M planted 31-mers in total (seed 5) sharded over the ranks, full locate
-    C5  1 Gchar EDS with 20% empty-word segments (seed 6), mixed 8-64-mers (seed 7), count-only
+    C5  1 Gchar EDS with 20% empty-word segments (seed 6), mixed 8-64-mers (seed 7); BASELINE
+        names no count-only mode for it and the reference always locates: bench.py's timed C5
+        leg is count-only (the COUNT_ONLY flag, labelled in the line) and its `located` leg
+        locates every pattern in pattern-range chunks whose records fit in HBM
 
 Pattern i of a stream is drawn from its own seeded generator (edsbwt_gen --first), so a
 rank generates exactly its contiguous shard of the stream: per-GPU configs (C2, C3, C5:
@@ -48,7 +51,8 @@ CONFIGS = {
     "c4": Workload("c4", "c3", 100_000_000, 3, 100_000_000, False, "31", "planted", 5, True, "c3",
                    "C4: the C3 index replicated, 100M planted 31-mers in total sharded over the GPUs, full position recovery"),
     "c5": Workload("c5", "c5", 1_000_000_000, 6, 200_000, True, "8,16,32,64", "mixed", 7, False, "c5",
-                   "C5: 1 Gchar synthetic EDS with 20% empty-string segments, mixed 8-64-mers per GPU, counts"),
+                   "C5: 1 Gchar synthetic EDS with 20% empty-string segments, mixed 8-64-mers per GPU; timed leg count-only "
+                   "(EDSBWT_COUNT_ONLY), every pattern also located in the `located` leg"),
 }
 
 
