@@ -496,7 +496,8 @@ def main():
                                         f" + counts gathered to rank 0 over {args.dist_backend} (rehearsal: counts staged "
                                         "through host memory)") if args.gather == "counts" else "")),
                        "dist_backend": args.dist_backend if world > 1 else None,
-                       "ktab_depth": idx.ktab_depth, "index_device_bytes": idx.device_bytes,
+                       "ktab_depth": idx.ktab_depth, "ltab_depth": idx.ltab_depth, "ltab_items": idx.ltab_items,
+                       "index_device_bytes": idx.device_bytes,
                        "host_numa_node": numa,
                        # every table the search reads (rank tables, k-mer table, samples) within the 256 MB MALL
                        "cache_resident": bool(idx.device_bytes <= MI355X_MALL_BYTES), "rank_tables_bytes": int(rank_bytes)},

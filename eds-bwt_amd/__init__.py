@@ -60,7 +60,8 @@ class EdsBwtError(RuntimeError):
 class _Info(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_uint64), ("n_words", ctypes.c_uint64), ("n_segments", ctypes.c_uint64),
                 ("sigma", ctypes.c_uint32), ("alphabet", ctypes.c_uint8 * 16), ("device_bytes", ctypes.c_uint64),
-                ("ktab_depth", ctypes.c_uint32), ("pair_blocks", ctypes.c_uint32), ("ktab_items", ctypes.c_uint64)]
+                ("ktab_depth", ctypes.c_uint32), ("pair_blocks", ctypes.c_uint32), ("ktab_items", ctypes.c_uint64),
+                ("ltab_depth", ctypes.c_uint32), ("ltab_groups", ctypes.c_uint32), ("ltab_items", ctypes.c_uint64)]
 
 
 class _Stats(ctypes.Structure):
@@ -237,6 +238,7 @@ class Index:
         self.alphabet = bytes(inf.alphabet[: inf.sigma])
         self.device_bytes = inf.device_bytes
         self.ktab_depth, self.ktab_items = inf.ktab_depth, inf.ktab_items
+        self.ltab_depth, self.ltab_groups, self.ltab_items = inf.ltab_depth, inf.ltab_groups, inf.ltab_items
         self.pair_blocks = bool(inf.pair_blocks)
 
     def close(self) -> None:

@@ -147,6 +147,8 @@ constexpr int kDeepK = 4;
 constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
+// ... and text items (count-only level walks) stop being made once they average at most this many
+constexpr double kTextStopItems = 32.0;
 // locate samples every 2^kSampleShift positions of a word (16 B per sampled row).  0: every
 // row, 16 B/row (C3: 1.66 GB of the 288 GB), and locate reads one sample per occurrence with
 // no LF walk and no occ-block read; EDSBWT_SAMPLE_SHIFT=2 keeps 1 in 4 (0.43 GB at C3)
@@ -161,7 +163,12 @@ constexpr double kKtabItems = 268435456.0;  // at least 2^28 intervals (2 GiB) .
 constexpr double kKtabHbmShare = 0.15;      // ... or as many as kKtabHbmShare of the free HBM holds at
 constexpr double kKtabBuildBytes = 40.0;    // the build's transient bytes per interval (capture + sort)
 constexpr uint32_t kKtabMinDepth = 2;
-constexpr double kKt1WideHbmShare = 2.5;  // the wide k-mer entries are built when free HBM > 2.5x their bytes
+constexpr double kKt1WideHbmShare = 2.5;
+// deep level start table (build_ltab): deepest depth tried, most L-mers, and the share of the
+// free HBM (after every other table) its intervals may take (C5: depth 8, ~9.5G intervals, 76 GB)
+constexpr double kLtabK = 8;
+constexpr uint64_t kLtabMaxEntries = 1ull << 20;
+constexpr double kLtabHbmShare = 0.5;  // the wide k-mer entries are built when free HBM > 2.5x their bytes
 // ... and no deeper than B^(K-1) <= kKtabOver * N: most longer D-mers do not occur (an
 // entry is 12 B; C2, 12.5M rows: depth 15 = 12.9 GB of the 288 GB, searches 4.6x faster
 // than at depth 11)
@@ -247,6 +254,19 @@ struct Engine {
     DBuf<uint64_t> ktab_one;  // per D-mer: its one interval inline, else list length and offset (k_ktab_one)
     DBuf<uint4> ktab_wide;    // ... or the wide form, 32 B per D-mer (k_ktab_wide; replaces ktab_one)
     DBuf<uint4> srow;         // per-row text-compare entries, 32 B per row (k_srow; KIdx::srow)
+    // deep level start table (build_ltab; kernels.hip k_ltab_*): every L-mer's walk items after
+    // its L characters, in lt_G groups by the L-mer's last characters (x mod lt_G); a level walk
+    // whose patterns are all at least L long starts at depth L from it (C5: L = 8)
+    uint32_t lt_depth = 0, lt_G = 0, lt_EG = 0;
+    uint64_t lt_items = 0;
+    DBuf<uint32_t> lt_off;                       // [lt_G][lt_EG + 1] u32 offsets within the group
+    std::vector<DBuf<uint32_t>> lt_b, lt_e;      // per group: interval starts / ends
+    DBuf<const uint32_t*> lt_pb, lt_pe;          // device arrays of the groups' pointers
+    DBuf<unsigned long long> lt_total;           // k_ltab_count's batch total
+    bool use_ltab = true;                        // per search (EDSBWT_NO_LTAB, EDSBWT_NO_KTAB clear it)
+    // most start items one level-table start takes before the batch goes to trie-subtree groups
+    // (EDSBWT_LTAB_START_MAX: tests force the grouped retry with a small value)
+    uint64_t lt_start_max = (uint64_t)env_double("EDSBWT_LTAB_START_MAX", 2147483647.0);
     bool use_ktab = true;  // per search (EDSBWT_NO_KTAB clears it)
     // rank entries (build_rank_entries, kernels.h): one 16-B load per interval end and step;
     // rent2 (sigma <= 5) answers two steps
@@ -268,6 +288,7 @@ struct Engine {
     struct Capture {
         uint32_t K = 0, B = 0;
         uint64_t budget = 0;
+        bool only_last = false;  // keep depth K's items only (the level table's groups)
         uint32_t depth = 0;
         uint64_t n = 0;
         DBuf<uint32_t> k, b, e;
@@ -422,6 +443,9 @@ struct Engine {
     // deep cutover thresholds (EDSBWT_DEEP_SHARE / EDSBWT_DEEP_ITEMS override, for tuning)
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
+    // text items stop being made when a cutover-eligible depth's lists average at most this many
+    // intervals per node (EDSBWT_TEXT_STOP; 1e30: at the first cutover-eligible depth, as round 3)
+    double text_stop_items = env_double("EDSBWT_TEXT_STOP", kTextStopItems);
     // direct start only from tables whose lists average at most this many intervals per D-mer
     double direct_items = env_double("EDSBWT_DIRECT_ITEMS", kDeepItems);
     uint32_t deep_k = [] {  // register list length of k_deep: 2, 3, 4 or 8
@@ -944,6 +968,120 @@ struct Engine {
         // last: the k-mer table's interval budget is a share of the free HBM, which the 32-B
         // per-row entries would take first (C5: 40 GB, the table then one depth shallower)
         build_srow();
+        // after the per-row entries: the level table's budget is a share of what HBM has left
+        build_ltab();
+    }
+
+    // Deep level start table: when the k-mer start table stopped shallow because its lists are
+    // long (C5: depth 3, 0.87G intervals; the items per depth then grow ~1.6x per depth up to
+    // depth 9), every L-mer's item list after its L characters is built too, group
+    // by group (the L-mers sharing their last two characters: one walk over B^L / B^2 patterns
+    // each, so the build's workspace is a group's, not the whole table's), and kept in those
+    // groups with u32 offsets.  A level walk whose patterns are all >= L long then starts at
+    // depth L (levels2), skipping the depths where most items and link runs are.  L is the
+    // deepest <= EDSBWT_LTAB_K (default kLtabK) whose table fits kLtabHbmShare of the free HBM
+    // (estimated from the first group, checked as groups complete).  EDSBWT_LTAB_K=0: off.
+    void build_ltab() {
+        const uint32_t B = sigma - 1;
+        uint32_t L = (uint32_t)env_double("EDSBWT_LTAB_K", kLtabK);
+        if (!L || B < 2 || !ktab_depth || ktab_depth + 2 > L || sigma + 2 > 8) return;
+        auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
+        while (L > ktab_depth + 1 && pw(L) > kLtabMaxEntries) L--;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); free_b = 0; }
+        const double budget = env_double("EDSBWT_LTAB_SHARE", kLtabHbmShare) * (double)free_b;
+        uint64_t sym = 0;
+        for (uint32_t v = 0; v < B; v++) sym |= (uint64_t)alpha[v + 1] << (8 * v);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (; L >= ktab_depth + 2; L--) {
+            const uint32_t G = (uint32_t)pw(2);
+            const uint64_t E = pw(L), EG = E / G;
+            if (EG > 0x7fffffffull) continue;
+            lt_off.ensure((size_t)G * (EG + 1));
+            lt_b.clear(); lt_e.clear();
+            lt_b.resize(G); lt_e.resize(G);
+            uint64_t tot = 0;
+            bool ok = true;
+            for (uint32_t g = 0; g < G && ok; g++) {
+                DBuf<uint8_t> kb;
+                DBuf<uint64_t> ko;
+                kb.ensure(EG * L);
+                ko.ensure(EG + 1);
+                launch(KC_TABLE, k_kmer_batch, EG, EG, L, B, sym, kb.p, ko.p, (uint64_t)G, (uint64_t)g);
+                res.ensure(EG); ovf_orig.ensure(EG);
+                zero(stats.p, kStatSlots * 8);
+                Capture c;
+                c.K = L; c.B = B; c.budget = 0x7fffffffull; c.only_last = true;
+                cap = &c;
+                const bool was_count_only = count_only;
+                count_only = true;
+                uint64_t abase = 0;
+                try {
+                    levels2(kb.p, ko.p, EG, false, res.p, abase, ovf_orig.p);
+                } catch (const TooBig&) {
+                    c.depth = 0;
+                }
+                cap = nullptr;
+                count_only = was_count_only;
+                st = edsbwt_stats{};
+                HIPCHK(hipStreamSynchronize(stream));
+                const uint64_t n = c.n;
+                tot += n;
+                // the first group's size x G estimates the table; every group is checked as it lands
+                if (c.depth != L || (double)tot * 8 > budget || (g == 0 && (double)n * G * 8 > budget)) {
+                    ok = false;
+                    if (trace) std::fprintf(stderr, "[edsbwt] level table depth %u: group %u holds %llu intervals (depth %u): too large\n", L, g,
+                                            (unsigned long long)n, c.depth);
+                    break;
+                }
+                lt_b[g].ensure(n);
+                lt_e[g].ensure(n);
+                if (n) {
+                    DBuf<uint64_t> k1, k2;
+                    DBuf<uint32_t> e2;
+                    k1.ensure(n); k2.ensure(n); e2.ensure(n);
+                    launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
+                    c.k.release(); c.b.release();
+                    size_t tb = 0;
+                    const int endbit = 32 + (int)bits_for(EG);
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+                    tmp.ensure(tb);
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+                    sync_check(nullptr, "hipcub call in build_ltab");
+                    k1.release();
+                    c.e.release();
+                    launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, lt_b[g].p);
+                    HIPCHK(hipMemcpyAsync(lt_e[g].p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+                    launch(KC_TABLE, k_ktab_bounds, EG + 1, EG, (const uint64_t*)k2.p, n, lt_off.p + (size_t)g * (EG + 1));
+                    HIPCHK(hipStreamSynchronize(stream));
+                } else {
+                    zero(lt_off.p + (size_t)g * (EG + 1), (EG + 1) * 4);
+                }
+            }
+            if (!ok) {
+                lt_b.clear(); lt_e.clear();
+                lt_off.release();
+                release_workspace();
+                continue;
+            }
+            std::vector<const uint32_t*> pb(G), pe(G);
+            for (uint32_t g = 0; g < G; g++) { pb[g] = lt_b[g].p; pe[g] = lt_e[g].p; }
+            lt_pb.ensure(G); lt_pe.ensure(G);
+            HIPCHK(hipMemcpy(lt_pb.p, pb.data(), G * sizeof(void*), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(lt_pe.p, pe.data(), G * sizeof(void*), hipMemcpyHostToDevice));
+            lt_total.ensure(1);
+            lt_depth = L;
+            lt_G = G;
+            lt_EG = (uint32_t)EG;
+            lt_items = tot;
+            device_bytes += tot * 8 + (uint64_t)G * (EG + 1) * 4;
+            release_workspace();
+            if (trace)
+                std::fprintf(stderr, "[edsbwt] level start table: depth %u, %u groups of %llu L-mers, %llu intervals, built in %.2f s\n", L, G,
+                             (unsigned long long)EG, (unsigned long long)tot,
+                             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+            return;
+        }
     }
 
     // Per-row text-compare entries (KIdx::srow, 32 B per row: C3 3.3 GB): with dense samples and
@@ -1080,7 +1218,7 @@ struct Engine {
         ko.ensure(P + 1);
         uint64_t sym = 0;
         for (uint32_t v = 0; v < B; v++) sym |= (uint64_t)alpha[v + 1] << (8 * v);
-        launch(KC_TABLE, k_kmer_batch, P, P, K, B, sym, kb.p, ko.p);
+        launch(KC_TABLE, k_kmer_batch, P, P, K, B, sym, kb.p, ko.p, (uint64_t)1, (uint64_t)0);
         res.ensure(P); ovf_orig.ensure(P);
         zero(stats.p, kStatSlots * 8);
         Capture c;
@@ -1811,12 +1949,82 @@ struct Engine {
         // k-mer start table: when every pattern is longer than its depth d0, the items of
         // depth d0 are the table's lists of the depth-d0 nodes' d0-mers (no steps 1..d0)
         uint32_t d0 = 0;
-        if (!cap && use_ktab && ktab_depth) {
+        bool from_lt = false;  // ... or from the deep level table, when every pattern is >= its depth
+        if (!cap && use_ktab && (ktab_depth || lt_depth)) {
             uint32_t lmin = 0;
             while (lmin <= Lmax && hist[lmin] == 0) lmin++;
-            if (lmin > ktab_depth) d0 = ktab_depth;
+            if (use_ltab && lt_depth && lmin >= lt_depth) {
+                d0 = lt_depth;
+                from_lt = true;
+            } else if (ktab_depth && lmin > ktab_depth) {
+                d0 = ktab_depth;
+            }
         }
-        if (d0) {
+        if (from_lt) {
+            const uint32_t M0 = (uint32_t)nodes_at[d0];
+            node_scan(d0, P);
+            launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, d0, (const uint32_t*)slen.p, sorted_chunk(d0, P), sigma,
+                   (const uint32_t*)lcp.p, (const uint32_t*)scan.p, (const uint32_t*)nid[0].p, nid[1].p, node_first.p, node_parent.p, node_char.p);
+            kt_kid.ensure(M0);
+            kt_cnt.ensure(M0);
+            zero(lt_total.p, 8);
+            launch(KC_NODES, bps == 3 ? k_ltab_count<3> : k_ltab_count<4>, M0, M0, d0, sigma - 1, (const uint32_t*)node_first.p,
+                   sorted_chunk(1, P), (const uint32_t*)lt_off.p, lt_G, lt_EG, kt_kid.p, kt_cnt.p, lt_total.p);
+            // a batch whose start items pass 2^31 (a whole C5 batch: ~9G) is searched in trie-subtree groups
+            if (read_u64(lt_total.p) > lt_start_max) throw TooBig("level table start over 2^31 items");
+            const uint32_t n0 = scan_u32(kt_cnt.p, kt_pos, M0);
+            iu[1].ensure(n0); ib[1].ensure(n0); ie[1].ensure(n0);
+            if (n0) {
+                const uint64_t waves = ((uint64_t)n0 + 64 * kLtabR - 1) / (64 * kLtabR);
+                launch_blocks(KC_NODES, k_ltab_emit, (size_t)std::min<uint64_t>((waves + 3) / 4, 1u << 20), n0, M0, (const uint32_t*)kt_kid.p,
+                              (const uint32_t*)kt_pos.p, (const uint32_t*)lt_off.p, lt_G, lt_EG, (const uint32_t* const*)lt_pb.p,
+                              (const uint32_t* const*)lt_pe.p, iu[1].p, ib[1].p, ie[1].p);
+            }
+            cur = 1;
+            Mcur = M0;
+            ncur = n0;
+            st.start_depth = d0;
+            st.trie_nodes += M0;
+            if (trace) std::fprintf(stderr, "[edsbwt] start at depth %u from the level table: nodes %u, items %u\n", d0, M0, n0);
+            if (ncur == 0) return 0;
+            if (hist[d0]) {
+                // patterns of length d0 end at the start: their nodes' lists (sorted by row in the
+                // table) are finished as a depth's finishers are — k_fin_emit over the packed items
+                node_occ.ensure(M0); foff.ensure(M0); fend.ensure(M0); fin.ensure(M0);
+                launch(KC_NODES, k_zero4, 3 * (size_t)M0, node_occ.p, (uint64_t)M0, foff.p, (uint64_t)M0, fend.p, (uint64_t)M0,
+                       (uint32_t*)nullptr, (uint64_t)0);
+                zero(lcnt.p, (NSHARD * 32 + 32) * 4);
+                launch(KC_FINISH, k_fin_flags, M0, M0, d0, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
+                const size_t cap_fin = count_only ? 0 : shard_bound(n0, 1);
+                if (!count_only) { efk.ensure(cap_fin * NSHARD); efv.ensure(cap_fin * NSHARD); }
+                launch(KC_FINISH, k_fin_emit, n0, n0, (const uint32_t*)iu[1].p, (const uint32_t*)ib[1].p, (const uint32_t*)ie[1].p,
+                       (const uint8_t*)fin.p, lcnt.p, count_only ? (uint64_t*)nullptr : efk.p, count_only ? (uint32_t*)nullptr : efv.p,
+                       (uint32_t)cap_fin, node_occ.p, X.rowbits, (const uint32_t*)nullptr, 0u);
+                uint32_t F = 0;
+                if (!count_only) {
+                    fetch_shards();
+                    F = shard_total(4);
+                }
+                fk.ensure(F); fv.ensure(F);
+                if (F) {
+                    unshard2(4, cap_fin, efk.p, efv.p, fk.p, fv.p, F);
+                    fk2.ensure(F); fv2.ensure(F);
+                    const int endbit = (int)std::min<uint32_t>(64, X.rowbits + bits_for(M0));
+                    size_t tb = 0;
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, fk.p, fk2.p, fv.p, fv2.p, cub_n(F), 0, endbit, stream));
+                    tmp.ensure(tb);
+                    timed(KC_FINISH, [&] { HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, fk.p, fk2.p, fv.p, fv2.p, cub_n(F), 0, endbit, stream)); });
+                    sync_check(nullptr, "hipcub call in levels2 (level table finishers)");
+                    launch(KC_FINISH, k_fin_bounds, F, F, (const uint64_t*)fk2.p, X.rowbits, foff.p, fend.p);
+                    ab.grow_keep(abase + F, stream);
+                    ae.grow_keep(abase + F, stream);
+                    launch(KC_FINISH, k_fin_archive, F, F, (const uint64_t*)fk2.p, (const uint32_t*)fv2.p, abase, X.rowbits, ab.p, ae.p);
+                }
+                launch(KC_FINISH, k_finish2, P, P, d0, (const uint32_t*)slen.p, (const uint32_t*)nid[1].p, (const uint32_t*)perm.p,
+                       (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r);
+                abase += F;
+            }
+        } else if (d0) {
             const uint32_t M0 = (uint32_t)nodes_at[d0];
             node_scan(d0, P);
             launch(KC_NODES, bps == 3 ? k_node_build<3> : k_node_build<4>, P, P, d0, (const uint32_t*)slen.p, sorted_chunk(d0, P), sigma,
@@ -1847,7 +2055,10 @@ struct Engine {
             const uint32_t M = (uint32_t)nodes_at[D];
             if (M == 0) break;
             const bool cut_static = !cap && allow_deep && d >= 1 && (double)M >= deep_share * (double)ge[D];
-            if (cut_static) text_stop = true;
+            // no new text items once the lists near the cutover's density (a text item walks at most
+            // 16 more characters, so the cutover waits that long at most); C5 from the level table
+            // starts where the cutover is already possible but lists are ~10^5 items per node
+            if (cut_static && (double)ncur <= text_stop_items * (double)Mcur) text_stop = true;
             if (cut_static && text_alive == 0 && (double)ncur <= deep_items * (double)Mcur) {
                 gend.ensure(Mcur);
                 if (d0 && d == d0) {
@@ -2021,6 +2232,13 @@ struct Engine {
             }
             if (cap) {  // table build: keep this depth's items as (D-mer, b, e) while they fit
                 if (nnext > cap->budget) break;
+                if (cap->only_last && D < cap->K) {  // the level table keeps depth K only
+                    if (nnext == 0) { cap->depth = cap->K; cap->n = 0; break; }  // no K-mer of this group occurs
+                    cur = nxt;
+                    Mcur = M;
+                    ncur = nnext;
+                    continue;
+                }
                 cap->k.ensure(nnext); cap->b.ensure(nnext); cap->e.ensure(nnext);
                 if (nnext) {
                     launch(KC_TABLE, k_unshard<uint32_t, uint32_t, uint32_t>, nnext, nnext, (const uint32_t*)fpre.p, (uint32_t)fcap,
@@ -2186,6 +2404,7 @@ struct Engine {
         const bool allow_deep = !(flags & EDSBWT_NO_DEEP);
         no_wide = (flags & EDSBWT_NO_WIDE) != 0;
         use_ktab = (flags & EDSBWT_NO_KTAB) == 0;
+        use_ltab = use_ktab && env_double("EDSBWT_NO_LTAB", 0) == 0;
         use_pairs = (flags & EDSBWT_NO_PAIRS) == 0 && env_double("EDSBWT_NO_PAIRS", 0) == 0;
         use_direct = (flags & EDSBWT_NO_DIRECT) == 0 && env_double("EDSBWT_NO_DIRECT", 0) == 0;
         // the single-row text compare answers with (word, offset): the reference walk and table
@@ -3854,6 +4073,9 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
     info->device_bytes = E.device_bytes;
     info->ktab_depth = E.ktab_depth;
     info->ktab_items = E.ktab_items;
+    info->ltab_depth = E.lt_depth;
+    info->ltab_groups = E.lt_G;
+    info->ltab_items = E.lt_items;
     info->pair_blocks = E.rent2.p != nullptr;
     return 0;
 }

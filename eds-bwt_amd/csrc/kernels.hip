@@ -3442,9 +3442,12 @@ __global__ void k_fill_u32(uint32_t* __restrict__ a, uint64_t n, uint32_t v) { G
 
 // every K-mer as a pattern: pattern i spells i's base-B digits, last character = digit 0
 // (so i mod B^D is the index of its last D characters); sym[v] = byte of code v + 1
-__global__ void k_kmer_batch(uint64_t P, uint32_t K, uint32_t B, uint64_t sym, uint8_t* __restrict__ bytes, uint64_t* __restrict__ off) {
+// (mul, add): pattern i spells x = i * mul + add instead (the level table's groups: every K-mer
+// whose last characters are those of `add`)
+__global__ void k_kmer_batch(uint64_t P, uint32_t K, uint32_t B, uint64_t sym, uint8_t* __restrict__ bytes, uint64_t* __restrict__ off,
+                             uint64_t mul, uint64_t add) {
     GRID_STRIDE(i, P) {
-        uint64_t x = i;
+        uint64_t x = i * mul + add;
         for (uint32_t t = 0; t < K; t++) {
             bytes[i * K + (K - 1 - t)] = (uint8_t)(sym >> (8 * (x % B)));
             x /= B;
@@ -3620,6 +3623,76 @@ __global__ void __launch_bounds__(256) k_ktab_emit_flat(uint32_t n0, uint32_t M,
         iu[q] = lo;
         ib[q] = tb[src];
         ie[q] = te[src];
+    }
+}
+
+// ------------------------------------------- level start table (engine.hip build_ltab)
+// The deep level start table holds, for every L-mer x over the non-'#' symbols, the order-free
+// walk's intervals after its L characters, sorted by row — as the k-mer start table above, for
+// a depth whose lists do not fit one u32-indexed array (C5: depth 8, ~9.5G intervals).  It is
+// kept in G groups by x mod G (the L-mer's last characters, the same split as run_grouped's
+// trie-subtree groups): group g's intervals lb[g][..], le[g][..] with u32 offsets
+// loff[g * (EG + 1) + x / G] (EG = B^L / G L-mers per group, loff[g * (EG + 1) + EG] = its count).
+
+// per depth-L node: its L-mer (from the node's first pattern's sorted key chunk 0, as
+// k_ktab_count) and its list length; the batch's total into *total (a search over more than
+// 2^31 - 1 start items is retried in trie-subtree groups)
+template <int BPS>
+__global__ void k_ltab_count(uint32_t M, uint32_t D, uint32_t B, const uint32_t* __restrict__ node_first, const uint64_t* __restrict__ k0,
+                             const uint32_t* __restrict__ loff, uint32_t G, uint32_t EG, uint32_t* __restrict__ kid,
+                             uint32_t* __restrict__ cnt, unsigned long long* __restrict__ total) {
+    constexpr uint32_t SPC = 64 / BPS;
+    GRID_STRIDE(u, M) {
+        const uint64_t key = k0[node_first[u]];
+        uint32_t x = 0, mul = 1;
+        bool ok = true;
+        for (uint32_t t = 0; t < D; t++) {
+            const uint32_t v = (uint32_t)(key >> (BPS * (SPC - 1 - t))) & ((1u << BPS) - 1u);
+            ok &= v >= 2 && v <= B + 1;
+            x += (v - 2) * mul;
+            mul *= B;
+        }
+        uint32_t c = 0;
+        if (ok) {
+            const uint32_t* o = loff + (size_t)(x % G) * (EG + 1) + x / G;
+            c = o[1] - o[0];
+        }
+        kid[u] = ok ? x : 0xFFFFFFFFu;
+        cnt[u] = c;
+        if (c) atomicAdd(total, (unsigned long long)c);
+    }
+}
+
+// the depth-L items: node u's list copied to pos[u] (exclusive scan of k_ltab_count's lengths).
+// A wave copies kLtabTile = 64 x kLtabR consecutive items, lane l the items tile + k * 64 + l
+// (coalesced); each lane finds the node of its first item by a binary search over pos and steps
+// forward from there (lists are long: mostly no step at all).  Empty nodes share their pos.
+constexpr uint32_t kLtabR = 16;
+__global__ void __launch_bounds__(256) k_ltab_emit(uint32_t n0, uint32_t M, const uint32_t* __restrict__ kid, const uint32_t* __restrict__ pos,
+                                                   const uint32_t* __restrict__ loff, uint32_t G, uint32_t EG,
+                                                   const uint32_t* const* __restrict__ lb, const uint32_t* const* __restrict__ le,
+                                                   uint32_t* __restrict__ iu, uint32_t* __restrict__ ib, uint32_t* __restrict__ ie) {
+    const uint32_t lane = threadIdx.x & 63;
+    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwave = ((size_t)gridDim.x * blockDim.x) >> 6;
+    for (size_t tile = wave * 64 * kLtabR; tile < n0; tile += nwave * 64 * kLtabR) {
+        const uint32_t q0 = (uint32_t)tile + lane;
+        if (q0 >= n0) continue;
+        uint32_t lo = 0, hi = M;  // pos[lo] <= q0 < pos[hi] (pos[M] = n0)
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pos[mid] <= q0) lo = mid; else hi = mid;
+        }
+        uint32_t nend = pos[lo + 1];
+        for (uint32_t k = 0; k < kLtabR; k++) {
+            const uint32_t q = q0 + k * 64;
+            if (q >= n0) break;
+            while (q >= nend) nend = pos[++lo + 1];
+            const uint32_t x = kid[lo], g = x % G;
+            const uint32_t src = loff[(size_t)g * (EG + 1) + x / G] + (q - pos[lo]);
+            iu[q] = lo;
+            ib[q] = lb[g][src];
+            ie[q] = le[g][src];
+        }
     }
 }
 

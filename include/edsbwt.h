@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EDSBWT_ABI_VERSION 3
+#define EDSBWT_ABI_VERSION 4
 
 enum {
     EDSBWT_OK = 0,
@@ -82,6 +82,9 @@ typedef struct {
                              every D-mer over the non-'#' symbols, built at open */
     uint32_t pair_blocks; /* 1 when the two-step rank blocks are built (sigma <= 5) */
     uint64_t ktab_items;  /* intervals held by that table */
+    uint32_t ltab_depth;  /* deep level start table (C5-like indexes): its depth L, 0 = none */
+    uint32_t ltab_groups; /* ... kept in groups by the L-mer's last characters */
+    uint64_t ltab_items;  /* intervals held by it */
 } edsbwt_index_info;
 
 /* Per-call counters and timings (filled by every edsbwt_search*). */

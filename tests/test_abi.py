@@ -19,7 +19,7 @@ def test_header_symbols_exported(edsbwt):
     assert "edsbwt_search" in names and "edsbwt_index_open" in names
     for n in names:
         assert hasattr(L, n), n
-    assert L.edsbwt_abi_version() == 3
+    assert L.edsbwt_abi_version() == 4
 
 
 def test_build_id_matches_sources(edsbwt):

@@ -168,6 +168,56 @@ def test_c5_style_gpu(oracle, edsbwt, tmp_path):
     _compare(oracle, edsbwt, base, pats, table_too=False)
 
 
+def test_level_table_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The deep level start table (engine.hip build_ltab; C5 at depth 8), forced on a small
+    C5-shaped EDS with a shallow k-mer table (EDSBWT_KTAB_K=3, EDSBWT_LTAB_K=6): batches whose
+    patterns are all >= 6 long start at depth 6 from it — patterns of exactly 6 finish at the
+    start — located and count-only, on the level path and with the deep cutover, in forced
+    trie-subtree groups (the whole C5 batch is grouped because its start passes 2^31 items:
+    tests/test_production_gpu.py), with text items stopped at the first cutover-eligible depth
+    (round 3's rule), against the oracle and against the same searches without the table
+    (EDSBWT_NO_LTAB); a batch holding a shorter pattern starts from the k-mer table instead."""
+    monkeypatch.setenv("EDSBWT_KTAB_K", "3")
+    monkeypatch.setenv("EDSBWT_LTAB_K", "6")
+    rng = random.Random(8686)
+    segs = edsgen.random_eds(rng, 5000, kmax=4, lmax=7, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.choice([6, 6, 7, 9, 12, 16, 24, 40])) or "ACGTAC" for _ in range(2500)]
+    pats += ["".join(rng.choice("ACGT") for _ in range(rng.choice([6, 8, 16, 32]))) for _ in range(1500)]
+    pats += [p[:2] + "N" + p[3:] for p in pats[:40]] + pats[:100]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    short = pats[:300] + ["ACGTA"]
+    sbuf, soffs = _pack(short)
+    soc, soo, _ = oracle.Engine(base, 8).search(sbuf, soffs)
+    with edsbwt.Index(base) as idx:
+        assert idx.ktab_depth == 3 and idx.ltab_depth == 6 and idx.ltab_groups == 16 and idx.ltab_items > 0
+        for kw in ({}, {"locate": False}, {"deep": False}, {"locate": False, "deep": False}, {"direct": False}):
+            gc, go = idx.search((buf, offs), **kw)
+            assert idx.stats()["start_depth"] == 6, kw
+            assert np.array_equal(gc, oc), kw
+            if kw.get("locate", True):
+                assert np.array_equal(go, oo), kw
+        gs, gso = idx.search((sbuf, soffs))
+        assert idx.stats()["start_depth"] == 3
+        assert np.array_equal(gs, soc) and np.array_equal(gso, soo)
+    for env in ({"EDSBWT_NO_LTAB": "1"}, {"EDSBWT_FORCE_GROUPS": "2"}, {"EDSBWT_FORCE_GROUPS": "1", "EDSBWT_TEXT_STOP": "1e30"}):
+        for k_, v_ in env.items():
+            monkeypatch.setenv(k_, v_)
+        with edsbwt.Index(base) as idx:
+            for kw in ({}, {"locate": False}):
+                gc, go = idx.search((buf, offs), **kw)
+                st = idx.stats()
+                assert st["start_depth"] == (3 if "EDSBWT_NO_LTAB" in env else 6), (env, kw)
+                if "EDSBWT_NO_LTAB" not in env:
+                    assert st["search_groups"] > 1, (env, kw)
+                assert np.array_equal(gc, oc), (env, kw)
+                if kw.get("locate", True):
+                    assert np.array_equal(go, oo), (env, kw)
+        for k_ in env:
+            monkeypatch.delenv(k_)
+
+
 @pytest.mark.parametrize("k", [1, 2])
 def test_grouped_search(oracle, edsbwt, tmp_path, monkeypatch, k):
     """The trie-subtree split a batch falls back to when a depth outgrows 32-bit counts
