@@ -354,9 +354,9 @@ def main():
         exchange(nocc)
         search_ms += 1e3 * (tb - ta)
         exch_ms += 1e3 * (time.perf_counter() - tb)
-        st_call = idx.stats()
-        walls.append(st_call["ms_wall"])
-        redo_calls += st_call["redo_searches"]
+        st_call = idx.stats_struct()  # one preallocated struct: no per-step dict building in the timed loop
+        walls.append(st_call.ms_wall)
+        redo_calls += st_call.redo_searches
         total_occ += nocc
     torch.cuda.synchronize()
     barrier()
@@ -426,15 +426,11 @@ def main():
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        kstats = {}
+        kacc = idx.kernel_acc()
         for _ in range(args.steps):
             _, dn = dev_step(profile="light")
             exchange(dn, d_counts)
-            st = idx.stats()
-            for k, v in st["kernels"].items():
-                a = kstats.setdefault(k, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
-                for f in a:
-                    a[f] += v[f]
+            idx.add_kernel_stats(kacc)  # HIP-event times of this call's kernel classes, summed in place
         torch.cuda.synchronize()
         barrier()
         d_elapsed = time.perf_counter() - t1
@@ -442,6 +438,7 @@ def main():
             tt = torch.tensor([d_elapsed], dtype=torch.float64, device=gdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d_elapsed = float(tt.item())
+        kstats = idx.kernel_acc_dict(kacc)
         dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": idx.stats(), "d_counts": d_counts}
         if not args.no_e2e and not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
             raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")

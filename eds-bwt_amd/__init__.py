@@ -351,11 +351,49 @@ class Index:
         s = _Stats()
         _check(lib().edsbwt_last_stats(self._h, ctypes.byref(s)))
         out = {k: getattr(s, k) for k, _ in _Stats._fields_ if k not in ("ms_kernel", "launches_kernel", "bytes_kernel", "lines_kernel")}
-        names = [lib().edsbwt_kernel_name(i).decode() for i in range(16)]
         out["kernels"] = {n: {"ms": s.ms_kernel[i], "launches": s.launches_kernel[i], "bytes": s.bytes_kernel[i],
                               "lines": s.lines_kernel[i]}
-                          for i, n in enumerate(names) if n}
+                          for i, n in enumerate(kernel_names()) if n}
         return out
+
+    # ---- cheap per-call statistics for timed loops (bench.py): one preallocated struct, no dict
+    def stats_struct(self) -> "_Stats":
+        """The last call's edsbwt_stats, refreshed into one struct owned by this Index."""
+        if getattr(self, "_st", None) is None:
+            self._st = _Stats()
+            st = self._st
+            self._st_views = [np.ctypeslib.as_array(st.ms_kernel), np.ctypeslib.as_array(st.launches_kernel),
+                              np.ctypeslib.as_array(st.bytes_kernel), np.ctypeslib.as_array(st.lines_kernel)]
+        _check(lib().edsbwt_last_stats(self._h, ctypes.byref(self._st)))
+        return self._st
+
+    @staticmethod
+    def kernel_acc() -> np.ndarray:
+        """Accumulator for add_kernel_stats: rows ms, launches, bytes, lines per kernel class."""
+        return np.zeros((4, 16), np.float64)
+
+    def add_kernel_stats(self, acc: np.ndarray) -> "_Stats":
+        """acc += the last call's per-class kernel times / launches / bytes / lines."""
+        st = self.stats_struct()
+        for r, v in enumerate(self._st_views):
+            acc[r] += v
+        return st
+
+    @staticmethod
+    def kernel_acc_dict(acc: np.ndarray) -> dict:
+        return {n: {"ms": float(acc[0, i]), "launches": int(acc[1, i]), "bytes": int(acc[2, i]), "lines": int(acc[3, i])}
+                for i, n in enumerate(kernel_names()) if n}
+
+
+_KNAMES = None
+
+
+def kernel_names() -> list:
+    """engine.hip kernel class names (edsbwt_kernel_name), cached."""
+    global _KNAMES
+    if _KNAMES is None:
+        _KNAMES = [lib().edsbwt_kernel_name(i).decode() for i in range(16)]
+    return _KNAMES
 
 
 def format_csv(occ: np.ndarray, threads: int = 8) -> bytes:
