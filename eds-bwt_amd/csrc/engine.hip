@@ -164,6 +164,8 @@ constexpr double kKtabHbmShare = 0.15;      // ... or as many as kKtabHbmShare o
 constexpr double kKtabBuildBytes = 40.0;    // the build's transient bytes per interval (capture + sort)
 constexpr uint32_t kKtabMinDepth = 2;
 constexpr double kKt1WideHbmShare = 2.5;
+// per-'#'-row link rows (KIdx::eofrow) up to this size (C3 243 MB; C5's 264M words would take 17 GB: not built)
+constexpr double kEofRowMaxBytes = 2.0e9;
 // deep level start table (build_ltab): deepest depth tried, most L-mers, and the share of the
 // free HBM (after every other table) its intervals may take (C5: depth 8, ~9.5G intervals, 76 GB)
 constexpr double kLtabK = 8;
@@ -202,6 +204,7 @@ struct Engine {
     DBuf<uint32_t> eof_seg, eof_word, seg_of_word, seg_start, seg_lo, da, offt, segtab;
     DBuf<uint32_t> seg_chain;  // bit s: seg_lo[s] != s - 1 (k_run_flags gathers seg_lo only there)
     DBuf<uint32_t> eof_key;    // [W] eof_seg[k] << 1 | chain bit of that segment (0: segment 1): KIdx::link_seg
+    DBuf<uint32_t> eofrow;     // [W][16] per-'#'-row link rows (KIdx::eofrow; sigma <= 7, W * 64 B <= kEofRowMaxBytes)
     DBuf<uint32_t> kpos;  // '#'-row rank of each word (inverse of eof_word): legacy output order
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
@@ -518,6 +521,7 @@ struct Engine {
         KIdx X;
         X.occ = occ.p;
         X.eof_seg = eof_seg.p;
+        X.eofrow = eofrow.p;
         // (segment ids below 2^31: the chain bit fits beside them)
         X.link_cb = link_cb_on && eof_key.p && S < 0x7fffffffu ? 1u : 0u;
         X.link_seg = X.link_cb ? eof_key.p : eof_seg.p;
@@ -960,6 +964,13 @@ struct Engine {
             segtab.ensure((size_t)(S + 2) * X0.seg_stride);
             device_bytes += (size_t)(S + 2) * X0.seg_stride * 4;
             launch(KC_TABLE, k_segtab, (size_t)S + 2, S, kidx(), segtab.p);
+            // k_deep's links from '#' rows: one line per row instead of eof_seg then segtab
+            // (C3: 3.8M words, 243 MB; EDSBWT_EOF_ROWS=0: off)
+            if (X0.seg_stride == 16 && (double)W * 64 <= kEofRowMaxBytes && env_double("EDSBWT_EOF_ROWS", 1) != 0) {
+                eofrow.ensure((size_t)W * 16);
+                launch(KC_TABLE, k_eofrow, (size_t)W * 16, W, (const uint32_t*)eof_seg.p, (const uint32_t*)segtab.p, eofrow.p);
+                device_bytes += (size_t)W * 64;
+            }
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (env_double("EDSBWT_LOCATE_SAMPLES", 1.0) != 0.0) build_samples();
@@ -2201,12 +2212,15 @@ struct Engine {
                 const uint32_t R = hsh[NSHARD * 32];
                 st.link_ranges += R;
                 st.intervals_stepped += R;
-                st.bytes_kernel[KC_STEP] += (uint64_t)R * (12 + 2 * sizeof(OccBlock));
+                st.bytes_kernel[KC_STEP] += (uint64_t)R * 12;  // the runs read (their lines: ST_STEP_BLOCKS)
                 nnext = shard_total(0);
             }
-            // two 64-B lines per interval step, plus the item streams
-            // (the lines actually read are counted by the kernels: lines_kernel)
-            st.bytes_kernel[KC_STEP] += (uint64_t)ncur * (12 + 2 * sizeof(OccBlock)) + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
+            // the item streams (12 B read per item, 12 B written per next item, 8 B per link key);
+            // the random lines the step kernels gather are counted by them (ST_STEP_BLOCKS, 64 B
+            // each, added in finish_stats): a text item reads none, a single row one, an interval
+            // whose ends share a line one (round 3 charged every item 2 x 64 B: C5's model then
+            // exceeded its DRAM traffic)
+            st.bytes_kernel[KC_STEP] += (uint64_t)ncur * 12 + (uint64_t)nnext * 12 + (uint64_t)nkeys * 8;
             if (trace) {
                 // single-row items and lines read by this depth's step (stats so far, less the last depth's)
                 small_copy(pinned_stats, stats.p, kStatSlots * 8);
@@ -2563,12 +2577,16 @@ struct Engine {
             // record bytes above (k_deep_fast).  k_deep_wide's lines are not counted.
             st.bytes_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS] * 64;
             st.lines_kernel[KC_DEEP] += sv[ST_DEEP_BLOCKS];
-            st.bytes_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS] * 64 + sv[ST_DEEP_HASH] * 4;
-            st.lines_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS];
+            // k_deep: its rank / segment / text lines, one line per '#' row it links from (eofrow, or
+            // eof_seg: its segment's table row is then among ST_DEEPQ_BLOCKS), and its queue entries
+            // (16 + 8 B streamed per queued pattern)
+            st.bytes_kernel[KC_DEEPQ] += (sv[ST_DEEPQ_BLOCKS] + sv[ST_DEEP_HASH]) * 64 + sv[ST_DEEPQ_PATS] * 24;
+            st.lines_kernel[KC_DEEPQ] += sv[ST_DEEPQ_BLOCKS] + sv[ST_DEEP_HASH];
             st.bytes_kernel[KC_DEEPW] += sv[ST_DW_BLOCKS] * 64;  // k_deep_wave (k_deep_wide counts none)
             st.lines_kernel[KC_DEEPW] += sv[ST_DW_BLOCKS];
             st.intervals_stepped += sv[ST_DW_STEPS];
             st.lines_kernel[KC_STEP] += sv[ST_STEP_BLOCKS];
+            st.bytes_kernel[KC_STEP] += sv[ST_STEP_BLOCKS] * 64;
             st.locate_lf_steps = sv[ST_LOC_STEPS];
             st.text_chars = sv[ST_TEXT_CHARS];
             st.text_rows = sv[ST_TEXT_ROWS];

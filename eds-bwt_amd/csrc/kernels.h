@@ -115,6 +115,11 @@ struct KIdx {
     // no seg_lo or bitmap read for a key without a chain; link_cb = 0: link_seg = eof_seg
     const uint32_t* link_seg;
     uint32_t link_cb;
+    // per-'#'-row link rows (sigma <= 7, nullptr: not built): eofrow[16 k ..] = the segment link
+    // table's row of segment s = eof_seg[k] with [15] = s (0: segment 1) — k_deep's link from a
+    // '#' row reads ONE line (its segment and that segment's ranks) instead of eof_seg[k] and
+    // then, dependent on it, segtab[s]
+    const uint32_t* eofrow;
 };
 
 }  // namespace edsbwt

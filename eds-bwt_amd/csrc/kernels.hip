@@ -324,7 +324,8 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_LVL_SINGLE = 16,  // k_lvl_items input items of one row (b == e)
                   ST_DF_LANE_ROUNDS = 17, ST_DF_WAVE_ROUNDS = 18,  // k_deep_fast: dependent load rounds of the
                   // lanes' patterns, and 64 x the slowest lane's per pattern slot (lane utilisation)
-                  ST_DW_BLOCKS = 19, ST_DW_STEPS = 20 };  // k_deep_wave's lines and interval steps
+                  ST_DW_BLOCKS = 19, ST_DW_STEPS = 20,  // k_deep_wave's lines and interval steps
+                  ST_DEEPQ_PATS = 21 };  // queue entries k_deep read
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -1613,7 +1614,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2) {
-    uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0;  // n_blk: occ blocks read (per lane, widened at the end)
+    uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;  // n_blk: occ blocks read (per lane, widened at the end)
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
@@ -1630,6 +1631,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         const size_t qi = (size_t)lo * qcap + ((uint32_t)j - spre[lo]);
         const uint4 w = q[qi];
         const uint32_t i = w.x, d0 = w.y;
+        n_q++;
         // q2 (packed direct start): input index and remaining symbols from the queue entry
         uint32_t pi, L;
         uint64_t rem = 0;
@@ -1732,12 +1734,12 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
-            uint32_t sb[K], se[K], raw[K];
+            uint32_t sb[K], se[K], raw[K], rawk[K];  // rawk: a '#'-rank of raw's segment (its eofrow line)
             uint32_t rn = 0;
 #pragma unroll
             for (int j = 0; j < K; j++) {
                 sb[j] = se[j] = 0;
-                raw[j] = 0;
+                raw[j] = rawk[j] = 0;
             }
 #pragma unroll
             for (int j = 0; j < K; j++) {
@@ -1746,7 +1748,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                     n_blk += 2 - rank2_any(X, cb[j], ce[j] + 1, c, h0, sb[j], h1, se[j]);
                     n_hash += h1 - h0;
                     for (uint32_t k = h0; k < h1; k++) {  // dollars_in_interval (:607-625)
-                        const uint32_t s = X.eof_seg[k];
+                        // the word's segment: from its link row (one line, the ranks come with it) or eof_seg
+                        const uint32_t s = X.eofrow ? X.eofrow[(size_t)k * 16 + 15] : X.eof_seg[k];
                         if (!s) continue;
                         // insert s into raw[0..rn) ascending, dropping duplicates
                         bool dup = false;
@@ -1755,13 +1758,18 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                             if ((uint32_t)t < rn && raw[t] == s) dup = true;
                         if (dup) continue;
                         if (rn == K) { over = true; break; }
-                        uint32_t vv = s;
+                        uint32_t vv = s, vk = k;
 #pragma unroll
                         for (int t = 0; t < K; t++) {
                             if ((uint32_t)t < rn) {
-                                if (raw[t] > vv) { const uint32_t tmp = raw[t]; raw[t] = vv; vv = tmp; }
+                                if (raw[t] > vv) {
+                                    const uint32_t tmp = raw[t], tk = rawk[t];
+                                    raw[t] = vv; rawk[t] = vk;
+                                    vv = tmp; vk = tk;
+                                }
                             } else if ((uint32_t)t == rn) {
                                 raw[t] = vv;
+                                rawk[t] = vk;
                             }
                         }
                         rn++;
@@ -1802,9 +1810,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             for (int t = 0; t < K; t++) {
                 if ((uint32_t)t < rn) {
                     const uint32_t s = raw[t];
-                    const uint32_t* e = X.segtab + (size_t)s * X.seg_stride;
+                    // the '#' row's link row was just read (a cache hit); else the segment's table row
+                    const uint32_t* e = X.eofrow ? X.eofrow + (size_t)rawk[t] * 16 : X.segtab + (size_t)s * X.seg_stride;
                     const uint32_t lo = e[0];
-                    n_blk++;
+                    if (!X.eofrow) n_blk++;
                     if (have && lo > run_s) { close_run(); have = false; }
                     if (!have) { run_x = e[1 + c]; have = true; }
                     run_y = e[X.seg_hi + c];
@@ -1859,6 +1868,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
     stat_add(ctr, ST_DEEPQ_STEPS, n_steps, sh);
     stat_add(ctr, ST_DEEP_HASH, n_hash, sh);
     stat_add(ctr, ST_DEEPQ_BLOCKS, n_blk, sh);
+    stat_add(ctr, ST_DEEPQ_PATS, n_q, sh);
     stat_add(ctr, ST_TEXT_CHARS, n_text, sh);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, sh);
 #ifdef EDSBWT_DEEP_CLOCKS
@@ -3314,6 +3324,15 @@ __global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
             e[1 + c] = r0[c];
             e[X.seg_hi + c] = r1[c];
         }
+    }
+}
+
+// per-'#'-row link rows (KIdx::eofrow): the segment link table's row of eof_seg[k], its segment in [15]
+__global__ void k_eofrow(uint32_t W, const uint32_t* __restrict__ eof_seg, const uint32_t* __restrict__ segtab, uint32_t* __restrict__ out) {
+    GRID_STRIDE(t, (size_t)W * 16) {
+        const size_t k = t >> 4;
+        const uint32_t j = (uint32_t)(t & 15), s = eof_seg[k];
+        out[t] = j == 15 ? s : segtab[(size_t)s * 16 + j];
     }
 }
 
