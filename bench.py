@@ -150,6 +150,21 @@ def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int,
     return {"value": sample / dt, "seconds": dt, "open_s": t_open, "counts": counts, "occ": occ, "ctr": ctr}
 
 
+def record_chunks(counts, budget: float) -> list:
+    """Cut points [0, ..., n] of contiguous pattern ranges holding at most `budget` records each
+    (greedy; a single pattern above the budget is a chunk of its own)."""
+    c = np.asarray(counts, np.int64)
+    cuts = [0]
+    csum = np.concatenate(([0], np.cumsum(c)))
+    n = c.size
+    while cuts[-1] < n:
+        a = cuts[-1]
+        # the furthest b with csum[b] - csum[a] <= budget, at least a + 1
+        b = int(np.searchsorted(csum, csum[a] + budget, side="right")) - 1
+        cuts.append(min(n, max(a + 1, b)))
+    return cuts
+
+
 def located_leg(idx, buf, offs, counts, dev, stream, first_id: int, budget: float, torch) -> dict:
     """C5's located leg: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
     and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so
@@ -159,14 +174,7 @@ def located_leg(idx, buf, offs, counts, dev, stream, first_id: int, budget: floa
     from the count-only leg, and its counts equal them.  Outside the timed legs, one pass."""
     npat = offs.size - 1
     c64 = counts.astype(np.int64)
-    cuts = [0]
-    acc = 0
-    for i in range(npat):  # greedy contiguous ranges of at most `budget` records
-        if acc + c64[i] > budget and i > cuts[-1]:
-            cuts.append(i)
-            acc = 0
-        acc += int(c64[i])
-    cuts.append(npat)
+    cuts = record_chunks(c64, budget)
     lens = np.diff(offs.astype(np.int64))
     chunks = []
     for a, b in zip(cuts[:-1], cuts[1:]):

@@ -142,6 +142,8 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_kernel_name.restype = ctypes.c_char_p
     L.edsbwt_format_csv.argtypes = [vp, u64, vp, u64, i32]
     L.edsbwt_format_csv.restype = u64
+    L.edsbwt_write_csv.argtypes = [vp, u64, i32, u64, i32]
+    L.edsbwt_write_csv.restype = ctypes.c_int64
     L.edsbwt_last_error.argtypes = []
     L.edsbwt_last_error.restype = ctypes.c_char_p
     L.edsbwt_abi_version.argtypes = []
@@ -394,6 +396,15 @@ def kernel_names() -> list:
     if _KNAMES is None:
         _KNAMES = [lib().edsbwt_kernel_name(i).decode() for i in range(16)]
     return _KNAMES
+
+
+def write_csv(occ: np.ndarray, fd: int, at: int = 0, threads: int = 8) -> int:
+    """CSV body rows written to file descriptor fd at byte offset `at` (edsbwt_write_csv)."""
+    occ = np.ascontiguousarray(occ, dtype=OCC_DTYPE)
+    n = int(lib().edsbwt_write_csv(occ.ctypes.data if occ.size else None, occ.size, fd, at, threads))
+    if n < 0:
+        raise OSError(ctypes.get_errno(), "edsbwt_write_csv failed")
+    return n
 
 
 def format_csv(occ: np.ndarray, threads: int = 8) -> bytes:

@@ -4,7 +4,10 @@
 // shrinks the host pipeline's uploads four-fold (engine.hip search_host_hsa).
 #include <immintrin.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -60,6 +63,68 @@ extern "C" uint64_t edsbwt_format_csv(const edsbwt_occ* occ, uint64_t nocc, char
         });
     for (auto& x : th) x.join();
     return sz[T];
+}
+
+// The same rows written straight to a file descriptor at byte offset `at` (the CLI's
+// <patterns>output_M_LF.csv after its header): each thread formats its contiguous range of
+// records into a private 8 MB buffer and pwrite()s it at the range's offset (the first pass
+// sizes the ranges), so no buffer of the whole CSV is built and the page-cache copies run in
+// parallel.  Returns the bytes written, or -1 (errno set) when a write fails.
+extern "C" int64_t edsbwt_write_csv(const edsbwt_occ* occ, uint64_t nocc, int fd, uint64_t at, int threads) {
+    if (threads < 1) threads = 1;
+    const uint64_t T = std::min<uint64_t>((uint64_t)threads, std::max<uint64_t>(1, nocc / 65536));
+    std::vector<uint64_t> sz(T + 1, 0);
+    auto lo = [&](uint64_t t) { return nocc * t / T; };
+    {
+        std::vector<std::thread> th;
+        for (uint64_t t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                uint64_t s = 0;
+                for (uint64_t i = lo(t); i < lo(t + 1); i++) s += row_len(occ[i]);
+                sz[t + 1] = s;
+            });
+        for (auto& x : th) x.join();
+    }
+    for (uint64_t t = 0; t < T; t++) sz[t + 1] += sz[t];
+    std::vector<int> err(T, 0);
+    std::vector<std::thread> th;
+    for (uint64_t t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            constexpr size_t kBuf = 8u << 20, kRowMax = 5 * 11;
+            std::vector<char> buf(kBuf);
+            uint64_t pos = at + sz[t];
+            char* p = buf.data();
+            auto flush = [&]() -> bool {
+                const size_t n = (size_t)(p - buf.data());
+                size_t done = 0;
+                while (done < n) {
+                    const ssize_t w = pwrite(fd, buf.data() + done, n - done, (off_t)(pos + done));
+                    if (w < 0) {
+                        if (errno == EINTR) continue;
+                        err[t] = errno;
+                        return false;
+                    }
+                    done += (size_t)w;
+                }
+                pos += n;
+                p = buf.data();
+                return true;
+            };
+            for (uint64_t i = lo(t); i < lo(t + 1); i++) {
+                if ((size_t)(p - buf.data()) + kRowMax > kBuf && !flush()) return;
+                const edsbwt_occ& o = occ[i];
+                p = put(p, o.pat, ndig(o.pat)); *p++ = '\t';
+                p = put(p, o.word, ndig(o.word)); *p++ = '\t';
+                p = put(p, o.seg, ndig(o.seg)); *p++ = '\t';
+                p = put(p, o.word_in_seg, ndig(o.word_in_seg)); *p++ = '\t';
+                p = put(p, o.offset, ndig(o.offset)); *p++ = '\n';
+            }
+            flush();
+        });
+    for (auto& x : th) x.join();
+    for (uint64_t t = 0; t < T; t++)
+        if (err[t]) { errno = err[t]; return -1; }
+    return (int64_t)sz[T];
 }
 
 // ---- fixed-length line packing.  A chunk of the pattern file (getline lines,

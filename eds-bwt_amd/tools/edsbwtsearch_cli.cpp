@@ -144,10 +144,14 @@ int main(int argc, char** argv) {
         return 1;
     }
     if (nocc) {
-        const uint64_t sz = edsbwt_format_csv(occ, nocc, nullptr, 0, 16);
-        std::vector<char> csv(sz);
-        edsbwt_format_csv(occ, nocc, csv.data(), sz, 16);
-        std::fwrite(csv.data(), 1, sz, fo);
+        // the rows go straight to the file: formatted per thread range and pwrite()n after the
+        // header (edsbwt_write_csv), no buffer of the whole CSV
+        std::fflush(fo);
+        const long at = std::ftell(fo);
+        if (at < 0 || edsbwt_write_csv(occ, nocc, fileno(fo), (uint64_t)at, 16) < 0) {
+            std::fprintf(stderr, "ERROR writing file %s\n", out.c_str());
+            return 1;
+        }
     }
     std::fclose(fo);
     // the console stream: which patterns reach the locate loop (the pattern without its first

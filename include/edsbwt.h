@@ -203,6 +203,11 @@ const char* edsbwt_kernel_name(int k);
  * the size needed when buf is NULL.  Multi-threaded. */
 uint64_t edsbwt_format_csv(const edsbwt_occ* occ, uint64_t nocc, char* buf, uint64_t cap, int threads);
 
+/* The same rows written to file descriptor fd at byte offset `at` (pwrite, several threads, no
+ * buffer of the whole CSV): the EDSBWTsearch CLI's <patterns>output_M_LF.csv body after its
+ * header (MOVE_EDSBWTSearch.cpp:55-64,365).  Returns the bytes written, or -1 with errno set. */
+int64_t edsbwt_write_csv(const edsbwt_occ* occ, uint64_t nocc, int fd, uint64_t at, int threads);
+
 const char* edsbwt_last_error(void);
 
 /* Index writer support (eds_transform --gpu; replaces gsufsort's suffix sort, EDS-BWTransform.sh:26

@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import numpy as np
+
 from conftest import ROOT
 
 
@@ -54,3 +56,24 @@ def test_read_pattern_file_getline(edsbwt, tmp_path):
     p.write_bytes(b"A\nC\n")
     buf, offs = edsbwt.read_pattern_file(str(p))
     assert len(offs) == 3
+
+
+def test_write_csv(edsbwt, tmp_path):
+    """edsbwt_write_csv (the CLI's pwrite path) writes the bytes edsbwt_format_csv builds, at
+    the given offset, with any thread count."""
+    rng = np.random.default_rng(9)
+    n = 300_000
+    occ = np.zeros(n, edsbwt.OCC_DTYPE)
+    for f, hi in (("pat", 10_000_000), ("word", 2**32 - 1), ("seg", 2**31), ("word_in_seg", 50), ("offset", 10**6)):
+        occ[f] = rng.integers(0, hi, size=n, dtype=np.uint64).astype(np.uint32)
+    want = edsbwt.format_csv(occ, threads=4)
+    for threads in (1, 3, 16):
+        p = tmp_path / f"o{threads}.csv"
+        with open(p, "wb") as f:
+            f.write(b"HEADER\n")
+            f.flush()
+            assert edsbwt.write_csv(occ, f.fileno(), 7, threads) == len(want)
+        assert p.read_bytes() == b"HEADER\n" + want
+    p = tmp_path / "empty.csv"
+    with open(p, "wb") as f:
+        assert edsbwt.write_csv(occ[:0], f.fileno(), 0, 4) == 0

@@ -256,7 +256,8 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
       pattern-major, every record spells its pattern in the .eds (orc_check_records).
     * The oracle's counts and records, in order, for: 8 patterns per length x planted class;
       up to 64 of the patterns the device walk sent to the wide lists / level re-run
-      (deep_overflow); the first and last pattern of every trie-subtree search group."""
+      (deep_overflow) and up to 64 of those its register-list walk k_deep finished; the first
+      and last pattern of every trie-subtree search group."""
     monkeypatch.setenv("EDSBWT_PATH_TAGS", "1")
     w = workloads.CONFIGS["c5"]
     wd = workloads.default_workdir()
@@ -297,12 +298,16 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
     assert (np.diff(pat0) >= 0).all() and np.array_equal(np.bincount(pat0, minlength=loc.size), cl.astype(np.int64))
     bad, first = oracle.check_records(eds, sb, so, ol, 1, threads=THREADS)
     assert bad == 0, (bad, ol[first])
-    # the targeted oracle sample
-    ovf = np.flatnonzero(tags & (edsbwt.PATH_WIDE | edsbwt.PATH_LEVELS))
-    assert ovf.size == dst["deep_overflow"], (ovf.size, dst["deep_overflow"])
-    ovf_s = ovf[np.linspace(0, ovf.size - 1, min(64, ovf.size)).astype(np.int64)] if ovf.size else ovf
+    # the targeted oracle sample: the rare paths of this walk (wide lists / level re-run: round 3
+    # had 433 such patterns at C5, none since the level start table; k_deep's register lists)
+    def spread(a, n):
+        return a[np.linspace(0, a.size - 1, min(n, a.size)).astype(np.int64)] if a.size else a
+    ovf = np.flatnonzero(tags & (edsbwt.PATH_WIDE | edsbwt.PATH_LEVELS | edsbwt.PATH_REDO))
+    assert np.flatnonzero(tags & (edsbwt.PATH_WIDE | edsbwt.PATH_LEVELS)).size == dst["deep_overflow"]
+    ovf_s = spread(ovf, 64)
+    deep_s = spread(np.flatnonzero(tags & edsbwt.PATH_DEEP), 64)
     gends = _group_ends(buf, offs, alphabet, st["search_groups"])
-    idx_s = np.unique(np.concatenate(samp + [ovf_s, gends]))
+    idx_s = np.unique(np.concatenate(samp + [ovf_s, deep_s, gends]))
     with edsbwt.Index(base) as idx:
         ss, soo = _subset(buf, offs, idx_s)
         cs, os_ = idx.search((ss, soo), first_pattern_id=1, locate=True)
@@ -319,6 +324,8 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
                    "located_patterns": int(loc.size), "located_records": int(ol.size), "located_s": round(t_loc, 2),
                    "located_by_length": {str(L): int((lens[loc] == L).sum()) for L in (8, 16, 32, 64)}, "check_records_bad": bad,
                    "deep_overflow": int(dst["deep_overflow"]), "deep_overflow_in_sample": int(ovf_s.size),
+                   "tagged_deep": int((tags & edsbwt.PATH_DEEP).astype(bool).sum()), "deep_in_sample": int(deep_s.size),
+                   "start_depth": int(st["start_depth"]),
                    "group_ends_in_sample": int(gends.size), "oracle_sample": int(idx_s.size), "oracle_sample_records": int(oo.size),
                    "oracle": "trie-sharing restatement (orc_search_batch_trie, pinned to the literal loop by tests/test_oracle.py)",
                    "oracle_s": round(t_orc, 1),
