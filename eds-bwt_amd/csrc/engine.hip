@@ -500,6 +500,16 @@ struct Engine {
     // spilled to VGPR lanes)
     int lvl_waves = (int)env_double("EDSBWT_LVL_WAVES", 7);
     int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 8);
+    // ... and computes the pattern keys itself, no k_keys_acgt (EDSBWT_FUSED_KEYS=0: off, A/B); the
+    // fused launch's inputs, set by direct() for run_deep
+    bool fused_keys = env_double("EDSBWT_FUSED_KEYS", 1) != 0;
+    struct FusedKeys {
+        bool on = false;
+        const uint8_t* bytes = nullptr;
+        const uint64_t* off = nullptr;
+        unsigned long long* n_term = nullptr;
+        uint32_t E = 0, lmin = 0, lmax = 0;
+    } fk_now;
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 4);  // k_deep<4, 3> likewise (4 unbounded)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
@@ -1679,10 +1689,20 @@ struct Engine {
         const uint4* kt1w = dstart && ktab_wide.p ? (const uint4*)ktab_wide.p : (const uint4*)nullptr;
         const bool kdd = pv && kt1w && !X.rent3 && deep_direct;
         if (!kdd) settle_res(r);  // (k_deep_direct writes every result; the other walks need zeros)
-        if (kdd) {
+        if (kdd && fk_now.on) {
+            // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
+            // written there, for k_deep and k_deep_wave)
+            auto kd0 = direct_waves >= 8 ? k_deep_direct<8, true> : direct_waves >= 7 ? k_deep_direct<7, true>
+                     : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
+            launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
+                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax);
+            fk_now.on = false;
+        } else if (kdd) {
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
                                                                                                         : k_deep_direct<1>;
-            launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p);
+            launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
+                   (const uint8_t*)nullptr, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned long long*)nullptr, 0u,
+                   0u, 0u);
         } else {
             auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
             launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
@@ -1841,9 +1861,25 @@ struct Engine {
             bhist.ensure(nbkt + 1);
             zero(bhist.p, (nbkt + 1) * 4);
         }
+        // fused: the deferred, input-ordered packed start with the wide entries (C3's path) computes
+        // the keys inside k_deep_direct (run_deep); its '#' / length check is deferred as k_keys_acgt's
+        const bool in_order = direct_sort_bits <= 0 || P < direct_sort_min;
+        fk_now = FusedKeys{};
+        if (fused_keys && defer_call && packed && !buckets && keys_packed && acgt_alpha && keys_swar && in_order && ktab_wide.p &&
+            !kidx().rent3 && deep_direct) {
+            fk_now.on = true;
+            fk_now.bytes = d_bytes;
+            fk_now.off = d_off;
+            fk_now.n_term = d_nterm;
+            fk_now.E = E;
+            fk_now.lmin = unmeasured ? D0 + 1 : 0u;
+            fk_now.lmax = unmeasured ? D0 + 16 : 0u;
+        }
         // key chunks (k_deep's queue reads them), D-mer ids and packed starts in one pass; the
         // packed start needs no chunks (EDSBWT_KEYS_PACKED=0: k_keys for it too)
-        if (packed && !buckets && keys_packed && acgt_alpha && keys_swar)
+        if (fk_now.on) {
+            // (k_deep_direct computes them)
+        } else if (packed && !buckets && keys_packed && acgt_alpha && keys_swar)
             launch(KC_TRIE, k_keys_acgt, P, d_bytes, d_off, P, len.p, d_nterm, D0, E, kid, pv_in.p, unmeasured ? D0 + 1 : 0u,
                    unmeasured ? D0 + 16 : 0u);
         else if (packed && !buckets && keys_packed)

@@ -587,6 +587,80 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) { return ~(((x & 0x7f
 // multiply-add per character.  The pattern's digits form V (its last character least
 // significant): kid = the low 2D bits, the packed start = the rest, closed by a 1 bit — the same
 // values k_keys_packed writes (its per-character loop is kept for patterns over 32 characters).
+// One pattern's D-mer id and packed start over {#, A, C, G, T} (k_keys_acgt, and the fused
+// direct start k_deep_direct<MINW, true>): its bytes from the block's LDS stage (sbuf, so = its
+// offset there) when staged, else from global memory.  x = the D-mer id (E when a byte is outside
+// the alphabet), rem = the remaining symbols closed by a 1 bit, term = '#' in the pattern or
+// (lmax != 0) a length outside [lmin, lmax].
+__device__ __forceinline__ void acgt_key(const uint8_t* __restrict__ bytes, uint64_t a, uint32_t L, bool staged, const uint32_t* sbuf,
+                                         uint32_t so, uint32_t D, uint32_t E, uint32_t lmin, uint32_t lmax, uint32_t& x_out,
+                                         uint64_t& rem_out, bool& term_out) {
+    uint64_t V = 0;
+    bool ok = true, term = lmax != 0 && (L < lmin || L > lmax);
+    if (L <= 32) {
+        for (uint32_t j = 0; j < L; j += 4) {
+            const uint32_t n = min(4u, L - j);
+            uint32_t w;
+            if (staged) {
+                const uint32_t o = so + j;
+                w = __builtin_amdgcn_alignbyte(sbuf[(o >> 2) + 1], sbuf[o >> 2], o & 3u);
+            } else {
+                w = 0;
+                for (uint32_t t = 0; t < n; t++) w |= (uint32_t)bytes[a + j + t] << (8 * t);
+            }
+            const uint32_t live = n == 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - n)));  // the n bytes in the pattern
+            const uint32_t mC = zero_bytes(w ^ 0x43434343u), mG = zero_bytes(w ^ 0x47474747u), mT = zero_bytes(w ^ 0x54545454u);
+            const uint32_t hit = zero_bytes(w ^ 0x41414141u) | mC | mG | mT;
+            ok &= (hit & live) == live;
+            term |= (zero_bytes(w ^ 0x23232323u) & live) != 0;
+            const uint32_t bad = ~hit & 0x80808080u;  // '#' or outside the alphabet: digit 3, as (0 - 1) & 3
+            const uint32_t q = ((mC | mT | bad) >> 7) | ((mG | mT | bad) >> 6);  // digit (A 0, C 1, G 2, T 3) per byte
+            const uint32_t pk = ((q & 3u) << 6) | (((q >> 8) & 3u) << 4) | (((q >> 16) & 3u) << 2) | ((q >> 24) & 3u);
+            V = (V << (2 * n)) | (pk >> (8 - 2 * n));
+        }
+        if (L <= D) {
+            x_out = ok ? (uint32_t)V : E;
+            rem_out = 1ull;
+        } else {
+            x_out = ok ? (uint32_t)(V & ((1ull << (2 * D)) - 1ull)) : E;
+            rem_out = (V >> (2 * D)) | (1ull << (2 * (L - D)));
+        }
+    } else {  // rare: longer patterns keep k_keys_packed's per-character order
+        uint32_t x = 0, mul = 1, nn = 0;
+        uint64_t rem = 0;
+        for (uint32_t t = 0; t < L; t++) {
+            const uint32_t ch = bytes[a + L - 1 - t];
+            const uint32_t v = ch == 'A' ? 1u : ch == 'C' ? 2u : ch == 'G' ? 3u : ch == 'T' ? 4u : 0u;
+            term |= ch == '#';
+            ok &= v != 0;
+            if (t < D) { x += (v - 1) * mul; mul *= 4u; }
+            else { rem |= (uint64_t)((v - 1) & 3u) << (2 * nn); nn++; }
+        }
+        rem |= 1ull << (2 * nn);
+        x_out = ok ? x : E;
+        rem_out = rem;
+    }
+    term_out = term;
+}
+
+// Stage the bytes of the block's patterns [base, base + nb) in LDS (16-B aligned words from
+// w0 = off[base] & ~15) when they fit kKeySpan and the buffer is 16-B aligned; every thread of
+// the block calls it.  Returns whether they were staged.
+__device__ __forceinline__ bool stage_patterns(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, size_t base, size_t nb,
+                                               uint4* sbuf4, uint64_t& w0) {
+    const uint64_t s0 = off[base], s1 = off[base + nb];
+    w0 = s0 & ~15ull;
+    const bool staged = s1 - w0 + 16 <= kKeySpan && ((uintptr_t)bytes & 15) == 0;
+    __syncthreads();
+    if (staged) {
+        const uint32_t nw = (uint32_t)((s1 - w0 + 15) / 16);
+        const uint4* src = reinterpret_cast<const uint4*>(bytes + w0);
+        for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x) sbuf4[t] = src[t];
+    }
+    __syncthreads();
+    return staged;
+}
+
 __global__ void __launch_bounds__(256) k_keys_acgt(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t P,
                                                    uint32_t* __restrict__ len, unsigned long long* __restrict__ n_term, uint32_t D,
                                                    uint32_t E, uint32_t* __restrict__ kid, uint64_t* __restrict__ pv, uint32_t lmin,
@@ -599,74 +673,20 @@ __global__ void __launch_bounds__(256) k_keys_acgt(const uint8_t* __restrict__ b
     unsigned long long nt = 0;
     for (size_t base = (size_t)blockIdx.x * blockDim.x; base < P; base += (size_t)gridDim.x * blockDim.x) {
         const size_t nb = min((size_t)blockDim.x, (size_t)P - base);
-        const uint64_t s0 = off[base], s1 = off[base + nb];
-        const uint64_t w0 = s0 & ~15ull;
-        const bool staged = s1 - w0 + 16 <= kKeySpan && ((uintptr_t)bytes & 15) == 0;
-        __syncthreads();
-        if (staged) {
-            const uint32_t nw = (uint32_t)((s1 - w0 + 15) / 16);
-            const uint4* src = reinterpret_cast<const uint4*>(bytes + w0);
-            for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x) sbuf4[t] = src[t];
-        }
-        __syncthreads();
+        uint64_t w0;
+        const bool staged = stage_patterns(bytes, off, base, nb, sbuf4, w0);
         const size_t i = base + threadIdx.x;
         if (i < P) {
             const uint64_t a = off[i];
             const uint32_t L = (uint32_t)(off[i + 1] - a);
             len[i] = L;
-            uint64_t V = 0;
-            bool ok = true, term = lmax != 0 && (L < lmin || L > lmax);
-            if (L <= 32) {
-                const uint32_t so = (uint32_t)(a - w0);
-                for (uint32_t j = 0; j < L; j += 4) {
-                    const uint32_t n = min(4u, L - j);
-                    uint32_t w;
-                    if (staged) {
-                        const uint32_t o = so + j;
-                        w = __builtin_amdgcn_alignbyte(sbuf[(o >> 2) + 1], sbuf[o >> 2], o & 3u);
-                    } else {
-                        w = 0;
-                        for (uint32_t t = 0; t < n; t++) w |= (uint32_t)bytes[a + j + t] << (8 * t);
-                    }
-                    const uint32_t live = n == 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - n)));  // the n bytes in the pattern
-                    const uint32_t mC = zero_bytes(w ^ 0x43434343u), mG = zero_bytes(w ^ 0x47474747u), mT = zero_bytes(w ^ 0x54545454u);
-                    const uint32_t hit = zero_bytes(w ^ 0x41414141u) | mC | mG | mT;
-                    ok &= (hit & live) == live;
-                    term |= (zero_bytes(w ^ 0x23232323u) & live) != 0;
-                    const uint32_t bad = ~hit & 0x80808080u;  // '#' or outside the alphabet: digit 3, as (0 - 1) & 3
-                    const uint32_t q = ((mC | mT | bad) >> 7) | ((mG | mT | bad) >> 6);  // digit (A 0, C 1, G 2, T 3) per byte
-                    const uint32_t pk = ((q & 3u) << 6) | (((q >> 8) & 3u) << 4) | (((q >> 16) & 3u) << 2) | ((q >> 24) & 3u);
-                    V = (V << (2 * n)) | (pk >> (8 - 2 * n));
-                }
-            } else {  // rare: longer patterns keep k_keys_packed's per-character order
-                uint32_t x = 0, mul = 1, nn = 0;
-                uint64_t rem = 0;
-                for (uint32_t t = 0; t < L; t++) {
-                    const uint32_t ch = bytes[a + L - 1 - t];
-                    const uint32_t v = ch == 'A' ? 1u : ch == 'C' ? 2u : ch == 'G' ? 3u : ch == 'T' ? 4u : 0u;
-                    term |= ch == '#';
-                    ok &= v != 0;
-                    if (t < D) { x += (v - 1) * mul; mul *= 4u; }
-                    else { rem |= (uint64_t)((v - 1) & 3u) << (2 * nn); nn++; }
-                }
-                nt += term;
-                rem |= 1ull << (2 * nn);
-                pv[i] = rem << 31 | (uint64_t)i;
-                kid[i] = ok ? x : E;
-                continue;
-            }
-            nt += term;
             uint32_t x;
             uint64_t rem;
-            if (L <= D) {
-                x = (uint32_t)V;
-                rem = 1ull;
-            } else {
-                x = (uint32_t)(V & ((1ull << (2 * D)) - 1ull));
-                rem = (V >> (2 * D)) | (1ull << (2 * (L - D)));
-            }
+            bool term;
+            acgt_key(bytes, a, L, staged, sbuf, (uint32_t)(a - w0), D, E, lmin, lmax, x, rem, term);
+            nt += term;
             pv[i] = rem << 31 | (uint64_t)i;
-            kid[i] = ok ? x : E;
+            kid[i] = x;
         }
     }
     nt = block_sum(nt, sh);
@@ -1416,30 +1436,63 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
 // generic key-chunk reader, list offsets and rent3 it needs fewer registers, and the walk is
 // latency-bound (C3: 6 waves per SIMD instead of 5 took k_deep_fast from 1.02 to 0.92 ms).
 // It writes every pattern's result (an empty list's too), so the result array needs no zeroing.
-template <int MINW>
+//
+// FUSED (the default on that path, EDSBWT_FUSED_KEYS=0: k_keys_acgt first): the pattern keys are
+// computed here from the pattern bytes (staged in LDS per block round, as k_keys_acgt stages
+// them) instead of being read back from k_keys_acgt's kid / pv arrays — one launch and ~0.3 GB of
+// C3 stream traffic less.  kid and len are still written for every pattern (k_deep and
+// k_deep_wave read the queued ones'), and '#' / unexpected lengths counted into n_term for the
+// deferred check.
+template <int MINW, bool FUSED = false>
 __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
                                                            uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
                                                            uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
                                                            const uint64_t* __restrict__ pv, uint32_t* __restrict__ perm_out,
-                                                           const uint4* __restrict__ kt1w, uint64_t* __restrict__ q2) {
+                                                           const uint4* __restrict__ kt1w, uint64_t* __restrict__ q2,
+                                                           const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                           uint32_t* __restrict__ len_out, uint32_t* __restrict__ kid_out,
+                                                           unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax) {
     uint32_t n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;  // per lane: < 2^32 (widened at the end)
+    unsigned long long nt = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
+    __shared__ uint4 sbuf4[FUSED ? kKeySpan / 16 + 2 : 1];
     UNIFORM_STRIDE(i, valid, P) {
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
-        const uint64_t v = valid ? pv[i] : 0ull;
-        const uint32_t pi = (uint32_t)(v & 0x7fffffffu);
-        const uint64_t rem = v >> 31;
-        const uint32_t L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
+        uint32_t pi, L, kx = 0;
+        uint64_t rem;
+        if constexpr (FUSED) {
+            const size_t base = i - threadIdx.x;
+            uint64_t w0;
+            const bool staged = stage_patterns(bytes, off, base, min((size_t)blockDim.x, (size_t)P - base), sbuf4, w0);
+            pi = (uint32_t)i;
+            rem = 0;
+            L = 0;
+            if (valid) {
+                const uint64_t a = off[i];
+                const uint32_t Lp = (uint32_t)(off[i + 1] - a);
+                bool term;
+                acgt_key(bytes, a, Lp, staged, reinterpret_cast<const uint32_t*>(sbuf4), (uint32_t)(a - w0), D0, E, lmin, lmax, kx, rem, term);
+                nt += term;
+                len_out[i] = Lp;
+                kid_out[i] = kx;
+                L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
+            }
+        } else {
+            const uint64_t v = valid ? pv[i] : 0ull;
+            pi = (uint32_t)(v & 0x7fffffffu);
+            rem = v >> 31;
+            L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
+        }
         if (valid) perm_out[i] = pi;
         // the D-mer's wide entry: its one interval inline (or its list's length), and for one
         // row with its text position, the row's sample and the 32 text characters before it
         uint64_t ent = 0, win1 = 0;
         uint4 s1 = make_uint4(0, 0, 0, 0);
         if (L > D0) {
-            const size_t u = nid[i];
+            const size_t u = FUSED ? kx : nid[i];
             const uint4 w0 = kt1w[2 * u];
             s1 = kt1w[2 * u + 1];
             ent = (uint64_t)w0.y << 32 | w0.x;
@@ -1591,6 +1644,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
     stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
+    if constexpr (FUSED) {
+        nt = block_sum(nt, ssum);
+        if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
+    }
 }
 
 // rank of `lane` among the set lanes of mask m

@@ -530,6 +530,23 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
                         assert np.array_equal(go, oo), (wide, sort_bits, srow, packed, kw)
                     if not kw:
                         assert st["text_rows"] > 1000, st
+    # the packed direct start with its keys computed inside k_deep_direct (the default on the
+    # deferred input-order path) against the separate key kernel (EDSBWT_FUSED_KEYS=0), with
+    # patterns outside the guessed lengths (the deferred check sends those batches to the redo)
+    for pats in (short, short + ["ACGT" * 4, "A" * (D0 + 17)]):
+        buf, offs = _pack(pats)
+        oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+        for fused in ("1", "0"):
+            monkeypatch.setenv("EDSBWT_FUSED_KEYS", fused)
+            for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED"):
+                monkeypatch.delenv(k_, raising=False)
+            with edsbwt.Index(base) as idx:
+                for kw in ({}, {"locate": False}):
+                    gc, go = idx.search((buf, offs), **kw)
+                    assert np.array_equal(gc, oc), (fused, kw, len(pats))
+                    if kw.get("locate", True):
+                        assert np.array_equal(go, oo), (fused, kw, len(pats))
+    monkeypatch.delenv("EDSBWT_FUSED_KEYS")
     E = (4 ** D0) + 1
     assert sizes["11"] - sizes["01"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
     assert sizes["11"] > sizes["10"]  # ... and the per-row entries
