@@ -22,7 +22,8 @@ B0="python3 bench.py --no-cpu --no-e2e --no-located --steps 3 --warmup 1"
 fail() { echo "FAIL $1"; tail -30 "$2"; exit 1; }
 for task in "$@"; do
   IFS=: read -r kind a b c d <<< "$task"
-  out=gpurun_out/${TAG}_${kind}${a:+_$a}
+  tag_a=${a//[^A-Za-z0-9_]/_}
+  out=gpurun_out/${TAG}_${kind}${tag_a:+_$tag_a}
   echo "[gpu.sh] $task -> $out ($(date +%T))"
   case $kind in
     suite)
