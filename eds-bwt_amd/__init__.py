@@ -142,8 +142,9 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_kernel_name.restype = ctypes.c_char_p
     L.edsbwt_format_csv.argtypes = [vp, u64, vp, u64, i32]
     L.edsbwt_format_csv.restype = u64
-    L.edsbwt_write_csv.argtypes = [vp, u64, i32, u64, i32]
-    L.edsbwt_write_csv.restype = ctypes.c_int64
+    if hasattr(L, "edsbwt_write_csv"):  # (an EDSBWT_LIB override built before ABI 4 lacks it)
+        L.edsbwt_write_csv.argtypes = [vp, u64, i32, u64, i32]
+        L.edsbwt_write_csv.restype = ctypes.c_int64
     L.edsbwt_last_error.argtypes = []
     L.edsbwt_last_error.restype = ctypes.c_char_p
     L.edsbwt_abi_version.argtypes = []

@@ -143,6 +143,10 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "%s\n", edsbwt_last_error());
         return 1;
     }
+    // EDSBWT_CLI_TIMES=1: the pattern loop's phases on stderr (search, CSV, console)
+    const bool times = std::getenv("EDSBWT_CLI_TIMES") != nullptr;
+    auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    if (times) std::fprintf(stderr, "[cli] search %.4f s (%llu patterns, %llu records)\n", since(), (unsigned long long)npat, (unsigned long long)nocc);
     if (nocc) {
         // the rows go straight to the file: formatted per thread range and pwrite()n after the
         // header (edsbwt_write_csv), no buffer of the whole CSV
@@ -154,6 +158,7 @@ int main(int argc, char** argv) {
         }
     }
     std::fclose(fo);
+    if (times) std::fprintf(stderr, "[cli] csv written %.4f s\n", since());
     // the console stream: which patterns reach the locate loop (the pattern without its first
     // character occurs, or the pattern is one character long) — one more count-only search
     std::vector<uint8_t> reach;
@@ -207,6 +212,7 @@ int main(int argc, char** argv) {
         }
         line = end + 1;
     }
+    if (times) std::fprintf(stderr, "[cli] console loop done %.4f s\n", since());
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::printf("bs took:%g", secs);
     std::fflush(stdout);

@@ -53,14 +53,15 @@ def main():
         if os.path.exists(csv_path):
             os.remove(csv_path)
         t = time.perf_counter()
-        r = subprocess.run([cli, base, pats, "--quiet"], capture_output=True)
+        r = subprocess.run([cli, base, pats, "--quiet"], capture_output=True, env=dict(os.environ, EDSBWT_CLI_TIMES="1"))
         wall = time.perf_counter() - t
         if r.returncode != 1:  # the reference exits 1 on success (mainMove_EDSBWT.cpp:61)
             sys.exit(f"EDSBWTsearch exited {r.returncode}: {r.stderr[-400:]!r}")
         m = re.search(rb"bs took:([0-9.e+-]+)$", r.stdout)
         found = re.search(rb"count_found = (\d+)", r.stderr)
+        phases = {m_.group(1).decode(): float(m_.group(2)) for m_ in re.finditer(rb"\[cli\] ([a-z ]+?) ([0-9.]+) s", r.stderr)}
         runs.append({"wall_s": round(wall, 3), "bs_took_s": float(m.group(1)) if m else None,
-                     "count_found": int(found.group(1)) if found else None})
+                     "count_found": int(found.group(1)) if found else None, "phases_s": phases})
         print(f"[cli] run: wall {wall:.3f}s, bs took {runs[-1]['bs_took_s']}", file=sys.stderr, flush=True)
     csv = open(csv_path, "rb").read()
     header = b"#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n"
