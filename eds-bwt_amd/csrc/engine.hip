@@ -3057,6 +3057,7 @@ struct Engine {
     // into stage_pack[sl]: returns its lines (0: the chunk is not of that form; send the bytes).
     // EDSBWT_PACK_LINES=0 turns it off.
     bool pack_lines = env_double("EDSBWT_PACK_LINES", 1) != 0;
+    bool pack_single = env_double("EDSBWT_PACK_SINGLE", 1) != 0;
     uint64_t pack_threads = 64;  // per call: EDSBWT_PACK_THREADS (at most the pool's)
     uint64_t pack_chunk(const uint8_t* s, uint64_t nb, const uint8_t* end, int sl, uint32_t* L_out) {
         if (!pack_lines) return 0;
@@ -3308,7 +3309,10 @@ struct Engine {
                     mark("upload", k);
                     uint32_t L = 0;
                     uint64_t Pk = 0;
-                    if (lines) Pk = pre_k == k ? (L = pre_L, pre_P) : pack_chunk(text + c.b0, nb, text_end, sl, &L);
+                    // a one-chunk batch's packing has nothing to overlap with: EDSBWT_PACK_SINGLE=0 sends
+                    // it raw (C2: 21 MB raw at ~56 GB/s against packing on the host first)
+                    if (lines && (nch > 1 || pack_single))
+                        Pk = pre_k == k ? (L = pre_L, pre_P) : pack_chunk(text + c.b0, nb, text_end, sl, &L);
                     pre_k = ~size_t(0);
                     if (Pk) {  // 2 bits per base over PCIe, unpacked on the device
                         const uint64_t pb = Pk * ((L + 3) / 4);
