@@ -205,6 +205,9 @@ struct Engine {
     DBuf<uint32_t> seg_chain;  // bit s: seg_lo[s] != s - 1 (k_run_flags gathers seg_lo only there)
     DBuf<uint32_t> eof_key;    // [W] eof_seg[k] << 1 | chain bit of that segment (0: segment 1): KIdx::link_seg
     DBuf<uint32_t> eofrow;     // [W][16] per-'#'-row link rows (KIdx::eofrow; sigma <= 7, W * 64 B <= kEofRowMaxBytes)
+    // the segment link table in 128-B rows with the text-item entries of KIdx::segtext (sigma <= 5;
+    // EDSBWT_SEGTEXT=0: 64-B rows, none); filled after the per-row text entries (build_segtext)
+    bool segtab_wide = false, have_segtext = false;
     DBuf<uint32_t> kpos;  // '#'-row rank of each word (inverse of eof_word): legacy output order
     DBuf<uint8_t> code_of;
     uint8_t h_code_of[256];
@@ -544,8 +547,9 @@ struct Engine {
         X.samples = samples.p;
         X.samp_dense = have_samples && samp_shift == 0 ? 1u : 0u;
         X.segtab = segtab.p;
-        X.seg_stride = sigma <= 7 ? 16u : 32u;
+        X.seg_stride = (sigma <= 7 && !segtab_wide) ? 16u : 32u;
         X.seg_hi = sigma <= 7 ? 8u : 9u;
+        X.segtext = have_segtext ? 1u : 0u;
         X.N = N; X.W = W; X.S = S; X.sigma = sigma;
         X.segbits = bits_for(S);
         X.rowbits = bits_for(N);
@@ -970,15 +974,16 @@ struct Engine {
         up(code_of, co);
         counters.ensure(32);
         {  // segment link table (k_deep)
+            segtab_wide = sigma <= 5 && env_double("EDSBWT_SEGTEXT", 1) != 0;
             const KIdx X0 = kidx();
             segtab.ensure((size_t)(S + 2) * X0.seg_stride);
             device_bytes += (size_t)(S + 2) * X0.seg_stride * 4;
             launch(KC_TABLE, k_segtab, (size_t)S + 2, S, kidx(), segtab.p);
             // k_deep's links from '#' rows: one line per row instead of eof_seg then segtab
             // (C3: 3.8M words, 243 MB; EDSBWT_EOF_ROWS=0: off)
-            if (X0.seg_stride == 16 && (double)W * 64 <= kEofRowMaxBytes && env_double("EDSBWT_EOF_ROWS", 1) != 0) {
+            if (X0.seg_hi == 8 && (double)W * 64 <= kEofRowMaxBytes && env_double("EDSBWT_EOF_ROWS", 1) != 0) {
                 eofrow.ensure((size_t)W * 16);
-                launch(KC_TABLE, k_eofrow, (size_t)W * 16, W, (const uint32_t*)eof_seg.p, (const uint32_t*)segtab.p, eofrow.p);
+                launch(KC_TABLE, k_eofrow, (size_t)W * 16, W, (const uint32_t*)eof_seg.p, (const uint32_t*)segtab.p, X0.seg_stride, eofrow.p);
                 device_bytes += (size_t)W * 64;
             }
             HIPCHK(hipStreamSynchronize(stream));
@@ -989,6 +994,7 @@ struct Engine {
         // last: the k-mer table's interval budget is a share of the free HBM, which the 32-B
         // per-row entries would take first (C5: 40 GB, the table then one depth shallower)
         build_srow();
+        build_segtext();
         // after the per-row entries: the level table's budget is a share of what HBM has left
         build_ltab();
     }
@@ -1103,6 +1109,14 @@ struct Engine {
                              std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
             return;
         }
+    }
+
+    // KIdx::segtext: each segment row's text-item entries, from the per-row text entries (k_segtext)
+    void build_segtext() {
+        if (!segtab_wide || !srow.p || sigma > 5) return;
+        launch(KC_TABLE, k_segtext, (size_t)S + 2, S, kidx(), segtab.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        have_segtext = true;
     }
 
     // Per-row text-compare entries (KIdx::srow, 32 B per row: C3 3.3 GB): with dense samples and
@@ -2233,7 +2247,8 @@ struct Engine {
                     // (a redo after a regrow adds no counts: the first launch counted every item)
                     launch(KC_STEP, lvl_waves >= 8 ? k_lvl_dollar<8> : k_lvl_dollar<1>, nkeys, (const uint32_t*)d_runs, (const uint32_t*)ru.p, (const uint32_t*)rb.p, (const uint32_t*)re.p,
                            (const uint64_t*)child_info.p, X, eu.p, eb.p, ee.p,
-                           (uint32_t)cap_next, lcnt.p, stats.p, fuse_fin && dfirst ? node_occ.p : (uint32_t*)nullptr);
+                           (uint32_t)cap_next, lcnt.p, stats.p, fuse_fin && dfirst ? node_occ.p : (uint32_t*)nullptr,
+                           titems ? (text_stop ? 1u : 3u) : 0u);
                     fetch_shards();  // sync B
                     const uint32_t m0 = shard_max(0);
                     if (m0 <= cap_next) break;

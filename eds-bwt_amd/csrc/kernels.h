@@ -120,6 +120,11 @@ struct KIdx {
     // '#' row reads ONE line (its segment and that segment's ranks) instead of eof_seg[k] and
     // then, dependent on it, segtab[s]
     const uint32_t* eofrow;
+    // segtext = 1: the segment link table's rows are 32 u32 (128 B, one DRAM request as the 64-B
+    // ones) and [16 + 2 (c - 1)], [17 + 2 (c - 1)] hold, for c = 1..4, the text-item form (kernels.hip
+    // kTextItem) of the ONE word of [seg_lo[s], s - 1] ending with c, when there is one: the dollar
+    // step then hands that single row on as a text item (no srow read at the next depth)
+    uint32_t segtext;
 };
 
 }  // namespace edsbwt

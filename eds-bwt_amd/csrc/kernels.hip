@@ -2352,15 +2352,18 @@ __device__ __forceinline__ void fin_flush(const uint32_t* hk, const uint32_t* hv
 
 __device__ __forceinline__ void lvl_emit(uint32_t mask, uint32_t emit, uint32_t cf, const uint32_t* rb, const uint32_t* re, const KIdx& X,
                                          uint32_t at, uint32_t cap, uint32_t* __restrict__ nu, uint32_t* __restrict__ nb,
-                                         uint32_t* __restrict__ ne, uint32_t* hk, uint32_t* hv, uint32_t* __restrict__ node_occ) {
+                                         uint32_t* __restrict__ ne, uint32_t* hk, uint32_t* hv, uint32_t* __restrict__ node_occ,
+                                         uint32_t tmask = 0, const uint2* tform = nullptr) {
+    // tmask bit c: child c's one row goes on as the text item tform[c] (k_lvl_dollar, KIdx::segtext)
 #pragma unroll
     for (uint32_t c = 0; c < 8; c++)
         if ((emit >> c) & 1) {
             const uint32_t child = cf + (uint32_t)__popc(mask & ((1u << c) - 1u));
             if (at < cap) {
                 nu[at] = child;
-                nb[at] = X.C[c] + rb[c];
-                ne[at] = X.C[c] + re[c] - 1;
+                const bool t = (tmask >> c) & 1u;
+                nb[at] = t ? tform[c].x : X.C[c] + rb[c];
+                ne[at] = t ? tform[c].y : X.C[c] + re[c] - 1;
             }
             at++;
             // (counted whether or not the append fits: a relaunch after a regrow passes no node_occ)
@@ -2573,7 +2576,9 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_dollar(const uint32_t* __rest
                                                     const uint32_t* __restrict__ de, const uint64_t* __restrict__ child_info, KIdx X,
                                                     uint32_t* __restrict__ nu, uint32_t* __restrict__ nb, uint32_t* __restrict__ ne,
                                                     uint32_t cap_next, uint32_t* __restrict__ cnt_all, unsigned long long* __restrict__ stats,
-                                                    uint32_t* __restrict__ node_occ) {
+                                                    uint32_t* __restrict__ node_occ, uint32_t text_mode) {
+    // text_mode bit 1 (text items made at this depth) with KIdx::segtext: a single-key run's child
+    // interval of ONE row goes on as that row's text item, read from the run's own segment row
     const uint32_t n = *dn;  // link runs, counted on the device by k_run_build
     unsigned long long n_blk = 0;  // occ blocks read
     // node_occ != nullptr (count only): finishing children's occurrences are summed here
@@ -2590,12 +2595,17 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_dollar(const uint32_t* __rest
         uint32_t rb[8], re[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) rb[t] = re[t] = 0;
+        uint2 tform[8];
+        bool one_seg = false;
+        const uint32_t* e0 = nullptr;
         if (valid) {
             const uint32_t u = du[i];
             const uint64_t ci = child_info[u];
-            const uint32_t* e0 = X.segtab + (size_t)db[i] * X.seg_stride;  // s_first: ranks at the run's first word
-            const uint32_t* e1 = X.segtab + (size_t)de[i] * X.seg_stride;  // s_last: ranks one past its last word
-            if (X.seg_stride == 16) {  // sigma <= 7: [lo, lo-ranks 1..7 | hi-ranks 8..14, pad] as 16-B vectors
+            const uint32_t s0 = db[i], s1 = de[i];
+            one_seg = s0 == s1;
+            e0 = X.segtab + (size_t)s0 * X.seg_stride;  // s_first: ranks at the run's first word
+            const uint32_t* e1 = X.segtab + (size_t)s1 * X.seg_stride;  // s_last: ranks one past its last word
+            if (X.seg_stride >= 16 && X.seg_hi == 8) {  // sigma <= 7: [lo, lo-ranks 1..7 | hi-ranks 8..14, pad] as 16-B vectors
                 const uint4 a0 = reinterpret_cast<const uint4*>(e0)[0], a1 = reinterpret_cast<const uint4*>(e0)[1];
                 const uint4 b0 = reinterpret_cast<const uint4*>(e1)[2], b1 = reinterpret_cast<const uint4*>(e1)[3];
                 rb[0] = a0.y; rb[1] = a0.z; rb[2] = a0.w; rb[3] = a1.x; rb[4] = a1.y; rb[5] = a1.z; rb[6] = a1.w;
@@ -2613,8 +2623,26 @@ __global__ void __launch_bounds__(256, MINW) k_lvl_dollar(const uint32_t* __rest
 #pragma unroll
         for (uint32_t c = 0; c < 8; c++)
             if (((mask >> c) & 1) && re[c] > rb[c]) emit |= 1u << c;
+        uint32_t tmask = 0;
+        if ((text_mode & 2u) && X.segtext && one_seg) {
+            // single rows of a one-key run: the word's text item from the run segment's row (same line)
+#pragma unroll
+            for (uint32_t c = 1; c <= 4; c++)
+                if (((emit >> c) & 1) && re[c] - rb[c] == 1) {
+                    tform[c] = reinterpret_cast<const uint2*>(e0 + 16)[c - 1];
+                    if (tform[c].x & kTextItem) tmask |= 1u << c;
+                }
+        }
         const uint32_t at = wave_append(cnt + 0, (uint32_t)__popc(emit));
-        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne, hk, hv, node_occ);
+        lvl_emit(mask, emit, cf, rb, re, X, at, cap_next, nu, nb, ne, hk, hv, node_occ, tmask, tform);
+        if (text_mode) {  // text items handed to the next depth (the deep cutover waits for none)
+            const uint64_t tb = __ballot(tmask != 0);
+            const uint32_t nt = (uint32_t)__popc(tmask);
+            uint32_t wsum = nt;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) wsum += __shfl_xor(wsum, o, 64);
+            if ((threadIdx.x & 63) == 0 && tb) atomicAdd(cnt + 5, wsum);
+        }
     }
     if (node_occ) {
         __syncthreads();
@@ -3385,11 +3413,48 @@ __global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
 }
 
 // per-'#'-row link rows (KIdx::eofrow): the segment link table's row of eof_seg[k], its segment in [15]
-__global__ void k_eofrow(uint32_t W, const uint32_t* __restrict__ eof_seg, const uint32_t* __restrict__ segtab, uint32_t* __restrict__ out) {
+__global__ void k_eofrow(uint32_t W, const uint32_t* __restrict__ eof_seg, const uint32_t* __restrict__ segtab, uint32_t stride,
+                         uint32_t* __restrict__ out) {
     GRID_STRIDE(t, (size_t)W * 16) {
         const size_t k = t >> 4;
         const uint32_t j = (uint32_t)(t & 15), s = eof_seg[k];
-        out[t] = j == 15 ? s : segtab[(size_t)s * 16 + j];
+        out[t] = j == 15 ? s : segtab[(size_t)s * stride + j];
+    }
+}
+
+// KIdx::segtext: per segment s, for c = 1..4, the text item of the one word of [seg_lo[s], s - 1]
+// whose last character is c (its row is LF of the word's '#' row w: C[c] + rank_c(L, w)), from that
+// row's srow entry as k_lvl_items would convert it: kTextItem | offset << 27 | segment, and the
+// 15 characters before the row (2 bits each) | its segment's chain bit << 31; 0 when no or several
+// words end with c, or the word is longer than 16
+__global__ void k_segtext(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
+    GRID_STRIDE(s, (size_t)S + 2) {
+        uint32_t* e = tab + s * X.seg_stride + 16;
+        uint32_t cnt[5] = {0, 0, 0, 0, 0}, row[5] = {0, 0, 0, 0, 0};
+        if (s >= 2) {
+            const uint32_t lo = X.seg_lo[s];
+            for (uint32_t w = X.seg_start[lo]; w < X.seg_start[s]; w++) {
+                uint32_t rk;
+                const uint32_t c = sym_rank(X.occ, w, &rk);
+                if (c >= 1 && c <= 4) {
+                    cnt[c]++;
+                    row[c] = X.C[c] + rk;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t c = 1; c <= 4; c++) {
+            uint32_t b = 0, f = 0;
+            if (cnt[c] == 1) {
+                const uint4 s0 = X.srow[2 * (size_t)row[c]], s1 = X.srow[2 * (size_t)row[c] + 1];
+                if (s0.y <= 15 && s0.z < kTextSeg) {
+                    b = kTextItem | (s0.y << 27) | s0.z;
+                    f = (s1.z & 0x7fffffffu) | ((s1.y & 1u) << 31);
+                }
+            }
+            e[2 * (c - 1)] = b;
+            e[2 * (c - 1) + 1] = f;
+        }
     }
 }
 

@@ -69,8 +69,9 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
             assert np.array_equal(gc5, oc) and np.array_equal(go5, oo)
     # the defaults' A/B fallbacks (read when an index opens): the finisher pass instead of the
     # fused count (k_fin_flags / k_fin_emit), no text items, eof_seg link keys without the chain
-    # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide)
-    for var in ("EDSBWT_FUSE_FINISH", "EDSBWT_TEXT_ITEMS", "EDSBWT_LINK_CB", "EDSBWT_DEEP_WAVE"):
+    # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
+    # the dollar step's text-item entries
+    for var in ("EDSBWT_FUSE_FINISH", "EDSBWT_TEXT_ITEMS", "EDSBWT_LINK_CB", "EDSBWT_DEEP_WAVE", "EDSBWT_SEGTEXT"):
         old = os.environ.get(var)
         os.environ[var] = "0"
         try:
