@@ -2260,6 +2260,9 @@ struct Engine {
                     small_copy(lcnt.p, pinned_big, NSHARD * 32 * 4);
                     cap_next = ncap;
                 }
+                // the dollar step makes text items too (KIdx::segtext): the count after it (a redo
+                // after a regrow counts some twice, which only delays the cutover)
+                if (titems) text_alive = shard_total(5);
                 const uint32_t R = hsh[NSHARD * 32];
                 st.link_ranges += R;
                 st.intervals_stepped += R;
