@@ -174,6 +174,10 @@ def located_leg(idx, buf, offs, counts, dev, stream, first_id: int, budget: floa
     from the count-only leg, and its counts equal them.  Outside the timed legs, one pass."""
     npat = offs.size - 1
     c64 = counts.astype(np.int64)
+    # at most the requested budget, and what the free HBM holds at ~64 B of locate workspace per
+    # record (records 20 B, the finishers' sort and archive, the interval shards)
+    free_b, _ = torch.cuda.mem_get_info(dev)
+    budget = min(budget, 0.6 * free_b / 64.0)
     cuts = record_chunks(c64, budget)
     lens = np.diff(offs.astype(np.int64))
     chunks = []
