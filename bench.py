@@ -227,6 +227,9 @@ def main():
                     help="profiling runs: only the device-resident leg (its kernel averages then match a rocprofv3 "
                          "trace of the whole run); the line's value is then the device-resident rate")
     ap.add_argument("--no-located", action="store_true", help="C5: skip the located leg")
+    ap.add_argument("--dist-self", action="store_true",
+                    help="run the N>1 exchange path (process group, RCCL gather of the device counts) with one rank too "
+                         "(launch with torchrun --nproc-per-node 1): exercises RCCL on a one-GPU box")
     ap.add_argument("--located-budget", type=float, default=1.0e9,
                     help="C5 located leg: most records per pattern-range chunk (20 B each, left in HBM)")
     ap.add_argument("--workdir", default=workloads.default_workdir())
@@ -238,8 +241,11 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # --dist-self: the exchange path (process group, all-gather of sizes, counts gathered over RCCL
+    # from the device mirror) even with one rank — it exercises RCCL on a one-GPU box
+    multi = world > 1 or args.dist_self
     if args.gather == "auto":
-        args.gather = "counts" if world > 1 else "none"
+        args.gather = "counts" if multi else "none"
     # the CPUs this process may use, before the NUMA pinning below; the CPU baseline uses them,
     # capped by the job's CPU share when the launcher states one (OMP_NUM_THREADS: 16 per GPU
     # on the GPU box, whose os.cpu_count() shows the whole machine)
@@ -263,8 +269,10 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     local = local % ndev  # rehearsal: several ranks may share one GPU (gloo)
     gdev = torch.device("cpu")
-    if world > 1:
+    if multi:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        for k_, v_ in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(free_port())), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k_, v_)  # --dist-self run bare: a one-rank group
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -324,7 +332,7 @@ def main():
         assert n == npat, (n, npat)
         return ptr, nocc
 
-    if world > 1 and args.gather == "counts" and args.dist_backend == "nccl":
+    if multi and args.gather == "counts" and args.dist_backend == "nccl":
         # the engine leaves each call's u32 counts in d_counts_x too (a device-to-device copy per
         # chunk): RCCL gathers them from HBM, no second upload of the counts
         idx.set_counts_mirror(d_counts_x.data_ptr(), npat)
@@ -333,7 +341,7 @@ def main():
         # the path's exchange step: every rank's (patterns, records) all-gathered — its offsets in
         # the output (each rank writes its slice); --gather counts also gathers the
         # per-pattern counts to rank 0 (RCCL/xGMI).  d_src: the device-resident leg's counts.
-        if world == 1:
+        if not multi:
             return
         sizes = shard.exchange_sizes(npat, nocc, gdev)
         if args.gather == "counts":
@@ -379,7 +387,7 @@ def main():
         e2e_stats = dict(e2e_stats, ms_wall=0.0, found=0)
         walls = [0.0]
     per_rank = [search_ms / args.steps, exch_ms / args.steps]
-    if world > 1:
+    if multi:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -400,7 +408,7 @@ def main():
 
     # ---- N > 1: every rank's first patterns against the oracle, outside the timed region
     rank_parity = None
-    if world > 1 and not args.no_cpu:
+    if multi and not args.no_cpu:
         n_par = min(16 if w.name == "c5" else 256, npat)
         pbuf, poffs = pkg.read_pattern_file(pats_path)
         ok = 0
@@ -446,7 +454,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         d_elapsed = time.perf_counter() - t1
-        if world > 1:
+        if multi:
             tt = torch.tensor([d_elapsed], dtype=torch.float64, device=gdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d_elapsed = float(tt.item())
@@ -498,13 +506,13 @@ def main():
                                         if dres else
                                         "(--no-device) edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> "
                                         "counts + records D2H (SURVEY §8(d)), plus the exchange step when N>1"),
-                       "exchange": ("none (one GPU)" if world == 1 else
+                       "exchange": ("none (one GPU)" if not multi else
                                     "sizes all-gathered (each rank keeps its counts + records as its output slice)"
                                     + ((" + counts gathered to rank 0 over RCCL (device counts mirror, xGMI)"
                                         if args.dist_backend == "nccl" else
                                         f" + counts gathered to rank 0 over {args.dist_backend} (rehearsal: counts staged "
                                         "through host memory)") if args.gather == "counts" else "")),
-                       "dist_backend": args.dist_backend if world > 1 else None,
+                       "dist_backend": args.dist_backend if multi else None,
                        "ktab_depth": idx.ktab_depth, "ltab_depth": idx.ltab_depth, "ltab_items": idx.ltab_items,
                        "index_device_bytes": idx.device_bytes,
                        "host_numa_node": numa,
@@ -583,7 +591,7 @@ def main():
             out["device_resident"] = {
                 "value": round(total_pats * args.steps / dres["elapsed"], 1), "ms_per_step": round(d_ms, 3),
                 "what": "pattern bytes + u64 offsets resident in HBM before the timed region; counts + records left in HBM"
-                        + ("; the exchange step (sizes all-gathered, counts gathered to rank 0) in every step" if world > 1 else ""),
+                        + ("; the exchange step (sizes all-gathered, counts gathered to rank 0) in every step" if multi else ""),
                 "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items()) if v["ms"]},
                 "kernel_lines_per_s": {k: round((v["lines"] / (v["ms"] * 1e-3)) if v["ms"] > 0 else 0.0, 1)
                                        for k, v in sorted(kstats.items()) if v["lines"]},
@@ -666,7 +674,7 @@ def main():
     text.free()
     counts_hb.free()
     idx.close()
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
