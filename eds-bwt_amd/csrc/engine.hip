@@ -148,7 +148,9 @@ constexpr double kDeepShare = 0.5;
 // ... and once a depth's lists average at most kDeepItems intervals per node
 constexpr double kDeepItems = 2.0;
 // ... and text items (count-only level walks) stop being made once they average at most this many
-constexpr double kTextStopItems = 32.0;
+// (C5 with the level start table, profiles/r04_ab_c5_*.json: at the first cutover-eligible depth
+// 973 ms, at 32 per node 989 ms)
+constexpr double kTextStopItems = 1e30;
 // locate samples every 2^kSampleShift positions of a word (16 B per sampled row).  0: every
 // row, 16 B/row (C3: 1.66 GB of the 288 GB), and locate reads one sample per occurrence with
 // no LF walk and no occ-block read; EDSBWT_SAMPLE_SHIFT=2 keeps 1 in 4 (0.43 GB at C3)
@@ -450,7 +452,7 @@ struct Engine {
     double deep_share = env_double("EDSBWT_DEEP_SHARE", kDeepShare);
     double deep_items = env_double("EDSBWT_DEEP_ITEMS", kDeepItems);
     // text items stop being made when a cutover-eligible depth's lists average at most this many
-    // intervals per node (EDSBWT_TEXT_STOP; 1e30: at the first cutover-eligible depth, as round 3)
+    // intervals per node (EDSBWT_TEXT_STOP; the default 1e30: at the first cutover-eligible depth, as round 3)
     double text_stop_items = env_double("EDSBWT_TEXT_STOP", kTextStopItems);
     // direct start only from tables whose lists average at most this many intervals per D-mer
     double direct_items = env_double("EDSBWT_DIRECT_ITEMS", kDeepItems);
@@ -981,7 +983,7 @@ struct Engine {
             launch(KC_TABLE, k_segtab, (size_t)S + 2, S, kidx(), segtab.p);
             // k_deep's links from '#' rows: one line per row instead of eof_seg then segtab
             // (C3: 3.8M words, 243 MB; EDSBWT_EOF_ROWS=0: off)
-            if (X0.seg_hi == 8 && (double)W * 64 <= kEofRowMaxBytes && env_double("EDSBWT_EOF_ROWS", 1) != 0) {
+            if (X0.seg_hi == 8 && (double)W * 64 <= kEofRowMaxBytes && env_double("EDSBWT_EOF_ROWS", 0) != 0) {
                 eofrow.ensure((size_t)W * 16);
                 launch(KC_TABLE, k_eofrow, (size_t)W * 16, W, (const uint32_t*)eof_seg.p, (const uint32_t*)segtab.p, X0.seg_stride, eofrow.p);
                 device_bytes += (size_t)W * 64;
@@ -1727,7 +1729,8 @@ struct Engine {
         HIPCHK(hipGetLastError());
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
-                  : K == 4 ? (bps == 3 ? (deepq_waves >= 6 ? k_deep<4, 3, 6> : deepq_waves >= 5 ? k_deep<4, 3, 5> : k_deep<4, 3>)
+                  : K == 4 ? (bps == 3 ? (X.eofrow ? k_deep<4, 3, 1, true>
+                                          : deepq_waves >= 6 ? k_deep<4, 3, 6> : deepq_waves >= 5 ? k_deep<4, 3, 5> : k_deep<4, 3>)
                                        : k_deep<4, 4>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,

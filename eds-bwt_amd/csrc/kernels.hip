@@ -1662,7 +1662,9 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
     }
 }
 
-template <int K, int BPS, int MINW = 1>  // MINW: waves per SIMD the register budget is held to (1: no bound)
+// EOFROW: links from '#' rows through KIdx::eofrow (one line per row; costs k_deep 6 VGPRs and a
+// wave per SIMD: C3 0.355 against 0.304 ms, profiles/r04_ab_c3_*.json — off by default)
+template <int K, int BPS, int MINW = 1, bool EOFROW = false>  // MINW: waves per SIMD the register budget is held to (1: no bound)
 __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
                                               const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind, uint64_t P,
@@ -1791,12 +1793,13 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
-            uint32_t sb[K], se[K], raw[K], rawk[K];  // rawk: a '#'-rank of raw's segment (its eofrow line)
+            uint32_t sb[K], se[K], raw[K], rawk[EOFROW ? K : 1];  // rawk: a '#'-rank of raw's segment (its eofrow line)
             uint32_t rn = 0;
 #pragma unroll
             for (int j = 0; j < K; j++) {
                 sb[j] = se[j] = 0;
-                raw[j] = rawk[j] = 0;
+                raw[j] = 0;
+                if constexpr (EOFROW) rawk[j] = 0;
             }
 #pragma unroll
             for (int j = 0; j < K; j++) {
@@ -1806,7 +1809,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                     n_hash += h1 - h0;
                     for (uint32_t k = h0; k < h1; k++) {  // dollars_in_interval (:607-625)
                         // the word's segment: from its link row (one line, the ranks come with it) or eof_seg
-                        const uint32_t s = X.eofrow ? X.eofrow[(size_t)k * 16 + 15] : X.eof_seg[k];
+                        const uint32_t s = EOFROW ? X.eofrow[(size_t)k * 16 + 15] : X.eof_seg[k];
                         if (!s) continue;
                         // insert s into raw[0..rn) ascending, dropping duplicates
                         bool dup = false;
@@ -1820,13 +1823,18 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                         for (int t = 0; t < K; t++) {
                             if ((uint32_t)t < rn) {
                                 if (raw[t] > vv) {
-                                    const uint32_t tmp = raw[t], tk = rawk[t];
-                                    raw[t] = vv; rawk[t] = vk;
-                                    vv = tmp; vk = tk;
+                                    const uint32_t tmp = raw[t];
+                                    raw[t] = vv;
+                                    vv = tmp;
+                                    if constexpr (EOFROW) {
+                                        const uint32_t tk = rawk[t];
+                                        rawk[t] = vk;
+                                        vk = tk;
+                                    }
                                 }
                             } else if ((uint32_t)t == rn) {
                                 raw[t] = vv;
-                                rawk[t] = vk;
+                                if constexpr (EOFROW) rawk[t] = vk;
                             }
                         }
                         rn++;
@@ -1868,9 +1876,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 if ((uint32_t)t < rn) {
                     const uint32_t s = raw[t];
                     // the '#' row's link row was just read (a cache hit); else the segment's table row
-                    const uint32_t* e = X.eofrow ? X.eofrow + (size_t)rawk[t] * 16 : X.segtab + (size_t)s * X.seg_stride;
+                    const uint32_t* e = EOFROW ? X.eofrow + (size_t)rawk[EOFROW ? t : 0] * 16 : X.segtab + (size_t)s * X.seg_stride;
                     const uint32_t lo = e[0];
-                    if (!X.eofrow) n_blk++;
+                    if (!EOFROW) n_blk++;
                     if (have && lo > run_s) { close_run(); have = false; }
                     if (!have) { run_x = e[1 + c]; have = true; }
                     run_y = e[X.seg_hi + c];

@@ -176,7 +176,7 @@ def test_level_table_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     start — located and count-only, on the level path and with the deep cutover, in forced
     trie-subtree groups (the whole C5 batch is grouped because its start passes 2^31 items:
     tests/test_production_gpu.py), with text items stopped at the first cutover-eligible depth
-    (round 3's rule), against the oracle and against the same searches without the table
+    (the default) or at 32 per node, against the oracle and against the same searches without the table
     (EDSBWT_NO_LTAB); a batch holding a shorter pattern starts from the k-mer table instead."""
     monkeypatch.setenv("EDSBWT_KTAB_K", "3")
     monkeypatch.setenv("EDSBWT_LTAB_K", "6")
@@ -202,7 +202,7 @@ def test_level_table_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         gs, gso = idx.search((sbuf, soffs))
         assert idx.stats()["start_depth"] == 3
         assert np.array_equal(gs, soc) and np.array_equal(gso, soo)
-    for env in ({"EDSBWT_NO_LTAB": "1"}, {"EDSBWT_FORCE_GROUPS": "2"}, {"EDSBWT_FORCE_GROUPS": "1", "EDSBWT_TEXT_STOP": "1e30"}):
+    for env in ({"EDSBWT_NO_LTAB": "1"}, {"EDSBWT_FORCE_GROUPS": "2"}, {"EDSBWT_FORCE_GROUPS": "1", "EDSBWT_TEXT_STOP": "32"}):
         for k_, v_ in env.items():
             monkeypatch.setenv(k_, v_)
         with edsbwt.Index(base) as idx:
