@@ -3435,13 +3435,17 @@ __global__ void k_eofrow(uint32_t W, const uint32_t* __restrict__ eof_seg, const
 // row's srow entry as k_lvl_items would convert it: kTextItem | offset << 27 | segment, and the
 // 15 characters before the row (2 bits each) | its segment's chain bit << 31; 0 when no or several
 // words end with c, or the word is longer than 16
+constexpr uint32_t kSegTextWords = 64;
 __global__ void k_segtext(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
     GRID_STRIDE(s, (size_t)S + 2) {
         uint32_t* e = tab + s * X.seg_stride + 16;
         uint32_t cnt[5] = {0, 0, 0, 0, 0}, row[5] = {0, 0, 0, 0, 0};
-        if (s >= 2) {
-            const uint32_t lo = X.seg_lo[s];
-            for (uint32_t w = X.seg_start[lo]; w < X.seg_start[s]; w++) {
+        // segments 2..S only (row S + 1 is the table's sentinel), and links of at most
+        // kSegTextWords words (a longer empty-word chain keeps the row path)
+        const uint32_t lo = (s >= 2 && s <= S) ? X.seg_lo[s] : 0u;
+        const uint32_t w0 = (s >= 2 && s <= S) ? X.seg_start[lo] : 0u, w1 = (s >= 2 && s <= S) ? X.seg_start[s] : 0u;
+        if (w1 - w0 <= kSegTextWords) {
+            for (uint32_t w = w0; w < w1; w++) {
                 uint32_t rk;
                 const uint32_t c = sym_rank(X.occ, w, &rk);
                 if (c >= 1 && c <= 4) {
