@@ -643,6 +643,39 @@ __device__ __forceinline__ void acgt_key(const uint8_t* __restrict__ bytes, uint
     term_out = term;
 }
 
+// acgt_key for a pattern of L <= 32 bytes held in registers: W[k] = its bytes 4k .. 4k + 3 (fully
+// unrolled, so W stays in VGPRs)
+__device__ __forceinline__ void acgt_key_regs(const uint32_t (&W)[8], uint32_t L, uint32_t D, uint32_t E, uint32_t lmin, uint32_t lmax,
+                                              uint32_t& x_out, uint64_t& rem_out, bool& term_out) {
+    uint64_t V = 0;
+    bool ok = true, term = lmax != 0 && (L < lmin || L > lmax);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t j = 4 * k;
+        if (j < L) {
+            const uint32_t n = min(4u, L - j);
+            const uint32_t w = W[k];
+            const uint32_t live = n == 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - n)));
+            const uint32_t mC = zero_bytes(w ^ 0x43434343u), mG = zero_bytes(w ^ 0x47474747u), mT = zero_bytes(w ^ 0x54545454u);
+            const uint32_t hit = zero_bytes(w ^ 0x41414141u) | mC | mG | mT;
+            ok &= (hit & live) == live;
+            term |= (zero_bytes(w ^ 0x23232323u) & live) != 0;
+            const uint32_t bad = ~hit & 0x80808080u;
+            const uint32_t q = ((mC | mT | bad) >> 7) | ((mG | mT | bad) >> 6);
+            const uint32_t pk = ((q & 3u) << 6) | (((q >> 8) & 3u) << 4) | (((q >> 16) & 3u) << 2) | ((q >> 24) & 3u);
+            V = (V << (2 * n)) | (pk >> (8 - 2 * n));
+        }
+    }
+    if (L <= D) {
+        x_out = ok ? (uint32_t)V : E;
+        rem_out = 1ull;
+    } else {
+        x_out = ok ? (uint32_t)(V & ((1ull << (2 * D)) - 1ull)) : E;
+        rem_out = (V >> (2 * D)) | (1ull << (2 * (L - D)));
+    }
+    term_out = term;
+}
+
 // Stage the bytes of the block's patterns [base, base + nb) in LDS (16-B aligned words from
 // w0 = off[base] & ~15) when they fit kKeySpan and the buffer is 16-B aligned; every thread of
 // the block calls it.  Returns whether they were staged.
@@ -1438,8 +1471,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
 // It writes every pattern's result (an empty list's too), so the result array needs no zeroing.
 //
 // FUSED (the default on that path, EDSBWT_FUSED_KEYS=0: k_keys_acgt first): the pattern keys are
-// computed here from the pattern bytes (staged in LDS per block round, as k_keys_acgt stages
-// them) instead of being read back from k_keys_acgt's kid / pv arrays — one launch and ~0.3 GB of
+// computed here from the pattern bytes (each lane's three 16-B words; C3 1.610 against 1.648 ms
+// with an LDS stage per block round, profiles/r04_ab2_c3_*.json) instead of being read back from
+// k_keys_acgt's kid / pv arrays — one launch and ~0.3 GB of
 // C3 stream traffic less.  kid and len are still written for every pattern (k_deep and
 // k_deep_wave read the queued ones'), and '#' / unexpected lengths counted into n_term for the
 // deferred check.
@@ -1457,16 +1491,15 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
-    __shared__ uint4 sbuf4[FUSED ? kKeySpan / 16 + 2 : 1];
     UNIFORM_STRIDE(i, valid, P) {
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
         uint32_t pi, L, kx = 0;
         uint64_t rem;
         if constexpr (FUSED) {
-            const size_t base = i - threadIdx.x;
-            uint64_t w0;
-            const bool staged = stage_patterns(bytes, off, base, min((size_t)blockDim.x, (size_t)P - base), sbuf4, w0);
+            // each lane loads its own pattern's bytes: the three 16-B words from a & ~15 cover
+            // L <= 32 bytes (the wave's 64 patterns are consecutive, so those loads share lines);
+            // no LDS stage, no block barrier between the lanes' walks
             pi = (uint32_t)i;
             rem = 0;
             L = 0;
@@ -1474,7 +1507,23 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 const uint64_t a = off[i];
                 const uint32_t Lp = (uint32_t)(off[i + 1] - a);
                 bool term;
-                acgt_key(bytes, a, Lp, staged, reinterpret_cast<const uint32_t*>(sbuf4), (uint32_t)(a - w0), D0, E, lmin, lmax, kx, rem, term);
+                if (Lp <= 32 && ((uintptr_t)bytes & 15) == 0) {
+                    const uint4* src = reinterpret_cast<const uint4*>(bytes + (a & ~15ull));
+                    const uint32_t so = (uint32_t)(a & 15), q = so >> 2, sb = so & 3;
+                    const uint4 v0 = src[0], v1 = Lp + so > 16 ? src[1] : make_uint4(0, 0, 0, 0),
+                                v2 = Lp + so > 32 ? src[2] : make_uint4(0, 0, 0, 0);
+                    const uint32_t r[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+                    uint32_t W[8];
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; k++) {  // bytes so + 4k .. so + 4k + 3 of the window (constant indices)
+                        const uint32_t x0 = q == 0 ? r[k] : q == 1 ? r[k + 1] : q == 2 ? r[k + 2] : r[k + 3];
+                        const uint32_t x1 = q == 0 ? r[k + 1] : q == 1 ? r[k + 2] : q == 2 ? r[k + 3] : r[k + 4];
+                        W[k] = __builtin_amdgcn_alignbyte(x1, x0, sb);
+                    }
+                    acgt_key_regs(W, Lp, D0, E, lmin, lmax, kx, rem, term);
+                } else {
+                    acgt_key(bytes, a, Lp, false, nullptr, 0u, D0, E, lmin, lmax, kx, rem, term);
+                }
                 nt += term;
                 len_out[i] = Lp;
                 kid_out[i] = kx;

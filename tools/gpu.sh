@@ -12,6 +12,7 @@
 #   pmc:<cfg>               separate PMC passes of the same command: FETCH_SIZE, WRITE_SIZE, the TCC
 #                           DRAM request counters, SQ stall + L2 counters (tools/profile_summary.py)
 #   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
+#   rccl:<cfg>[:<patterns>] one rank through the exchange path over RCCL (bench.py --dist-self)
 #   cli:<cfg>               the EDSBWTsearch CLI timed on the config's index and pattern file
 #   ab:<cfg>:<VAR=a,VAR2=b>[:<VAR=c>...] A/B bench lines (no CPU leg) under env settings
 # Outputs: gpurun_out/<tag>_<task>*.{json,log}.
@@ -51,6 +52,11 @@ for task in "$@"; do
       n=${a:-2}; cfg=${b:-c4}
       timeout -k 10 1100 python bench.py --gpus $n --config $cfg --steps 3 --warmup 1 --dist-backend gloo ${c:+--patterns $c} > ${out}_${b}.json 2> ${out}_${b}.log || fail rehearse ${out}_${b}.log
       head -c 400 ${out}_${b}.json; echo ;;
+    rccl)
+      # the N>1 exchange path with one rank on this GPU: process group over RCCL, sizes all-gathered,
+      # counts gathered from the engine's device mirror (bench.py --dist-self)
+      timeout -k 10 600 python bench.py --dist-self --config ${a:-c3} --steps 5 --warmup 2 --no-cpu ${b:+--patterns $b} > ${out}.json 2> ${out}.log || fail rccl ${out}.log
+      head -c 400 ${out}.json; echo ;;
     cli)
       timeout -k 10 900 python tools/cli_timing.py --config ${a:-c3} > ${out}.json 2> ${out}.log || fail cli ${out}.log
       cat ${out}.json ;;
