@@ -261,6 +261,12 @@ def main():
     if args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
 
+    # the JSON line is the only thing on stdout: libraries that print there (RCCL's version banner
+    # at communicator init) write to stderr instead
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -670,7 +676,7 @@ def main():
                         cb["counts"][diff[:8]].tolist(), counts_last[:samp_n][diff[:8]].tolist())
             except Exception as e:  # the GPU line is still valid
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     text.free()
     counts_hb.free()
     idx.close()
