@@ -566,8 +566,17 @@ def main():
                         "traffic": traffic, "traffic_source": tsrc}
 
             per_class = {k: v for k in ("deep", "deep_list", "deep_wide", "step", "locate") if (v := kclass(k))}
-            dom = max((k for k in kstats if k != "scan"), key=lambda k: kstats[k]["ms"])
-            dk = per_class.get(dom) or kclass(dom)
+            # the dominant timed class (under a PMC pass the event times may be missing: then the
+            # first class that has them)
+            timed_k = [k for k in kstats if k != "scan" and kclass(k)]
+            dom = max(timed_k, key=lambda k: kstats[k]["ms"]) if timed_k else None
+            dk = (per_class.get(dom) or kclass(dom)) if dom else None
+            if dk is None:
+                dk = {"kernels": None, "achieved": None, "frac": None, "traffic": None, "traffic_source": None, "traffic_frac": None,
+                      "avg_launch_ms": None, "bytes_per_launch": None, "lines_per_launch": None, "lines_per_s": None,
+                      "frac_of_gather_ceiling": None}
+                dom = dom or "none"
+                kstats.setdefault(dom, {"ms": 0.0, "launches": 0, "bytes": 0, "lines": 0})
             # SURVEY §8(d)'s per-step model: two 64-B lines per interval step, whichever kernel
             # takes it (level step, dollar step, deep walk), over the whole device-resident step
             survey_b = 2 * 64 * dstat["intervals_stepped"]

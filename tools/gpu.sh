@@ -9,8 +9,9 @@
 #   bench:<cfg>[:<steps>[:<warmup>]]     one bench.py line (CPU baseline included)
 #   quick:<cfg>[:<steps>]   a bench line without the CPU leg
 #   trace:<cfg>             rocprofv3 --kernel-trace --stats of the device-resident leg
-#   pmc:<cfg>               separate PMC passes of the same command: FETCH_SIZE, WRITE_SIZE, the TCC
-#                           DRAM request counters, SQ stall + L2 counters (tools/profile_summary.py)
+#   prof:<cfg>              kernel trace + separate PMC passes of the same command (FETCH_SIZE, WRITE_SIZE,
+#                           the TCC DRAM request counters, SQ stall + L2), summarised and shrunk on the box
+#                           (tools/profile_summary.py -> <out>_summary.json, <out>_traffic.json)
 #   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
 #   rccl:<cfg>[:<patterns>] one rank through the exchange path over RCCL (bench.py --dist-self)
 #   cli:<cfg>               the EDSBWTsearch CLI timed on the config's index and pattern file
@@ -41,13 +42,23 @@ for task in "$@"; do
       timeout -k 10 600 python bench.py --no-cpu --config ${a:-c3} --steps ${b:-10} --warmup 2 > ${out}.json 2> ${out}.log || fail quick ${out}.log
       head -c 400 ${out}.json; echo ;;
     trace)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- $B0 --config ${a:-c3} > ${out}.json 2> ${out}.log || fail trace ${out}.log ;;
-    pmc)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- $B0 --config ${a:-c3} > ${out}.json 2> ${out}.log || fail trace ${out}.log
+      python3 tools/prof_reduce.py ${out}_trace ;;
+    prof)
+      # kernel trace + the four PMC passes of one command, summarised here (profile_summary.py:
+      # per-class rocprof averages, DRAM bytes / requests per launch -> <out>_traffic.json) and
+      # shrunk (prof_reduce.py) so gpurun_out/ stays under gpurun's copy-back cap
       cfg=${a:-c3}
-      timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d ${out}_fetch -o pmc --output-format csv -- $B0 --config $cfg > ${out}_fetch.json 2> ${out}_fetch.log || fail pmc_fetch ${out}_fetch.log
-      timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d ${out}_write -o pmc --output-format csv -- $B0 --config $cfg > ${out}_write.json 2> ${out}_write.log || fail pmc_write ${out}_write.log
-      timeout -s KILL 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_tccreq -o pmc --output-format csv -- $B0 --config $cfg > ${out}_tccreq.json 2> ${out}_tccreq.log || fail pmc_tcc ${out}_tccreq.log
-      timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY TCC_HIT_sum TCC_MISS_sum -d ${out}_sq -o pmc --output-format csv -- $B0 --config $cfg > ${out}_sq.json 2> ${out}_sq.log || fail pmc_sq ${out}_sq.log ;;
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- $B0 --config $cfg > ${out}_trace.json 2> ${out}_trace.log || fail prof_trace ${out}_trace.log
+      grep -v "^[A-Z].*version :\|^Hostname\|^Librccl" ${out}_trace.json | tail -1 > ${out}_bench.json
+      timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d ${out}_fetch -o pmc --output-format csv -- $B0 --config $cfg > /dev/null 2> ${out}_fetch.log || fail pmc_fetch ${out}_fetch.log
+      timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d ${out}_write -o pmc --output-format csv -- $B0 --config $cfg > /dev/null 2> ${out}_write.log || fail pmc_write ${out}_write.log
+      timeout -s KILL 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_BUBBLE_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_tccreq -o pmc --output-format csv -- $B0 --config $cfg > /dev/null 2> ${out}_tccreq.log || fail pmc_tcc ${out}_tccreq.log
+      timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY TCC_HIT_sum TCC_MISS_sum -d ${out}_sq -o pmc --output-format csv -- $B0 --config $cfg > /dev/null 2> ${out}_sq.log || fail pmc_sq ${out}_sq.log
+      python3 tools/prof_reduce.py ${out}_trace ${out}_fetch ${out}_write ${out}_tccreq ${out}_sq
+      python3 tools/profile_summary.py ${out}_trace ${out}_fetch ${out}_write ${out}_bench.json ${out}_summary.json --tcc ${out}_tccreq \
+          --traffic ${out}_traffic.json --source "tools/gpu.sh prof:$cfg (rocprofv3 --pmc passes of $B0 --config $cfg)" > /dev/null || fail prof_summary ${out}_trace.log
+      tail -c 300 ${out}_traffic.json; echo ;;
     rehearse)
       n=${a:-2}; cfg=${b:-c4}
       timeout -k 10 1100 python bench.py --gpus $n --config $cfg --steps 3 --warmup 1 --dist-backend gloo ${c:+--patterns $c} > ${out}_${b}.json 2> ${out}_${b}.log || fail rehearse ${out}_${b}.log

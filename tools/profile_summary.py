@@ -76,19 +76,21 @@ def main():
     for v in per.values():
         v["avg_us"] = 1e3 * v["total_ms"] / max(1, v["calls"])
     pmc = collections.defaultdict(lambda: {"fetch_bytes": 0.0, "write_bytes": 0.0, "dispatches": 0})
+    # (tools/prof_reduce.py may have summed the rows per (kernel, counter): "Dispatches" then
+    # holds the number of dispatches each sum covers)
     for d, key in ((a.fetch_dir, "fetch_bytes"), (a.write_dir, "write_bytes")):
         for r in csv.DictReader(open(first_csv(d, "counter_collection.csv"))):
             k = short(r["Kernel_Name"])
             v = float(r["Counter_Value"]) * 1024.0
             pmc[k][key] += FETCH_FACTOR_GATHER64 * v if key == "fetch_bytes" else v
             if key == "fetch_bytes":
-                pmc[k]["dispatches"] += 1
+                pmc[k]["dispatches"] += int(r.get("Dispatches") or 1)
     tcc = collections.defaultdict(lambda: collections.defaultdict(float))
     if a.tcc:
         for r in csv.DictReader(open(first_csv(a.tcc, "counter_collection.csv"))):
             tcc[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
             if r["Counter_Name"] == "TCC_EA0_RDREQ_sum":
-                tcc[short(r["Kernel_Name"])]["dispatches"] += 1
+                tcc[short(r["Kernel_Name"])]["dispatches"] += int(r.get("Dispatches") or 1)
     # registers, LDS and the occupancy they allow, per kernel (kernel trace columns).  gfx950:
     # 512 VGPRs per lane per SIMD shared by the arch and accumulation registers (granule 8),
     # at most 8 waves per SIMD, 160 KB of LDS per CU (4 SIMDs)
