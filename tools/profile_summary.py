@@ -39,14 +39,23 @@ CLASSES = {
     "deep_list": ("k_deep",),
     "deep_wide": ("k_deep_wave", "k_deep_wide"),
     "locate": ("k_locate", "k_locate_pp", "k_locate_big"),
+    # the link key sort (KC_LINKSORT, hipcub SortKeys on u64 keys: the only keys-only radix sort
+    # the engine runs); one "launch" = one sort = one global-offsets kernel + its onesweep passes
+    "link_sort": ("rocprim_sortkeys_offsets", "rocprim_sortkeys"),
 }
+# the kernel whose dispatches count a class's launches, where one launch is several kernels
+CLASS_UNIT = {"link_sort": "rocprim_sortkeys_offsets"}
 FETCH_FACTOR_GATHER64 = 1.0
 
 
 def short(name: str) -> str:
     n = name.split("(")[0]
     n = n.replace("void ", "").replace("edsbwt::", "")
-    return n.split("<")[0] if not n.startswith("rocprim") else "rocprim"
+    if not n.startswith("rocprim"):
+        return n.split("<")[0]
+    if "radix_sort" in name and "empty_type" in name:
+        return "rocprim_sortkeys_offsets" if "global_offsets" in name else "rocprim_sortkeys"
+    return "rocprim"
 
 
 def main():
@@ -110,16 +119,17 @@ def main():
     bench = json.load(open(a.bench_json))
     classes = {}
     for c, ks in CLASSES.items():
-        calls = sum(per[k]["calls"] for k in ks if k in per)
+        unit = (CLASS_UNIT[c],) if c in CLASS_UNIT else ks
+        calls = sum(per[k]["calls"] for k in unit if k in per)
         tot = sum(per[k]["total_ms"] for k in ks if k in per)
-        disp = sum(pmc[k]["dispatches"] for k in ks if k in pmc)
+        disp = sum(pmc[k]["dispatches"] for k in unit if k in pmc)
         fb = sum(pmc[k]["fetch_bytes"] for k in ks if k in pmc)
         wb = sum(pmc[k]["write_bytes"] for k in ks if k in pmc)
         classes[c] = {"rocprof_calls": calls, "rocprof_avg_launch_ms": tot / max(1, calls),
                       "pmc_hbm_bytes_per_launch": (fb + wb) / max(1, disp),
                       "pmc_fetch_bytes_per_launch": fb / max(1, disp), "pmc_write_bytes_per_launch": wb / max(1, disp)}
         if a.tcc:
-            td = sum(tcc[k]["dispatches"] for k in ks if k in tcc)
+            td = sum(tcc[k]["dispatches"] for k in unit if k in tcc)
             dram = 32.0 * sum(tcc[k]["TCC_EA0_RDREQ_DRAM_32B_sum"] for k in ks if k in tcc)
             req = sum(tcc[k]["TCC_EA0_RDREQ_sum"] for k in ks if k in tcc)
             classes[c].update({"pmc_dram_read_bytes_per_launch": dram / max(1, td), "pmc_read_requests_per_launch": req / max(1, td),
