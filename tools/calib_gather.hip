@@ -20,6 +20,7 @@
 //   calib_gather --tlb [table_MB ...]     gather16 with 64-bit indices over tables up to 128 GB: the
 //                        rate of random 16-B loads as the table outgrows the GPU's address translation
 //                        caches (the wide k-mer table is 34 GB at C3)
+//   calib_gather --scatter [table_MB ...] random 16-B stores (the per-pattern result writes)
 //   calib_gather --window [table_MB ...]  one 16-B load per random 64-B block within a window that
 //                        slides over the table (row-bucketed items): accesses/s per window size
 // Algorithmic bytes are known exactly, so running this under
@@ -99,6 +100,42 @@ static void tlb(size_t mb, uint32_t* sink, hipEvent_t a, hipEvent_t b) {
     const double loads = (double)grid * block * iters;
     std::printf("{\"shape\": \"gather16_tlb\", \"table_MB\": %zu, \"loads\": %.0f, \"best_ms\": %.4f, \"loads_per_s\": %.4g}\n", mb,
                 loads, best, loads / (best * 1e-3));
+    std::fflush(stdout);
+    CK(hipFree(t));
+}
+
+// random 16-B stores (the deep kernels' per-pattern result writes, Res[o] at input order o): under
+// --pmc TCC_EA0_RDREQ_sum / TCC_EA0_WRREQ_sum they show whether a partial-line store costs a DRAM read
+__global__ void __launch_bounds__(256) k_scatter16(uint4* __restrict__ t, uint64_t n16, uint32_t iters, uint32_t seed) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t h = mix(g ^ seed);
+    for (uint32_t i = 0; i < iters; i++) {
+        h = mix(h + i);
+        const uint64_t x = ((uint64_t)mix(h ^ 0x9e3779b9u) << 32 | h) % n16;
+        t[x] = make_uint4(h, g, i, seed);
+    }
+}
+
+static void scatter(size_t mb, hipEvent_t a, hipEvent_t b) {
+    const size_t bytes = mb << 20;
+    uint4* t;
+    CK(hipMalloc(&t, bytes));
+    CK(hipMemset(t, 7, bytes));
+    const uint32_t grid = 256 * 32, block = 256, iters = 64;
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; rep++) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_scatter16, dim3(grid), dim3(block), 0, 0, t, (uint64_t)(bytes / 16), iters, 31u + rep);
+        CK(hipGetLastError());
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (rep > 0 && ms < best) best = ms;
+    }
+    const double stores = (double)grid * block * iters;
+    std::printf("{\"shape\": \"scatter16\", \"table_MB\": %zu, \"stores\": %.0f, \"launches\": 5, \"best_ms\": %.4f, \"stores_per_s\": %.4g}\n",
+                mb, stores, best, stores / (best * 1e-3));
     std::fflush(stdout);
     CK(hipFree(t));
 }
@@ -230,11 +267,12 @@ static void windows(size_t mb, uint32_t* sink, hipEvent_t a, hipEvent_t b) {
 
 int main(int argc, char** argv) {
     std::vector<size_t> mbs;
-    bool chain_only = false, window_only = false, tlb_only = false;
+    bool chain_only = false, window_only = false, tlb_only = false, scatter_only = false;
     for (int i = 1; i < argc; i++) {
         if (std::string(argv[i]) == "--chain") chain_only = true;
         else if (std::string(argv[i]) == "--window") window_only = true;
         else if (std::string(argv[i]) == "--tlb") tlb_only = true;
+        else if (std::string(argv[i]) == "--scatter") scatter_only = true;
         else {
             char* end = nullptr;
             const unsigned long long v = std::strtoull(argv[i], &end, 10);
@@ -258,6 +296,10 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&b));
     if (tlb_only) {
         for (size_t mb : mbs) tlb(mb, sink, a, b);
+        return 0;
+    }
+    if (scatter_only) {
+        for (size_t mb : mbs) scatter(mb, a, b);
         return 0;
     }
     for (size_t mb : mbs)

@@ -12,6 +12,7 @@
 #   prof:<cfg>              kernel trace + separate PMC passes of the same command (FETCH_SIZE, WRITE_SIZE,
 #                           the TCC DRAM request counters, SQ stall + L2), summarised and shrunk on the box
 #                           (tools/profile_summary.py -> <out>_summary.json, <out>_traffic.json)
+#   calib:<mode>:<MB,MB..>  tools/_build/calib_gather --<mode> under a PMC pass of the TCC request counters
 #   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
 #   rccl:<cfg>[:<patterns>] one rank through the exchange path over RCCL (bench.py --dist-self)
 #   cli:<cfg>               the EDSBWTsearch CLI timed on the config's index and pattern file
@@ -43,7 +44,9 @@ for task in "$@"; do
       head -c 400 ${out}.json; echo ;;
     trace)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- $B0 --config ${a:-c3} > ${out}.json 2> ${out}.log || fail trace ${out}.log
-      python3 tools/prof_reduce.py ${out}_trace ;;
+      python3 tools/trace_split.py ${out}_trace > ${out}_split.txt 2>&1 || true  # the last search's kernels, before the trace is shrunk
+      python3 tools/prof_reduce.py ${out}_trace
+      cat ${out}_split.txt ;;
     prof)
       # kernel trace + the four PMC passes of one command, summarised here (profile_summary.py:
       # per-class rocprof averages, DRAM bytes / requests per launch -> <out>_traffic.json) and
@@ -59,6 +62,12 @@ for task in "$@"; do
       python3 tools/profile_summary.py ${out}_trace ${out}_fetch ${out}_write ${out}_bench.json ${out}_summary.json --tcc ${out}_tccreq \
           --traffic ${out}_traffic.json --source "tools/gpu.sh prof:$cfg (rocprofv3 --pmc passes of $B0 --config $cfg)" > /dev/null || fail prof_summary ${out}_trace.log
       tail -c 300 ${out}_traffic.json; echo ;;
+    calib)
+      # tools/_build/calib_gather --<a> <sizes, comma-separated> under one PMC pass of the TCC request
+      # counters (requests per access of a shape: random 16-B stores, large-table gathers)
+      timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_pmc -o pmc --output-format csv -- tools/_build/calib_gather --$a ${b//,/ } > ${out}.json 2> ${out}.log || fail calib ${out}.log
+      python3 tools/prof_reduce.py ${out}_pmc
+      cat ${out}.json; find ${out}_pmc -name "*counter_collection.csv" -exec cat {} \; ;;
     rehearse)
       n=${a:-2}; cfg=${b:-c4}
       timeout -k 10 1100 python bench.py --gpus $n --config $cfg --steps 3 --warmup 1 --dist-backend gloo ${c:+--patterns $c} > ${out}_${b}.json 2> ${out}_${b}.log || fail rehearse ${out}_${b}.log
