@@ -492,6 +492,13 @@ struct Engine {
     static constexpr uint32_t kFlagNoDefer = 0x80000000u;    // internal flag: the checked path
     uint32_t defer_wide_cap = 0;
     const uint32_t* defer_ovf2 = nullptr;
+    // fused counts (deferred direct start, count-only or per-pattern locate): k_deep_direct, k_deep
+    // and k_deep_wave write every final count into the caller's counts and add found / occurrences
+    // / intervals into the stats shards that k_gather_checks folds, so finish_deferred runs no
+    // k_count_found pass over the results (EDSBWT_FUSED_COUNTS=0: the pass)
+    bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
+    uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
+    bool fc_done = false;           // ... and k_deep_direct took them
     static constexpr uint32_t kWideCap = 16384;
     static constexpr uint32_t kWaveGrid = 2048;  // k_deep_wave's waves (each strides over the wide list)
     // wide lists one wavefront per pattern (k_deep_wave); EDSBWT_DEEP_WAVE=0: one lane per pattern (k_deep_wide, A/B)
@@ -515,7 +522,11 @@ struct Engine {
         unsigned long long* n_term = nullptr;
         uint32_t E = 0, lmin = 0, lmax = 0;
     } fk_now;
-    int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 4);  // k_deep<4, 3> likewise (4 unbounded)
+    // k_deep<4, 3> likewise (5 or 6; C3 0.371 / 0.478 ms against 0.369 unbounded, profiles/r03_ab_occupancy.txt).
+    // The unbounded builds (96 VGPRs) miscounted the README KAT on some round-4 boxes (TATT 0 instead
+    // of 4) while the 5- and 6-wave builds of the same source were exact: they are not dispatched
+    // (k_deep<4, 4> likewise held to 5 waves)
+    int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 5);
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -1705,20 +1716,23 @@ struct Engine {
         const uint4* kt1w = dstart && ktab_wide.p ? (const uint4*)ktab_wide.p : (const uint4*)nullptr;
         const bool kdd = pv && kt1w && !X.rent3 && deep_direct;
         if (!kdd) settle_res(r);  // (k_deep_direct writes every result; the other walks need zeros)
+        // fused counts: only on the deferred direct start (its three kernels write every final count)
+        uint32_t* const fc = kdd && defer ? fc_counts : nullptr;
+        if (fc) fc_done = true;
         if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
             // written there, for k_deep and k_deep_wave)
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8, true> : direct_waves >= 7 ? k_deep_direct<7, true>
                      : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
-                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax);
+                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc);
             fk_now.on = false;
         } else if (kdd) {
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
                                                                                                         : k_deep_direct<1>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
                    (const uint8_t*)nullptr, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned long long*)nullptr, 0u,
-                   0u, 0u);
+                   0u, 0u, fc);
         } else {
             auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
             launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
@@ -1730,12 +1744,12 @@ struct Engine {
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? (X.eofrow ? k_deep<4, 3, 1, true>
-                                          : deepq_waves >= 6 ? k_deep<4, 3, 6> : deepq_waves >= 5 ? k_deep<4, 3, 5> : k_deep<4, 3>)
-                                       : k_deep<4, 4>)
+                                          : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
+                                       : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
-               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr);
+               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc);
         tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
@@ -1758,7 +1772,7 @@ struct Engine {
                 if (deep_wave)
                     launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(wcap, kWaveGrid) * 64, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
                            d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
-                           (const uint32_t*)ovf.p, stats.p);
+                           (const uint32_t*)ovf.p, stats.p, fc);
                 else
                     launch(KC_DEEPW, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
                            d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
@@ -1782,7 +1796,7 @@ struct Engine {
             if (deep_wave)
                 launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(nw, kWaveGrid) * 64, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
-                       (const uint32_t*)nullptr, stats.p);
+                       (const uint32_t*)nullptr, stats.p, (uint32_t*)nullptr);
             else
                 launch(KC_DEEPW, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
@@ -2485,6 +2499,11 @@ struct Engine {
         st.patterns = P;
         defer = false;
         defer_call = defer_ok && !(flags & (kFlagNoDefer | EDSBWT_LEGACY_ORDER)) && !force_groups && !sticky_groups;
+        fc_done = false;
+        fc_counts = nullptr;
+        if (defer_call && fused_counts && (deep_wave || no_wide) &&
+            (!locate || (loc_mode == 2 && kidx().samp_dense && locate_pp)))  // (finish_deferred's per-pattern locate)
+            fc_counts = d_counts;
         if (P == 0) return 0;
         struct EvPair {  // released on every exit, including exceptions
             hipEvent_t a = nullptr, b = nullptr;
@@ -2716,8 +2735,10 @@ struct Engine {
         const bool per_pattern = locate && loc_mode == 2 && X.samp_dense && locate_pp;
         last_locate_pp = per_pattern;
         if (locate && !per_pattern) occ64.ensure(P);
-        launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
-                      locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
+        if (!fc_done)  // (fused counts: written by the deep kernels, folded by k_gather_checks; search() enables
+                       // them only where this pass would not also build the task scan input)
+            launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
+                          locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
         emit_c8(P, d_counts);
         uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
         if (per_pattern) {

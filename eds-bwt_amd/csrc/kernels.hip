@@ -271,6 +271,10 @@ constexpr uint32_t kResRow = 0x80000000u;
 // text compare, k_deep_fast): off = offset << 32 | word, occ = 1 — no row, no archive
 constexpr uint32_t kResPos = 0x40000000u;
 constexpr uint32_t kResCnt = 0x3FFFFFFFu;  // the interval count in cnt
+// k_deep queue entry (i, D0, ~0u, D-mer id) on the direct start: the pattern starts from its
+// D-mer's list, read from the wide k-mer entry; lists of up to kWideInline intervals are held
+// inline there
+constexpr int kWideInline = 3;
 // a kResPos result carries the whole record: cnt = kResRow | kResPos | word-in-segment (< 2^30),
 // occ = segment; its occurrence count is 1
 __device__ __forceinline__ uint32_t res_occ(const Res& r) { return (r.cnt & kResPos) ? 1u : r.occ; }
@@ -325,7 +329,10 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_DF_LANE_ROUNDS = 17, ST_DF_WAVE_ROUNDS = 18,  // k_deep_fast: dependent load rounds of the
                   // lanes' patterns, and 64 x the slowest lane's per pattern slot (lane utilisation)
                   ST_DW_BLOCKS = 19, ST_DW_STEPS = 20,  // k_deep_wave's lines and interval steps
-                  ST_DEEPQ_PATS = 21 };  // queue entries k_deep read
+                  ST_DEEPQ_PATS = 21,  // queue entries k_deep read
+                  // fused counts (deferred direct start): the deep kernels write each final count and add
+                  // found / occurrences / intervals here; k_gather_checks folds them (no k_count_found pass)
+                  ST_FC_FOUND = 22, ST_FC_OCC = 23, ST_FC_TASKS = 24 };
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -338,6 +345,25 @@ __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats,
     v = block_sum(v, sh);
     if (threadIdx.x == 0 && v) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + k, v);
 }
+
+// a final result's count into counts[o] (fused counts) and the lane's found / occurrence / interval sums
+struct CountSums {
+    unsigned long long f = 0, occ = 0, tasks = 0;
+    __device__ __forceinline__ void put(uint32_t* __restrict__ counts, size_t o, uint32_t occ_, uint32_t cnt) {
+        if (!counts) return;
+        counts[o] = occ_;
+        f += occ_ > 0;
+        occ += occ_;
+        tasks += cnt;
+    }
+    // every thread of the block
+    __device__ __forceinline__ void flush(const uint32_t* counts, unsigned long long* __restrict__ ctr, unsigned long long* sh) {
+        if (!counts) return;
+        stat_add(ctr, ST_FC_FOUND, f, sh);
+        stat_add(ctr, ST_FC_OCC, occ, sh);
+        stat_add(ctr, ST_FC_TASKS, tasks, sh);
+    }
+};
 
 // ------------------------------------------------------ sharded appends
 // Appends are wave-aggregated: one atomic per wave per buffer.  Call with every
@@ -1249,7 +1275,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
         const uint32_t n0 = L <= D0 ? 0u : dtab ? ((ent >> 63) ? 1u : (uint32_t)(ent >> 32)) : iend[u] - ioff[u];
         if (n0 > 1) {
             want = 1;
-            w = make_uint4((uint32_t)i, D0, ~0u, 0u);
+            // (the wide table: k_deep reads the list from the D-mer's entry, w.w)
+            w = make_uint4((uint32_t)i, D0, ~0u, kt1w ? u : 0u);
         } else if (n0 == 1) {
             uint32_t b, e;
             uint32_t g1 = ~0u;  // the row's text position when the table entry holds it
@@ -1485,8 +1512,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                                                            const uint4* __restrict__ kt1w, uint64_t* __restrict__ q2,
                                                            const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                            uint32_t* __restrict__ len_out, uint32_t* __restrict__ kid_out,
-                                                           unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax) {
+                                                           unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax,
+                                                           uint32_t* __restrict__ counts) {
     uint32_t n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;  // per lane: < 2^32 (widened at the end)
+    CountSums cs;  // counts != nullptr: each final count written here (fused counts)
     unsigned long long nt = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
@@ -1540,19 +1569,24 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         // row with its text position, the row's sample and the 32 text characters before it
         uint64_t ent = 0, win1 = 0;
         uint4 s1 = make_uint4(0, 0, 0, 0);
+        uint32_t u = 0;
         if (L > D0) {
-            const size_t u = FUSED ? kx : nid[i];
-            const uint4 w0 = kt1w[2 * u];
-            s1 = kt1w[2 * u + 1];
+            u = FUSED ? kx : nid[i];
+            const uint4 w0 = kt1w[2 * (size_t)u];
+            s1 = kt1w[2 * (size_t)u + 1];
             ent = (uint64_t)w0.y << 32 | w0.x;
             win1 = (uint64_t)w0.w << 32 | w0.z;
+            n_blk++;  // the entry's 32 B: one line
         }
         const uint32_t n0 = L <= D0 ? 0u : (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
         if (n0 > 1) {
             want = 1;
-            w = make_uint4((uint32_t)i, D0, ~0u, 0u);
+            w = make_uint4((uint32_t)i, D0, ~0u, u);
         } else if (n0 == 0) {
-            if (valid) put_res(res, pi, 0, 0u, 0u);  // no list: count 0 (every result is written here or by k_deep)
+            if (valid) {
+                put_res(res, pi, 0, 0u, 0u);  // no list: count 0 (every result is written here or by k_deep)
+                cs.put(counts, pi, 0u, 0u);
+            }
         } else {
             uint32_t b, e, g1 = ~0u;
             if (X.kt1_pos && ((ent >> 62) & 1)) {
@@ -1584,9 +1618,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                     s = X.samples[b];
                     g = X.gpos[b];
                     n_blk += 3;
-                } else {
-                    n_blk += 1;
-                }
+                }  // (else the wide entry's, counted with it)
                 n_trow++;
                 const uint32_t m = L - d, k = min(s.y, m);
                 if (k) {
@@ -1605,6 +1637,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                         n_text += m;
                         d = L;
                         put_res(res, pi, (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                        cs.put(counts, pi, 1u, 1u);
                     }
                     break;
                 }
@@ -1678,6 +1711,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             } else if (!posres) {
                 if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
                 else put_res(res, pi, abase + i * K, 0u, 0u);
+                cs.put(counts, pi, alive ? e - b + 1 : 0u, alive ? 1u : 0u);
             }
         }
         if (want) put_res(res, pi, 0, 0u, 0u);  // the zeroed result the later walks expect
@@ -1693,6 +1727,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
     stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
+    cs.flush(counts, ctr, ssum);
     if constexpr (FUSED) {
         nt = block_sum(nt, ssum);
         if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
@@ -1721,8 +1756,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               const uint32_t* __restrict__ iend, const uint32_t* __restrict__ ib,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
-                                              uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2) {
-    uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;  // n_blk: occ blocks read (per lane, widened at the end)
+                                              uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2,
+                                              const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts) {
+    uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;
+    CountSums cs;  // n_blk: occ blocks read (per lane, widened at the end)
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
@@ -1754,9 +1791,29 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         }
         uint32_t cb[K], ce[K];
         uint32_t cn;
-        if (w.z == ~0u) {  // from the node's items at the cutover depth
+        if (w.z == ~0u && kt1w) {
+            // (kt1w: the direct start, whose lists all come from the wide k-mer table; a kernel
+            // argument, so this is a uniform branch inside the lanes' two-way one) the list's
+            // length, offset and (<= 3 intervals) the intervals themselves from the D-mer's 32-B
+            // wide entry, w.w = the D-mer (k_ktab_wide) — one line instead of the nid, ioff / iend,
+            // ib and ie reads below
+            const uint4 a0 = kt1w[2 * (size_t)w.w], a1 = kt1w[2 * (size_t)w.w + 1];
+            n_blk++;
+            cn = a0.y;
+            if (cn > K) { flag_push(ovf, (uint32_t)i); continue; }
+            const bool inl = cn <= kWideInline;
+            if (!inl) n_blk += 2;
+            const uint32_t lb[kWideInline] = {a0.z, a1.x, a1.z}, le[kWideInline] = {a0.w, a1.y, a1.w};
+#pragma unroll
+            for (int t = 0; t < K; t++) {
+                const bool on = (uint32_t)t < cn;
+                cb[t] = !on ? 0u : inl && t < kWideInline ? lb[t < kWideInline ? t : 0] : ib[a0.x + t];
+                ce[t] = !on ? 0u : inl && t < kWideInline ? le[t < kWideInline ? t : 0] : ie[a0.x + t];
+            }
+        } else if (w.z == ~0u) {  // from the node's items at the cutover depth
             const uint32_t u = nid[i];
             cn = iend[u] - ioff[u];
+            n_blk += 4;  // nid, ioff / iend, and the list's lines in ib and ie
             if (cn > K) { flag_push(ovf, (uint32_t)i); continue; }
 #pragma unroll
             for (int t = 0; t < K; t++) {
@@ -1815,6 +1872,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                             n_text += m;
                             posres = true;
                             put_res(res, q2 ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                            cs.put(counts, q2 ? pi : perm[i], 1u, 1u);
                             break;
                         }
                     } else {
@@ -1967,6 +2025,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         const uint64_t at = abase + (uint64_t)i * K;
         if (cn == 1) {
             put_res(res, o, cb[0], 1u | kResRow, ce[0] - cb[0] + 1);
+            cs.put(counts, o, ce[0] - cb[0] + 1, 1u);
             continue;
         }
 #pragma unroll
@@ -1977,6 +2036,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 occ += ce[t] - cb[t] + 1;
             }
         put_res(res, o, at, cn, occ);
+        cs.put(counts, o, occ, cn);
     }
     __shared__ unsigned long long sh[4];
     stat_add(ctr, ST_DEEPQ_STEPS, n_steps, sh);
@@ -1985,6 +2045,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
     stat_add(ctr, ST_DEEPQ_PATS, n_q, sh);
     stat_add(ctr, ST_TEXT_CHARS, n_text, sh);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, sh);
+    cs.flush(counts, ctr, sh);
 #ifdef EDSBWT_DEEP_CLOCKS
     stat_add(ctr, ST_CLK_RANK, c_rank, sh);
     stat_add(ctr, ST_CLK_RUNS, c_runs, sh);
@@ -2146,8 +2207,9 @@ __global__ void __launch_bounds__(256) k_deep_wave(uint64_t P, uint32_t D0, cons
                                                   const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                                   uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                                   uint32_t* __restrict__ ovf2, const uint32_t* __restrict__ ntodo_dev,
-                                                  unsigned long long* __restrict__ ctr) {
+                                                  unsigned long long* __restrict__ ctr, uint32_t* __restrict__ counts) {
     (void)P;
+    CountSums cs;  // (lane 0 of each wave puts its patterns' counts)
     __shared__ uint32_t s_seg[4][kWaveHash], s_tmp[4][kWaveHash];
     __shared__ uint32_t s_b[4][192], s_e[4][192];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2256,18 +2318,25 @@ __global__ void __launch_bounds__(256) k_deep_wave(uint64_t P, uint32_t D0, cons
         const uint32_t o = perm[i];
         const uint64_t at = abase + (uint64_t)j * 64;
         if (cn == 1) {
-            if (lane == 0) put_res(res, o, cb, 1u | kResRow, ce - cb + 1);
+            if (lane == 0) {
+                put_res(res, o, cb, 1u | kResRow, ce - cb + 1);
+                cs.put(counts, o, ce - cb + 1, 1u);
+            }
             continue;
         }
         uint32_t occ = lane < cn ? ce - cb + 1 : 0u;
 #pragma unroll
         for (int q = 32; q >= 1; q >>= 1) occ += __shfl_xor(occ, q, 64);
         if (lane < cn) { ab[at + lane] = cb; ae[at + lane] = ce; }
-        if (lane == 0) put_res(res, o, at, cn, occ);
+        if (lane == 0) {
+            put_res(res, o, at, cn, occ);
+            cs.put(counts, o, occ, cn);
+        }
     }
     __shared__ unsigned long long ssum[4];
     stat_add(ctr, ST_DW_BLOCKS, n_blk, ssum);
     stat_add(ctr, ST_DW_STEPS, n_steps, ssum);
+    cs.flush(counts, ctr, ssum);
 }
 
 __global__ void k_list_flagged(uint64_t P, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ fscan, uint32_t* __restrict__ out) {
@@ -3716,6 +3785,10 @@ __global__ void k_ktab_wide(uint64_t E, const uint32_t* __restrict__ off, const 
             s = samples[b[o]];
         } else {
             ent = n == 1 ? (1ull << 63 | (uint64_t)e[o] << 32 | b[o]) : ((uint64_t)n << 32 | o);
+            if (n >= 2 && n <= kWideInline) {  // a short list inline (k_deep's start): (b, e) pairs
+                win = (uint64_t)e[o] << 32 | b[o];
+                s = make_uint4(b[o + 1], e[o + 1], n > 2 ? b[o + 2] : 0u, n > 2 ? e[o + 2] : 0u);
+            }
         }
         w[2 * u] = make_uint4((uint32_t)ent, (uint32_t)(ent >> 32), (uint32_t)win, (uint32_t)(win >> 32));
         w[2 * u + 1] = s;
@@ -3923,7 +3996,12 @@ __global__ void k_gather_checks(const unsigned long long* __restrict__ counters,
                                 uint32_t* __restrict__ chk, unsigned long long* __restrict__ pstats) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
-        const unsigned long long term = counters[10], found = counters[1], occ = counters[12], tasks = counters[13];
+        unsigned long long term = counters[10], found = counters[1], occ = counters[12], tasks = counters[13];
+        for (uint32_t sh = 0; sh < kStatShards && (sh + 1) * kStatStride <= nstats; sh++) {  // fused counts (deep kernels)
+            found += stats[sh * kStatStride + ST_FC_FOUND];
+            occ += stats[sh * kStatStride + ST_FC_OCC];
+            tasks += stats[sh * kStatStride + ST_FC_TASKS];
+        }
         chk[0] = (uint32_t)term; chk[1] = (uint32_t)(term >> 32);
         chk[2] = *ovf;
         chk[3] = *ovf2;

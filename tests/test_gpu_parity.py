@@ -70,10 +70,11 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # the defaults' A/B fallbacks (read when an index opens): the finisher pass instead of the
     # fused count (k_fin_flags / k_fin_emit), no text items, eof_seg link keys without the chain
     # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
-    # the dollar step's text-item entries
-    for var in ("EDSBWT_FUSE_FINISH", "EDSBWT_TEXT_ITEMS", "EDSBWT_LINK_CB", "EDSBWT_DEEP_WAVE", "EDSBWT_SEGTEXT"):
+    # the dollar step's text-item entries, and k_deep's other dispatched build (6 waves per SIMD)
+    for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
+                     ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "6")):
         old = os.environ.get(var)
-        os.environ[var] = "0"
+        os.environ[var] = val
         try:
             with edsbwt.Index(base) as idx:
                 for kw in ({}, {"locate": False}, {"locate": False, "deep": False}, {"locate": False, "deep": False, "ktab": False}):

@@ -246,6 +246,15 @@ def _group_ends(buf, offs, alphabet, G):
     return np.unique(np.array(out, np.int64))
 
 
+def _progress(msg: str) -> None:
+    """A stage line appended to $EDSBWT_TEST_PROGRESS (tools/gpu.sh points it into gpurun_out/),
+    so a long production test shows progress while pytest captures its output."""
+    path = os.environ.get("EDSBWT_TEST_PROGRESS")
+    if path:
+        with open(path, "a") as f:
+            f.write(f"[c5 parity] {msg} ({time.strftime('%H:%M:%S')})\n")
+
+
 def test_c5_production_parity(oracle, edsbwt, monkeypatch):
     """C5 (BASELINE configs[4]): the 1 Gchar EDS with 20% empty-word segments and the 200K
     mixed 8/16/32/64-mer batch of bench.py's C5 line.
@@ -263,8 +272,10 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
     wd = workloads.default_workdir()
     workloads.ensure_built()
     t0 = time.time()
+    _progress("index")
     eds, base = workloads.build_index(w, wd)
     t_index = time.time() - t0
+    _progress(f"index ready in {t_index:.0f} s")
     lo, hi = workloads.shard(w, 0, 1)
     pats = workloads.pattern_file(w, eds, wd, lo, hi)
     planted = workloads.planted_mask(pats)
@@ -284,6 +295,7 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
         t = time.time()
         counts, _ = idx.search((buf, offs), first_pattern_id=lo + 1, locate=False)
         t_count = time.time() - t
+        _progress(f"count-only batch in {t_count:.1f} s")
         st = idx.stats()
         dc, _, tags, dst = _device_tags(edsbwt, idx, buf, offs, lo + 1, locate=False)
         assert np.array_equal(dc, counts)
@@ -291,6 +303,7 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
         t = time.time()
         cl, ol = idx.search((sb, so), first_pattern_id=1, locate=True)
         t_loc = time.time() - t
+        _progress(f"located {loc.size} patterns in {t_loc:.1f} s")
         alphabet = idx.alphabet
     assert (counts[planted] > 0).all()
     assert np.array_equal(cl, counts[loc]) and int(cl.astype(np.uint64).sum()) == ol.size
@@ -298,6 +311,7 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
     assert (np.diff(pat0) >= 0).all() and np.array_equal(np.bincount(pat0, minlength=loc.size), cl.astype(np.int64))
     bad, first = oracle.check_records(eds, sb, so, ol, 1, threads=THREADS)
     assert bad == 0, (bad, ol[first])
+    _progress("records spelled")
     # the targeted oracle sample: the rare paths of this walk (wide lists / level re-run: round 3
     # had 433 such patterns at C5, none since the level start table; k_deep's register lists)
     def spread(a, n):
@@ -314,6 +328,7 @@ def test_c5_production_parity(oracle, edsbwt, monkeypatch):
     assert np.array_equal(cs, counts[idx_s])
     eng = oracle.Engine(base, 8)
     t = time.time()
+    _progress(f"oracle sample of {idx_s.size} patterns")
     oc, oo, _ = eng.search(ss, soo, first_pattern_id=1, threads=THREADS, trie=True)
     t_orc = time.time() - t
     eng.close()

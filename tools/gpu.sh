@@ -30,10 +30,12 @@ for task in "$@"; do
   echo "[gpu.sh] $task -> $out ($(date +%T))"
   case $kind in
     suite)
+      export EDSBWT_TEST_PROGRESS=$PWD/${out}_progress.log  # (stage lines of the long production tests)
       timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > ${out}_pytest.log 2>&1 || fail suite ${out}_pytest.log
       tail -2 ${out}_pytest.log
       timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > ${out}_smoke.log 2>&1 || fail smoke ${out}_smoke.log ;;
     test)
+      export EDSBWT_TEST_PROGRESS=$PWD/${out}_progress.log
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "$a" > ${out}.log 2>&1 || fail test ${out}.log
       tail -2 ${out}.log ;;
     bench)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel time of the last search in a rocprofv3 kernel trace (from its last k_keys,
-or the last k_lmax when the batch built a trie) — the device-resident leg of bench.py.
+"""Per-kernel time of the last search in a rocprofv3 kernel trace (from its last k_zero_multi,
+k_keys, or the last k_lmax when the batch built a trie) — the device-resident leg of bench.py.
     python tools/trace_split.py <trace_dir> [--all-searches]"""
 import collections
 import csv
@@ -19,7 +19,9 @@ def main():
     d = sys.argv[1]
     f = sorted(glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True))[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).startswith(("k_keys", "k_lmax"))]
+    # a search starts with its zeroing launch (k_zero_multi, deferred checks), k_keys (packed
+    # start) or k_lmax (trie)
+    starts = [i for i, r in enumerate(rows) if short(r["Kernel_Name"]).startswith(("k_keys", "k_lmax", "k_zero_multi"))]
     last = starts[-1]
     agg = collections.OrderedDict()
     t0 = int(rows[last]["Start_Timestamp"])
