@@ -2501,9 +2501,8 @@ struct Engine {
         defer_call = defer_ok && !(flags & (kFlagNoDefer | EDSBWT_LEGACY_ORDER)) && !force_groups && !sticky_groups;
         fc_done = false;
         fc_counts = nullptr;
-        if (defer_call && fused_counts && (deep_wave || no_wide) &&
-            (!locate || (loc_mode == 2 && kidx().samp_dense && locate_pp)))  // (finish_deferred's per-pattern locate)
-            fc_counts = d_counts;
+        // (count-only; the per-pattern locate writes them in k_locate_pp instead, finish_deferred)
+        if (defer_call && fused_counts && (deep_wave || no_wide) && !locate) fc_counts = d_counts;
         if (P == 0) return 0;
         struct EvPair {  // released on every exit, including exceptions
             hipEvent_t a = nullptr, b = nullptr;
@@ -2727,7 +2726,8 @@ struct Engine {
     uint64_t finish_deferred(uint64_t P, uint32_t first_id, bool locate, int loc_mode, uint32_t* d_counts, hipEvent_t e1) {
         const KIdx X = kidx();
         // (counters, the scan's first slot and the check words were zeroed by search())
-        uint64_t occ_cap = std::min<uint64_t>(0xffffffffull, std::max<uint64_t>({rec.cap, 2 * P + 65536, (uint64_t)(occ_per_pat * 1.25 * (double)P)}));
+        // (< 2^32 - 1: a fused occurrence sum saturates there)
+        uint64_t occ_cap = std::min<uint64_t>(0xfffffffeull, std::max<uint64_t>({rec.cap, 2 * P + 65536, (uint64_t)(occ_per_pat * 1.25 * (double)P)}));
         uint64_t task_cap = std::min<uint64_t>(0xffffffffull, std::max<uint64_t>({trow.cap, 2 * P + 65536, (uint64_t)(tasks_per_pat * 1.25 * (double)P)}));
         if (defer_cap) occ_cap = task_cap = defer_cap;
         // dense samples: records straight from each pattern's result (k_locate_pp / k_locate_big),
@@ -2735,11 +2735,13 @@ struct Engine {
         const bool per_pattern = locate && loc_mode == 2 && X.samp_dense && locate_pp;
         last_locate_pp = per_pattern;
         if (locate && !per_pattern) occ64.ensure(P);
-        if (!fc_done)  // (fused counts: written by the deep kernels, folded by k_gather_checks; search() enables
-                       // them only where this pass would not also build the task scan input)
+        // fused counts: written by the deep kernels (count-only) or by k_locate_pp (per-pattern
+        // locate, whose offsets scan reads the results), their sums folded by k_gather_checks
+        const bool loc_counts = per_pattern && fused_counts;
+        if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
-        emit_c8(P, d_counts);
+        if (!loc_counts) emit_c8(P, d_counts);
         uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
         if (per_pattern) {
             // record offsets: a u32 scan of the counts themselves (a total past 2^32 fails the
@@ -2747,21 +2749,30 @@ struct Engine {
             oscan.ensure(P + 1);
             uint32_t* o32 = reinterpret_cast<uint32_t*>(oscan.p);
             size_t tb = 0;
-            HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_counts, o32 + 1, cub_n(P), stream));
-            tmp.ensure(tb);
-            timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, d_counts, o32 + 1, cub_n(P), stream)); });
+            if (loc_counts) {  // the counts straight from the results (k_locate_pp writes them)
+                using It = hipcub::TransformInputIterator<uint32_t, ResOcc, const Res*>;
+                const It in((const Res*)res.p, ResOcc{});
+                HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, o32 + 1, cub_n(P), stream));
+                tmp.ensure(tb);
+                timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, in, o32 + 1, cub_n(P), stream)); });
+            } else {
+                HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_counts, o32 + 1, cub_n(P), stream));
+                tmp.ensure(tb);
+                timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, d_counts, o32 + 1, cub_n(P), stream)); });
+            }
             hmark("locate scan");
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);
             zero(lbig.p, 4);
             launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p,
-                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p);
+                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr);
             timed(KC_LOCATE, [&] {
                 hipLaunchKernelGGL(k_locate_big, dim3(256), dim3(256), 0, stream, (const uint32_t*)lbig.p, (const Res*)res.p,
                                    (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
             });
             HIPCHK(hipGetLastError());
             task_cap = ~0ull;  // no task buffers in this path
+            if (loc_counts) emit_c8(P, d_counts);
         } else if (locate) {
             inclusive_scan_u64(occ64.p, oscan, P, false);  // packed: occurrences << 32 | tasks (totals checked below)
             hmark("locate scan");

@@ -332,7 +332,7 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_DEEPQ_PATS = 21,  // queue entries k_deep read
                   // fused counts (deferred direct start): the deep kernels write each final count and add
                   // found / occurrences / intervals here; k_gather_checks folds them (no k_count_found pass)
-                  ST_FC_FOUND = 22, ST_FC_OCC = 23, ST_FC_TASKS = 24 };
+                  ST_FC_FOUND = 22, ST_FC_OCC = 23 };
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -346,22 +346,24 @@ __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats,
     if (threadIdx.x == 0 && v) atomicAdd(stats + (blockIdx.x % kStatShards) * kStatStride + k, v);
 }
 
-// a final result's count into counts[o] (fused counts) and the lane's found / occurrence / interval sums
+// a final result's count into counts[o] (fused counts), and the lane's found / occurrence sums in
+// two u32 registers: the occurrence sum saturates at 2^32 - 1, which fails the deferred checks'
+// record-capacity test (a batch with that many records is searched again on the checked path).
+// The interval total is not kept: the deferred path that fuses counts (per-pattern locate or
+// count-only) never builds the task list it bounds
 struct CountSums {
-    unsigned long long f = 0, occ = 0, tasks = 0;
-    __device__ __forceinline__ void put(uint32_t* __restrict__ counts, size_t o, uint32_t occ_, uint32_t cnt) {
+    uint32_t f = 0, occ = 0;
+    __device__ __forceinline__ void put(uint32_t* __restrict__ counts, size_t o, uint32_t occ_) {
         if (!counts) return;
         counts[o] = occ_;
         f += occ_ > 0;
-        occ += occ_;
-        tasks += cnt;
+        occ = occ + occ_ < occ ? 0xFFFFFFFFu : occ + occ_;
     }
     // every thread of the block
     __device__ __forceinline__ void flush(const uint32_t* counts, unsigned long long* __restrict__ ctr, unsigned long long* sh) {
         if (!counts) return;
         stat_add(ctr, ST_FC_FOUND, f, sh);
         stat_add(ctr, ST_FC_OCC, occ, sh);
-        stat_add(ctr, ST_FC_TASKS, tasks, sh);
     }
 };
 
@@ -925,6 +927,13 @@ __global__ void k_node_flags(const uint32_t* __restrict__ slen, const uint32_t* 
 // nscan = exclusive scan of flags (P+1 entries); skey = the sorted patterns'
 // reversed-code chunk holding depth D (BPS bits per symbol, most significant first)
 // node-start flag of pattern i at depth D (scanned on the fly by the host's transform scan)
+// a result's occurrence count (the per-pattern locate's scan input, read straight from the results)
+struct ResOcc {
+    __host__ __device__ __forceinline__ uint32_t operator()(const Res& r) const {
+        return (r.cnt & 0x40000000u) ? 1u : r.occ;  // res_occ (kResPos: one occurrence)
+    }
+};
+
 struct NodeFlag {
     const uint32_t* slen;
     const uint32_t* lcp;
@@ -1585,7 +1594,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         } else if (n0 == 0) {
             if (valid) {
                 put_res(res, pi, 0, 0u, 0u);  // no list: count 0 (every result is written here or by k_deep)
-                cs.put(counts, pi, 0u, 0u);
+                cs.put(counts, pi, 0u);
             }
         } else {
             uint32_t b, e, g1 = ~0u;
@@ -1637,7 +1646,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                         n_text += m;
                         d = L;
                         put_res(res, pi, (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
-                        cs.put(counts, pi, 1u, 1u);
+                        cs.put(counts, pi, 1u);
                     }
                     break;
                 }
@@ -1711,7 +1720,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             } else if (!posres) {
                 if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
                 else put_res(res, pi, abase + i * K, 0u, 0u);
-                cs.put(counts, pi, alive ? e - b + 1 : 0u, alive ? 1u : 0u);
+                cs.put(counts, pi, alive ? e - b + 1 : 0u);
             }
         }
         if (want) put_res(res, pi, 0, 0u, 0u);  // the zeroed result the later walks expect
@@ -1872,7 +1881,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                             n_text += m;
                             posres = true;
                             put_res(res, q2 ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
-                            cs.put(counts, q2 ? pi : perm[i], 1u, 1u);
+                            cs.put(counts, q2 ? pi : perm[i], 1u);
                             break;
                         }
                     } else {
@@ -2025,7 +2034,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         const uint64_t at = abase + (uint64_t)i * K;
         if (cn == 1) {
             put_res(res, o, cb[0], 1u | kResRow, ce[0] - cb[0] + 1);
-            cs.put(counts, o, ce[0] - cb[0] + 1, 1u);
+            cs.put(counts, o, ce[0] - cb[0] + 1);
             continue;
         }
 #pragma unroll
@@ -2036,7 +2045,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 occ += ce[t] - cb[t] + 1;
             }
         put_res(res, o, at, cn, occ);
-        cs.put(counts, o, occ, cn);
+        cs.put(counts, o, occ);
     }
     __shared__ unsigned long long sh[4];
     stat_add(ctr, ST_DEEPQ_STEPS, n_steps, sh);
@@ -2320,7 +2329,7 @@ __global__ void __launch_bounds__(256) k_deep_wave(uint64_t P, uint32_t D0, cons
         if (cn == 1) {
             if (lane == 0) {
                 put_res(res, o, cb, 1u | kResRow, ce - cb + 1);
-                cs.put(counts, o, ce - cb + 1, 1u);
+                cs.put(counts, o, ce - cb + 1);
             }
             continue;
         }
@@ -2330,7 +2339,7 @@ __global__ void __launch_bounds__(256) k_deep_wave(uint64_t P, uint32_t D0, cons
         if (lane < cn) { ab[at + lane] = cb; ae[at + lane] = ce; }
         if (lane == 0) {
             put_res(res, o, at, cn, occ);
-            cs.put(counts, o, occ, cn);
+            cs.put(counts, o, occ);
         }
     }
     __shared__ unsigned long long ssum[4];
@@ -3168,7 +3177,11 @@ constexpr uint32_t kLocStage = 1024;
 __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, const uint32_t* __restrict__ oscan, uint32_t first_id,
                                                    KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
-                                                   uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats) {
+                                                   uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats,
+                                                   uint32_t* __restrict__ counts) {
+    // counts != nullptr (the deferred per-pattern locate): each pattern's count is written here and
+    // found / occurrences summed (fused counts), the scan having read the results directly
+    CountSums cs;
     __shared__ uint32_t sw[kLocStage * 5];
     __shared__ uint64_t s_lo, s_hi;
     __shared__ unsigned long long sh[4];
@@ -3183,6 +3196,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
             r = res[i];
             occ = res_occ(r);
             base = oscan[i];  // exclusive scan of the counts
+            cs.put(counts, i, occ);
         }
         if (threadIdx.x == 0) s_lo = base;
         if (i == plast) s_hi = base + occ;
@@ -3239,6 +3253,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
         __syncthreads();
     }
     stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
+    cs.flush(counts, stats, sh);
 }
 __global__ void __launch_bounds__(256) k_locate_big(const uint32_t* __restrict__ big, const Res* __restrict__ res,
                                                     const uint32_t* __restrict__ oscan, uint32_t first_id, KIdx X,
@@ -4000,7 +4015,6 @@ __global__ void k_gather_checks(const unsigned long long* __restrict__ counters,
         for (uint32_t sh = 0; sh < kStatShards && (sh + 1) * kStatStride <= nstats; sh++) {  // fused counts (deep kernels)
             found += stats[sh * kStatStride + ST_FC_FOUND];
             occ += stats[sh * kStatStride + ST_FC_OCC];
-            tasks += stats[sh * kStatStride + ST_FC_TASKS];
         }
         chk[0] = (uint32_t)term; chk[1] = (uint32_t)(term >> 32);
         chk[2] = *ovf;

@@ -13,6 +13,7 @@
 #                           the TCC DRAM request counters, SQ stall + L2), summarised and shrunk on the box
 #                           (tools/profile_summary.py -> <out>_summary.json, <out>_traffic.json)
 #   calib:<mode>:<MB,MB..>  tools/_build/calib_gather --<mode> under a PMC pass of the TCC request counters
+#   hostmarks:<cfg>         EDSBWT_TRACE=2 host timeline of the last searches (the fixed per-call cost)
 #   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
 #   rccl:<cfg>[:<patterns>] one rank through the exchange path over RCCL (bench.py --dist-self)
 #   cli:<cfg>               the EDSBWTsearch CLI timed on the config's index and pattern file
@@ -70,6 +71,10 @@ for task in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_pmc -o pmc --output-format csv -- tools/_build/calib_gather --$a ${b//,/ } > ${out}.json 2> ${out}.log || fail calib ${out}.log
       python3 tools/prof_reduce.py ${out}_pmc
       cat ${out}.json; find ${out}_pmc -name "*counter_collection.csv" -exec cat {} \; ;;
+    hostmarks)
+      # host time of every launch inside each search (EDSBWT_TRACE=2) of a short device-resident run
+      EDSBWT_TRACE=2 timeout -k 10 300 $B0 --config ${a:-c2} > ${out}.json 2> ${out}.log || fail hostmarks ${out}.log
+      tail -120 ${out}.log > ${out}_tail.txt; rm -f ${out}.log; tail -60 ${out}_tail.txt ;;
     rehearse)
       n=${a:-2}; cfg=${b:-c4}
       timeout -k 10 1100 python bench.py --gpus $n --config $cfg --steps 3 --warmup 1 --dist-backend gloo ${c:+--patterns $c} > ${out}_${b}.json 2> ${out}_${b}.log || fail rehearse ${out}_${b}.log
