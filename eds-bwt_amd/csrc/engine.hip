@@ -497,6 +497,7 @@ struct Engine {
     // / intervals into the stats shards that k_gather_checks folds, so finish_deferred runs no
     // k_count_found pass over the results (EDSBWT_FUSED_COUNTS=0: the pass)
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
+    bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
     uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
     bool fc_done = false;           // ... and k_deep_direct took them
     static constexpr uint32_t kWideCap = 16384;
@@ -2737,7 +2738,10 @@ struct Engine {
         if (locate && !per_pattern) occ64.ensure(P);
         // fused counts: written by the deep kernels (count-only) or by k_locate_pp (per-pattern
         // locate, whose offsets scan reads the results), their sums folded by k_gather_checks
-        const bool loc_counts = per_pattern && fused_counts;
+        // (EDSBWT_LOCATE_COUNTS=1: the per-pattern locate's counts from k_locate_pp, its scan over the
+        // results — C3 1.608 / 1.620 against 1.617 ms with k_count_found, profiles/r04_ab4_c3_*.json: the
+        // scan reading 16-B results and the locate kernel's count stores cost what the pass saves)
+        const bool loc_counts = per_pattern && fused_counts && locate_counts;
         if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
