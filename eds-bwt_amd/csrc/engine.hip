@@ -388,7 +388,7 @@ struct Engine {
                         &gscan, &g_map, &dqpre, &kt_kid, &kt_cnt, &kt_pos})
             b->release();
         for (auto* b : {&keys, &kc, &kc2, &skey, &child_info, &lkeys, &lkeys2, &occ64, &oscan, &tc64, &tscan64, &tout, &blk_first, &lk,
-                        &lk2, &sub_len, &sub_off, &fk, &fk2, &ekeys, &efk, &g_len, &g_off, &dq2, &pv_in, &pv_out})
+                        &lk2, &sub_len, &sub_off, &fk, &fk2, &ekeys, &efk, &g_len, &g_off, &dq2, &pv_in, &pv_out, &tile_sum, &tile_pre})
             b->release();
         for (auto* b : {&node_char, &tmp, &sub_bytes, &fin, &g_bytes}) b->release();
         res.release(); sub_res.release(); g_res.release();
@@ -498,6 +498,8 @@ struct Engine {
     // k_count_found pass over the results (EDSBWT_FUSED_COUNTS=0: the pass)
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
     bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
+    bool tile_scan = env_double("EDSBWT_TILE_SCAN", 1) != 0;
+    DBuf<uint64_t> tile_sum, tile_pre;  // per-pattern locate: occurrences per 256-pattern tile, and their exclusive scan
     uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
     bool fc_done = false;           // ... and k_deep_direct took them
     static constexpr uint32_t kWideCap = 16384;
@@ -2742,7 +2744,17 @@ struct Engine {
         // results — C3 1.608 / 1.620 against 1.617 ms with k_count_found, profiles/r04_ab4_c3_*.json: the
         // scan reading 16-B results and the locate kernel's count stores cost what the pass saves)
         const bool loc_counts = per_pattern && fused_counts && locate_counts;
-        if (!fc_done && !loc_counts)
+        // per-pattern locate: record offsets per 256-pattern tile (k_count_tiles, a scan over tiles,
+        // the offsets inside a tile in k_locate_pp) instead of a scan over every pattern's count
+        // (EDSBWT_TILE_SCAN=0: the latter)
+        const bool tiles = per_pattern && !loc_counts && tile_scan;
+        const uint64_t ntile = (P + 255) / 256;
+        if (tiles) {
+            tile_sum.ensure(ntile);
+            tile_pre.ensure(ntile);
+            launch_reduce(KC_FINISH, k_count_tiles, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
+                          (unsigned long long*)tile_sum.p);
+        } else if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
         if (!loc_counts) emit_c8(P, d_counts);
@@ -2753,7 +2765,11 @@ struct Engine {
             oscan.ensure(P + 1);
             uint32_t* o32 = reinterpret_cast<uint32_t*>(oscan.p);
             size_t tb = 0;
-            if (loc_counts) {  // the counts straight from the results (k_locate_pp writes them)
+            if (tiles) {
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_sum.p, tile_pre.p, cub_n(ntile), stream));
+                tmp.ensure(tb);
+                timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, tile_sum.p, tile_pre.p, cub_n(ntile), stream)); });
+            } else if (loc_counts) {  // the counts straight from the results (k_locate_pp writes them)
                 using It = hipcub::TransformInputIterator<uint32_t, ResOcc, const Res*>;
                 const It in((const Res*)res.p, ResOcc{});
                 HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, o32 + 1, cub_n(P), stream));
@@ -2768,8 +2784,10 @@ struct Engine {
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);
             zero(lbig.p, 4);
-            launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p,
-                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr);
+            // (k_locate_pp runs in 256-thread blocks: its tiles are k_count_tiles')
+            launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, o32, first_id, X, (const uint32_t*)ab.p,
+                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
+                   tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);
             timed(KC_LOCATE, [&] {
                 hipLaunchKernelGGL(k_locate_big, dim3(256), dim3(256), 0, stream, (const uint32_t*)lbig.p, (const Res*)res.p,
                                    (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);

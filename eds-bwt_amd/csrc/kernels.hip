@@ -314,6 +314,24 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long x, un
     return t;
 }
 
+// exclusive prefix sum of x over the 256 threads of the block (every thread calls; sw: 4 slots)
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long x, unsigned long long* sw) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(inc, (unsigned)o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    __syncthreads();  // sw may still be read by the previous call
+    if (lane == 63) sw[w] = inc;
+    __syncthreads();
+    unsigned long long pre = 0;
+    for (uint32_t k = 0; k < w; k++) pre += sw[k];
+    return pre + inc - x;
+}
+
+
 
 // statistics counters: block-reduced, then one atomic per block into one of kStatShards
 // 128-B lines (the host folds the shards), so no address takes every block's add.
@@ -3174,14 +3192,18 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
 // per record from every lane (records of patterns left to k_locate_big, which runs next on the
 // stream, are written over by it)
 constexpr uint32_t kLocStage = 1024;
-__global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, const uint32_t* __restrict__ oscan, uint32_t first_id,
+__global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, uint32_t* __restrict__ oscan, uint32_t first_id,
                                                    KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
                                                    uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats,
-                                                   uint32_t* __restrict__ counts) {
+                                                   uint32_t* __restrict__ counts, const unsigned long long* __restrict__ tile_pre) {
     // counts != nullptr (the deferred per-pattern locate): each pattern's count is written here and
-    // found / occurrences summed (fused counts), the scan having read the results directly
+    // found / occurrences summed (fused counts), the scan having read the results directly.
+    // tile_pre != nullptr: each 256-pattern tile's first record (k_count_tiles + a scan over tiles);
+    // the offsets inside a tile come from a block scan here, and oscan is written only for the
+    // patterns k_locate_big takes
     CountSums cs;
+    __shared__ unsigned long long s_scan[4];
     __shared__ uint32_t sw[kLocStage * 5];
     __shared__ uint64_t s_lo, s_hi;
     __shared__ unsigned long long sh[4];
@@ -3195,9 +3217,10 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
         if (i < P) {
             r = res[i];
             occ = res_occ(r);
-            base = oscan[i];  // exclusive scan of the counts
+            if (!tile_pre) base = oscan[i];  // exclusive scan of the counts
             cs.put(counts, i, occ);
         }
+        if (tile_pre) base = tile_pre[p0 / blockDim.x] + block_excl_scan(occ, s_scan);  // (block-uniform branch)
         if (threadIdx.x == 0) s_lo = base;
         if (i == plast) s_hi = base + occ;
         __syncthreads();
@@ -3220,6 +3243,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
                 emit(base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
                 my_off += off;
             } else if (occ > kLocBig) {
+                if (tile_pre) oscan[i] = (uint32_t)base;  // (< occ_cap < 2^32) k_locate_big's offset
                 flag_push(big, (uint32_t)i);
             } else {
                 uint64_t o = base;
@@ -3660,6 +3684,38 @@ __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res
         f += oc > 0;
         so += oc;
         st += res_cnt(r);
+    }
+    f = block_sum(f, sh);
+    so = block_sum(so, sh);
+    st = block_sum(st, sh);
+    if (threadIdx.x == 0) {
+        if (f) atomicAdd(found, f);
+        if (so) atomicAdd(sums, so);
+        if (st) atomicAdd(sums + 1, st);
+    }
+}
+
+// the per-pattern locate's counts pass: k_count_found's counts and totals, and the occurrence sum
+// of each 256-pattern tile (k_locate_pp's tiles), whose exclusive scan gives every tile its first
+// record — a scan over tiles instead of over patterns (C3: 39K entries against 10M)
+__global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
+                                                     unsigned long long* __restrict__ found, unsigned long long* __restrict__ sums,
+                                                     unsigned long long* __restrict__ tile_sum) {
+    __shared__ unsigned long long sh[4];
+    unsigned long long f = 0, so = 0, st = 0;
+    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < P; p0 += (uint64_t)gridDim.x * blockDim.x) {  // block-uniform
+        const uint64_t i = p0 + threadIdx.x;
+        uint32_t oc = 0;
+        if (i < P) {
+            const Res r = res[i];
+            oc = res_occ(r);
+            counts[i] = oc;
+            f += oc > 0;
+            so += oc;
+            st += res_cnt(r);
+        }
+        const unsigned long long t = block_sum(oc, sh);
+        if (threadIdx.x == 0) tile_sum[p0 / blockDim.x] = t;
     }
     f = block_sum(f, sh);
     so = block_sum(so, sh);
