@@ -499,7 +499,7 @@ struct Engine {
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
     bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
     bool tile_scan = env_double("EDSBWT_TILE_SCAN", 1) != 0;
-    DBuf<uint64_t> tile_sum, tile_pre;  // per-pattern locate: occurrences per 256-pattern tile, and their exclusive scan
+    DBuf<uint64_t> tile_sum, tile_pre;  // per-pattern locate: occurrences per 64-pattern tile, and their exclusive scan
     uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
     bool fc_done = false;           // ... and k_deep_direct took them
     static constexpr uint32_t kWideCap = 16384;
@@ -2744,11 +2744,12 @@ struct Engine {
         // results — C3 1.608 / 1.620 against 1.617 ms with k_count_found, profiles/r04_ab4_c3_*.json: the
         // scan reading 16-B results and the locate kernel's count stores cost what the pass saves)
         const bool loc_counts = per_pattern && fused_counts && locate_counts;
-        // per-pattern locate: record offsets per 256-pattern tile (k_count_tiles, a scan over tiles,
+        // per-pattern locate: record offsets per 64-pattern tile (k_count_tiles, a scan over tiles,
         // the offsets inside a tile in k_locate_pp) instead of a scan over every pattern's count
-        // (EDSBWT_TILE_SCAN=0: the latter)
+        // (EDSBWT_TILE_SCAN=0: the latter; C3 1.607 / 1.610 against 1.635 ms with 256-pattern
+        // tiles, profiles/r04_ab5_c3_*.json)
         const bool tiles = per_pattern && !loc_counts && tile_scan;
-        const uint64_t ntile = (P + 255) / 256;
+        const uint64_t ntile = (P + 63) / 64;
         if (tiles) {
             tile_sum.ensure(ntile);
             tile_pre.ensure(ntile);
@@ -2784,7 +2785,7 @@ struct Engine {
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);
             zero(lbig.p, 4);
-            // (k_locate_pp runs in 256-thread blocks: its tiles are k_count_tiles')
+            // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
             launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, o32, first_id, X, (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
                    tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);

@@ -314,21 +314,16 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long x, un
     return t;
 }
 
-// exclusive prefix sum of x over the 256 threads of the block (every thread calls; sw: 4 slots)
-__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long x, unsigned long long* sw) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// exclusive prefix sum of x over the 64 lanes of the wave
+__device__ __forceinline__ unsigned long long wave_excl_scan(unsigned long long x) {
+    const uint32_t lane = threadIdx.x & 63;
     unsigned long long inc = x;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const unsigned long long y = __shfl_up(inc, (unsigned)o, 64);
         if (lane >= (uint32_t)o) inc += y;
     }
-    __syncthreads();  // sw may still be read by the previous call
-    if (lane == 63) sw[w] = inc;
-    __syncthreads();
-    unsigned long long pre = 0;
-    for (uint32_t k = 0; k < w; k++) pre += sw[k];
-    return pre + inc - x;
+    return inc - x;
 }
 
 
@@ -3199,11 +3194,10 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
                                                    uint32_t* __restrict__ counts, const unsigned long long* __restrict__ tile_pre) {
     // counts != nullptr (the deferred per-pattern locate): each pattern's count is written here and
     // found / occurrences summed (fused counts), the scan having read the results directly.
-    // tile_pre != nullptr: each 256-pattern tile's first record (k_count_tiles + a scan over tiles);
-    // the offsets inside a tile come from a block scan here, and oscan is written only for the
+    // tile_pre != nullptr: each 64-pattern tile's first record (k_count_tiles + a scan over tiles);
+    // the offsets inside a tile come from a wave scan here, and oscan is written only for the
     // patterns k_locate_big takes
     CountSums cs;
-    __shared__ unsigned long long s_scan[4];
     __shared__ uint32_t sw[kLocStage * 5];
     __shared__ uint64_t s_lo, s_hi;
     __shared__ unsigned long long sh[4];
@@ -3220,7 +3214,11 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
             if (!tile_pre) base = oscan[i];  // exclusive scan of the counts
             cs.put(counts, i, occ);
         }
-        if (tile_pre) base = tile_pre[p0 / blockDim.x] + block_excl_scan(occ, s_scan);  // (block-uniform branch)
+        if (tile_pre) {  // (a uniform branch) the wave's tile: its first record + the offsets inside it
+            const uint64_t w0 = p0 + (threadIdx.x & ~63u);
+            const unsigned long long inw = wave_excl_scan(occ);
+            if (w0 < P) base = tile_pre[w0 >> 6] + inw;
+        }
         if (threadIdx.x == 0) s_lo = base;
         if (i == plast) s_hi = base + occ;
         __syncthreads();
@@ -3696,8 +3694,9 @@ __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res
 }
 
 // the per-pattern locate's counts pass: k_count_found's counts and totals, and the occurrence sum
-// of each 256-pattern tile (k_locate_pp's tiles), whose exclusive scan gives every tile its first
-// record — a scan over tiles instead of over patterns (C3: 39K entries against 10M)
+// of each 64-pattern tile (one wave of k_locate_pp), whose exclusive scan gives every tile its
+// first record — a scan over tiles instead of over patterns (C3: 156K entries against 10M), and
+// no block barrier per tile (wave shuffles)
 __global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
                                                      unsigned long long* __restrict__ found, unsigned long long* __restrict__ sums,
                                                      unsigned long long* __restrict__ tile_sum) {
@@ -3714,8 +3713,8 @@ __global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res
             so += oc;
             st += res_cnt(r);
         }
-        const unsigned long long t = block_sum(oc, sh);
-        if (threadIdx.x == 0) tile_sum[p0 / blockDim.x] = t;
+        const unsigned long long t = wave_sum(oc);
+        if ((threadIdx.x & 63) == 0 && i < P) tile_sum[i >> 6] = t;  // (p0 is a multiple of 64)
     }
     f = block_sum(f, sh);
     so = block_sum(so, sh);

@@ -70,9 +70,12 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # the defaults' A/B fallbacks (read when an index opens): the finisher pass instead of the
     # fused count (k_fin_flags / k_fin_emit), no text items, eof_seg link keys without the chain
     # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
-    # the dollar step's text-item entries, and k_deep's other dispatched build (6 waves per SIMD)
+    # the dollar step's text-item entries, k_deep's other dispatched build (6 waves per SIMD), the
+    # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
+    # counts instead of per-tile record offsets, and the locate kernel's own counts
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
-                     ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "6")):
+                     ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "6"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
+                     ("EDSBWT_LOCATE_COUNTS", "1")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
