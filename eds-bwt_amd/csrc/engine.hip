@@ -2753,8 +2753,7 @@ struct Engine {
         if (tiles) {
             tile_sum.ensure(ntile);
             tile_pre.ensure(ntile);
-            launch_reduce(KC_FINISH, k_count_tiles, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
-                          (unsigned long long*)tile_sum.p);
+            launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
         } else if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);

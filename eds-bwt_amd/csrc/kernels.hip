@@ -3698,32 +3698,22 @@ __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res
 // first record — a scan over tiles instead of over patterns (C3: 156K entries against 10M), and
 // no block barrier per tile (wave shuffles)
 __global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
-                                                     unsigned long long* __restrict__ found, unsigned long long* __restrict__ sums,
-                                                     unsigned long long* __restrict__ tile_sum) {
+                                                     unsigned long long* __restrict__ stats, unsigned long long* __restrict__ tile_sum) {
+    // (a grid of up to 16384 blocks: the found / occurrence sums go to the sharded stats, folded by
+    // k_gather_checks — the deferred path of this pass checks no interval total)
     __shared__ unsigned long long sh[4];
-    unsigned long long f = 0, so = 0, st = 0;
+    CountSums cs;
     for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < P; p0 += (uint64_t)gridDim.x * blockDim.x) {  // block-uniform
         const uint64_t i = p0 + threadIdx.x;
         uint32_t oc = 0;
         if (i < P) {
-            const Res r = res[i];
-            oc = res_occ(r);
-            counts[i] = oc;
-            f += oc > 0;
-            so += oc;
-            st += res_cnt(r);
+            oc = res_occ(res[i]);
+            cs.put(counts, i, oc);
         }
         const unsigned long long t = wave_sum(oc);
         if ((threadIdx.x & 63) == 0 && i < P) tile_sum[i >> 6] = t;  // (p0 is a multiple of 64)
     }
-    f = block_sum(f, sh);
-    so = block_sum(so, sh);
-    st = block_sum(st, sh);
-    if (threadIdx.x == 0) {
-        if (f) atomicAdd(found, f);
-        if (so) atomicAdd(sums, so);
-        if (st) atomicAdd(sums + 1, st);
-    }
+    cs.flush(counts, stats, sh);
 }
 
 // per depth D: trie nodes M_D = #{i : lcp[i] < D <= slen[i]} (difference array over D)
