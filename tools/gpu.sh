@@ -13,6 +13,7 @@
 #                           the TCC DRAM request counters, SQ stall + L2), summarised and shrunk on the box
 #                           (tools/profile_summary.py -> <out>_summary.json, <out>_traffic.json)
 #   calib:<mode>:<MB,MB..>  tools/_build/calib_gather --<mode> under a PMC pass of the TCC request counters
+#   e2etrace:<cfg>          EDSBWT_TRACE=1 timeline of the end-to-end leg's last calls
 #   hostmarks:<cfg>         EDSBWT_TRACE=2 host timeline of the last searches (the fixed per-call cost)
 #   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
 #   rccl:<cfg>[:<patterns>] one rank through the exchange path over RCCL (bench.py --dist-self)
@@ -71,6 +72,10 @@ for task in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_pmc -o pmc --output-format csv -- tools/_build/calib_gather --$a ${b//,/ } > ${out}.json 2> ${out}.log || fail calib ${out}.log
       python3 tools/prof_reduce.py ${out}_pmc
       cat ${out}.json; find ${out}_pmc -name "*counter_collection.csv" -exec cat {} \; ;;
+    e2etrace)
+      # the end-to-end leg's pipeline timeline (EDSBWT_TRACE=1: upload / search / download marks per chunk)
+      EDSBWT_TRACE=1 timeout -k 10 300 python3 bench.py --no-cpu --no-device --no-located --steps 3 --warmup 1 --config ${a:-c2} > ${out}.json 2> ${out}.log || fail e2etrace ${out}.log
+      grep -E "\] t +[0-9.]+ ms" ${out}.log | tail -40 > ${out}_tail.txt || true; rm -f ${out}.log; cat ${out}_tail.txt ;;
     hostmarks)
       # host time of every launch inside each search (EDSBWT_TRACE=2) of a short device-resident run
       EDSBWT_TRACE=2 timeout -k 10 300 $B0 --config ${a:-c2} > ${out}.json 2> ${out}.log || fail hostmarks ${out}.log
@@ -93,7 +98,7 @@ for task in "$@"; do
         [ -z "$spec" ] && continue
         i=$((i+1))
         env ${spec//,/ } timeout -k 10 600 python bench.py --no-cpu --no-located --config $cfg --steps 5 --warmup 2 > ${out}_$i.json 2> ${out}_$i.log || fail ab ${out}_$i.log
-        python3 -c "import json;d=json.load(open('${out}_$i.json'));r=d.get('device_resident',{});print('$spec', d['value'], d['ms_per_step'], r.get('kernel_ms_per_step'))"
+        python3 -c "import json;d=json.load(open('${out}_$i.json'));r=d.get('device_resident',{});e=d.get('e2e') or {};print('$spec', d['value'], d['ms_per_step'], r.get('kernel_ms_per_step'), 'e2e median', e.get('ms_wall_median'))"
       done ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
