@@ -1742,15 +1742,17 @@ struct Engine {
                    nid_d, goff, gend, gb, gee, X, abase, K, ab.p, ae.p, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1,
                    pv ? dq2.p : (uint64_t*)nullptr, kt1w);
         }
-        hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
-        HIPCHK(hipGetLastError());
+        if (trace) {  // (k_deep sums the shard counters itself; the trace line below reads the total)
+            hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
+            HIPCHK(hipGetLastError());
+        }
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? (X.eofrow ? k_deep<4, 3, 1, true>
                                           : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
                                        : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
-        launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)dqpre.p, (uint32_t)qcap, d, lens,
+        launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
                pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc);
         tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);

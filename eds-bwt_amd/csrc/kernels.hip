@@ -1771,7 +1771,7 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
 // EOFROW: links from '#' rows through KIdx::eofrow (one line per row; costs k_deep 6 VGPRs and a
 // wave per SIMD: C3 0.355 against 0.304 ms, profiles/r04_ab_c3_*.json — off by default)
 template <int K, int BPS, int MINW = 1, bool EOFROW = false>  // MINW: waves per SIMD the register budget is held to (1: no bound)
-__global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qpre, uint32_t qcap, uint32_t D0,
+__global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qcnt, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
                                               const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind, uint64_t P,
                                               const uint32_t* __restrict__ nid, const uint32_t* __restrict__ ioff,
@@ -1785,8 +1785,26 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
+    // the shards' prefix sums of the producers' queue counters (qcnt[s * 32]), by the block's first
+    // wave (no k_queue_prefix launch)
     __shared__ uint32_t spre[NSHARD + 1];
-    for (uint32_t t = threadIdx.x; t <= NSHARD; t += blockDim.x) spre[t] = qpre[t];
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        uint32_t carry = 0;
+        for (uint32_t b0 = 0; b0 < NSHARD; b0 += 64) {
+            const uint32_t t = b0 + lane;
+            const uint32_t v = t < NSHARD ? qcnt[t * 32] : 0u;
+            uint32_t inc = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, (unsigned)o, 64);
+                if (lane >= (uint32_t)o) inc += y;
+            }
+            if (t < NSHARD) spre[t] = carry + inc - v;
+            carry += __shfl(inc, 63, 64);
+        }
+        if (lane == 0) spre[NSHARD] = carry;
+    }
     __syncthreads();
     const uint32_t total = spre[NSHARD];
     GRID_STRIDE(j, total) {
