@@ -499,6 +499,9 @@ struct Engine {
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
     bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
     bool tile_scan = env_double("EDSBWT_TILE_SCAN", 1) != 0;
+    // k_locate_pp's LDS record stage (512 or 1024 records; 512 lets 8 blocks share a CU: the
+    // locate class 0.190 against 0.189 ms at C3, profiles/r04_ab_locstage_c3_*.json — not the bound)
+    uint32_t loc_stage = (uint32_t)env_double("EDSBWT_LOC_STAGE", 1024);
     DBuf<uint64_t> tile_sum, tile_pre;  // per-pattern locate: occurrences per 64-pattern tile, and their exclusive scan
     uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
     bool fc_done = false;           // ... and k_deep_direct took them
@@ -2787,7 +2790,8 @@ struct Engine {
             lbig.ensure(P + 1);
             zero(lbig.p, 4);
             // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
-            launch(KC_LOCATE, k_locate_pp, P, P, (const Res*)res.p, o32, first_id, X, (const uint32_t*)ab.p,
+            launch(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>, P, P, (const Res*)res.p, o32, first_id, X,
+                   (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
                    tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);
             timed(KC_LOCATE, [&] {

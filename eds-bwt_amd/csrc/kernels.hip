@@ -3205,6 +3205,7 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
 // per record from every lane (records of patterns left to k_locate_big, which runs next on the
 // stream, are written over by it)
 constexpr uint32_t kLocStage = 1024;
+template <uint32_t STAGE = kLocStage>  // records staged per block (STAGE x 20 B of LDS: 1024 -> 7 blocks per CU)
 __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, uint32_t* __restrict__ oscan, uint32_t first_id,
                                                    KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
@@ -3216,7 +3217,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
     // the offsets inside a tile come from a wave scan here, and oscan is written only for the
     // patterns k_locate_big takes
     CountSums cs;
-    __shared__ uint32_t sw[kLocStage * 5];
+    __shared__ uint32_t sw[STAGE * 5];
     __shared__ uint64_t s_lo, s_hi;
     __shared__ unsigned long long sh[4];
     unsigned long long my_off = 0;
@@ -3241,7 +3242,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
         if (i == plast) s_hi = base + occ;
         __syncthreads();
         const uint64_t lo = s_lo, hi = min(s_hi, occ_cap);
-        const bool stage = hi >= lo && hi - lo <= kLocStage;
+        const bool stage = hi >= lo && hi - lo <= STAGE;
         auto emit = [&](uint64_t o, uint32_t pat, uint32_t word, uint32_t seg, uint32_t wis, uint32_t off) {
             if (stage) {
                 uint32_t* d = sw + (o - lo) * 5;
