@@ -2539,10 +2539,11 @@ struct Engine {
             oscan.ensure(P + 1);
             const uint64_t nb = direct_buckets();
             if (nb) bhist.ensure(nb + 1);
+            lbig.ensure(P + 1);  // (the per-pattern locate's big list: its counter is zeroed here)
             // (the result array only when the search does not turn out to be k_deep_direct's, which
             // writes every result: res_unzeroed, settled by run_batch / run_deep)
             zero_many({{stats.p, kStatSlots * 8}, {counters.p, 24 * 8}, {tflag.p, 4}, {hcnt.p, 4},
-                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}});
+                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}, {lbig.p, 4}});
             res_unzeroed = true;
         } else {
             zero(res.p, P * sizeof(Res));
@@ -2787,8 +2788,7 @@ struct Engine {
             }
             hmark("locate scan");
             rec.ensure(occ_cap);
-            lbig.ensure(P + 1);
-            zero(lbig.p, 4);
+            lbig.ensure(P + 1);  // (its counter zeroed with the others at the search's start)
             // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
             launch(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>, P, P, (const Res*)res.p, o32, first_id, X,
                    (const uint32_t*)ab.p,
