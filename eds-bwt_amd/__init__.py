@@ -105,7 +105,7 @@ def lib() -> ctypes.CDLL:
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise EdsBwtError(-4, f"{LIB_PATH} not built: run __graft_entry__.build() (make -C eds-bwt_amd)")
-    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL, use_errno=True)  # (edsbwt_write_csv reports pwrite's errno)
     L.edsbwt_build_id.argtypes = []
     L.edsbwt_build_id.restype = ctypes.c_char_p
     built = L.edsbwt_build_id().decode()

@@ -165,6 +165,7 @@ constexpr double kKtabItems = 268435456.0;  // at least 2^28 intervals (2 GiB) .
 constexpr double kKtabHbmShare = 0.15;      // ... or as many as kKtabHbmShare of the free HBM holds at
 constexpr double kKtabBuildBytes = 40.0;    // the build's transient bytes per interval (capture + sort)
 constexpr uint32_t kKtabMinDepth = 2;
+// the wide k-mer entries (32 B per D-mer) are built when the free HBM exceeds this many times their bytes
 constexpr double kKt1WideHbmShare = 2.5;
 // per-'#'-row link rows (KIdx::eofrow) up to this size (C3 243 MB; C5's 264M words would take 17 GB: not built)
 constexpr double kEofRowMaxBytes = 2.0e9;
@@ -172,7 +173,7 @@ constexpr double kEofRowMaxBytes = 2.0e9;
 // free HBM (after every other table) its intervals may take (C5: depth 8, ~9.5G intervals, 76 GB)
 constexpr double kLtabK = 8;
 constexpr uint64_t kLtabMaxEntries = 1ull << 20;
-constexpr double kLtabHbmShare = 0.5;  // the wide k-mer entries are built when free HBM > 2.5x their bytes
+constexpr double kLtabHbmShare = 0.5;  // (the share of the free HBM named above)
 // ... and no deeper than B^(K-1) <= kKtabOver * N: most longer D-mers do not occur (an
 // entry is 12 B; C2, 12.5M rows: depth 15 = 12.9 GB of the 288 GB, searches 4.6x faster
 // than at depth 11)
@@ -528,10 +529,9 @@ struct Engine {
         unsigned long long* n_term = nullptr;
         uint32_t E = 0, lmin = 0, lmax = 0;
     } fk_now;
-    // k_deep<4, 3> likewise (5 or 6; C3 0.371 / 0.478 ms against 0.369 unbounded, profiles/r03_ab_occupancy.txt).
-    // The unbounded builds (96 VGPRs) miscounted the README KAT on some round-4 boxes (TATT 0 instead
-    // of 4) while the 5- and 6-wave builds of the same source were exact: they are not dispatched
-    // (k_deep<4, 4> likewise held to 5 waves)
+    // k_deep<4, 3> likewise (5 or 6; C3 0.371 / 0.478 ms against 0.369 unbounded, profiles/r03_ab_occupancy.txt);
+    // 1: the unbounded builds (k_deep<4, 3, 1>, <4, 4, 1>, the '#'-row link rows' <4, 3, 1, true>) —
+    // every build is run through the parity tests (tests/test_gpu_parity.py::test_k_deep_builds_gpu)
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 5);
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
@@ -550,7 +550,7 @@ struct Engine {
         return b;
     }
     KIdx kidx() const {
-        KIdx X;
+        KIdx X{};  // (every field set below; value-initialised so a new one cannot reach a kernel unset)
         X.occ = occ.p;
         X.eof_seg = eof_seg.p;
         X.eofrow = eofrow.p;
@@ -590,6 +590,8 @@ struct Engine {
         X.kt1_pos = kt1_pos ? 1u : 0u;
         X.rk16 = use_rk16 ? rk16.p : nullptr;
         X.rk16sup = use_rk16 ? rk16sup.p : nullptr;
+        X.kt_E = (uint32_t)std::min<uint64_t>(ktab_entries, 0xffffffffu);
+        X.kt_n = (uint32_t)std::min<uint64_t>(ktab_items, 0xffffffffu);
         return X;
     }
 
@@ -890,6 +892,8 @@ struct Engine {
         acgt_alpha = H.sigma == 5 && H.code_of[(uint8_t)'#'] == 0 && H.code_of[(uint8_t)'A'] == 1 && H.code_of[(uint8_t)'C'] == 2 &&
                      H.code_of[(uint8_t)'G'] == 3 && H.code_of[(uint8_t)'T'] == 4;
         if (W > N) throw Fail(EDSBWT_E_FORMAT, "more words than rows");
+        // rows are u32 (Parameters.h:71); the top values mark k_deep's queue entries (kernels.hip kQNode / kQWide)
+        if (N > 0xFFFFFFF0u) throw Fail(EDSBWT_E_UNSUPPORTED, "more than 2^32 - 16 BWT rows");
         // occ blocks (parallel over block ranges)
         const size_t nblk = (size_t)N / kOccRows + 1;
         std::vector<OccBlock> hb(nblk);
@@ -1049,59 +1053,77 @@ struct Engine {
             uint64_t tot = 0;
             bool ok = true;
             for (uint32_t g = 0; g < G && ok; g++) {
-                DBuf<uint8_t> kb;
-                DBuf<uint64_t> ko;
-                kb.ensure(EG * L);
-                ko.ensure(EG + 1);
-                launch(KC_TABLE, k_kmer_batch, EG, EG, L, B, sym, kb.p, ko.p, (uint64_t)G, (uint64_t)g);
-                res.ensure(EG); ovf_orig.ensure(EG);
-                zero(stats.p, kStatSlots * 8);
-                Capture c;
-                c.K = L; c.B = B; c.budget = 0x7fffffffull; c.only_last = true;
-                cap = &c;
-                const bool was_count_only = count_only;
-                count_only = true;
-                uint64_t abase = 0;
                 try {
-                    levels2(kb.p, ko.p, EG, false, res.p, abase, ovf_orig.p);
-                } catch (const TooBig&) {
-                    c.depth = 0;
-                }
-                cap = nullptr;
-                count_only = was_count_only;
-                st = edsbwt_stats{};
-                HIPCHK(hipStreamSynchronize(stream));
-                const uint64_t n = c.n;
-                tot += n;
-                // the first group's size x G estimates the table; every group is checked as it lands
-                if (c.depth != L || (double)tot * 8 > budget || (g == 0 && (double)n * G * 8 > budget)) {
-                    ok = false;
-                    if (trace) std::fprintf(stderr, "[edsbwt] level table depth %u: group %u holds %llu intervals (depth %u): too large\n", L, g,
-                                            (unsigned long long)n, c.depth);
-                    break;
-                }
-                lt_b[g].ensure(n);
-                lt_e[g].ensure(n);
-                if (n) {
-                    DBuf<uint64_t> k1, k2;
-                    DBuf<uint32_t> e2;
-                    k1.ensure(n); k2.ensure(n); e2.ensure(n);
-                    launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
-                    c.k.release(); c.b.release();
-                    size_t tb = 0;
-                    const int endbit = 32 + (int)bits_for(EG);
-                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
-                    tmp.ensure(tb);
-                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
-                    sync_check(nullptr, "hipcub call in build_ltab");
-                    k1.release();
-                    c.e.release();
-                    launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, lt_b[g].p);
-                    HIPCHK(hipMemcpyAsync(lt_e[g].p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
-                    launch(KC_TABLE, k_ktab_bounds, EG + 1, EG, (const uint64_t*)k2.p, n, lt_off.p + (size_t)g * (EG + 1));
+                    DBuf<uint8_t> kb;
+                    DBuf<uint64_t> ko;
+                    kb.ensure(EG * L);
+                    ko.ensure(EG + 1);
+                    launch(KC_TABLE, k_kmer_batch, EG, EG, L, B, sym, kb.p, ko.p, (uint64_t)G, (uint64_t)g);
+                    res.ensure(EG); ovf_orig.ensure(EG);
+                    zero(stats.p, kStatSlots * 8);
+                    Capture c;
+                    // the group walk's items bounded by what the free HBM holds at the build's transient
+                    // bytes per item (a walk past it stops short of depth L: this L is given up)
+                    size_t fg = 0, tg = 0;
+                    if (hipMemGetInfo(&fg, &tg) != hipSuccess) { (void)hipGetLastError(); fg = 0; }
+                    c.K = L; c.B = B; c.only_last = true;
+                    c.budget = std::min<uint64_t>(0x7fffffffull, (uint64_t)(0.5 * (double)fg / kKtabBuildBytes));
+                    cap = &c;
+                    const bool was_count_only = count_only;
+                    count_only = true;
+                    uint64_t abase = 0;
+                    try {
+                        levels2(kb.p, ko.p, EG, false, res.p, abase, ovf_orig.p);
+                    } catch (const TooBig&) {
+                        c.depth = 0;
+                    } catch (const Fail& f) {
+                        // an optional table: a device allocation that fails during its build gives up
+                        // this depth (a shallower one, or none, is tried) instead of failing the open
+                        if (f.code != EDSBWT_E_NOMEM) { cap = nullptr; count_only = was_count_only; throw; }
+                        (void)hipGetLastError();
+                        c.depth = 0;
+                    }
+                    cap = nullptr;
+                    count_only = was_count_only;
+                    st = edsbwt_stats{};
                     HIPCHK(hipStreamSynchronize(stream));
-                } else {
-                    zero(lt_off.p + (size_t)g * (EG + 1), (EG + 1) * 4);
+                    const uint64_t n = c.n;
+                    tot += n;
+                    // the first group's size x G estimates the table; every group is checked as it lands
+                    if (c.depth != L || (double)tot * 8 > budget || (g == 0 && (double)n * G * 8 > budget)) {
+                        ok = false;
+                        if (trace) std::fprintf(stderr, "[edsbwt] level table depth %u: group %u holds %llu intervals (depth %u): too large\n", L, g,
+                                                (unsigned long long)n, c.depth);
+                        break;
+                    }
+                    lt_b[g].ensure(n);
+                    lt_e[g].ensure(n);
+                    if (n) {
+                        DBuf<uint64_t> k1, k2;
+                        DBuf<uint32_t> e2;
+                        k1.ensure(n); k2.ensure(n); e2.ensure(n);
+                        launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
+                        c.k.release(); c.b.release();
+                        size_t tb = 0;
+                        const int endbit = 32 + (int)bits_for(EG);
+                        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+                        tmp.ensure(tb);
+                        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+                        sync_check(nullptr, "hipcub call in build_ltab");
+                        k1.release();
+                        c.e.release();
+                        launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, lt_b[g].p);
+                        HIPCHK(hipMemcpyAsync(lt_e[g].p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+                        launch(KC_TABLE, k_ktab_bounds, EG + 1, EG, (const uint64_t*)k2.p, n, lt_off.p + (size_t)g * (EG + 1));
+                        HIPCHK(hipStreamSynchronize(stream));
+                    } else {
+                        zero(lt_off.p + (size_t)g * (EG + 1), (EG + 1) * 4);
+                    }
+                } catch (const Fail& f) {
+                    // (the group's sort buffers or lists did not fit: as a walk past the budget)
+                    if (f.code != EDSBWT_E_NOMEM) throw;
+                    (void)hipGetLastError();
+                    ok = false;
                 }
             }
             if (!ok) {
@@ -1749,11 +1771,12 @@ struct Engine {
             hipLaunchKernelGGL(k_queue_prefix, dim3(1), dim3(64), 0, stream, (const uint32_t*)lcnt.p, dqpre.p);
             HIPCHK(hipGetLastError());
         }
+        const bool unb = deepq_waves <= 1;
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
-                  : K == 4 ? (bps == 3 ? (X.eofrow ? k_deep<4, 3, 1, true>
-                                          : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
-                                       : k_deep<4, 4, 5>)
+                  : K == 4 ? (bps == 3 ? (X.eofrow ? (unb ? k_deep<4, 3, 1, true> : k_deep<4, 3, 5, true>)
+                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
+                                       : unb ? k_deep<4, 4, 1> : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
@@ -2654,6 +2677,13 @@ struct Engine {
     uint64_t finish_stats(uint64_t P, bool locate, bool use_table, int loc_mode, uint64_t OCC, hipEvent_t e0, hipEvent_t e1) {
         {
             const std::vector<uint64_t> sv = fold_pinned_stats();
+#ifdef EDSBWT_DEBUG_CHECKS
+            // the debug build's device invariant checks (kernels.hip DBG_CHECK): a failed one is an error
+            if (sv[ST_DBG_QUEUE] | sv[ST_DBG_PACKED] | sv[ST_DBG_WIDE] | sv[ST_DBG_LIST])
+                throw Fail(EDSBWT_E_DEVICE, "debug checks failed: queue " + std::to_string(sv[ST_DBG_QUEUE]) + ", packed start " +
+                                                std::to_string(sv[ST_DBG_PACKED]) + ", wide entry " + std::to_string(sv[ST_DBG_WIDE]) +
+                                                ", list " + std::to_string(sv[ST_DBG_LIST]));
+#endif
             st.intervals_stepped += sv[ST_DEEP_STEPS] + sv[ST_DEEPQ_STEPS];
             st.link_hash_rows += sv[ST_DEEP_HASH];
             // the 64-B lines the deep kernels gather (occ blocks or the 16-B rank entries' lines; a
@@ -4180,6 +4210,15 @@ extern "C" {
 
 int edsbwt_abi_version(void) { return EDSBWT_ABI_VERSION; }
 const char* edsbwt_last_error(void) { return edsbwt::g_err.c_str(); }
+
+int edsbwt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
 const char* edsbwt_kernel_name(int k) { return (k >= 0 && k < edsbwt::KC_COUNT) ? edsbwt::kKNames[k] : ""; }
 
 int edsbwt_index_open(const char* base, int device, uint32_t a_balance, edsbwt_index** out) {

@@ -125,6 +125,10 @@ struct KIdx {
     // kTextItem) of the ONE word of [seg_lo[s], s - 1] ending with c, when there is one: the dollar
     // step then hands that single row on as a text item (no srow read at the next depth)
     uint32_t segtext;
+    // the k-mer start table's D-mers (B^depth; entry kt_E is the empty list of D-mers outside the
+    // alphabet) and intervals: the bounds a queued direct-start list is checked against in the
+    // debug build (-DEDSBWT_DEBUG_CHECKS)
+    uint32_t kt_E, kt_n;
 };
 
 }  // namespace edsbwt

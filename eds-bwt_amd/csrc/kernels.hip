@@ -271,9 +271,12 @@ constexpr uint32_t kResRow = 0x80000000u;
 // text compare, k_deep_fast): off = offset << 32 | word, occ = 1 — no row, no archive
 constexpr uint32_t kResPos = 0x40000000u;
 constexpr uint32_t kResCnt = 0x3FFFFFFFu;  // the interval count in cnt
-// k_deep queue entry (i, D0, ~0u, D-mer id) on the direct start: the pattern starts from its
-// D-mer's list, read from the wide k-mer entry; lists of up to kWideInline intervals are held
-// inline there
+// k_deep queue entries (i, d, z, w): z = b, w = e — the pattern goes on from depth d with the one
+// interval [b, e] (rows < 2^32 - 16, engine.hip); z = kQNode — from its node's items at the cutover
+// depth (nid / ioff / iend); z = kQWide, w = the D-mer id — on the direct start with the wide k-mer
+// table, from the D-mer's list read from its wide entry, where lists of up to kWideInline
+// intervals are held inline.  The producer names the kind (k_deep does not infer it)
+constexpr uint32_t kQNode = 0xFFFFFFFFu, kQWide = 0xFFFFFFFEu;
 constexpr int kWideInline = 3;
 // a kResPos result carries the whole record: cnt = kResRow | kResPos | word-in-segment (< 2^30),
 // occ = segment; its occurrence count is 1
@@ -288,6 +291,11 @@ __device__ __forceinline__ uint64_t rtext_window(const uint64_t* __restrict__ rt
     if (!sh) return a;
     return (a >> sh) | (rt[q + 1] << (64u - sh));
 }
+// the packed start's remaining symbols (2 bits each, closed by a 1 bit): symbols past the 32nd
+// (a pattern too long for the packed start, which the deferred checks send to the redo) are
+// dropped rather than shifted out of range; and its length back from the closing bit
+__device__ __forceinline__ uint64_t pk_digit(uint64_t v, uint32_t n) { return n < 32 ? v << (2 * n) : 0ull; }
+__device__ __forceinline__ uint32_t pk_len(uint32_t D0, uint64_t rem) { return rem ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : D0; }
 // rare per-pattern events (deep-kernel overflows): lst[0] counts, the pattern ids follow
 __device__ __forceinline__ void flag_push(uint32_t* __restrict__ lst, uint32_t i) { lst[1 + atomicAdd(lst, 1u)] = i; }
 __device__ __forceinline__ void put_res(Res* __restrict__ r, size_t o, uint64_t off, uint32_t cnt, uint32_t occ) {
@@ -345,7 +353,20 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_DEEPQ_PATS = 21,  // queue entries k_deep read
                   // fused counts (deferred direct start): the deep kernels write each final count and add
                   // found / occurrences / intervals here; k_gather_checks folds them (no k_count_found pass)
-                  ST_FC_FOUND = 22, ST_FC_OCC = 23 };
+                  ST_FC_FOUND = 22, ST_FC_OCC = 23,
+                  // debug build (-DEDSBWT_DEBUG_CHECKS, libedsbwt_dbg.so): failed invariant checks per kind;
+                  // search() throws when any is non-zero (engine.hip check_debug)
+                  ST_DBG_QUEUE = 24, ST_DBG_PACKED = 25, ST_DBG_WIDE = 26, ST_DBG_LIST = 27 };
+#ifdef EDSBWT_DEBUG_CHECKS
+#define DBG_CHECK(cond, var) \
+    do {                     \
+        if (!(cond)) (var)++; \
+    } while (0)
+#else
+#define DBG_CHECK(cond, var) \
+    do {                     \
+    } while (0)
+#endif
 // k_deep phase clocks (profiling build, -DEDSBWT_DEEP_CLOCKS): shader cycles summed over lanes
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
@@ -540,10 +561,10 @@ __global__ void __launch_bounds__(256) k_keys(const uint8_t* __restrict__ bytes,
                         const uint64_t k = t < SPC ? kc0 : kc1;
                         const uint32_t v = (uint32_t)(k >> (BPS * (SPC - 1 - (t < SPC ? t : t - SPC)))) & ((1u << BPS) - 1u);
                         ok &= v >= 2 && v <= B + 1;
-                        rem |= (uint64_t)((v - 2) & 3u) << (2 * n);
+                        rem |= pk_digit((v - 2) & 3u, n);
                         n++;
                     }
-                    rem |= 1ull << (2 * n);
+                    rem |= pk_digit(1, n);
                     pv[i] = rem << 31 | (uint64_t)i;
                 }
                 kid[i] = ok ? x : E;
@@ -607,12 +628,12 @@ __global__ void __launch_bounds__(256) k_keys_packed(const uint8_t* __restrict__
                     x += (v - 1) * mul;
                     mul *= B;
                 } else {
-                    rem |= (uint64_t)((v - 1) & 3u) << (2 * n);
+                    rem |= pk_digit((v - 1) & 3u, n);
                     n++;
                 }
             }
             nt += term;
-            rem |= 1ull << (2 * n);
+            rem |= pk_digit(1, n);
             pv[i] = rem << 31 | (uint64_t)i;
             kid[i] = ok ? x : E;
         }
@@ -664,7 +685,7 @@ __device__ __forceinline__ void acgt_key(const uint8_t* __restrict__ bytes, uint
             rem_out = 1ull;
         } else {
             x_out = ok ? (uint32_t)(V & ((1ull << (2 * D)) - 1ull)) : E;
-            rem_out = (V >> (2 * D)) | (1ull << (2 * (L - D)));
+            rem_out = (V >> (2 * D)) | pk_digit(1, L - D);
         }
     } else {  // rare: longer patterns keep k_keys_packed's per-character order
         uint32_t x = 0, mul = 1, nn = 0;
@@ -675,9 +696,9 @@ __device__ __forceinline__ void acgt_key(const uint8_t* __restrict__ bytes, uint
             term |= ch == '#';
             ok &= v != 0;
             if (t < D) { x += (v - 1) * mul; mul *= 4u; }
-            else { rem |= (uint64_t)((v - 1) & 3u) << (2 * nn); nn++; }
+            else { rem |= pk_digit((v - 1) & 3u, nn); nn++; }
         }
-        rem |= 1ull << (2 * nn);
+        rem |= pk_digit(1, nn);
         x_out = ok ? x : E;
         rem_out = rem;
     }
@@ -712,7 +733,7 @@ __device__ __forceinline__ void acgt_key_regs(const uint32_t (&W)[8], uint32_t L
         rem_out = 1ull;
     } else {
         x_out = ok ? (uint32_t)(V & ((1ull << (2 * D)) - 1ull)) : E;
-        rem_out = (V >> (2 * D)) | (1ull << (2 * (L - D)));
+        rem_out = (V >> (2 * D)) | pk_digit(1, L - D);
     }
     term_out = term;
 }
@@ -1274,7 +1295,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
             pvv = v;
             pi = (uint32_t)(v & 0x7fffffffu);
             rem = v >> 31;
-            L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
+            L = valid ? pk_len(D0, rem) : 0u;
             if (valid) perm_out[i] = pi;
         } else {
             pi = valid && ind ? perm[i] : (uint32_t)i;
@@ -1298,7 +1319,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
         if (n0 > 1) {
             want = 1;
             // (the wide table: k_deep reads the list from the D-mer's entry, w.w)
-            w = make_uint4((uint32_t)i, D0, ~0u, kt1w ? u : 0u);
+            w = make_uint4((uint32_t)i, D0, kt1w ? kQWide : kQNode, kt1w ? u : 0u);
         } else if (n0 == 1) {
             uint32_t b, e;
             uint32_t g1 = ~0u;  // the row's text position when the table entry holds it
@@ -1578,13 +1599,13 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 nt += term;
                 len_out[i] = Lp;
                 kid_out[i] = kx;
-                L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
+                L = pk_len(D0, rem);
             }
         } else {
             const uint64_t v = valid ? pv[i] : 0ull;
             pi = (uint32_t)(v & 0x7fffffffu);
             rem = v >> 31;
-            L = valid ? D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2 : 0u;
+            L = valid ? pk_len(D0, rem) : 0u;
         }
         if (valid) perm_out[i] = pi;
         // the D-mer's wide entry: its one interval inline (or its list's length), and for one
@@ -1603,7 +1624,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         const uint32_t n0 = L <= D0 ? 0u : (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
         if (n0 > 1) {
             want = 1;
-            w = make_uint4((uint32_t)i, D0, ~0u, u);
+            w = make_uint4((uint32_t)i, D0, kQWide, u);
         } else if (n0 == 0) {
             if (valid) {
                 put_res(res, pi, 0, 0u, 0u);  // no list: count 0 (every result is written here or by k_deep)
@@ -1782,6 +1803,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts) {
     uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;
     CountSums cs;  // n_blk: occ blocks read (per lane, widened at the end)
+#ifdef EDSBWT_DEBUG_CHECKS
+    uint32_t dbg_q = 0, dbg_p = 0, dbg_w = 0, dbg_l = 0;
+#endif
 #ifdef EDSBWT_DEEP_CLOCKS
     unsigned long long c_rank = 0, c_runs = 0, c_rest = 0, c_steps = 0, c_hsteps = 0;
 #endif
@@ -1814,8 +1838,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             if (spre[mid] <= (uint32_t)j) lo = mid; else hi = mid;
         }
         const size_t qi = (size_t)lo * qcap + ((uint32_t)j - spre[lo]);
+        DBG_CHECK((uint32_t)j - spre[lo] < qcap, dbg_q);  // a slot its producer wrote
         const uint4 w = q[qi];
         const uint32_t i = w.x, d0 = w.y;
+        DBG_CHECK(i < P && d0 >= D0, dbg_q);
         n_q++;
         // q2 (packed direct start): input index and remaining symbols from the queue entry
         uint32_t pi, L;
@@ -1824,23 +1850,29 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             const uint64_t v = q2[qi];
             pi = (uint32_t)(v & 0x7fffffffu);
             rem = v >> 31;
-            L = D0 + (uint32_t)(63 - __builtin_clzll(rem)) / 2;
+            DBG_CHECK(rem != 0 && pi < P, dbg_p);
+            L = pk_len(D0, rem);
+            DBG_CHECK(L <= D0 + 16 && d0 <= L, dbg_p);
         } else {
             pi = ind ? perm[i] : i;  // slen and key chunks in input order (k_deep_fast)
             L = slen[pi];
         }
         uint32_t cb[K], ce[K];
         uint32_t cn;
-        if (w.z == ~0u && kt1w) {
-            // (kt1w: the direct start, whose lists all come from the wide k-mer table; a kernel
-            // argument, so this is a uniform branch inside the lanes' two-way one) the list's
-            // length, offset and (<= 3 intervals) the intervals themselves from the D-mer's 32-B
-            // wide entry, w.w = the D-mer (k_ktab_wide) — one line instead of the nid, ioff / iend,
-            // ib and ie reads below
+        if (w.z == kQWide) {
+            // the list's length, offset and (<= 3 intervals) the intervals themselves from the
+            // D-mer's 32-B wide entry, w.w = the D-mer (k_ktab_wide) — one line instead of the nid,
+            // ioff / iend, ib and ie reads below.  (Only producers given the wide table write this
+            // kind; without it the pattern goes to the wide-list walk, which reads its node's list)
+            DBG_CHECK(kt1w != nullptr && w.w <= X.kt_E, dbg_w);
+            if (!kt1w || w.w > X.kt_E) { flag_push(ovf, (uint32_t)i); continue; }
             const uint4 a0 = kt1w[2 * (size_t)w.w], a1 = kt1w[2 * (size_t)w.w + 1];
             n_blk++;
             cn = a0.y;
-            if (cn > K) { flag_push(ovf, (uint32_t)i); continue; }
+            // a queued D-mer has a list of >= 2 intervals (one interval is never queued from the
+            // start), held in ktab_b / ktab_e at a0.x
+            DBG_CHECK(cn >= 2 && (uint64_t)a0.x + cn <= X.kt_n, dbg_w);
+            if (cn > K || (cn > kWideInline && (uint64_t)a0.x + cn > X.kt_n)) { flag_push(ovf, (uint32_t)i); continue; }
             const bool inl = cn <= kWideInline;
             if (!inl) n_blk += 2;
             const uint32_t lb[kWideInline] = {a0.z, a1.x, a1.z}, le[kWideInline] = {a0.w, a1.y, a1.w};
@@ -1850,7 +1882,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 cb[t] = !on ? 0u : inl && t < kWideInline ? lb[t < kWideInline ? t : 0] : ib[a0.x + t];
                 ce[t] = !on ? 0u : inl && t < kWideInline ? le[t < kWideInline ? t : 0] : ie[a0.x + t];
             }
-        } else if (w.z == ~0u) {  // from the node's items at the cutover depth
+        } else if (w.z == kQNode) {  // from the node's items at the cutover depth
             const uint32_t u = nid[i];
             cn = iend[u] - ioff[u];
             n_blk += 4;  // nid, ioff / iend, and the list's lines in ib and ie
@@ -1867,6 +1899,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             cb[0] = w.z;
             ce[0] = w.w;
         }
+#ifdef EDSBWT_DEBUG_CHECKS
+        for (int t = 0; t < K; t++)
+            if ((uint32_t)t < cn && !(cb[t] <= ce[t] && ce[t] < X.N)) dbg_l++;
+#endif
         SymReader<BPS> sym{k0, krest, P, pi};
         auto code_at = [&](uint32_t dd) -> uint32_t { return q2 ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };
         bool over = false, posres = false;
@@ -2086,6 +2122,12 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
     stat_add(ctr, ST_TEXT_CHARS, n_text, sh);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, sh);
     cs.flush(counts, ctr, sh);
+#ifdef EDSBWT_DEBUG_CHECKS
+    stat_add(ctr, ST_DBG_QUEUE, dbg_q, sh);
+    stat_add(ctr, ST_DBG_PACKED, dbg_p, sh);
+    stat_add(ctr, ST_DBG_WIDE, dbg_w, sh);
+    stat_add(ctr, ST_DBG_LIST, dbg_l, sh);
+#endif
 #ifdef EDSBWT_DEEP_CLOCKS
     stat_add(ctr, ST_CLK_RANK, c_rank, sh);
     stat_add(ctr, ST_CLK_RUNS, c_runs, sh);

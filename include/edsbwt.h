@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EDSBWT_ABI_VERSION 4
+#define EDSBWT_ABI_VERSION 5
 
 enum {
     EDSBWT_OK = 0,
@@ -130,6 +130,12 @@ typedef struct {
  * parameter (kept for CLI compatibility; the device LF table does not need it). */
 int edsbwt_index_open(const char* base, int device, uint32_t a_balance, edsbwt_index** out);
 void edsbwt_index_close(edsbwt_index* idx);
+
+/* GPUs this process sees (0 when none).  The reference's pattern loop (MOVE_EDSBWTSearch.cpp:
+ * 111-136) is a sequence of independent searches over one read-only index, so N devices take
+ * contiguous line ranges of the pattern file, one index each (EDSBWTsearch --gpus N; SURVEY.md
+ * §5 / §8(e)); this is how a host program sizes N. */
+int edsbwt_device_count(void);
 int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info);
 
 /* Replaces the pattern loop + backwardSearch (MOVE_EDSBWTSearch.cpp:97-155, 228-374).

@@ -1101,3 +1101,104 @@ def test_counts_mirror_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             idx.search((buf, offs), first_pattern_id=9)
         assert (small.cpu().numpy() == -7).all()
         idx.set_counts_mirror(0, 0)
+
+
+# every k_deep build the engine can dispatch (engine.hip run_deep): the register-list lengths
+# (EDSBWT_DEEP_K 2 / 3 / 4 / 8), the 4-interval build unbounded (EDSBWT_DEEPQ_WAVES=1) and held to
+# 5 / 6 waves per SIMD, and the '#'-row link-row variant (EDSBWT_EOF_ROWS=1) unbounded and at 5 waves
+K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDSBWT_DEEPQ_WAVES": "6"},
+                 {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "5"},
+                 {"EDSBWT_DEEP_K": "2"}, {"EDSBWT_DEEP_K": "3"}, {"EDSBWT_DEEP_K": "8"}]
+
+
+@pytest.mark.parametrize("build", K_DEEP_BUILDS, ids=lambda b: ",".join(f"{k[7:]}={v}" for k, v in b.items()))
+def test_k_deep_builds_gpu(oracle, edsbwt, tmp_path, monkeypatch, build):
+    """Each k_deep instantiation exact against the oracle: the README KAT
+    (README.md:144-167, the search that once miscounted TATT), random EDSs with empty words and
+    'N', and the direct start whose multi-interval D-mer lists k_deep reads from the wide
+    entries (inline lists of 2-3 intervals and offset lists), each through the search variants
+    that reach k_deep (default, count-only, the walk from depth 0, the trie start, no pair
+    entries, no text compare) and repeated, with fresh allocations poisoned where the process
+    runs with EDSBWT_POISON (tools/kdeep_stress.py is the many-repetition form of this test)."""
+    for k, v in build.items():
+        monkeypatch.setenv(k, v)
+    kat = _build(oracle, tmp_path, open(os.path.join(GOLDEN, "test.eds")).read(), "test")
+    cases = [(kat, ["TATT", "ACT", "TTAT"]), (kat, ["TATT", "ACT", "TTAT", "TTA", "GTT", "T"])]
+    for seed in (0, 7):
+        rng = random.Random(100 + seed)
+        segs = edsgen.random_eds(rng, rng.randint(20, 400), alphabet="ACGTN" if seed % 3 == 0 else "ACGT", lmax=3 + seed,
+                                 p_empty=0.25)
+        base = _build(oracle, tmp_path, edsgen.eds_text(segs), f"r{seed}")
+        pats = [(edsgen.planted(rng, segs, m) if rng.random() < 0.6 else None) or "".join(rng.choice("ACGT") for _ in range(m))
+                for m in (rng.randint(1, 24) for _ in range(400))]
+        cases.append((base, pats))
+    rng = random.Random(3232)
+    segs = _covid_like(rng, 700)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    cov = _build(oracle, tmp_path, edsgen.eds_text(segs), "cov")
+    cases.append((cov, [edsgen.planted(rng, segs, rng.randint(16, 31)) or "ACGT" * 8 for _ in range(3000)]))
+    for base, pats in cases:
+        buf, offs = _pack(pats)
+        oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+        if base == cov:
+            monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")  # the direct start from this small table
+        with edsbwt.Index(base) as idx:
+            for kw in ({}, {"locate": False}, {"ktab": False}, {"direct": False}, {"pairs": False}, {"text": False}):
+                for _ in range(3):
+                    gc, go = idx.search((buf, offs), **kw)
+                    assert np.array_equal(gc, oc), (build, base, kw)
+                    if kw.get("locate", True):
+                        assert np.array_equal(go, oo), (build, base, kw)
+        monkeypatch.delenv("EDSBWT_DIRECT_ITEMS", raising=False)
+
+
+@pytest.mark.parametrize("gpus", [2, 3, 5])
+def test_cli_gpus_shards(oracle, tmp_path, gpus):
+    """EDSBWTsearch --gpus N (the pattern loop MOVE_EDSBWTSearch.cpp:111-136 sharded into N
+    contiguous line ranges, one index each — here N handles on the box's one GPU): the CSV is
+    byte-identical to --gpus 1's and to the oracle's, count lines equal, in MOVE order, count-only
+    and legacy order; the console transcript (no --quiet) equals the single-device one; a file with
+    fewer lines than shards works."""
+    import re
+    import subprocess
+    from conftest import ROOT
+    rng = random.Random(600 + gpus)
+    segs = edsgen.random_eds(rng, 700, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(3, 20)) or "ACGT" for _ in range(1500)]
+    pats += ["", "N", "GATTACA", "AC\r"] + ["".join(rng.choice("ACGT") for _ in range(rng.randint(1, 16))) for _ in range(500)]
+    rng.shuffle(pats)
+    cli = os.path.join(ROOT, "eds-bwt_amd", "_build", "EDSBWTsearch")
+
+    def run(name, text, *extra):
+        p = tmp_path / name
+        p.write_text(text)
+        r = subprocess.run([cli, base, str(p)] + list(extra), capture_output=True, text=True)
+        assert r.returncode == 1, r.stderr[-500:]
+        return p, r
+
+    for trailing in ("\n", ""):
+        text = "\n".join(pats) + trailing
+        p1, r1 = run(f"one{len(trailing)}.txt", text, "--quiet")
+        pn, rn = run(f"many{len(trailing)}.txt", text, "--quiet", "--gpus", str(gpus))
+        csv1 = open(str(p1) + "output_M_LF.csv", "rb").read()
+        assert open(str(pn) + "output_M_LF.csv", "rb").read() == csv1
+        assert rn.stderr.split("count_found")[1] == r1.stderr.split("count_found")[1]
+    ctr, _ = oracle.Engine(base).search_file(str(p1), str(tmp_path / "orc.csv"))
+    assert open(tmp_path / "orc.csv", "rb").read() == csv1
+    for extra in (["--count-only"], ["--legacy"]):
+        pa, ra = run("a.txt", "\n".join(pats) + "\n", "--quiet", *extra)
+        pb, rb = run("b.txt", "\n".join(pats) + "\n", "--quiet", "--gpus", str(gpus), *extra)
+        out = "output.csv" if "--legacy" in extra else "output_M_LF.csv"
+        assert open(str(pa) + out, "rb").read() == open(str(pb) + out, "rb").read()
+        assert ra.stderr.split("count_found")[1] == rb.stderr.split("count_found")[1]
+    # the console stream (reach search sharded too)
+    _, c1 = run("c1.txt", "\n".join(pats[:300]) + "\n")
+    _, cn = run("c1.txt", "\n".join(pats[:300]) + "\n", "--gpus", str(gpus))
+    strip = lambda s: re.sub(r"bs took:[0-9.e+-]+", "bs took:", s)
+    assert strip(cn.stdout) == strip(c1.stdout) and cn.stderr == c1.stderr
+    # fewer lines than shards
+    pf, rf = run("few.txt", "TTAT\nACGT\n", "--quiet", "--gpus", "4")
+    _, r2 = run("few1.txt", "TTAT\nACGT\n", "--quiet")
+    assert open(str(pf) + "output_M_LF.csv", "rb").read() == open(str(tmp_path / "few1.txt") + "output_M_LF.csv", "rb").read()

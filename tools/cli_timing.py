@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--runs", type=int, default=2)
     ap.add_argument("--check", type=int, default=512)
+    ap.add_argument("--log", default=None, help="write the last run's stderr here (EDSBWT_TRACE=2 host marks)")
+    ap.add_argument("--cli-args", default="", help="extra EDSBWTsearch arguments (e.g. '--gpus 2')")
     args = ap.parse_args()
     w = workloads.CONFIGS[args.config]
     wd = workloads.default_workdir()
@@ -53,8 +55,10 @@ def main():
         if os.path.exists(csv_path):
             os.remove(csv_path)
         t = time.perf_counter()
-        r = subprocess.run([cli, base, pats, "--quiet"], capture_output=True, env=dict(os.environ, EDSBWT_CLI_TIMES="1"))
+        r = subprocess.run([cli, base, pats, "--quiet"] + args.cli_args.split(), capture_output=True, env=dict(os.environ, EDSBWT_CLI_TIMES="1"))
         wall = time.perf_counter() - t
+        if args.log:
+            open(args.log, "wb").write(r.stderr[-2_000_000:])
         if r.returncode != 1:  # the reference exits 1 on success (mainMove_EDSBWT.cpp:61)
             sys.exit(f"EDSBWTsearch exited {r.returncode}: {r.stderr[-400:]!r}")
         m = re.search(rb"bs took:([0-9.e+-]+)$", r.stdout)
