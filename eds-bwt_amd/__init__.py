@@ -126,6 +126,11 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_search_lines.argtypes = [vp, vp, u64, u32, u32, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(vp),
                                       ctypes.POINTER(u64)]
     L.edsbwt_search_lines.restype = i32
+    if hasattr(L, "edsbwt_prepare"):  # (ABI 5)
+        L.edsbwt_prepare.argtypes = [vp, u64, u64, u64, u32]
+        L.edsbwt_prepare.restype = i32
+        L.edsbwt_device_count.argtypes = []
+        L.edsbwt_device_count.restype = i32
     L.edsbwt_host_alloc.argtypes = [u64, ctypes.POINTER(vp)]
     L.edsbwt_host_alloc.restype = i32
     L.edsbwt_host_free.argtypes = [vp]
@@ -307,6 +312,12 @@ class Index:
             lib().edsbwt_occ_free(occ_p.value)
             return npat.value, 0, nocc.value
         return npat.value, occ_p.value or 0, nocc.value
+
+    def prepare(self, text_bytes: int, npat: int, *, records_hint: int = 0, locate: bool = True) -> None:
+        """edsbwt_prepare: set the host pipeline up for a search_lines batch of about this size
+        (synthetic lines; nothing of the batch is searched), so its first call runs at steady state."""
+        flags = LOCATE if locate else COUNT_ONLY
+        _check(lib().edsbwt_prepare(self._h, int(text_bytes), int(npat), int(records_hint), flags))
 
     @staticmethod
     def occ_view(ptr: int, n: int) -> np.ndarray:

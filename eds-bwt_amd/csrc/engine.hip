@@ -3117,6 +3117,7 @@ struct Engine {
     void arena_register();
     void arena_release();
     void arena_checkout();
+    void arena_checkin();
     bool arena_checked_out();
 
     struct Chunk { uint64_t b0, b1, p0, p1, dpos; };  // byte range; pattern range (offsets mode); device place (eager)
@@ -3696,6 +3697,55 @@ struct Engine {
         return total;
     }
 
+    // edsbwt_prepare: the setup a host-memory batch of ~text_bytes bytes / npat lines would otherwise
+    // pay inside its first call — the pipeline's threads, streams and copy-engine agents, every
+    // slot's page-locked and device buffers at this batch's chunk sizes, the search workspace of a
+    // chunk, and the page-locked record arena (records_hint records; 0: 1.25 per line) — done by one
+    // run of the same pipeline over SYNTHETIC lines of the batch's mean length (random symbols of
+    // the index's alphabet: nothing of the caller's batch is searched, and its results are dropped).
+    // The reference does the index load and M_LF setup before its clock (MOVE_EDSBWTSearch.cpp:23-95,
+    // 109); this is the same for the GPU pipeline, so the first real call runs at steady state.
+    void prepare_lines(uint64_t text_bytes, uint64_t npat, uint64_t records_hint, uint32_t flags) {
+        if (!npat || !text_bytes) return;
+        const uint64_t L = std::max<uint64_t>(1, std::min<uint64_t>(255, (text_bytes + npat - 1) / npat - 1));
+        const uint64_t nsyn = std::min<uint64_t>(npat, std::max<uint64_t>(1, text_bytes / (L + 1)));
+        const uint64_t nb = nsyn * (L + 1);
+        uint8_t* text = nullptr;
+        uint32_t* counts = nullptr;
+        if (hipHostMalloc((void**)&text, nb, hipHostMallocDefault) != hipSuccess) throw Fail(EDSBWT_E_NOMEM, "hipHostMalloc (prepare)");
+        if (hipHostMalloc((void**)&counts, nsyn * 4, hipHostMallocDefault) != hipSuccess) {
+            (void)hipHostFree(text);
+            throw Fail(EDSBWT_E_NOMEM, "hipHostMalloc (prepare)");
+        }
+        struct Free {
+            void* a;
+            void* b;
+            ~Free() { (void)hipHostFree(a); (void)hipHostFree(b); }
+        } fr{text, counts};
+        // random symbols of the alphabet (alpha[1..sigma-1]; alpha[0] is '#'), one xorshift per line
+        const uint32_t B = std::max(1u, sigma - 1);
+        pipe_init();
+        const unsigned T = (unsigned)std::min<uint64_t>(pool.size(), std::max<uint64_t>(1, nsyn >> 16));
+        pool.run(T, [&](unsigned t) {
+            for (uint64_t i = nsyn * t / T; i < nsyn * (t + 1) / T; i++) {
+                uint64_t x = 0x9E3779B97F4A7C15ull * (i + 1);
+                uint8_t* q = text + i * (L + 1);
+                for (uint64_t j = 0; j < L; j++) {
+                    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                    q[j] = alpha[1 + (uint32_t)(x % B)];
+                }
+                q[L] = '\n';
+            }
+        });
+        edsbwt_occ* occ = nullptr;
+        uint64_t np = 0;
+        search_host(text, nb, nullptr, 0, true, 1, flags & (EDSBWT_LOCATE | EDSBWT_COUNT_ONLY | EDSBWT_LOCATE_TABLE), counts, nsyn, &occ, &np);
+        if (occ) arena_checkin();  // (the synthetic records are dropped: the arena stays the engine's)
+        const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
+        if (locate) arena_ensure(records_hint ? records_hint : npat + npat / 4);
+        st = edsbwt_stats{};
+    }
+
     // The pattern loop of MOVE_EDSBWT (MOVE_EDSBWTSearch.cpp:97-155) over a batch in host memory,
     // timed as SURVEY §8(d) defines patterns/s: from the first H2D of the patterns to the last
     // D2H of counts and records.  lines != 0: `text` is the pattern file as it lies on disk
@@ -4031,6 +4081,12 @@ void Engine::arena_checkout() {
     std::lock_guard<std::mutex> g(R.m);
     R.own[arena] = {this, true};
 }
+void Engine::arena_checkin() {
+    auto& R = occ_registry();
+    std::lock_guard<std::mutex> g(R.m);
+    auto it = R.own.find(arena);
+    if (it != R.own.end()) it->second.second = false;
+}
 bool Engine::arena_checked_out() {
     if (!arena) return false;
     auto& R = occ_registry();
@@ -4313,6 +4369,16 @@ int edsbwt_search_lines(edsbwt_index* idx, const char* text, uint64_t len, uint3
     HIPCHK(hipSetDevice(E.device));
     uint64_t n = E.search_host((const uint8_t*)text, len, nullptr, 0, true, first_pattern_id, flags, counts, counts_cap, occ, npat);
     if (nocc) *nocc = n;
+    return 0;
+    ABI_CATCH
+}
+
+int edsbwt_prepare(edsbwt_index* idx, uint64_t text_bytes, uint64_t npat, uint64_t records_hint, uint32_t flags) {
+    if (!idx) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    Engine& E = *idx->eng;
+    HIPCHK(hipSetDevice(E.device));
+    E.prepare_lines(text_bytes, npat, records_hint, flags);
     return 0;
     ABI_CATCH
 }

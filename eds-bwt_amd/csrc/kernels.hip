@@ -1859,13 +1859,16 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         }
         uint32_t cb[K], ce[K];
         uint32_t cn;
-        if (w.z == kQWide) {
+        // a list start (kQWide / kQNode) or one interval: the only divergent branch on the entry's
+        // kind; wide or node list is the uniform kt1w (a kernel argument).  (A divergent three-way
+        // branch on the kind here made the unbounded build fault — rounds 4 and 5)
+        if (w.z >= kQWide && kt1w) {
             // the list's length, offset and (<= 3 intervals) the intervals themselves from the
             // D-mer's 32-B wide entry, w.w = the D-mer (k_ktab_wide) — one line instead of the nid,
-            // ioff / iend, ib and ie reads below.  (Only producers given the wide table write this
-            // kind; without it the pattern goes to the wide-list walk, which reads its node's list)
-            DBG_CHECK(kt1w != nullptr && w.w <= X.kt_E, dbg_w);
-            if (!kt1w || w.w > X.kt_E) { flag_push(ovf, (uint32_t)i); continue; }
+            // ioff / iend, ib and ie reads below.  Producers given the wide table write kQWide;
+            // another kind, or a D-mer past the table, goes to the wide-list walk (node lists)
+            DBG_CHECK(w.z == kQWide && w.w <= X.kt_E, dbg_w);
+            if (w.z != kQWide || w.w > X.kt_E) { flag_push(ovf, (uint32_t)i); continue; }
             const uint4 a0 = kt1w[2 * (size_t)w.w], a1 = kt1w[2 * (size_t)w.w + 1];
             n_blk++;
             cn = a0.y;
@@ -1882,7 +1885,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 cb[t] = !on ? 0u : inl && t < kWideInline ? lb[t < kWideInline ? t : 0] : ib[a0.x + t];
                 ce[t] = !on ? 0u : inl && t < kWideInline ? le[t < kWideInline ? t : 0] : ie[a0.x + t];
             }
-        } else if (w.z == kQNode) {  // from the node's items at the cutover depth
+        } else if (w.z >= kQWide) {  // from the node's items at the cutover depth
+            DBG_CHECK(w.z == kQNode, dbg_q);
             const uint32_t u = nid[i];
             cn = iend[u] - ioff[u];
             n_blk += 4;  // nid, ioff / iend, and the list's lines in ib and ie

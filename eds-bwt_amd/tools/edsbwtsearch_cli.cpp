@@ -212,9 +212,23 @@ int main(int argc, char** argv) {
     FILE* fo = std::fopen(out.c_str(), "wb");
     if (!fo) return fail(("ERROR opening file " + out + " to write output").c_str());
     std::fputs(legacy ? "#Pat\t$_i\tD[i]\tS_j\tS_j[r]\n" : "#Pat\t$_i\tD[i]\tS_j\tS_j[r] \n", fo);
-    const auto t0 = std::chrono::steady_clock::now();
     const uint32_t flags = count_only ? EDSBWT_COUNT_ONLY
                                       : (EDSBWT_LOCATE | (table ? EDSBWT_LOCATE_TABLE : 0) | (legacy ? EDSBWT_LEGACY_ORDER : 0));
+    // setup before the clock, as the reference loads its index and M_LF before :109: each device's
+    // pipeline, buffers and record arena sized for its shard (edsbwt_prepare: synthetic lines of the
+    // shard's mean length, none of the pattern file's)
+    if (std::getenv("EDSBWT_CLI_NO_PREPARE") == nullptr) {
+        each(N, [&](size_t k) {
+            Shard& x = sh[k];
+            if (x.nlines && edsbwt_prepare(x.idx, x.b1 - x.b0, x.nlines, 0, flags)) { x.rc = -1; x.err = edsbwt_last_error(); }
+        });
+        for (auto& x : sh)
+            if (x.rc) {
+                std::fclose(fo);
+                return fail(x.err.c_str());
+            }
+    }
+    const auto t0 = std::chrono::steady_clock::now();
     // the pattern loop: every shard's lines on its own device, concurrently
     each(N, [&](size_t k) {
         Shard& x = sh[k];

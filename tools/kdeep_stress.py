@@ -122,6 +122,7 @@ def main() -> int:
                 old = {k: os.environ.get(k) for k in envs}
                 os.environ.update(envs)
                 buf, offs, oc, oo = ref[name]
+                print(f"[kdeep_stress] build {b} case {name}", flush=True)
                 try:
                     with eb.Index(base) as idx:
                         for kw in VARIANTS:
@@ -131,6 +132,10 @@ def main() -> int:
                                 except eb.EdsBwtError as e:
                                     report["errors"].append({"build": b, "case": name, "kw": kw, "rep": r, "error": str(e)})
                                     print("ERROR", b, name, kw, r, e, flush=True)
+                                    if e.code == -4:  # a device fault: nothing more runs on this GPU
+                                        if a.out:
+                                            open(a.out, "w").write(json.dumps(report, indent=1))
+                                        os._exit(3)
                                     continue
                                 report["runs"] += 1
                                 okc = np.array_equal(gc, oc)
