@@ -533,6 +533,9 @@ struct Engine {
     // 1: the unbounded builds (k_deep<4, 3, 1>, <4, 4, 1>, the '#'-row link rows' <4, 3, 1, true>) —
     // every build is run through the parity tests (tests/test_gpu_parity.py::test_k_deep_builds_gpu)
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 5);
+    // k_deep takes two characters per rank entry when no interval of its list meets a link
+    // (rent2, as k_deep_direct; EDSBWT_DEEPQ_PAIRS=0: one character per step)
+    uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -1780,7 +1783,7 @@ struct Engine {
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
-               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc);
+               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc, deepq_pairs);
         tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;

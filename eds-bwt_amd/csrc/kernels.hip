@@ -1800,7 +1800,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2,
-                                              const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts) {
+                                              const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts, uint32_t qpairs) {
     uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;
     CountSums cs;  // n_blk: occ blocks read (per lane, widened at the end)
 #ifdef EDSBWT_DEBUG_CHECKS
@@ -1909,7 +1909,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
 #endif
         SymReader<BPS> sym{k0, krest, P, pi};
         auto code_at = [&](uint32_t dd) -> uint32_t { return q2 ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };
-        bool over = false, posres = false;
+        bool over = false, posres = false, pskip = false;
         for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
             if (X.rtext && X.text_deep && cn == 1 && cb[0] == ce[0]) {
@@ -1979,6 +1979,65 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             const uint32_t code = code_at(d);
             if (code >= X.sigma) { cn = 0; break; }
             const uint32_t c = code;
+            // two characters at once (qpairs, rent2): one pair entry per interval end gives the rank
+            // of (c, c2) and of the rows coded '#' or (c, '#'); when no interval holds such a row,
+            // neither step links (MOVE_EDSBWTSearch.cpp:512-563 is not reached) and every interval
+            // maps to [PC[p] + rank_p(b), PC[p] + rank_p(e + 1)) — DESIGN.md §3.  Else (or after a
+            // failed try: pskip) one step as below.  The list order is kept, so merges are the same
+            if (qpairs && X.rent2 && !pskip && d + 1 < L) {
+                const uint32_t c2 = code_at(d + 1);
+                if (c2 != 0 && c2 < X.sigma) {
+                    const uint32_t p = 1 + (c - 1) * X.sigma + c2;
+                    uint32_t pb[K], pe[K];
+                    bool clean = true;
+#pragma unroll
+                    for (int j = 0; j < K; j++) {
+                        pb[j] = pe[j] = 0;
+                        if ((uint32_t)j < cn) {
+                            const uint32_t x0r = cb[j], x1r = ce[j] + 1;
+                            const uint4 v0 = X.rent2[(size_t)(x0r >> 5) * X.r2stride + p - 1];
+                            const uint4 v1 = X.rent2[(size_t)(x1r >> 5) * X.r2stride + p - 1];
+                            uint32_t h0, h1;
+                            rent_rank(v0, x0r, pb[j], h0);
+                            rent_rank(v1, x1r, pe[j], h1);
+                            n_blk += (x0r >> 5) == (x1r >> 5) ? 1 : 2;
+                            clean = clean && h0 == h1;
+                        }
+                    }
+                    if (clean) {
+                        uint32_t nn = 0, last_e = 0;
+                        uint32_t nb[K], ne[K];
+#pragma unroll
+                        for (int t = 0; t < K; t++) nb[t] = ne[t] = 0;
+#pragma unroll
+                        for (int j = 0; j < K; j++) {
+                            if ((uint32_t)j < cn && pe[j] > pb[j]) {
+                                const uint32_t b2 = X.PC[p] + pb[j], e2 = X.PC[p] + pe[j] - 1;
+                                if (nn && b2 == last_e + 1) {
+#pragma unroll
+                                    for (int t = 0; t < K; t++)
+                                        if ((uint32_t)t + 1 == nn) ne[t] = e2;
+                                } else {
+#pragma unroll
+                                    for (int t = 0; t < K; t++)
+                                        if ((uint32_t)t == nn) { nb[t] = b2; ne[t] = e2; }
+                                    nn++;
+                                }
+                                last_e = e2;
+                            }
+                        }
+                        n_steps += 2 * cn;
+                        cn = nn;
+#pragma unroll
+                        for (int t = 0; t < K; t++) { cb[t] = nb[t]; ce[t] = ne[t]; }
+                        d++;  // (and the loop's d++: both characters consumed)
+                        continue;
+                    }
+                    pskip = true;
+                }
+            } else {
+                pskip = false;
+            }
             // ranks at both ends of every current interval: '#'-rows (link) and c (step)
             uint32_t sb[K], se[K], raw[K], rawk[EOFROW ? K : 1];  // rawk: a '#'-rank of raw's segment (its eofrow line)
             uint32_t rn = 0;

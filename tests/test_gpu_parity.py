@@ -72,10 +72,11 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
     # the dollar step's text-item entries, k_deep's other dispatched build (6 waves per SIMD), the
     # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
-    # counts instead of per-tile record offsets, and the locate kernel's own counts
+    # counts instead of per-tile record offsets, the locate kernel's own counts, and k_deep one
+    # character per step (no pair entries)
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "6"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
-                     ("EDSBWT_LOCATE_COUNTS", "1")):
+                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -421,6 +422,7 @@ def test_pair_blocks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     that meet '#' rows after the first — identical counts, records and step counts with
     the pair blocks on and off, and equal to the oracle."""
     monkeypatch.setenv("EDSBWT_TRIPLES", "1")  # three-step entries too (off by default)
+    monkeypatch.setenv("EDSBWT_DEEPQ_PAIRS", "0")  # (k_deep's pair steps count a list's two steps at once)
     rng = random.Random(355)
     segs = _covid_like(rng, 800)
     if any(w == "" for w in segs[1]):
