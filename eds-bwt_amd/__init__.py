@@ -61,7 +61,8 @@ class _Info(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_uint64), ("n_words", ctypes.c_uint64), ("n_segments", ctypes.c_uint64),
                 ("sigma", ctypes.c_uint32), ("alphabet", ctypes.c_uint8 * 16), ("device_bytes", ctypes.c_uint64),
                 ("ktab_depth", ctypes.c_uint32), ("pair_blocks", ctypes.c_uint32), ("ktab_items", ctypes.c_uint64),
-                ("ltab_depth", ctypes.c_uint32), ("ltab_groups", ctypes.c_uint32), ("ltab_items", ctypes.c_uint64)]
+                ("ltab_depth", ctypes.c_uint32), ("ltab_groups", ctypes.c_uint32), ("ltab_items", ctypes.c_uint64),
+                ("open_peak_bytes", ctypes.c_uint64), ("open_seconds", ctypes.c_double)]
 
 
 class _Stats(ctypes.Structure):
@@ -248,6 +249,7 @@ class Index:
         self.ktab_depth, self.ktab_items = inf.ktab_depth, inf.ktab_items
         self.ltab_depth, self.ltab_groups, self.ltab_items = inf.ltab_depth, inf.ltab_groups, inf.ltab_items
         self.pair_blocks = bool(inf.pair_blocks)
+        self.open_peak_bytes, self.open_seconds = inf.open_peak_bytes, inf.open_seconds
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -74,6 +74,18 @@ static inline int cub_n(uint64_t n) {
             throw Fail(EDSBWT_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));          \
     } while (0)
 
+// device bytes the engines' DBufs hold (this process), and the most held at once since the last
+// reset: index_open reports the peak of its builds (edsbwt_index_info::open_peak_bytes)
+struct DevMem {
+    static inline std::atomic<uint64_t> live{0}, peak{0};
+    static void add(uint64_t n) {
+        const uint64_t v = live.fetch_add(n) + n;
+        uint64_t p = peak.load();
+        while (v > p && !peak.compare_exchange_weak(p, v)) {}
+    }
+    static void sub(uint64_t n) { live.fetch_sub(n); }
+};
+
 template <class T>
 struct DBuf {
     T* p = nullptr;
@@ -89,13 +101,14 @@ struct DBuf {
     ~DBuf() { release(); }  // index_close frees the HBM the index and its workspace hold
     void ensure(size_t n) {
         if (n <= cap && p) return;
-        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        if (p) { (void)hipFree(p); DevMem::sub(cap * sizeof(T)); p = nullptr; cap = 0; }
         size_t c = std::max<size_t>(n, 1024);
         if (hipMalloc(&p, c * sizeof(T)) != hipSuccess) {
             p = nullptr;
             throw Fail(EDSBWT_E_NOMEM, "hipMalloc of " + std::to_string(c * sizeof(T)) + " bytes failed");
         }
         cap = c;
+        DevMem::add(c * sizeof(T));
         if (poison()) { (void)hipMemsetD32((hipDeviceptr_t)p, poison_value(), c * sizeof(T) / 4); (void)hipDeviceSynchronize(); }
     }
     // EDSBWT_POISON=<u32> (debugging): fresh allocations are filled with that 32-bit word
@@ -119,16 +132,21 @@ struct DBuf {
         T* q = nullptr;
         if (hipMalloc(&q, c * sizeof(T)) != hipSuccess) throw Fail(EDSBWT_E_NOMEM, "hipMalloc (grow) failed");
         if (poison()) { (void)hipMemsetD32((hipDeviceptr_t)q, poison_value(), c * sizeof(T) / 4); (void)hipDeviceSynchronize(); }
+        DevMem::add(c * sizeof(T));
         if (p) {
             HIPCHK(hipMemcpyAsync(q, p, cap * sizeof(T), hipMemcpyDeviceToDevice, s));
             HIPCHK(hipStreamSynchronize(s));
             (void)hipFree(p);
+            DevMem::sub(cap * sizeof(T));
         }
         p = q;
         cap = c;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            DevMem::sub(cap * sizeof(T));
+        }
         p = nullptr;
         cap = 0;
     }
@@ -165,6 +183,11 @@ constexpr double kKtabItems = 268435456.0;  // at least 2^28 intervals (2 GiB) .
 constexpr double kKtabHbmShare = 0.15;      // ... or as many as kKtabHbmShare of the free HBM holds at
 constexpr double kKtabBuildBytes = 40.0;    // the build's transient bytes per interval (capture + sort)
 constexpr uint32_t kKtabMinDepth = 2;
+// the whole-table walk's transient bytes per K-mer (the trie of B^K patterns: keys, sort buffers,
+// nodes, items of two depths) and the share of the free HBM it may take before the table is built
+// group by group (build_ktab_grouped: C3's 4^15 15-mers in 16 walks of 4^13)
+constexpr double kKtabWalkBytes = 100.0;
+constexpr double kKtabWalkShare = 0.25;
 // the wide k-mer entries (32 B per D-mer) are built when the free HBM exceeds this many times their bytes
 constexpr double kKt1WideHbmShare = 2.5;
 // per-'#'-row link rows (KIdx::eofrow) up to this size (C3 243 MB; C5's 264M words would take 17 GB: not built)
@@ -298,6 +321,7 @@ struct Engine {
         uint32_t K = 0, B = 0;
         uint64_t budget = 0;
         bool only_last = false;  // keep depth K's items only (the level table's groups)
+        uint32_t reached = 0;    // deepest depth whose items stayed within the budget
         uint32_t depth = 0;
         uint64_t n = 0;
         DBuf<uint32_t> k, b, e;
@@ -869,6 +893,9 @@ struct Engine {
 
     // ------------------------------------------------------------ index
     void open(const std::string& base, int dev) {
+        const auto t_open = std::chrono::steady_clock::now();
+        const uint64_t live0 = DevMem::live.load();
+        DevMem::peak.store(live0);
         device = dev;
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -1023,7 +1050,14 @@ struct Engine {
         build_segtext();
         // after the per-row entries: the level table's budget is a share of what HBM has left
         build_ltab();
+        open_peak_bytes = DevMem::peak.load() - live0;
+        open_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_open).count();
+        if (trace)
+            std::fprintf(stderr, "[edsbwt] index open: %.2f s, %llu device bytes held, peak %llu while building\n", open_seconds,
+                         (unsigned long long)device_bytes, (unsigned long long)open_peak_bytes);
     }
+    uint64_t open_peak_bytes = 0;  // DevMem peak over this open (tables + transient build workspace)
+    double open_seconds = 0;
 
     // Deep level start table: when the k-mer start table stopped shallow because its lists are
     // long (C5: depth 3, 0.87G intervals; the items per depth then grow ~1.6x per depth up to
@@ -1290,53 +1324,77 @@ struct Engine {
         const double over = env_double("EDSBWT_KTAB_OVER", kKtabOver);
         while (K > 2 && (pw(K) > max_entries || (double)pw(K - 1) > over * (double)N)) K--;
         if (pw(K) > max_entries) return;
-        const uint64_t P = pw(K);
-        DBuf<uint8_t> kb;
-        DBuf<uint64_t> ko;
-        kb.ensure(P * K);
-        ko.ensure(P + 1);
         uint64_t sym = 0;
         for (uint32_t v = 0; v < B; v++) sym |= (uint64_t)alpha[v + 1] << (8 * v);
-        launch(KC_TABLE, k_kmer_batch, P, P, K, B, sym, kb.p, ko.p, (uint64_t)1, (uint64_t)0);
-        res.ensure(P); ovf_orig.ensure(P);
-        zero(stats.p, kStatSlots * 8);
-        Capture c;
-        c.K = K; c.B = B; c.budget = budget;
-        cap = &c;
-        const bool was_count_only = count_only;
-        count_only = true;
-        uint64_t abase = 0;
-        try {
-            levels2(kb.p, ko.p, P, false, res.p, abase, ovf_orig.p);
-        } catch (const TooBig&) {
-            // a depth past the budget outgrew 32-bit counts: keep what was captured
+        // the walk over all B^K K-mers at once keeps ~kKtabWalkBytes per K-mer of transient workspace
+        // (C3: 4^15 K-mers, > 100 GB): when that passes kKtabWalkShare of the free HBM the table is
+        // built in B^2 groups (build_ktab_grouped); a group walk that outgrows the budget names the
+        // depth it reached, and the whole-table walk runs there (C5: depth 3)
+        uint32_t depth = 0;
+        uint64_t n = 0;
+        // (EDSBWT_KTAB_GROUPED: 0 never, 2 always — tests — else by the workspace estimate)
+        const double gmode = env_double("EDSBWT_KTAB_GROUPED", 1);
+        const bool grouped = B >= 2 && K >= 4 && gmode != 0 &&
+                             (gmode == 2 || (double)pw(K) * kKtabWalkBytes > kKtabWalkShare * (double)free_b);
+        if (grouped) {
+            const uint32_t r = build_ktab_grouped(K, budget, sym);
+            if (r == K) {
+                depth = K;
+                n = ktab_items;
+            } else {
+                K = std::max(2u, r);
+            }
         }
-        cap = nullptr;
-        count_only = was_count_only;
-        st = edsbwt_stats{};
-        HIPCHK(hipStreamSynchronize(stream));
-        if (c.depth < kKtabMinDepth || c.n == 0) {
-            release_workspace();
-            return;
+        if (!depth) {
+            const uint64_t P = pw(K);
+            DBuf<uint8_t> kb;
+            DBuf<uint64_t> ko;
+            kb.ensure(P * K);
+            ko.ensure(P + 1);
+            launch(KC_TABLE, k_kmer_batch, P, P, K, B, sym, kb.p, ko.p, (uint64_t)1, (uint64_t)0);
+            res.ensure(P); ovf_orig.ensure(P);
+            zero(stats.p, kStatSlots * 8);
+            Capture c;
+            c.K = K; c.B = B; c.budget = budget;
+            cap = &c;
+            const bool was_count_only = count_only;
+            count_only = true;
+            uint64_t abase = 0;
+            try {
+                levels2(kb.p, ko.p, P, false, res.p, abase, ovf_orig.p);
+            } catch (const TooBig&) {
+                // a depth past the budget outgrew 32-bit counts: keep what was captured
+            }
+            cap = nullptr;
+            count_only = was_count_only;
+            st = edsbwt_stats{};
+            HIPCHK(hipStreamSynchronize(stream));
+            if (c.depth < kKtabMinDepth || c.n == 0) {
+                release_workspace();
+                return;
+            }
+            const uint64_t E = pw(c.depth);
+            n = c.n;
+            DBuf<uint64_t> k1, k2;
+            DBuf<uint32_t> e2;
+            k1.ensure(n); k2.ensure(n); e2.ensure(n);
+            launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
+            size_t tb = 0;
+            const int endbit = 32 + (int)bits_for(E);
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+            tmp.ensure(tb);
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+            sync_check(nullptr, "hipcub call in build_ktab");
+            ktab_off.ensure(E + 2);  // [E, E+1): the empty list of D-mers outside the alphabet (direct start)
+            ktab_b.ensure(n);
+            ktab_e.ensure(n);
+            launch(KC_TABLE, k_ktab_bounds, E + 1, E, (const uint64_t*)k2.p, n, ktab_off.p);
+            HIPCHK(hipMemcpyAsync(ktab_off.p + E + 1, ktab_off.p + E, 4, hipMemcpyDeviceToDevice, stream));
+            launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, ktab_b.p);
+            HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+            depth = c.depth;
         }
-        const uint64_t E = pw(c.depth), n = c.n;
-        DBuf<uint64_t> k1, k2;
-        DBuf<uint32_t> e2;
-        k1.ensure(n); k2.ensure(n); e2.ensure(n);
-        launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
-        size_t tb = 0;
-        const int endbit = 32 + (int)bits_for(E);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
-        tmp.ensure(tb);
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
-        sync_check(nullptr, "hipcub call at engine.hip:624");
-        ktab_off.ensure(E + 2);  // [E, E+1): the empty list of D-mers outside the alphabet (direct start)
-        ktab_b.ensure(n);
-        ktab_e.ensure(n);
-        launch(KC_TABLE, k_ktab_bounds, E + 1, E, (const uint64_t*)k2.p, n, ktab_off.p);
-        HIPCHK(hipMemcpyAsync(ktab_off.p + E + 1, ktab_off.p + E, 4, hipMemcpyDeviceToDevice, stream));
-        launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, ktab_b.p);
-        HIPCHK(hipMemcpyAsync(ktab_e.p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+        const uint64_t E = pw(depth);
         if (N < 0x80000000u) {  // inline single intervals need bit 63 free
             kt1_pos = have_text && gpos.p && N < 0x40000000u && tlen < 0x80000000ull && env_double("EDSBWT_KT1_POS", 1) != 0;
             // the wide form when a one-row entry can carry its sample and text window (dense
@@ -1361,13 +1419,118 @@ struct Engine {
             }
         }
         HIPCHK(hipStreamSynchronize(stream));
-        ktab_depth = c.depth;
+        ktab_depth = depth;
         ktab_items = n;
         ktab_entries = E;
         device_bytes += (E + 1) * 4 + n * 8;
         release_workspace();
         if (trace) std::fprintf(stderr, "[edsbwt] k-mer start table: depth %u, %llu D-mers, %llu intervals\n", ktab_depth,
                                 (unsigned long long)E, (unsigned long long)n);
+    }
+
+    // The k-mer start table at depth K in G = B^2 groups — the K-mers sharing their last two
+    // characters, one level walk of B^K / G patterns each (k_kmer_batch with stride G), captured at
+    // depth K and sorted by (D-mer, row) per group — then concatenated into the table's layout
+    // (k_ktab_group_lens, a scan, k_ktab_group_copy): the same table as the whole-table walk's, with
+    // 1/G of its transient workspace.  Returns K when built; else the deepest depth the failing
+    // group's walk reached within its share of the budget (nothing built).
+    uint32_t build_ktab_grouped(uint32_t K, uint64_t budget, uint64_t sym) {
+        const uint32_t B = sigma - 1;
+        auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
+        const uint32_t G = (uint32_t)pw(2);
+        const uint64_t E = pw(K), EG = E / G;
+        // a group walk past 2/G of the budget at any depth ends the attempt (the groups are alike)
+        const uint64_t gbudget = std::max<uint64_t>(1, 2 * budget / G);
+        DBuf<uint32_t> goff;
+        goff.ensure((size_t)G * (EG + 1));
+        std::vector<DBuf<uint32_t>> gb(G), ge(G);
+        uint64_t tot = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t g = 0; g < G; g++) {
+            Capture c;
+            {
+                DBuf<uint8_t> kb;
+                DBuf<uint64_t> ko;
+                kb.ensure(EG * K);
+                ko.ensure(EG + 1);
+                launch(KC_TABLE, k_kmer_batch, EG, EG, K, B, sym, kb.p, ko.p, (uint64_t)G, (uint64_t)g);
+                res.ensure(EG); ovf_orig.ensure(EG);
+                zero(stats.p, kStatSlots * 8);
+                c.K = K; c.B = B; c.only_last = true; c.budget = gbudget;
+                cap = &c;
+                const bool was_count_only = count_only;
+                count_only = true;
+                uint64_t abase = 0;
+                try {
+                    levels2(kb.p, ko.p, EG, false, res.p, abase, ovf_orig.p);
+                } catch (const TooBig&) {
+                    c.depth = 0;
+                }
+                cap = nullptr;
+                count_only = was_count_only;
+                st = edsbwt_stats{};
+                HIPCHK(hipStreamSynchronize(stream));
+            }
+            tot += c.n;
+            if (c.depth != K || (double)tot > (double)budget) {
+                if (trace) std::fprintf(stderr, "[edsbwt] k-mer table depth %u, group %u: reached depth %u within %llu items\n", K, g,
+                                        c.reached, (unsigned long long)gbudget);
+                release_workspace();
+                return std::min(c.reached, K - 1);
+            }
+            const uint64_t n = c.n;
+            gb[g].ensure(n);
+            ge[g].ensure(n);
+            uint32_t* go = goff.p + (size_t)g * (EG + 1);
+            if (n) {
+                DBuf<uint64_t> k1, k2;
+                DBuf<uint32_t> e2;
+                k1.ensure(n); k2.ensure(n); e2.ensure(n);
+                launch(KC_TABLE, k_ktab_keys, n, n, (const uint32_t*)c.k.p, (const uint32_t*)c.b.p, k1.p);
+                c.k.release(); c.b.release();
+                size_t tb = 0;
+                const int endbit = 32 + (int)bits_for(EG);
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+                tmp.ensure(tb);
+                HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k1.p, k2.p, c.e.p, e2.p, cub_n(n), 0, endbit, stream));
+                sync_check(nullptr, "hipcub call in build_ktab_grouped");
+                k1.release();
+                c.e.release();
+                launch(KC_TABLE, k_ktab_split, n, n, (const uint64_t*)k2.p, gb[g].p);
+                HIPCHK(hipMemcpyAsync(ge[g].p, e2.p, n * 4, hipMemcpyDeviceToDevice, stream));
+                launch(KC_TABLE, k_ktab_bounds, EG + 1, EG, (const uint64_t*)k2.p, n, go);
+                HIPCHK(hipStreamSynchronize(stream));
+            } else {
+                zero(go, (EG + 1) * 4);
+            }
+        }
+        release_workspace();
+        // the groups' lists in D-mer order: lengths, their scan (the table's offsets), the copy
+        std::vector<const uint32_t*> pb(G), pe(G);
+        for (uint32_t g = 0; g < G; g++) { pb[g] = gb[g].p; pe[g] = ge[g].p; }
+        DBuf<const uint32_t*> dpb, dpe;
+        dpb.ensure(G); dpe.ensure(G);
+        HIPCHK(hipMemcpy(dpb.p, pb.data(), G * sizeof(void*), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dpe.p, pe.data(), G * sizeof(void*), hipMemcpyHostToDevice));
+        DBuf<uint32_t> len;
+        len.ensure(E);
+        launch(KC_TABLE, k_ktab_group_lens, E, E, G, EG, (const uint32_t*)goff.p, len.p);
+        ktab_off.ensure(E + 2);  // [E, E+1): the empty list of D-mers outside the alphabet (direct start)
+        const uint32_t n = scan_u32(len.p, ktab_off, E);
+        len.release();
+        if ((uint64_t)n != tot) throw Fail(EDSBWT_E_DEVICE, "k-mer table groups: list total mismatch");
+        HIPCHK(hipMemcpyAsync(ktab_off.p + E + 1, ktab_off.p + E, 4, hipMemcpyDeviceToDevice, stream));
+        ktab_b.ensure(std::max<uint64_t>(tot, 1));
+        ktab_e.ensure(std::max<uint64_t>(tot, 1));
+        launch(KC_TABLE, k_ktab_group_copy, E, E, G, EG, (const uint32_t*)goff.p, (const uint32_t* const*)dpb.p,
+               (const uint32_t* const*)dpe.p, (const uint32_t*)ktab_off.p, ktab_b.p, ktab_e.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        ktab_items = tot;
+        if (trace)
+            std::fprintf(stderr, "[edsbwt] k-mer start table built in %u groups of %llu K-mers: %llu intervals in %.2f s\n", G,
+                         (unsigned long long)EG, (unsigned long long)tot,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        return K;
     }
 
     // Locate samples: one (word, offset) per row whose offset in its word is a multiple
@@ -2351,6 +2514,7 @@ struct Engine {
             }
             if (cap) {  // table build: keep this depth's items as (D-mer, b, e) while they fit
                 if (nnext > cap->budget) break;
+                cap->reached = D;
                 if (cap->only_last && D < cap->K) {  // the level table keeps depth K only
                     if (nnext == 0) { cap->depth = cap->K; cap->n = 0; break; }  // no K-mer of this group occurs
                     cur = nxt;
@@ -4313,6 +4477,8 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
     info->ltab_depth = E.lt_depth;
     info->ltab_groups = E.lt_G;
     info->ltab_items = E.lt_items;
+    info->open_peak_bytes = E.open_peak_bytes;
+    info->open_seconds = E.open_seconds;
     info->pair_blocks = E.rent2.p != nullptr;
     return 0;
 }

@@ -3922,6 +3922,31 @@ __global__ void k_ktab_keys(uint64_t n, const uint32_t* __restrict__ km, const u
     GRID_STRIDE(t, n) key[t] = (uint64_t)km[t] << 32 | b[t];
 }
 
+// the k-mer start table built group by group (engine.hip build_ktab_grouped): group g holds the
+// D-mers x = xl * G + g (the D-mers sharing their last two characters) with its own offsets
+// goff[g * (EG + 1) + xl] into its lists pb[g] / pe[g].  len[x] = D-mer x's list length; then each
+// D-mer's list copied to the table's layout at off[x] (the exclusive scan of len)
+__global__ void k_ktab_group_lens(uint64_t E, uint32_t G, uint64_t EG, const uint32_t* __restrict__ goff, uint32_t* __restrict__ len) {
+    GRID_STRIDE(x, E) {
+        const uint64_t g = x % G, xl = x / G;
+        const uint32_t* o = goff + g * (EG + 1) + xl;
+        len[x] = o[1] - o[0];
+    }
+}
+__global__ void k_ktab_group_copy(uint64_t E, uint32_t G, uint64_t EG, const uint32_t* __restrict__ goff,
+                                  const uint32_t* const* __restrict__ pb, const uint32_t* const* __restrict__ pe,
+                                  const uint32_t* __restrict__ off, uint32_t* __restrict__ b, uint32_t* __restrict__ e) {
+    GRID_STRIDE(x, E) {
+        const uint64_t g = x % G, xl = x / G;
+        const uint32_t* o = goff + g * (EG + 1) + xl;
+        const uint32_t a = o[0], n = o[1] - o[0], to = off[x];
+        for (uint32_t t = 0; t < n; t++) {
+            b[to + t] = pb[g][a + t];
+            e[to + t] = pe[g][a + t];
+        }
+    }
+}
+
 // off[x] = first item of D-mer x in the sorted keys (off[E] = n)
 __global__ void k_ktab_bounds(uint64_t E, const uint64_t* __restrict__ key, uint64_t n, uint32_t* __restrict__ off) {
     GRID_STRIDE(x, E + 1) {

@@ -85,6 +85,10 @@ typedef struct {
     uint32_t ltab_depth;  /* deep level start table (C5-like indexes): its depth L, 0 = none */
     uint32_t ltab_groups; /* ... kept in groups by the L-mer's last characters */
     uint64_t ltab_items;  /* intervals held by it */
+    uint64_t open_peak_bytes; /* most device memory the engine held at once while opening (tables +
+                                 their builds' transient workspace): the per-rank HBM a deployment
+                                 that opens several indexes on one GPU must leave for each open */
+    double open_seconds;      /* wall time of edsbwt_index_open */
 } edsbwt_index_info;
 
 /* Per-call counters and timings (filled by every edsbwt_search*). */

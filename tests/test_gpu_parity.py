@@ -1232,3 +1232,49 @@ def test_prepare_then_search_lines_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             idx.prepare(0, 0)
             gc3, go3 = _lines_search(edsbwt, idx, text)
             assert np.array_equal(gc3, oc) and np.array_equal(go3, oo)
+
+
+@pytest.mark.parametrize("shape", ["covid", "c5"])
+def test_kmer_table_grouped_build_gpu(oracle, edsbwt, tmp_path, monkeypatch, shape):
+    """The k-mer start table built group by group (engine.hip build_ktab_grouped: the K-mers
+    sharing their last two characters walked together, their lists concatenated into the table's
+    layout; C3's production table is built this way so its transient workspace is 1/16 of the
+    whole-table walk's) equals the whole-table walk's: same depth, intervals and device bytes, and
+    searches through it equal the oracle — direct start and trie start, located and count-only.
+    On a C5-shaped EDS with a small interval budget the group walk outgrows its share and the
+    build falls back to the whole-table walk at the depth the group reached."""
+    rng = random.Random(77 if shape == "covid" else 78)
+    if shape == "covid":
+        segs = _covid_like(rng, 500)
+        if any(w == "" for w in segs[1]):
+            segs[1] = ["A"]
+    else:
+        segs = edsgen.random_eds(rng, 4000, kmax=4, lmax=7, p_empty=0.2)
+        monkeypatch.setenv("EDSBWT_KTAB_ITEMS", "20000")
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
+    info = {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("EDSBWT_KTAB_GROUPED", mode)
+        with edsbwt.Index(base) as idx:
+            info[mode] = (idx.ktab_depth, idx.ktab_items, idx.device_bytes)
+            D = idx.ktab_depth
+            assert D >= 2 and idx.open_peak_bytes > 0
+            pats = [edsgen.planted(rng, segs, rng.randint(D + 1, D + 16)) or "ACGT" * 8 for _ in range(1500)]
+            pats += ["".join(rng.choice("ACGT") for _ in range(rng.randint(D + 1, D + 12))) for _ in range(300)]
+            pats += [edsgen.planted(rng, segs, rng.randint(1, D)) or "AC" for _ in range(200)]  # trie start
+            buf, offs = _pack(pats)
+            oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+            for kw in ({}, {"locate": False}):
+                gc, go = idx.search((buf, offs), **kw)
+                assert np.array_equal(gc, oc), (mode, kw)
+                if kw.get("locate", True):
+                    assert np.array_equal(go, oo), (mode, kw)
+            long_ = [p for p in pats if len(p) > D]
+            lb, lo = _pack(long_)
+            lc, loo, _ = oracle.Engine(base, 8).search(lb, lo)
+            gc, go = idx.search((lb, lo))
+            assert idx.stats()["start_depth"] == D
+            assert np.array_equal(gc, lc) and np.array_equal(go, loo)
+    if shape == "covid":
+        assert info["0"] == info["2"], info
