@@ -521,6 +521,7 @@ def main():
                        "dist_backend": args.dist_backend if multi else None,
                        "ktab_depth": idx.ktab_depth, "ltab_depth": idx.ltab_depth, "ltab_items": idx.ltab_items,
                        "index_device_bytes": idx.device_bytes,
+                       "index_open_peak_bytes": getattr(idx, "open_peak_bytes", None),
                        "host_numa_node": numa,
                        # every table the search reads (rank tables, k-mer table, samples) within the 256 MB MALL
                        "cache_resident": bool(idx.device_bytes <= MI355X_MALL_BYTES), "rank_tables_bytes": int(rank_bytes)},
