@@ -562,6 +562,13 @@ struct Engine {
     // 1: the unbounded builds (k_deep<4, 3, 1>, <4, 4, 1>, the '#'-row link rows' <4, 3, 1, true>) —
     // every build is run through the parity tests (tests/test_gpu_parity.py::test_k_deep_builds_gpu)
     int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 5);
+    // locate tasks one wave per pattern when lists average more than kTasksWaveRatio intervals
+    // (EDSBWT_TASKS_WAVE=0: k_tasks, one lane per pattern, always)
+    static constexpr uint64_t kTasksWaveRatio = 8;
+    int tasks_wave = (int)env_double("EDSBWT_TASKS_WAVE", 1);  // (2: always — tests)
+    // located finishers at the level table's start take their archive ranges straight from the
+    // emitted (row-sorted) items (EDSBWT_LT_FIN_DIRECT=0: k_fin_emit + sort, as at other depths)
+    bool lt_fin_direct = env_double("EDSBWT_LT_FIN_DIRECT", 1) != 0;
     // k_deep takes two characters per rank entry when no interval of its list meets a link
     // (rent2, as k_deep_direct; EDSBWT_DEEPQ_PAIRS=0: one character per step)
     uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
@@ -2277,7 +2284,23 @@ struct Engine {
             st.trie_nodes += M0;
             if (trace) std::fprintf(stderr, "[edsbwt] start at depth %u from the level table: nodes %u, items %u\n", d0, M0, n0);
             if (ncur == 0) return 0;
-            if (hist[d0]) {
+            if (hist[d0] && !count_only && lt_fin_direct) {
+                // patterns of length d0 end at the start, and their nodes' lists come out of the
+                // table sorted by row: the items go to the archive as they are (C5's 8-mers:
+                // ~1.5e5 intervals each, which the finisher path would append and radix-sort)
+                node_occ.ensure(M0); foff.ensure(M0); fend.ensure(M0); fin.ensure(M0);
+                launch(KC_FINISH, k_fin_flags, M0, M0, d0, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
+                launch_grid(KC_FINISH, k_fin_lt, (unsigned)std::min<uint64_t>(((uint64_t)M0 + 3) / 4, 65536), M0, (const uint8_t*)fin.p,
+                            (const uint32_t*)kt_pos.p, (const uint32_t*)kt_cnt.p, (const uint32_t*)ib[1].p, (const uint32_t*)ie[1].p,
+                            foff.p, fend.p, node_occ.p);
+                ab.grow_keep(abase + n0, stream);
+                ae.grow_keep(abase + n0, stream);
+                HIPCHK(hipMemcpyAsync(ab.p + abase, ib[1].p, (size_t)n0 * 4, hipMemcpyDeviceToDevice, stream));
+                HIPCHK(hipMemcpyAsync(ae.p + abase, ie[1].p, (size_t)n0 * 4, hipMemcpyDeviceToDevice, stream));
+                launch(KC_FINISH, k_finish2, P, P, d0, (const uint32_t*)slen.p, (const uint32_t*)nid[1].p, (const uint32_t*)perm.p,
+                       (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r);
+                abase += n0;
+            } else if (hist[d0]) {
                 // patterns of length d0 end at the start: their nodes' lists (sorted by row in the
                 // table) are finished as a depth's finishers are — k_fin_emit over the packed items
                 node_occ.ensure(M0); foff.ensure(M0); fend.ensure(M0); fin.ensure(M0);
@@ -2846,9 +2869,23 @@ struct Engine {
             if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
                 blk_first.ensure(OCC / kLocRun + 1);
-                launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, tsc,
-                       (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p,
-                       ~0ull, ~0ull, (uint32_t*)(counters.p + 20));
+                if (TT <= 0x7fffffffull && (tasks_wave == 2 || (tasks_wave == 1 && TT > kTasksWaveRatio * P))) {
+                    // long lists (C5's 8-mers): tasks one wave per pattern, their offsets one scan
+                    tc64.ensure(TT);
+                    launch_grid(KC_LOCPREP, k_tasks_wave, (unsigned)std::min<uint64_t>((P + 3) / 4, 65536), P, (const Res*)res.p, tsc,
+                                (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tc64.p, tpat.p);
+                    size_t tb = 0;
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tc64.p, tout.p, cub_n(TT), stream));
+                    tmp.ensure(tb);
+                    timed(KC_LOCPREP, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, tc64.p, tout.p, cub_n(TT), stream)); });
+                    sync_check(nullptr, "hipcub call (task offsets)");
+                    const uint64_t nblk = (OCC + kLocRun - 1) / kLocRun;
+                    launch(KC_LOCPREP, k_blk_first, nblk, nblk, (const uint64_t*)tout.p, TT, blk_first.p);
+                } else {
+                    launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, tsc,
+                           (const uint64_t*)oscan.p, (const uint32_t*)ab.p, (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p,
+                           ~0ull, ~0ull, (uint32_t*)(counters.p + 20));
+                }
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
                        (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p,

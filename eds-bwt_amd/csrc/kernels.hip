@@ -3041,6 +3041,30 @@ __global__ void k_fin_flags(uint32_t M, uint32_t D, const uint32_t* __restrict__
     GRID_STRIDE(u, M) fin[u] = slen[node_first[u]] == D;
 }
 
+// finishers at the level table's start (patterns of length L, engine.hip levels2): a node's items are
+// [kt_pos[u], + kt_cnt[u]) as k_ltab_emit wrote them, already sorted by row (the table's order), so
+// its archive range is that range (the items copied to the archive whole) and only its occurrence
+// total is summed — one wave per node, no emit, sort or bounds pass
+__global__ void __launch_bounds__(256) k_fin_lt(uint32_t M, const uint8_t* __restrict__ fin, const uint32_t* __restrict__ kt_pos,
+                                                const uint32_t* __restrict__ kt_cnt, const uint32_t* __restrict__ ib,
+                                                const uint32_t* __restrict__ ie, uint32_t* __restrict__ foff, uint32_t* __restrict__ fend,
+                                                uint32_t* __restrict__ node_occ) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t u = w0; u < M; u += nw) {  // (wave-uniform)
+        if (!fin[u]) continue;
+        const uint32_t a = kt_pos[u], n = kt_cnt[u];
+        unsigned long long s = 0;
+        for (uint32_t t = lane; t < n; t += 64) s += (unsigned long long)(ie[a + t] - ib[a + t]) + 1;
+        s = wave_sum(s);
+        if (lane == 0) {
+            foff[u] = a;
+            fend[u] = a + n;
+            node_occ[u] = (uint32_t)s;
+        }
+    }
+}
+
 // per node [off, end) in the sorted finisher keys
 __global__ void k_fin_bounds(uint32_t F, const uint64_t* __restrict__ fk, uint32_t rowbits, uint32_t* __restrict__ foff,
                              uint32_t* __restrict__ fend) {
@@ -3178,6 +3202,44 @@ __global__ void k_tasks(uint64_t P, const Res* __restrict__ res,
             for (uint64_t k = (base + kLocRun - 1) / kLocRun; k * kLocRun < base + len; k++) blk_first[k] = t0 + q;
             base += len;
         }
+    }
+}
+
+// The same tasks for batches whose patterns hold long lists (C5's 8-mers: ~1.5e5 intervals each,
+// which k_tasks walks one lane per pattern): one wave per pattern, its lanes striding over the
+// pattern's intervals — each task's row, pattern and length; the record offsets are then one scan
+// of the lengths (records follow the tasks in order) and k_blk_first finds each record block's
+// first task, so no lane walks a whole list
+__global__ void __launch_bounds__(256) k_tasks_wave(uint64_t P, const Res* __restrict__ res, const uint64_t* __restrict__ tscan,
+                                                    const uint64_t* __restrict__ oscan, const uint32_t* __restrict__ ab,
+                                                    const uint32_t* __restrict__ ae, uint32_t* __restrict__ trow,
+                                                    uint64_t* __restrict__ tlen, uint32_t* __restrict__ tpat) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = w0; i < P; i += nw) {  // (wave-uniform)
+        const uint64_t t0 = tscan ? tscan[i] : (oscan[i] & 0xffffffffull);
+        const Res r = res[i];
+        const uint32_t n = res_cnt(r);
+        const bool direct_row = (r.cnt & kResRow) != 0;
+        for (uint32_t q = lane; q < n; q += 64) {
+            const uint64_t a = r.off + q;
+            const uint32_t row = (r.cnt & kResPos) ? ~0u : direct_row ? (uint32_t)r.off : ab[a];
+            trow[t0 + q] = row;
+            tlen[t0 + q] = direct_row ? (uint64_t)res_occ(r) : (uint64_t)(ae[a] - row) + 1;
+            tpat[t0 + q] = (uint32_t)i;
+        }
+    }
+}
+// blk_first[k] = the task holding record k * kLocRun (tout: the tasks' first records, ascending)
+__global__ void k_blk_first(uint64_t nblk, const uint64_t* __restrict__ tout, uint64_t TT, uint64_t* __restrict__ blk_first) {
+    GRID_STRIDE(k, nblk) {
+        const uint64_t o = k * kLocRun;
+        uint64_t lo = 0, hi = TT;  // last task with tout <= o
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (tout[mid] <= o) lo = mid; else hi = mid;
+        }
+        blk_first[k] = lo;
     }
 }
 

@@ -207,7 +207,10 @@ def test_level_table_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         gs, gso = idx.search((sbuf, soffs))
         assert idx.stats()["start_depth"] == 3
         assert np.array_equal(gs, soc) and np.array_equal(gso, soo)
-    for env in ({"EDSBWT_NO_LTAB": "1"}, {"EDSBWT_FORCE_GROUPS": "2"}, {"EDSBWT_FORCE_GROUPS": "1", "EDSBWT_TEXT_STOP": "32"}):
+    # ... and the located finishers at the table's start through the emit + sort path, locate tasks
+    # one wave per pattern (the path of C5's long 8-mer lists) and one lane per pattern
+    for env in ({"EDSBWT_NO_LTAB": "1"}, {"EDSBWT_FORCE_GROUPS": "2"}, {"EDSBWT_FORCE_GROUPS": "1", "EDSBWT_TEXT_STOP": "32"},
+                {"EDSBWT_LT_FIN_DIRECT": "0"}, {"EDSBWT_TASKS_WAVE": "2"}, {"EDSBWT_TASKS_WAVE": "0", "EDSBWT_LT_FIN_DIRECT": "0"}):
         for k_, v_ in env.items():
             monkeypatch.setenv(k_, v_)
         with edsbwt.Index(base) as idx:
@@ -215,7 +218,7 @@ def test_level_table_gpu(oracle, edsbwt, tmp_path, monkeypatch):
                 gc, go = idx.search((buf, offs), **kw)
                 st = idx.stats()
                 assert st["start_depth"] == (3 if "EDSBWT_NO_LTAB" in env else 6), (env, kw)
-                if "EDSBWT_NO_LTAB" not in env:
+                if "EDSBWT_FORCE_GROUPS" in env:
                     assert st["search_groups"] > 1, (env, kw)
                 assert np.array_equal(gc, oc), (env, kw)
                 if kw.get("locate", True):
