@@ -2937,6 +2937,12 @@ struct Engine {
                 std::fprintf(stderr, "[edsbwt] k_deep_fast: %llu dependent load rounds over the lanes' patterns, %llu lane slots: lane utilisation %.3f\n",
                              (unsigned long long)sv[ST_DF_LANE_ROUNDS], (unsigned long long)sv[ST_DF_WAVE_ROUNDS],
                              (double)sv[ST_DF_LANE_ROUNDS] / (double)sv[ST_DF_WAVE_ROUNDS]);
+            if (trace && (sv[ST_CLK_DD_ONE] | sv[ST_CLK_DD_SROW]))
+                std::fprintf(stderr, "[edsbwt] k_deep_direct loads: one-row D-mer entries %llu, per-row text entries %llu, segment rows %llu, "
+                                     "whole-word rows %llu, rank-entry lines %llu, interval steps %llu, text rows %llu\n",
+                             (unsigned long long)sv[ST_CLK_DD_ONE], (unsigned long long)sv[ST_CLK_DD_SROW], (unsigned long long)sv[ST_CLK_DD_SEG],
+                             (unsigned long long)sv[ST_CLK_DD_WROW], (unsigned long long)sv[ST_DEEP_PAIR_LINES],
+                             (unsigned long long)sv[ST_DEEP_STEPS], (unsigned long long)sv[ST_TEXT_ROWS]);
             if (trace && sv[ST_CLK_STEPS])
                 std::fprintf(stderr, "[edsbwt] k_deep lane-steps %llu (with '#' rows %llu): cycles/step rank+link %.0f, runs %.0f, rest %.0f\n",
                              (unsigned long long)sv[ST_CLK_STEPS], (unsigned long long)sv[ST_CLK_HASH_STEPS],
@@ -3286,7 +3292,10 @@ struct Engine {
     // few of 255 and more as (pattern, count) pairs, and a host thread widens them into the
     // caller's counts while the next chunk downloads: a quarter of the counts' PCIe bytes.
     // EDSBWT_SMALL_COUNTS=0: 4 bytes each.
-    bool small_counts = env_double("EDSBWT_SMALL_COUNTS", 1) != 0;
+    // Only beside records: a count-only call's counts go straight to the caller's page-locked array
+    // as u32 (C2: 4 MB in ~0.07 ms, against 1 MB of bytes plus their widening on the host, ~0.1 ms
+    // and a thread wake-up on the critical path).  EDSBWT_SMALL_COUNTS=0: never, 2: count-only too.
+    int small_counts = (int)env_double("EDSBWT_SMALL_COUNTS", 1);
     static uint64_t c8_bytes(uint64_t P) { return (P + 7) / 8 * 8 + 8; }  // bytes, then the exception count (u32)
     void expand_c8(uint32_t* c, const uint8_t* c8, uint64_t P, const uint2* exc, uint32_t nexc) {
         const unsigned T = (unsigned)std::min<uint64_t>(cpool.size(), std::max<uint64_t>(1, P / 262144));
@@ -3608,7 +3617,7 @@ struct Engine {
         uint64_t h2d = 0, d2h = 0, packed = 0;
         // small counts (expand_c8): widened on a thread of their own, chunk by chunk as they
         // land, so the downloads never wait for it
-        const bool derive_counts = small_counts;
+        const bool derive_counts = small_counts == 2 || (small_counts == 1 && locate);
         size_t counted = 0;
         std::vector<Job> landed;
         const uint8_t* text_end = text + (nch ? ch.back().b1 : 0);
