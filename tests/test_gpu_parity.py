@@ -710,14 +710,21 @@ def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
             buf, offs = _pack(lines)
             oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=5)
             text = ("\n".join(lines) + ("\n" if trailing else "")).encode()
-            for pack in ("1", "0"):
+            for pack, mb in (("1", "0.02"), ("0", "0.02"), ("1", "")):  # "": one chunk, its line blocks streamed
                 monkeypatch.setenv("EDSBWT_PACK_LINES", pack)
-                monkeypatch.setenv("EDSBWT_CHUNK_MB", "0.02")
-                monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+                if mb:
+                    monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
+                    monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+                else:
+                    monkeypatch.delenv("EDSBWT_CHUNK_MB", raising=False)
+                    monkeypatch.delenv("EDSBWT_CHUNK_SINGLE_MB", raising=False)
                 with edsbwt.Index(base) as idx:
                     gc, go = _lines_search(edsbwt, idx, text, first_id=5, pinned=pinned)
                     st = idx.stats()
-                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack)
+                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack, mb)
+                if not mb:
+                    assert st["chunks"] == 1
+                    continue
                 if pack == "1" and lines is pats:
                     assert st["bytes_h2d"] <= len(lines) * ((L + 3) // 4)  # every chunk went packed
                 elif pack == "1":
