@@ -165,49 +165,46 @@ def record_chunks(counts, budget: float) -> list:
     return cuts
 
 
-def located_leg(idx, buf, offs, counts, dev, stream, first_id: int, budget: float, torch) -> dict:
-    """C5's located leg: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
-    and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so
-    the batch is searched WITH locate in contiguous pattern-id ranges (chunks) whose records
-    fit `budget`; each chunk's counts + records are left in HBM (device-resident, as the timed
-    leg) and the next chunk reuses the record buffer.  Per chunk: its records == Σ its counts
-    from the count-only leg, and its counts equal them.  Outside the timed legs, one pass."""
-    npat = offs.size - 1
+def located_chunks(buf, offs, counts, dev, budget: float, torch) -> tuple:
+    """C5's located search: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
+    and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so the
+    batch is searched WITH locate in contiguous pattern-id ranges (chunks) whose records fit
+    `budget` (at most what the free HBM holds at ~64 B of locate workspace per record); each
+    chunk's counts + records are left in HBM and the next chunk reuses the buffers.  Returns the
+    chunks (pattern range, device bytes, offsets, counts) and the budget."""
     c64 = counts.astype(np.int64)
-    # at most the requested budget, and what the free HBM holds at ~64 B of locate workspace per
-    # record (records 20 B, the finishers' sort and archive, the interval shards)
     free_b, _ = torch.cuda.mem_get_info(dev)
     budget = min(budget, 0.6 * free_b / 64.0)
     cuts = record_chunks(c64, budget)
-    lens = np.diff(offs.astype(np.int64))
     chunks = []
     for a, b in zip(cuts[:-1], cuts[1:]):
         o = offs[a:b + 1].astype(np.int64) - int(offs[a])
         chunks.append((a, b, torch.from_numpy(buf[int(offs[a]):int(offs[b])].copy()).to(dev), torch.from_numpy(o).to(dev),
                        torch.zeros(max(1, b - a), dtype=torch.int32, device=dev)))
     torch.cuda.synchronize()
-    per, recs, ok, t_all = [], 0, True, 0.0
+    return chunks, budget
+
+
+def located_pass(idx, chunks, counts, stream, first_id: int, torch, kacc=None, check=False) -> dict:
+    """Every chunk searched with locate (device-resident: its bytes and offsets in HBM, counts and
+    records left there); kacc: the HIP-event kernel times summed in; check: each chunk's records
+    == Σ its counts from the count-only search and its counts equal them (synchronises per chunk)."""
+    per, recs, ok = [], 0, True
     for a, b, db, do, dc in chunks:
-        torch.cuda.synchronize()
         t = time.perf_counter()
         _, n = idx.search_device(db.data_ptr(), do.data_ptr(), b - a, dc.data_ptr(), first_pattern_id=first_id + a, locate=True,
-                                 stream=stream)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t
-        t_all += dt
-        want = int(c64[a:b].sum())
-        cm = bool(np.array_equal(dc.cpu().numpy().view(np.uint32)[:b - a], counts[a:b]))
-        ok = ok and cm and n == want
+                                 stream=stream, profile="light" if kacc is not None else False)
+        if kacc is not None:
+            idx.add_kernel_stats(kacc)
         recs += n
-        per.append({"patterns": [a, b], "records": int(n), "records_expected": want, "counts_match": cm, "s": round(dt, 3)})
-        log(f"[bench] located chunk [{a}, {b}): {n} records in {dt:.2f}s")
-    by_len = {str(L): {"patterns": int((lens == L).sum()), "records": int(c64[lens == L].sum())} for L in np.unique(lens)}
-    return {"patterns": npat, "records": int(recs), "chunks": len(chunks), "records_budget_per_chunk": int(budget),
-            "seconds": round(t_all, 3), "patterns_per_sec": round(npat / t_all, 1), "records_per_sec": round(recs / t_all, 1),
-            "records_equal_counts": ok, "lengths": by_len, "per_chunk": per,
-            "what": "every pattern of the batch searched WITH locate (counts + 20-B records left in HBM, device-resident), "
-                    "in contiguous pattern-id chunks whose records fit the budget; records == the count-only leg's counts per "
-                    "chunk; one pass outside the timed legs"}
+        if check:
+            torch.cuda.synchronize()
+            want = int(counts[a:b].astype(np.int64).sum())
+            cm = bool(np.array_equal(dc.cpu().numpy().view(np.uint32)[:b - a], counts[a:b]))
+            ok = ok and cm and n == want
+            per.append({"patterns": [a, b], "records": int(n), "records_expected": want, "counts_match": cm,
+                        "s": round(time.perf_counter() - t, 3)})
+    return {"records": recs, "ok": ok, "per_chunk": per}
 
 
 def main():
@@ -434,8 +431,9 @@ def main():
                        "what": "each rank's first n_per_rank patterns (its first_pattern_id offset) against the oracle "
                                "(literal MOVE_EDSBWTSearch restatement), all-reduced (min)"}
 
-    # ---- timed: device-resident (bytes + offsets in HBM, results left in HBM)
+    # ---- timed: device-resident (bytes + offsets in HBM, results left in HBM); C5: the located search
     dres = None
+    located_timed = w.name == "c5" and not args.no_located
     if not args.no_device:
         buf, offs = pkg.read_pattern_file(pats_path)
         d_bytes = torch.from_numpy(buf).to(dev)
@@ -449,28 +447,52 @@ def main():
         for _ in range(max(1, args.warmup)):
             _, dn = dev_step()
             exchange(dn, d_counts)
+        located = None
+        if located_timed:
+            # C5: the timed step is the located search (the reference always locates), in record-budget
+            # chunks; the count-only warm-up above gave the counts the chunks are cut by
+            counts_c = d_counts.cpu().numpy().view(np.uint32)[:npat].copy()
+            chunks, budget = located_chunks(buf, offs, counts_c, dev, args.located_budget, torch)
+            chk = located_pass(idx, chunks, counts_c, stream, first_id, torch, check=True)  # warm-up pass, checked
+            lens = np.diff(offs.astype(np.int64))
+            c64 = counts_c.astype(np.int64)
+            located = {"chunks": len(chunks), "records_budget_per_chunk": int(budget), "records_per_step": int(chk["records"]),
+                       "records_equal_counts": chk["ok"], "per_chunk_check": chk["per_chunk"],
+                       "lengths": {str(L): {"patterns": int((lens == L).sum()), "records": int(c64[lens == L].sum())}
+                                   for L in np.unique(lens)},
+                       "what": "the timed step: every pattern searched WITH locate (counts + 20-B records left in HBM, "
+                               "device-resident) in contiguous pattern-id chunks whose records fit the budget; checked once "
+                               "(records == the count-only counts per chunk) before the timed steps"}
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         kacc = idx.kernel_acc()
         for _ in range(args.steps):
-            _, dn = dev_step(profile="light")
-            exchange(dn, d_counts)
-            idx.add_kernel_stats(kacc)  # HIP-event times of this call's kernel classes, summed in place
+            if located_timed:
+                lp = located_pass(idx, chunks, counts_c, stream, first_id, torch, kacc=kacc)
+                exchange(lp["records"])
+            else:
+                _, dn = dev_step(profile="light")
+                exchange(dn, d_counts)
+                idx.add_kernel_stats(kacc)  # HIP-event times of this call's kernel classes, summed in place
         torch.cuda.synchronize()
         barrier()
         d_elapsed = time.perf_counter() - t1
+        if located is not None:
+            located["seconds_per_step"] = round(d_elapsed / args.steps, 4)
+            located["records_per_sec"] = round(located["records_per_step"] * args.steps / d_elapsed, 1)
         if multi:
             tt = torch.tensor([d_elapsed], dtype=torch.float64, device=gdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d_elapsed = float(tt.item())
         kstats = idx.kernel_acc_dict(kacc)
         dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": idx.stats(), "d_counts": d_counts}
-        if not args.no_e2e and not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
+        if not located_timed and not args.no_e2e and not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
             raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")
-        if w.name == "c5" and rank == 0 and not args.no_located:
-            dres["located"] = located_leg(idx, buf, offs, d_counts.cpu().numpy().view(np.uint32)[:npat].copy(), dev, stream,
-                                          first_id, args.located_budget, torch)
+        if located is not None:
+            if not located["records_equal_counts"]:
+                raise SystemExit("bench.py: located chunks' records differ from the count-only counts")
+            dres["located"] = located
 
     if rank == 0:
         total_pats = npat * world if w.per_gpu else (args.patterns or w.patterns)  # every rank's shard
@@ -493,7 +515,8 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "value_kind": ("device_resident: pattern bytes + offsets in HBM -> counts + records left in HBM (since round 3; "
-                           "rounds 1-2 reported the PCIe-inclusive rate, now e2e.value)" if dres else
+                           "rounds 1-2 reported the PCIe-inclusive rate, now e2e.value)"
+                           + ("; C5: the located search in record-budget chunks (round 5)" if located_timed else "") if dres else
                            "end_to_end (--no-device): host memory -> host memory"),
             "higher_is_better": True,
             "scaling": "weak" if w.per_gpu else "strong",
@@ -505,7 +528,8 @@ def main():
                        "index_rows": rows, "words": idx.n_words, "segments": idx.n_segments,
                        "locate": ({"sampled": "per-row samples (word, offset, segment, word-in-segment), one read per occurrence",
                                    "walk": "lf-walk to '#' (reference)", "table": "per-row table"}[args.locate]
-                                  if locate else "count-only"),
+                                  if locate else ("per-row samples, the located search in record-budget chunks is the timed "
+                                                  "step (`located`); the e2e leg is count-only" if located_timed else "count-only")),
                        "parallelism": f"pattern-shard x{world}",
                        "timed_region": ("edsbwt_search_device: pattern bytes + offsets resident in HBM -> counts + records "
                                         "in HBM, plus the exchange step when N>1; the PCIe-inclusive rate is `e2e`"

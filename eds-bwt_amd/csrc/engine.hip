@@ -2937,6 +2937,12 @@ struct Engine {
                 std::fprintf(stderr, "[edsbwt] k_deep_fast: %llu dependent load rounds over the lanes' patterns, %llu lane slots: lane utilisation %.3f\n",
                              (unsigned long long)sv[ST_DF_LANE_ROUNDS], (unsigned long long)sv[ST_DF_WAVE_ROUNDS],
                              (double)sv[ST_DF_LANE_ROUNDS] / (double)sv[ST_DF_WAVE_ROUNDS]);
+            if (trace && (sv[ST_CLK_DD_ONE] | sv[ST_CLK_DD_SROW]))
+                std::fprintf(stderr, "[edsbwt] k_deep_direct loads: one-row D-mer entries %llu, per-row text entries %llu, segment rows %llu, "
+                                     "whole-word rows %llu, rank-entry lines %llu, interval steps %llu, text rows %llu\n",
+                             (unsigned long long)sv[ST_CLK_DD_ONE], (unsigned long long)sv[ST_CLK_DD_SROW], (unsigned long long)sv[ST_CLK_DD_SEG],
+                             (unsigned long long)sv[ST_CLK_DD_WROW], (unsigned long long)sv[ST_DEEP_PAIR_LINES],
+                             (unsigned long long)sv[ST_DEEP_STEPS], (unsigned long long)sv[ST_TEXT_ROWS]);
             if (trace && sv[ST_CLK_STEPS])
                 std::fprintf(stderr, "[edsbwt] k_deep lane-steps %llu (with '#' rows %llu): cycles/step rank+link %.0f, runs %.0f, rest %.0f\n",
                              (unsigned long long)sv[ST_CLK_STEPS], (unsigned long long)sv[ST_CLK_HASH_STEPS],
@@ -3286,7 +3292,10 @@ struct Engine {
     // few of 255 and more as (pattern, count) pairs, and a host thread widens them into the
     // caller's counts while the next chunk downloads: a quarter of the counts' PCIe bytes.
     // EDSBWT_SMALL_COUNTS=0: 4 bytes each.
-    bool small_counts = env_double("EDSBWT_SMALL_COUNTS", 1) != 0;
+    // Only beside records: a count-only call's counts go straight to the caller's page-locked array
+    // as u32 (C2: 4 MB in ~0.07 ms, against 1 MB of bytes plus their widening on the host, ~0.1 ms
+    // and a thread wake-up on the critical path).  EDSBWT_SMALL_COUNTS=0: never, 2: count-only too.
+    int small_counts = (int)env_double("EDSBWT_SMALL_COUNTS", 1);
     static uint64_t c8_bytes(uint64_t P) { return (P + 7) / 8 * 8 + 8; }  // bytes, then the exception count (u32)
     void expand_c8(uint32_t* c, const uint8_t* c8, uint64_t P, const uint2* exc, uint32_t nexc) {
         const unsigned T = (unsigned)std::min<uint64_t>(cpool.size(), std::max<uint64_t>(1, P / 262144));
@@ -3399,6 +3408,7 @@ struct Engine {
     // EDSBWT_PACK_LINES=0 turns it off.
     bool pack_lines = env_double("EDSBWT_PACK_LINES", 1) != 0;
     bool pack_single = env_double("EDSBWT_PACK_SINGLE", 1) != 0;
+    bool pack_streamed = env_double("EDSBWT_PACK_STREAMED", 1) != 0;  // (one-chunk batches: pack_chunk_streamed)
     uint64_t pack_threads = 64;  // per call: EDSBWT_PACK_THREADS (at most the pool's)
     uint64_t pack_chunk(const uint8_t* s, uint64_t nb, const uint8_t* end, int sl, uint32_t* L_out) {
         if (!pack_lines) return 0;
@@ -3414,6 +3424,39 @@ struct Engine {
             if (!edsbwt_pack_lines(s, nb, L, P * t / T, P * (t + 1) / T, end, out)) bad.store(1, std::memory_order_relaxed);
         });
         if (bad.load()) return 0;
+        *L_out = L;
+        return P;
+    }
+    // pack_chunk for a one-chunk batch, in kPackSub line blocks each sent on the up engine as soon as
+    // it is packed (C2: the 5 MB of packed lines cross PCIe while the later blocks are packed, instead
+    // of after the whole chunk).  Returns P (0: not fixed-length A/C/G/T lines — every copy started
+    // has finished; the caller sends the chunk raw); the copies are complete when it returns.
+    static constexpr int kPackSub = 4;
+    uint64_t pack_chunk_streamed(const uint8_t* s, uint64_t nb, const uint8_t* end, int sl, uint32_t* L_out, hsa_signal_t* sigs) {
+        if (!pack_lines) return 0;
+        uint32_t L = 0;
+        const uint64_t P = edsbwt_lines_fixed(s, nb, &L);
+        if (!P) return 0;
+        const uint64_t S = (L + 3) / 4;
+        stage_pack[sl].ensure(P * S + 16);
+        hpack[sl].ensure(P * S + 16);
+        uint8_t* out = static_cast<uint8_t*>(stage_pack[sl].p);
+        int started = 0;
+        bool ok = true;
+        for (int j = 0; j < kPackSub && ok; j++) {
+            const uint64_t p0 = P * j / kPackSub, p1 = P * (j + 1) / kPackSub;
+            if (p1 == p0) continue;
+            const uint64_t n = p1 - p0;
+            const unsigned T = (unsigned)std::min<uint64_t>(std::min<uint64_t>(pool.size(), pack_threads), std::max<uint64_t>(1, n / 16384));
+            std::atomic<int> bad{0};
+            pool.run(T, [&](unsigned t) {
+                if (!edsbwt_pack_lines(s, nb, L, p0 + n * t / T, p0 + n * (t + 1) / T, end, out)) bad.store(1, std::memory_order_relaxed);
+            });
+            if (bad.load()) { ok = false; break; }
+            hsa_copy_start(hpack[sl].p + p0 * S, out + p0 * S, n * S, false, eng_up, sigs[started++]);
+        }
+        for (int j = 0; j < started; j++) hsa_wait(sigs[j]);
+        if (!ok) return 0;
         *L_out = L;
         return P;
     }
@@ -3608,7 +3651,7 @@ struct Engine {
         uint64_t h2d = 0, d2h = 0, packed = 0;
         // small counts (expand_c8): widened on a thread of their own, chunk by chunk as they
         // land, so the downloads never wait for it
-        const bool derive_counts = small_counts;
+        const bool derive_counts = small_counts == 2 || (small_counts == 1 && locate);
         size_t counted = 0;
         std::vector<Job> landed;
         const uint8_t* text_end = text + (nch ? ch.back().b1 : 0);
@@ -3630,11 +3673,19 @@ struct Engine {
         if (arena_checked_out()) arena_release();  // the caller still holds the last records: start a new buffer
         std::thread tu([&] {
             hsa_signal_t sig{};
-            bool have_sig = false;
+            hsa_signal_t ssig[kPackSub] = {};  // the streamed packing's block copies
+            bool have_sig = false, have_ssig = false;
             try {
                 HIPCHK(hipSetDevice(device));
                 if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) throw Fail(EDSBWT_E_DEVICE, "hsa_signal_create failed");
                 have_sig = true;
+                if (nch == 1 && lines && pack_streamed) {
+                    int made = 0;
+                    while (made < kPackSub && hsa_signal_create(1, 0, nullptr, &ssig[made]) == HSA_STATUS_SUCCESS) made++;
+                    have_ssig = made == kPackSub;
+                    if (!have_ssig)
+                        for (int j = 0; j < made; j++) hsa_signal_destroy(ssig[j]);
+                }
                 size_t pre_k = ~size_t(0);  // the chunk packed ahead (pre_P lines of pre_L bases; 0: raw)
                 uint64_t pre_P = 0;
                 uint32_t pre_L = 0;
@@ -3652,7 +3703,23 @@ struct Engine {
                     uint64_t Pk = 0;
                     // a one-chunk batch's packing has nothing to overlap with: EDSBWT_PACK_SINGLE=0 sends
                     // it raw (C2: 21 MB raw at ~56 GB/s against packing on the host first)
-                    if (lines && (nch > 1 || pack_single))
+                    if (lines && nch == 1 && pack_single && pack_streamed && have_ssig) {
+                        // one chunk: its packed line blocks cross PCIe as they are packed
+                        Pk = pack_chunk_streamed(text + c.b0, nb, text_end, sl, &L, ssig);
+                        if (Pk) {
+                            prep_packed(sl, nb, Pk, L);
+                            HIPCHK(hipEventRecord(prep_done[sl], up));
+                            mark("uploaded", k);
+                            {
+                                std::lock_guard<std::mutex> g(m);
+                                uploaded = k + 1;
+                                h2d += Pk * ((L + 3) / 4);
+                                packed++;
+                            }
+                            cv.notify_all();
+                            continue;
+                        }
+                    } else if (lines && (nch > 1 || pack_single))
                         Pk = pre_k == k ? (L = pre_L, pre_P) : pack_chunk(text + c.b0, nb, text_end, sl, &L);
                     pre_k = ~size_t(0);
                     if (Pk) {  // 2 bits per base over PCIe, unpacked on the device
@@ -3721,6 +3788,8 @@ struct Engine {
                 fail(std::current_exception());
             }
             if (have_sig) hsa_signal_destroy(sig);
+            if (have_ssig)
+                for (auto& x : ssig) hsa_signal_destroy(x);
         });
         std::thread td([&] {
             hsa_signal_t sig{};

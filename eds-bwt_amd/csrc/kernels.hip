@@ -356,7 +356,10 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
                   ST_FC_FOUND = 22, ST_FC_OCC = 23,
                   // debug build (-DEDSBWT_DEBUG_CHECKS, libedsbwt_dbg.so): failed invariant checks per kind;
                   // search() throws when any is non-zero (engine.hip check_debug)
-                  ST_DBG_QUEUE = 24, ST_DBG_PACKED = 25, ST_DBG_WIDE = 26, ST_DBG_LIST = 27 };
+                  ST_DBG_QUEUE = 24, ST_DBG_PACKED = 25, ST_DBG_WIDE = 26, ST_DBG_LIST = 27,
+                  // profiling build (-DEDSBWT_DEEP_CLOCKS): k_deep_direct's loads by kind — per-row text
+                  // entries, segment-table rows, whole-word rows, and D-mer entries of one row
+                  ST_CLK_DD_SROW = 28, ST_CLK_DD_SEG = 29, ST_CLK_DD_WROW = 30, ST_CLK_DD_ONE = 31 };
 #ifdef EDSBWT_DEBUG_CHECKS
 #define DBG_CHECK(cond, var) \
     do {                     \
@@ -371,9 +374,11 @@ enum : uint32_t { ST_DEEP_STEPS = 0, ST_DEEP_HASH = 1, ST_LOC_STEPS = 2, ST_STEP
 #ifdef EDSBWT_DEEP_CLOCKS
 #define DEEP_CLK(v) const uint64_t v = __builtin_readcyclecounter()
 #define DEEP_CLK_ADD(acc, x) acc += (x)
+#define DD_CNT(v) (v)++
 #else
 #define DEEP_CLK(v)
 #define DEEP_CLK_ADD(acc, x)
+#define DD_CNT(v)
 #endif
 __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats, uint32_t k, unsigned long long v, unsigned long long* sh) {
     v = block_sum(v, sh);
@@ -1567,6 +1572,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     CountSums cs;  // counts != nullptr: each final count written here (fused counts)
     // tsum (input order, FUSED): each wave's 64 patterns are one record-offset tile; its sum of the
     // counts written here is stored, k_deep / k_deep_wave add their patterns' counts after it
+#ifdef EDSBWT_DEEP_CLOCKS
+    uint32_t c_srow = 0, c_seg = 0, c_wrow = 0, c_one = 0;
+#endif
     unsigned long long nt = 0;
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
@@ -1651,6 +1659,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             auto code_at = [&](uint32_t dd) -> uint32_t { return 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u); };
             bool alive = true, pair_skip = false, posres = false;
             uint32_t d = D0;
+            if (g1 != ~0u) DD_CNT(c_one);
             // the row's sample and text window: the wide entry's for the first row (have), loaded
             // for rows reached through a link
             uint4 s = s1;
@@ -1666,6 +1675,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                     tw = (uint64_t)t2.w << 32 | t2.z;
                     have = true;
                     n_blk += 1;
+                    DD_CNT(c_srow);
                 } else if (!have) {
                     s = X.samples[b];
                     g = X.gpos[b];
@@ -1700,6 +1710,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 if (c >= X.sigma) {
                     b = e = X.wrow[s.x];
                     n_blk++;
+                    DD_CNT(c_wrow);
                     break;
                 }
                 if (s.z < 2) {
@@ -1711,6 +1722,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
                 n_blk++;
                 n_steps++;
+                DD_CNT(c_seg);
                 if (ry <= rx) {
                     alive = false;
                     d = L;
@@ -1784,6 +1796,12 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
     stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
     cs.flush(counts, ctr, ssum);
+#ifdef EDSBWT_DEEP_CLOCKS
+    stat_add(ctr, ST_CLK_DD_SROW, c_srow, ssum);
+    stat_add(ctr, ST_CLK_DD_SEG, c_seg, ssum);
+    stat_add(ctr, ST_CLK_DD_WROW, c_wrow, ssum);
+    stat_add(ctr, ST_CLK_DD_ONE, c_one, ssum);
+#endif
     if constexpr (FUSED) {
         nt = block_sum(nt, ssum);
         if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);

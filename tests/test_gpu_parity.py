@@ -710,14 +710,21 @@ def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
             buf, offs = _pack(lines)
             oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=5)
             text = ("\n".join(lines) + ("\n" if trailing else "")).encode()
-            for pack in ("1", "0"):
+            for pack, mb in (("1", "0.02"), ("0", "0.02"), ("1", "")):  # "": one chunk, its line blocks streamed
                 monkeypatch.setenv("EDSBWT_PACK_LINES", pack)
-                monkeypatch.setenv("EDSBWT_CHUNK_MB", "0.02")
-                monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+                if mb:
+                    monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
+                    monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+                else:
+                    monkeypatch.delenv("EDSBWT_CHUNK_MB", raising=False)
+                    monkeypatch.delenv("EDSBWT_CHUNK_SINGLE_MB", raising=False)
                 with edsbwt.Index(base) as idx:
                     gc, go = _lines_search(edsbwt, idx, text, first_id=5, pinned=pinned)
                     st = idx.stats()
-                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack)
+                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack, mb)
+                if not mb:
+                    assert st["chunks"] == 1
+                    continue
                 if pack == "1" and lines is pats:
                     assert st["bytes_h2d"] <= len(lines) * ((L + 3) // 4)  # every chunk went packed
                 elif pack == "1":
@@ -1281,3 +1288,29 @@ def test_kmer_table_grouped_build_gpu(oracle, edsbwt, tmp_path, monkeypatch, sha
             assert np.array_equal(gc, lc) and np.array_equal(go, loo)
     if shape == "covid":
         assert info["0"] == info["2"], info
+
+
+@pytest.mark.parametrize("small", ["1", "2", "0"])
+def test_count_only_counts_paths_gpu(oracle, edsbwt, tmp_path, monkeypatch, small):
+    """A count-only search_lines call downloads its counts as u32 straight into the caller's array
+    (the default), or as bytes widened on the host (EDSBWT_SMALL_COUNTS=2, the located calls' form,
+    with counts of 255 and more as exceptions); located calls keep the byte counts unless
+    EDSBWT_SMALL_COUNTS=0.  Same counts either way, pinned and pageable, one chunk and many."""
+    monkeypatch.setenv("EDSBWT_SMALL_COUNTS", small)
+    rng = random.Random(2222)
+    segs = _covid_like(rng, 300)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(1, 30)) or "ACGT" for _ in range(4000)] + ["A", "C", "G", "T", "", "N"]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
+    assert (oc >= 255).any()  # the byte form's exceptions occur
+    text = ("\n".join(pats) + "\n").encode()
+    for mb in ("0.01", "64"):
+        monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
+        monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
+        with edsbwt.Index(base) as idx:
+            for pinned in (True, False):
+                gc, _ = _lines_search(edsbwt, idx, text, locate=False, pinned=pinned)
+                assert np.array_equal(gc, oc), (mb, pinned)
+                gl, gol = _lines_search(edsbwt, idx, text, pinned=pinned)
+                assert np.array_equal(gl, oc) and np.array_equal(gol, oo), (mb, pinned)

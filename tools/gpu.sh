@@ -9,7 +9,7 @@
 #   bench:<cfg>[:<steps>[:<warmup>]]     one bench.py line (CPU baseline included)
 #   quick:<cfg>[:<steps>]   a bench line without the CPU leg
 #   trace:<cfg>             rocprofv3 --kernel-trace --stats of the device-resident leg
-#   prof:<cfg>              kernel trace + separate PMC passes of the same command (FETCH_SIZE, WRITE_SIZE,
+#   prof:<cfg>[:loc]        kernel trace + separate PMC passes of the same command (FETCH_SIZE, WRITE_SIZE,
 #                           the TCC DRAM request counters, SQ stall + L2), summarised and shrunk on the box
 #                           (tools/profile_summary.py -> <out>_summary.json, <out>_traffic.json)
 #   calib:<mode>:<MB,MB..>  tools/_build/calib_gather --<mode> under a PMC pass of the TCC request counters
@@ -57,6 +57,8 @@ for task in "$@"; do
       # per-class rocprof averages, DRAM bytes / requests per launch -> <out>_traffic.json) and
       # shrunk (prof_reduce.py) so gpurun_out/ stays under gpurun's copy-back cap
       cfg=${a:-c3}
+      # prof:c5:loc profiles the located leg (C5's timed step since round 5) instead of skipping it
+      [ "$b" = "loc" ] && B0="python3 bench.py --no-cpu --no-e2e --steps 2 --warmup 1"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d ${out}_trace -o trace --output-format csv -- $B0 --config $cfg > ${out}_trace.json 2> ${out}_trace.log || fail prof_trace ${out}_trace.log
       grep -v "^[A-Z].*version :\|^Hostname\|^Librccl" ${out}_trace.json | tail -1 > ${out}_bench.json
       timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d ${out}_fetch -o pmc --output-format csv -- $B0 --config $cfg > /dev/null 2> ${out}_fetch.log || fail pmc_fetch ${out}_fetch.log

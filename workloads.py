@@ -51,8 +51,8 @@ CONFIGS = {
     "c4": Workload("c4", "c3", 100_000_000, 3, 100_000_000, False, "31", "planted", 5, True, "c3",
                    "C4: the C3 index replicated, 100M planted 31-mers in total sharded over the GPUs, full position recovery"),
     "c5": Workload("c5", "c5", 1_000_000_000, 6, 200_000, True, "8,16,32,64", "mixed", 7, False, "c5",
-                   "C5: 1 Gchar synthetic EDS with 20% empty-string segments, mixed 8-64-mers per GPU; timed leg count-only "
-                   "(EDSBWT_COUNT_ONLY), every pattern also located in the `located` leg"),
+                   "C5: 1 Gchar synthetic EDS with 20% empty-string segments, mixed 8-64-mers per GPU; timed leg: the "
+                   "located search (every occurrence's record, in record-budget chunks); the e2e leg is count-only"),
 }
 
 
