@@ -1,6 +1,6 @@
 #!/bin/bash
 # gpurun with retries while no box/slot is free (nothing ran, nothing charged); any other outcome returns
-for i in 1 2 3 4 5 6 7 8 9 10; do
+for i in $(seq 1 ${R:-10}); do
   out=$(timeout 2400 /usr/local/graft/bin/gpurun --timeout ${T:-1200} -- "$1" 2>&1)
   if echo "$out" | grep -q "status=transient"; then echo "[gpr] attempt $i: no box ($(date +%T))"; sleep 120; continue; fi
   echo "$out" | tail -${N:-25}; exit 0
