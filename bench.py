@@ -309,8 +309,11 @@ def main():
     first_id = lo + 1
     t = time.time()
     if world > 1 and ndev < world:
-        # ranks sharing a GPU (gloo rehearsal) open the index one at a time: the k-mer table
-        # build's transient workspace is sized for a whole GPU
+        # ranks sharing a GPU (gloo rehearsal) open the index one at a time, each sizing its optional
+        # tables (k-mer table budget, wide entries, per-row text entries, level table) for its share
+        # of the device (EDSBWT_HBM_SHARE; the production config otherwise: no depth overrides)
+        share = 0.9 * ndev / world
+        os.environ.setdefault("EDSBWT_HBM_SHARE", f"{share:.4f}")
         idx = None
         for r in range(world):
             if r == rank:

@@ -635,6 +635,22 @@ struct Engine {
     }
 
     // ------------------------------------------------------------ helpers
+    // The free HBM the index's optional tables are sized by (k-mer table budget, wide entries,
+    // per-row text entries, level table): the device's free memory, and with EDSBWT_HBM_SHARE = f < 1
+    // at most f of the device's memory less what this index already holds — several processes
+    // sharing one GPU (bench.py's 8-rank rehearsal sets f = 1 / ranks per GPU) each size their
+    // tables for their share instead of the first-come ones taking the device
+    size_t hbm_free(size_t* total_out = nullptr) const {
+        size_t f = 0, t = 0;
+        if (hipMemGetInfo(&f, &t) != hipSuccess) { (void)hipGetLastError(); f = t = 0; }
+        if (total_out) *total_out = t;
+        const double share = env_double("EDSBWT_HBM_SHARE", 1.0);
+        if (share > 0 && share < 1.0) {
+            const double cap = share * (double)t - (double)device_bytes;
+            f = std::min<size_t>(f, cap > 0 ? (size_t)cap : 0);
+        }
+        return f;
+    }
     static unsigned grid_for(size_t n) { return (unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 16384)); }
 
     // timing events of an attempt that will not be reported go back to the pool
@@ -1087,7 +1103,7 @@ struct Engine {
         auto pw = [&](uint32_t k) { uint64_t v = 1; for (uint32_t t = 0; t < k; t++) v *= B; return v; };
         while (L > ktab_depth + 1 && pw(L) > kLtabMaxEntries) L--;
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); free_b = 0; }
+        free_b = hbm_free(&total_b);
         const double budget = env_double("EDSBWT_LTAB_SHARE", kLtabHbmShare) * (double)free_b;
         uint64_t sym = 0;
         for (uint32_t v = 0; v < B; v++) sym |= (uint64_t)alpha[v + 1] << (8 * v);
@@ -1114,7 +1130,7 @@ struct Engine {
                     // the group walk's items bounded by what the free HBM holds at the build's transient
                     // bytes per item (a walk past it stops short of depth L: this L is given up)
                     size_t fg = 0, tg = 0;
-                    if (hipMemGetInfo(&fg, &tg) != hipSuccess) { (void)hipGetLastError(); fg = 0; }
+                    fg = hbm_free(&tg);
                     c.K = L; c.B = B; c.only_last = true;
                     c.budget = std::min<uint64_t>(0x7fffffffull, (uint64_t)(0.5 * (double)fg / kKtabBuildBytes));
                     cap = &c;
@@ -1216,7 +1232,7 @@ struct Engine {
         if (!have_text || !have_samples || samp_shift != 0 || !samples.p || !gpos.p || !rtext.p) return;
         if (env_double("EDSBWT_SROW", 1) == 0) return;
         size_t fb = 0, tb_ = 0;
-        if (hipMemGetInfo(&fb, &tb_) != hipSuccess) { (void)hipGetLastError(); fb = 0; }
+        fb = hbm_free(&tb_);
         if ((double)fb < 4.0 * (double)N * 32) return;
         srow.ensure(2 * (size_t)N);
         launch(KC_TABLE, k_srow, N, (uint64_t)N, (const uint4*)samples.p, (const uint32_t*)gpos.p, (const uint64_t*)rtext.p,
@@ -1325,7 +1341,7 @@ struct Engine {
         uint32_t K = (uint32_t)env_double("EDSBWT_KTAB_K", kKtabK);
         // the interval budget scales with the device's free HBM (EDSBWT_KTAB_ITEMS overrides)
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) { (void)hipGetLastError(); free_b = 0; }
+        free_b = hbm_free(&total_b);
         const double by_hbm = kKtabHbmShare * (double)free_b / kKtabBuildBytes;
         const uint64_t budget = (uint64_t)env_double("EDSBWT_KTAB_ITEMS", std::max(kKtabItems, by_hbm));
         K = std::min(K, 16u);  // a search reads a node's D-mer from its sorted key chunk 0 (>= 16 symbols)
@@ -1413,7 +1429,7 @@ struct Engine {
             // samples, the text) and HBM holds 32 B per D-mer with room to spare (C3: 4^15 D-mers,
             // 34 GB); EDSBWT_KT1_WIDE=0: the 8-B entries
             size_t fb = 0, tb_ = 0;
-            if (hipMemGetInfo(&fb, &tb_) != hipSuccess) { (void)hipGetLastError(); fb = 0; }
+            fb = hbm_free(&tb_);
             const uint64_t wide_b = (E + 1) * 32;
             const bool wide = kt1_pos && have_samples && samp_shift == 0 && samples.p && rtext.p &&
                               (double)fb > kKt1WideHbmShare * (double)wide_b && env_double("EDSBWT_KT1_WIDE", 1) != 0;
