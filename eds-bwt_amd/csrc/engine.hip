@@ -3304,6 +3304,55 @@ struct Engine {
             for (auto& x : th) x.join();
         }
     } pool, cpool;  // cpool: the counts thread's (expand_c8)
+    // the host pipeline's upload, download and counts threads, kept for the engine's life: a call
+    // hands each its closure and waits for it (C2's one-chunk call: no thread creation on its
+    // critical path)
+    struct Worker {
+        std::thread th;
+        std::mutex m;
+        std::condition_variable cv;
+        std::function<void()> job;
+        bool busy = false, stop = false;
+        void run(std::function<void()> f) {
+            if (!th.joinable())
+                th = std::thread([this] {
+                    for (;;) {
+                        std::function<void()> g;
+                        {
+                            std::unique_lock<std::mutex> lk(m);
+                            cv.wait(lk, [&] { return stop || (busy && job); });
+                            if (stop) return;
+                            g = std::move(job);
+                            job = nullptr;
+                        }
+                        g();
+                        {
+                            std::lock_guard<std::mutex> lk(m);
+                            busy = false;
+                        }
+                        cv.notify_all();
+                    }
+                });
+            {
+                std::lock_guard<std::mutex> lk(m);
+                job = std::move(f);
+                busy = true;
+            }
+            cv.notify_all();
+        }
+        void wait() {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return !busy; });
+        }
+        ~Worker() {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                stop = true;
+            }
+            cv.notify_all();
+            if (th.joinable()) th.join();
+        }
+    } w_up, w_down, w_cnt;
     // With records the counts cross PCIe as one byte each (k_counts_u8: most are small), the
     // few of 255 and more as (pattern, count) pairs, and a host thread widens them into the
     // caller's counts while the next chunk downloads: a quarter of the counts' PCIe bytes.
@@ -3687,7 +3736,7 @@ struct Engine {
             cv.notify_all();
         };
         if (arena_checked_out()) arena_release();  // the caller still holds the last records: start a new buffer
-        std::thread tu([&] {
+        w_up.run([&] {
             hsa_signal_t sig{};
             hsa_signal_t ssig[kPackSub] = {};  // the streamed packing's block copies
             bool have_sig = false, have_ssig = false;
@@ -3807,7 +3856,7 @@ struct Engine {
             if (have_ssig)
                 for (auto& x : ssig) hsa_signal_destroy(x);
         });
-        std::thread td([&] {
+        w_down.run([&] {
             hsa_signal_t sig{};
             bool have_sig = false;
             try {
@@ -3879,9 +3928,8 @@ struct Engine {
             }
             if (have_sig) hsa_signal_destroy(sig);
         });
-        std::thread tc;
         if (derive_counts)
-            tc = std::thread([&] {
+            w_cnt.run([&] {
                 try {
                     for (size_t k = 0; k < nch; k++) {
                         Job j;
@@ -3981,9 +4029,9 @@ struct Engine {
             closed = true;
         }
         cv.notify_all();
-        tu.join();
-        td.join();
-        if (tc.joinable()) tc.join();
+        w_up.wait();
+        w_down.wait();
+        if (derive_counts) w_cnt.wait();
         (void)hipStreamSynchronize(up);
         if (counts_mirror) (void)hipStreamSynchronize(stream);  // the mirror is complete when the call returns
         if (err) {
