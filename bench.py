@@ -165,45 +165,100 @@ def record_chunks(counts, budget: float) -> list:
     return cuts
 
 
-def located_chunks(buf, offs, counts, dev, budget: float, torch) -> tuple:
+def suffix_order(buf, offs, k: int = 8) -> np.ndarray:
+    """Pattern indices ordered by their last k characters read backwards (the first k levels of the
+    reversed-pattern trie the search walks: MOVE_EDSBWTSearch.cpp:240-258 starts each pattern at its
+    last character), stable: patterns sharing a trie node at depth <= k are contiguous in the order,
+    so record-budget batches cut in it (located_chunks) share almost no trie nodes.  A pattern shorter
+    than k sorts before its longer extensions (missing characters count as 0)."""
+    b = np.asarray(buf, np.uint8)
+    o = np.asarray(offs, np.int64)
+    lens = np.diff(o)
+    key = np.zeros(lens.size, np.uint64)
+    for j in range(k):
+        pos = o[1:] - 1 - j
+        c = np.where(lens > j, b[np.clip(pos, 0, max(0, b.size - 1))] if b.size else 0, 0).astype(np.uint64)
+        key |= c << np.uint64(8 * (k - 1 - j))
+    return np.argsort(key, kind="stable")
+
+
+def located_chunks(buf, offs, counts, dev, budget: float, torch, first_id: int, order: str = "suffix") -> tuple:
     """C5's located search: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
     and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so the
-    batch is searched WITH locate in contiguous pattern-id ranges (chunks) whose records fit
-    `budget` (at most what the free HBM holds at ~64 B of locate workspace per record); each
-    chunk's counts + records are left in HBM and the next chunk reuses the buffers.  Returns the
-    chunks (pattern range, device bytes, offsets, counts) and the budget."""
+    batch is searched WITH locate in batches (chunks) whose records fit `budget` (at most what the
+    free HBM holds at ~64 B of locate workspace per record); each chunk's counts + records are left
+    in HBM and the next chunk reuses the buffers.  The chunks are cut in suffix_order(), not in line
+    order: contiguous line ranges share the shallow trie nodes (C5: ~62K depth-8 nodes whose lists
+    hold ~1.5e5 intervals each), which every range would walk again (round 5: 12 line-range chunks
+    walked 1.19 s of level steps against 0.61 s for the whole batch count-only).  Each chunk reports
+    its patterns' file line numbers through an id map (edsbwt_search_device_ids).  Returns the chunks
+    (pattern indices, device bytes, offsets, ids, counts), the budget and the host seconds the
+    ordering and gathering took (setup, before the timed steps, like the uploads)."""
+    t = time.perf_counter()
     c64 = counts.astype(np.int64)
     free_b, _ = torch.cuda.mem_get_info(dev)
     budget = min(budget, 0.6 * free_b / 64.0)
-    cuts = record_chunks(c64, budget)
+    order = suffix_order(buf, offs) if order == "suffix" else np.arange(c64.size)
+    cuts = record_chunks(c64[order], budget)
+    lens = np.diff(offs.astype(np.int64))
     chunks = []
     for a, b in zip(cuts[:-1], cuts[1:]):
-        o = offs[a:b + 1].astype(np.int64) - int(offs[a])
-        chunks.append((a, b, torch.from_numpy(buf[int(offs[a]):int(offs[b])].copy()).to(dev), torch.from_numpy(o).to(dev),
-                       torch.zeros(max(1, b - a), dtype=torch.int32, device=dev)))
+        sel = order[a:b]
+        so = np.concatenate(([0], np.cumsum(lens[sel]))).astype(np.int64)
+        # the chunk's pattern bytes in its order: one gather of every selected byte
+        starts = offs[sel].astype(np.int64)
+        src = (np.repeat(starts - so[:-1], lens[sel]) + np.arange(int(so[-1]), dtype=np.int64)) if so[-1] else np.zeros(0, np.int64)
+        cb = np.asarray(buf)[src] if src.size else np.zeros(1, np.uint8)
+        ids = (sel.astype(np.int64) + first_id).astype(np.uint32)
+        chunks.append((sel, torch.from_numpy(np.ascontiguousarray(cb)).to(dev), torch.from_numpy(so).to(dev),
+                       torch.from_numpy(ids.view(np.int32)).to(dev), torch.zeros(max(1, b - a), dtype=torch.int32, device=dev)))
     torch.cuda.synchronize()
-    return chunks, budget
+    return chunks, budget, time.perf_counter() - t
 
 
-def located_pass(idx, chunks, counts, stream, first_id: int, torch, kacc=None, check=False) -> dict:
-    """Every chunk searched with locate (device-resident: its bytes and offsets in HBM, counts and
-    records left there); kacc: the HIP-event kernel times summed in; check: each chunk's records
-    == Σ its counts from the count-only search and its counts equal them (synchronises per chunk)."""
+def pat_column(p_occ: int, n: int, dev, torch):
+    """The #Pat column of n device records (20-B edsbwt_occ at device address p_occ) as a device
+    int32 tensor: one strided device-to-device copy (hipMemcpy2D), no host round trip."""
+    import ctypes
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    if n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy2D.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                    ctypes.c_size_t, ctypes.c_int]
+        rc = hip.hipMemcpy2D(out.data_ptr(), 4, p_occ, 20, 4, n, 3)  # 3: hipMemcpyDeviceToDevice
+        if rc != 0:
+            raise RuntimeError(f"hipMemcpy2D of the records' #Pat column failed ({rc})")
+    return out
+
+
+def located_pass(idx, chunks, counts, stream, torch, kacc=None, check=False) -> dict:
+    """Every chunk searched with locate (device-resident: its bytes, offsets and ids in HBM, counts
+    and records left there); kacc: the HIP-event kernel times summed in; check: each chunk's records
+    == Σ its counts from the count-only search, its counts equal them and its records name its
+    patterns' line numbers (pattern-major in the chunk's order; synchronises per chunk)."""
     per, recs, ok = [], 0, True
-    for a, b, db, do, dc in chunks:
+    for sel, db, do, di, dc in chunks:
         t = time.perf_counter()
-        _, n = idx.search_device(db.data_ptr(), do.data_ptr(), b - a, dc.data_ptr(), first_pattern_id=first_id + a, locate=True,
-                                 stream=stream, profile="light" if kacc is not None else False)
+        p_occ, n = idx.search_device(db.data_ptr(), do.data_ptr(), sel.size, dc.data_ptr(), ids=di.data_ptr(), locate=True,
+                                     stream=stream, profile="light" if kacc is not None else False)
         if kacc is not None:
             idx.add_kernel_stats(kacc)
         recs += n
         if check:
             torch.cuda.synchronize()
-            want = int(counts[a:b].astype(np.int64).sum())
-            cm = bool(np.array_equal(dc.cpu().numpy().view(np.uint32)[:b - a], counts[a:b]))
-            ok = ok and cm and n == want
-            per.append({"patterns": [a, b], "records": int(n), "records_expected": want, "counts_match": cm,
-                        "s": round(time.perf_counter() - t, 3)})
+            want_c = counts[sel]
+            want = int(want_c.astype(np.int64).sum())
+            cm = bool(np.array_equal(dc.cpu().numpy().view(np.uint32)[:sel.size], want_c))
+            pm = True
+            if n:
+                # the records' #Pat column: pattern-major in the chunk's order, ids[i] count(i) times
+                got = pat_column(p_occ, n, db.device, torch)
+                want_p = torch.repeat_interleave(di, torch.from_numpy(want_c.astype(np.int64)).to(db.device))
+                pm = bool(torch.equal(got, want_p))
+                del got, want_p
+            ok = ok and cm and pm and n == want
+            per.append({"patterns": int(sel.size), "records": int(n), "records_expected": want, "counts_match": cm,
+                        "pat_column_match": pm, "s": round(time.perf_counter() - t, 3)})
     return {"records": recs, "ok": ok, "per_chunk": per}
 
 
@@ -229,6 +284,8 @@ def main():
                          "(launch with torchrun --nproc-per-node 1): exercises RCCL on a one-GPU box")
     ap.add_argument("--located-budget", type=float, default=1.0e9,
                     help="C5 located leg: most records per pattern-range chunk (20 B each, left in HBM)")
+    ap.add_argument("--located-order", default="suffix", choices=("suffix", "lines"),
+                    help="C5 located leg: batches cut in the patterns' suffix order (default) or in line order")
     ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
     ap.add_argument("--gather", default="auto", choices=("auto", "none", "counts"),
@@ -455,24 +512,28 @@ def main():
             # C5: the timed step is the located search (the reference always locates), in record-budget
             # chunks; the count-only warm-up above gave the counts the chunks are cut by
             counts_c = d_counts.cpu().numpy().view(np.uint32)[:npat].copy()
-            chunks, budget = located_chunks(buf, offs, counts_c, dev, args.located_budget, torch)
-            chk = located_pass(idx, chunks, counts_c, stream, first_id, torch, check=True)  # warm-up pass, checked
+            chunks, budget, setup_s = located_chunks(buf, offs, counts_c, dev, args.located_budget, torch, first_id,
+                                                      order=args.located_order)
+            chk = located_pass(idx, chunks, counts_c, stream, torch, check=True)  # warm-up pass, checked
             lens = np.diff(offs.astype(np.int64))
             c64 = counts_c.astype(np.int64)
             located = {"chunks": len(chunks), "records_budget_per_chunk": int(budget), "records_per_step": int(chk["records"]),
                        "records_equal_counts": chk["ok"], "per_chunk_check": chk["per_chunk"],
                        "lengths": {str(L): {"patterns": int((lens == L).sum()), "records": int(c64[lens == L].sum())}
                                    for L in np.unique(lens)},
+                       "order": args.located_order, "setup_s": round(setup_s, 3),
                        "what": "the timed step: every pattern searched WITH locate (counts + 20-B records left in HBM, "
-                               "device-resident) in contiguous pattern-id chunks whose records fit the budget; checked once "
-                               "(records == the count-only counts per chunk) before the timed steps"}
+                               "device-resident) in batches whose records fit the budget, cut in the patterns' suffix order "
+                               "(--located-order suffix; 'lines': contiguous line ranges) with each record's #Pat the pattern's "
+                               "line number (id map); checked once (records == the count-only counts, and the #Pat column, "
+                               "per chunk) before the timed steps; setup_s: the host ordering + gathers + uploads, untimed"}
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         kacc = idx.kernel_acc()
         for _ in range(args.steps):
             if located_timed:
-                lp = located_pass(idx, chunks, counts_c, stream, first_id, torch, kacc=kacc)
+                lp = located_pass(idx, chunks, counts_c, stream, torch, kacc=kacc)
                 exchange(lp["records"])
             else:
                 _, dn = dev_step(profile="light")

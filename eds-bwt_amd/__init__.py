@@ -124,6 +124,9 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_search.restype = i32
     L.edsbwt_search_device.argtypes = [vp, vp, vp, u64, u32, u32, vp, ctypes.POINTER(vp), ctypes.POINTER(u64), vp]
     L.edsbwt_search_device.restype = i32
+    if hasattr(L, "edsbwt_search_device_ids"):  # (ABI 6)
+        L.edsbwt_search_device_ids.argtypes = [vp, vp, vp, u64, vp, u32, vp, ctypes.POINTER(vp), ctypes.POINTER(u64), vp]
+        L.edsbwt_search_device_ids.restype = i32
     L.edsbwt_search_lines.argtypes = [vp, vp, u64, u32, u32, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(vp),
                                       ctypes.POINTER(u64)]
     L.edsbwt_search_lines.restype = i32
@@ -337,17 +340,22 @@ class Index:
     def search_device(self, d_bytes: int, d_offsets: int, npat: int, d_counts: int, *, first_pattern_id: int = 1,
                       locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
                       stream: int = 0, walk: bool = False, ktab: bool = True, direct: bool = True,
-                      pairs: bool = True, text: bool = True):
+                      pairs: bool = True, text: bool = True, ids: int = 0):
         """Device-resident batch (pointers are device addresses, e.g. torch data_ptr()).
-        Returns (device pointer of the records, number of records)."""
+        ids: device array of npat u32 — pattern i is reported as #Pat ids[i] (edsbwt_search_device_ids)
+        instead of first_pattern_id + i.  Returns (device pointer of the records, number of records)."""
         pflag = {False: 0, True: PROFILE, "light": PROFILE_LIGHT}[profile]
         flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | pflag | (0 if deep else NO_DEEP) \
             | (LOCATE_WALK if walk else 0) | (0 if ktab else NO_KTAB) | (0 if direct else NO_DIRECT) \
             | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT)
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
-        _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,
-                                          ctypes.byref(occ_p), ctypes.byref(nocc), stream or None))
+        if ids:
+            _check(lib().edsbwt_search_device_ids(self._h, d_bytes, d_offsets, npat, ids, flags, d_counts,
+                                                  ctypes.byref(occ_p), ctypes.byref(nocc), stream or None))
+        else:
+            _check(lib().edsbwt_search_device(self._h, d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts,
+                                              ctypes.byref(occ_p), ctypes.byref(nocc), stream or None))
         return occ_p.value or 0, nocc.value
 
     def set_counts_mirror(self, d_counts: int, cap: int) -> None:

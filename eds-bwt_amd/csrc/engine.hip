@@ -276,6 +276,8 @@ struct Engine {
     bool keys_swar = env_double("EDSBWT_KEYS_SWAR", 1) != 0;
     bool locate_pp = env_double("EDSBWT_LOCATE_TASKS", 0) == 0;  // deferred path: per-pattern locate
     DBuf<uint32_t> lbig;  // patterns with more than kLocBig records (k_locate_big)
+    // edsbwt_search_device_ids: the #Pat of batch pattern i is pat_ids[i] (device; null: first_id + i)
+    const uint32_t* pat_ids = nullptr;
     DBuf<uint64_t> pv_in, pv_out;
     DBuf<uint32_t> bhist, bscan;  // direct start buckets (k_keys histogram, its scan / scatter cursors)
     // (measured on C3, 10M patterns: k_keys' histogram atomics +0.2 ms and the scatter 0.69 ms
@@ -2904,9 +2906,9 @@ struct Engine {
                 }
                 rec.ensure(OCC);
                 launch(KC_LOCATE, k_locate, OCC, OCC, TT, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
-                       (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p,
+                       (const uint64_t*)blk_first.p, first_id, pat_ids, X, loc_mode, rec.p, stats.p, (const Res*)res.p,
                        (const unsigned long long*)nullptr, (const uint32_t*)nullptr);
-                if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);
+                if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);  // (refused with pat_ids)
             }
         }
         small_copy(pinned_stats, stats.p, kStatSlots * 8);
@@ -3071,13 +3073,13 @@ struct Engine {
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);  // (its counter zeroed with the others at the search's start)
             // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
-            launch(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>, P, P, (const Res*)res.p, o32, first_id, X,
+            launch(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>, P, P, (const Res*)res.p, o32, first_id, pat_ids, X,
                    (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
                    tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);
             timed(KC_LOCATE, [&] {
                 hipLaunchKernelGGL(k_locate_big, dim3(256), dim3(256), 0, stream, (const uint32_t*)lbig.p, (const Res*)res.p,
-                                   (const uint32_t*)o32, first_id, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
+                                   (const uint32_t*)o32, first_id, pat_ids, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
             });
             HIPCHK(hipGetLastError());
             task_cap = ~0ull;  // no task buffers in this path
@@ -3091,7 +3093,7 @@ struct Engine {
             launch(KC_LOCPREP, k_tasks, P, P, (const Res*)res.p, (const uint64_t*)nullptr, (const uint64_t*)oscan.p, (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, trow.p, tout.p, tpat.p, blk_first.p, occ_cap, task_cap, oflow);
             launch(KC_LOCATE, k_locate, occ_cap, occ_cap, task_cap, (const uint64_t*)tout.p, (const uint32_t*)trow.p, (const uint32_t*)tpat.p,
-                   (const uint64_t*)blk_first.p, first_id, X, loc_mode, rec.p, stats.p, (const Res*)res.p,
+                   (const uint64_t*)blk_first.p, first_id, pat_ids, X, loc_mode, rec.p, stats.p, (const Res*)res.p,
                    (const unsigned long long*)(counters.p + 12), (const uint32_t*)oflow);
         }
         uint32_t* ck = chk();
@@ -4678,9 +4680,9 @@ int edsbwt_index_get_info(const edsbwt_index* idx, edsbwt_index_info* info) {
     return 0;
 }
 
-int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t npat,
-                         uint32_t first_pattern_id, uint32_t flags, uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc,
-                         void* stream) {
+static int search_device_impl(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t npat,
+                              uint32_t first_pattern_id, const uint32_t* d_ids, uint32_t flags, uint32_t* d_counts, edsbwt_occ** d_occ,
+                              uint64_t* nocc, void* stream) {
     if (!idx || (!d_counts && npat) || (npat && (!d_bytes || !d_offsets))) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
     ABI_TRY
     Engine& E = *idx->eng;
@@ -4699,11 +4701,28 @@ int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64
         E.ptag_n = npat;
         E.tag_now = true;
     }
+    struct IdsReset { const uint32_t*& p; ~IdsReset() { p = nullptr; } } ir{E.pat_ids};
+    E.pat_ids = d_ids;
     uint64_t n = E.search(d_bytes, d_offsets, npat, first_pattern_id, flags, d_counts);
     if (d_occ) *d_occ = n ? E.rec.p : nullptr;
     if (nocc) *nocc = n;
     return 0;
     ABI_CATCH
+}
+
+int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t npat,
+                         uint32_t first_pattern_id, uint32_t flags, uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc,
+                         void* stream) {
+    return search_device_impl(idx, d_bytes, d_offsets, npat, first_pattern_id, nullptr, flags, d_counts, d_occ, nocc, stream);
+}
+
+int edsbwt_search_device_ids(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t npat,
+                             const uint32_t* d_ids, uint32_t flags, uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc,
+                             void* stream) {
+    if (npat && !d_ids) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    // the legacy engine order sorts records by #Pat = first_pattern_id + i (no id map)
+    if (flags & EDSBWT_LEGACY_ORDER) { edsbwt::g_err = "EDSBWT_LEGACY_ORDER with an id map"; return EDSBWT_E_ARG; }
+    return search_device_impl(idx, d_bytes, d_offsets, npat, 0, d_ids, flags, d_counts, d_occ, nocc, stream);
 }
 
 int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_offsets, uint64_t npat, uint32_t first_pattern_id,

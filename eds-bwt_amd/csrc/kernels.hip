@@ -3261,6 +3261,12 @@ __global__ void k_blk_first(uint64_t nblk, const uint64_t* __restrict__ tout, ui
     }
 }
 
+// the #Pat a record reports for batch pattern i: first_id + i, or ids[i] when the caller's batch
+// is a subset of its pattern file in another order (edsbwt_search_device_ids)
+__device__ __forceinline__ uint32_t pat_id(const uint32_t* __restrict__ ids, uint32_t first_id, uint64_t i) {
+    return ids ? ids[i] : first_id + (uint32_t)i;
+}
+
 // locate (:328-369): walk LF until L = '#'; the walk length is the offset in the
 // word, the '#'-rank gives EOF_ID, the segment bitvector gives (D, S_j).
 // mode 0: the reference's full walk; 1: per-row (word, offset) table; 2: walk until
@@ -3270,7 +3276,7 @@ __global__ void k_blk_first(uint64_t nblk, const uint64_t* __restrict__ tout, ui
 // tasks (at most kLocRun + 1, from blk_first) are staged in LDS
 __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
                                                 const uint32_t* __restrict__ tpat, const uint64_t* __restrict__ blk_first, uint32_t first_id,
-                                                KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats,
+                                                const uint32_t* __restrict__ ids, KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats,
                                                 const Res* __restrict__ res, const unsigned long long* __restrict__ tot_dev,
                                                 const uint32_t* __restrict__ oflow) {
     // tot_dev (deferred checks): OCC and TT are the batch's totals on the device, the launch
@@ -3309,7 +3315,7 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
             off = (uint32_t)(rr.off >> 32);
             my_off += off;
             edsbwt_occ r;
-            r.pat = first_id + pat;
+            r.pat = pat_id(ids, first_id, pat);
             r.word = word;
             r.seg = rr.occ;
             r.word_in_seg = rr.cnt & kResCnt;
@@ -3323,7 +3329,7 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
             const uint4 s = X.samples[x];
             my_off += s.y;
             edsbwt_occ r;
-            r.pat = first_id + pat;
+            r.pat = pat_id(ids, first_id, pat);
             r.word = s.x;
             r.seg = s.z;
             r.word_in_seg = s.w;
@@ -3346,7 +3352,7 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
                     my_steps += off;
                     my_off += off + s.y;
                     edsbwt_occ r;
-                    r.pat = first_id + pat;
+                    r.pat = pat_id(ids, first_id, pat);
                     r.word = s.x;
                     r.seg = s.z;
                     r.word_in_seg = s.w;
@@ -3375,7 +3381,7 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
         my_off += off;
         const uint32_t seg = X.seg_of_word[word];
         edsbwt_occ r;
-        r.pat = first_id + pat;
+        r.pat = pat_id(ids, first_id, pat);
         r.word = word;
         r.seg = seg;
         r.word_in_seg = word - X.seg_start[seg];
@@ -3409,7 +3415,7 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
 constexpr uint32_t kLocStage = 1024;
 template <uint32_t STAGE = kLocStage>  // records staged per block (STAGE x 20 B of LDS: 1024 -> 7 blocks per CU)
 __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, uint32_t* __restrict__ oscan, uint32_t first_id,
-                                                   KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
+                                                   const uint32_t* __restrict__ ids, KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
                                                    uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats,
                                                    uint32_t* __restrict__ counts, const unsigned long long* __restrict__ tile_pre) {
@@ -3454,7 +3460,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
             }
         };
         if (i < P && occ) {
-            const uint32_t pat = first_id + (uint32_t)i;
+            const uint32_t pat = pat_id(ids, first_id, i);
             if (base + occ > occ_cap) {
                 atomicOr(oflow, 1u);
             } else if (r.cnt & kResPos) {
@@ -3499,15 +3505,15 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
     cs.flush(counts, stats, sh);
 }
 __global__ void __launch_bounds__(256) k_locate_big(const uint32_t* __restrict__ big, const Res* __restrict__ res,
-                                                    const uint32_t* __restrict__ oscan, uint32_t first_id, KIdx X,
-                                                    const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
+                                                    const uint32_t* __restrict__ oscan, uint32_t first_id, const uint32_t* __restrict__ ids,
+                                                    KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                     edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
     unsigned long long my_off = 0;
     const uint32_t nbig = big[0];
     for (uint32_t j = blockIdx.x; j < nbig; j += gridDim.x) {  // block-uniform
         const uint32_t i = big[1 + j];
         const Res r = res[i];
-        const uint32_t occ = res_occ(r), pat = first_id + i;
+        const uint32_t occ = res_occ(r), pat = pat_id(ids, first_id, i);
         const uint64_t base = oscan[i];
         const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
         uint64_t start = 0;

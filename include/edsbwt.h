@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EDSBWT_ABI_VERSION 5
+#define EDSBWT_ABI_VERSION 6
 
 enum {
     EDSBWT_OK = 0,
@@ -183,6 +183,17 @@ const char* edsbwt_build_id(void);
 int edsbwt_search_device(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets,
                          uint64_t npat, uint32_t first_pattern_id, uint32_t flags,
                          uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc, void* stream);
+
+/* The same over a batch that is a subset of the pattern file in another order: pattern i is
+ * reported as #Pat = d_ids[i] (device array of npat ids) instead of first_pattern_id + i; counts
+ * and records follow the batch's order.  The reference's loop searches and locates each line on
+ * its own (MOVE_EDSBWTSearch.cpp:111-136, 328-369), so the lines can be batched in any order: a
+ * located search too large for HBM is cut into batches of patterns sharing their last characters
+ * (one subtree of the reversed-pattern trie each, so no two batches walk the same trie nodes)
+ * instead of contiguous line ranges.  E_ARG with EDSBWT_LEGACY_ORDER. */
+int edsbwt_search_device_ids(edsbwt_index* idx, const uint8_t* d_bytes, const uint64_t* d_offsets,
+                             uint64_t npat, const uint32_t* d_ids, uint32_t flags,
+                             uint32_t* d_counts, edsbwt_occ** d_occ, uint64_t* nocc, void* stream);
 
 /* Tests: the kernels each pattern of the last edsbwt_search_device call went through, when the
  * process runs with EDSBWT_PATH_TAGS=1 (else E_ARG): out[i] for pattern i, i < n (n <= that

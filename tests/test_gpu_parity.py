@@ -1314,3 +1314,74 @@ def test_count_only_counts_paths_gpu(oracle, edsbwt, tmp_path, monkeypatch, smal
                 assert np.array_equal(gc, oc), (mb, pinned)
                 gl, gol = _lines_search(edsbwt, idx, text, pinned=pinned)
                 assert np.array_equal(gl, oc) and np.array_equal(gol, oo), (mb, pinned)
+
+
+def _device_search(edsbwt, idx, pats, ids=None, first_id=1, locate=True):
+    """search_device (or search_device_ids when ids is given) of pats: counts and records."""
+    import ctypes
+    torch = pytest.importorskip("torch")
+    buf, offs = _pack(pats)
+    d_bytes = torch.from_numpy(buf.copy() if buf.size else np.zeros(1, np.uint8)).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_counts = torch.zeros(max(1, len(pats)), dtype=torch.int32, device="cuda")
+    d_ids = torch.from_numpy(np.asarray(ids, np.uint32).view(np.int32)).cuda() if ids is not None else None
+    ptr, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), len(pats), d_counts.data_ptr(), first_pattern_id=first_id,
+                               locate=locate, ids=d_ids.data_ptr() if d_ids is not None else 0)
+    torch.cuda.synchronize()
+    occ = np.zeros(n, edsbwt.OCC_DTYPE)
+    if n:
+        hip = ctypes.CDLL("libamdhip64.so")
+        assert hip.hipMemcpy(ctypes.c_void_p(occ.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(n * 20), 2) == 0
+    return d_counts.cpu().numpy().view(np.uint32)[:len(pats)].copy(), occ
+
+
+@pytest.mark.parametrize("shape", ["level_table", "direct"])
+def test_search_device_ids_gpu(oracle, edsbwt, tmp_path, monkeypatch, shape):
+    """edsbwt_search_device_ids: a batch cut into suffix-ordered sub-batches (bench.py's C5 located
+    chunks) reports each record's #Pat as the pattern's line number from the id map; the counts
+    and records of every sub-batch equal the oracle's for those lines, pattern-major in the
+    sub-batch's order — on the level-table start with trie-subtree groups (C5's path) and on the
+    direct start with its per-pattern locate (k_locate_pp / k_locate_big)."""
+    import bench
+    rng = random.Random(7070)
+    if shape == "level_table":
+        monkeypatch.setenv("EDSBWT_KTAB_K", "3")
+        monkeypatch.setenv("EDSBWT_LTAB_K", "6")
+        monkeypatch.setenv("EDSBWT_FORCE_GROUPS", "2")
+        segs = edsgen.random_eds(rng, 5000, kmax=4, lmax=7, p_empty=0.2)
+        pats = [edsgen.planted(rng, segs, rng.choice([6, 6, 7, 12, 24])) or "ACGTAC" for _ in range(2000)]
+        pats += ["".join(rng.choice("ACGT") for _ in range(rng.choice([6, 8, 16]))) for _ in range(800)]
+    else:
+        monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
+        segs = _covid_like(rng, 300)
+        pats = [edsgen.planted(rng, segs, rng.randint(12, 31)) or "ACGTACGTACGTA" for _ in range(2500)]
+        pats += ["A", "C", "GT"] * 5 + ["".join(rng.choice("ACGT") for _ in range(20)) for _ in range(500)]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    buf, offs = _pack(pats)
+    first_id = 101
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=first_id)
+    ostart = np.zeros(len(pats) + 1, np.int64)
+    ostart[1:] = np.cumsum(oc.astype(np.int64))
+    order = bench.suffix_order(buf, offs.astype(np.int64), k=6)
+    cuts = [0, len(pats) // 3, len(pats) // 3 + 1, len(pats)]
+    with edsbwt.Index(base) as idx:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            sel = order[a:b]
+            gc, go = _device_search(edsbwt, idx, [pats[i] for i in sel], ids=sel + first_id)
+            if shape == "level_table":
+                assert idx.stats()["start_depth"] == 6 or b - a == 1
+            assert np.array_equal(gc, oc[sel]), (a, b)
+            want = np.concatenate([oo[ostart[i]:ostart[i + 1]] for i in sel]) if sel.size else oo[:0]
+            assert np.array_equal(go, want), (a, b)
+        # the whole batch in line order through the id map == first_pattern_id
+        ids = np.arange(len(pats)) + first_id
+        gc, go = _device_search(edsbwt, idx, pats, ids=ids)
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        gc2, go2 = _device_search(edsbwt, idx, pats, first_id=first_id)
+        assert np.array_equal(go2, oo)
+        # the legacy engine order sorts by #Pat: refused with an id map
+        import ctypes
+        L = edsbwt.lib()
+        occ_p, nocc = ctypes.c_void_p(), ctypes.c_uint64()
+        assert L.edsbwt_search_device_ids(idx._h, None, None, 0, None, edsbwt.LOCATE | edsbwt.LEGACY_ORDER, None,
+                                          ctypes.byref(occ_p), ctypes.byref(nocc), None) == -5
