@@ -16,6 +16,10 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -50,6 +54,45 @@ extern "C" int edsbwt_pack_lines(const uint8_t* s, uint64_t nb, uint32_t L, uint
 namespace edsbwt {
 
 static thread_local std::string g_err;
+
+// EDSBWT_SEGV_TRACE=1 (diagnostics): a fault in the process prints the faulting thread's native
+// frames (library offsets: addr2line -f -C -e libedsbwt.so <offset>) to stderr, then the handler
+// that was installed before (e.g. Python's faulthandler) runs
+static struct sigaction g_old_act[32];
+static void segv_trace(int sig, siginfo_t* si, void* uc) {
+    char head[160];
+    const int n0 = std::snprintf(head, sizeof head, "[edsbwt] signal %d at address %p in thread %ld (pid %d)\n", sig, si ? si->si_addr : nullptr,
+                                 (long)syscall(SYS_gettid), (int)getpid());
+    if (n0 > 0) (void)!write(2, head, (size_t)n0);
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    backtrace_symbols_fd(fr, n, 2);
+    Dl_info di{};
+    if (dladdr((void*)&segv_trace, &di) && di.dli_fbase) {
+        const int m = std::snprintf(head, sizeof head, "[edsbwt] libedsbwt.so base %p\n", di.dli_fbase);
+        if (m > 0) (void)!write(2, head, (size_t)m);
+    }
+    struct sigaction& o = g_old_act[sig & 31];
+    sigaction(sig, &o, nullptr);
+    if (o.sa_flags & SA_SIGINFO) {
+        if (o.sa_sigaction) { o.sa_sigaction(sig, si, uc); return; }
+    } else if (o.sa_handler != SIG_DFL && o.sa_handler != SIG_IGN) {
+        o.sa_handler(sig);
+        return;
+    }
+    raise(sig);
+}
+__attribute__((constructor)) static void segv_trace_install() {
+    const char* e = std::getenv("EDSBWT_SEGV_TRACE");
+    if (!e || !*e || *e == '0') return;
+    for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL}) {
+        struct sigaction a{};
+        a.sa_sigaction = segv_trace;
+        a.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigemptyset(&a.sa_mask);
+        sigaction(sig, &a, &g_old_act[sig & 31]);
+    }
+}
 
 struct Fail : std::runtime_error {
     int code;
