@@ -575,8 +575,10 @@ struct Engine {
     DBuf<uint64_t> tile_sum, tile_pre;  // per-pattern locate: occurrences per 64-pattern tile, and their exclusive scan
     uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
     // ... and on the per-pattern locate's fused direct start with the record-offset tile sums
-    // (EDSBWT_TILE_FUSE=0: k_count_tiles reads the results instead)
-    bool tile_fuse = env_double("EDSBWT_TILE_FUSE", 1) != 0;
+    // (EDSBWT_TILE_FUSE=1; off by default: the tiles need the input-order start and per-put atomics in
+    // k_deep, which cost more than the k_count_tiles pass they save — C3 1.85 / 1.83 ms fused against
+    // 1.69 ms with k_count_tiles, k_deep_direct 1.11 against 0.96 ms, profiles/r05_ab_c3_tile_fuse_*.json)
+    bool tile_fuse = env_double("EDSBWT_TILE_FUSE", 0) != 0;
     bool fc_tiles_want = false, tiles_done = false;
     uint32_t* fc_locate_counts = nullptr;
     bool fc_done = false;           // ... and k_deep_direct took them
