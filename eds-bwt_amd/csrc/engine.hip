@@ -173,7 +173,16 @@ struct DBuf {
         if (n <= cap && p) return;
         size_t c = std::max<size_t>({n, cap + cap / 2, 1024});
         T* q = nullptr;
-        if (hipMalloc(&q, c * sizeof(T)) != hipSuccess) throw Fail(EDSBWT_E_NOMEM, "hipMalloc (grow) failed");
+        if (hipMalloc(&q, c * sizeof(T)) != hipSuccess) {
+            // the 1.5x headroom does not fit beside the old buffer: exactly n, or fail
+            (void)hipGetLastError();
+            c = std::max<size_t>(n, 1024);
+            if (hipMalloc(&q, c * sizeof(T)) != hipSuccess) {
+                (void)hipGetLastError();
+                throw Fail(EDSBWT_E_NOMEM, "hipMalloc (grow) of " + std::to_string(c * sizeof(T)) + " bytes failed (" +
+                                               std::to_string(cap * sizeof(T)) + " held)");
+            }
+        }
         if (poison()) { (void)hipMemsetD32((hipDeviceptr_t)q, poison_value(), c * sizeof(T) / 4); (void)hipDeviceSynchronize(); }
         DevMem::add(c * sizeof(T));
         if (p) {
@@ -2351,18 +2360,20 @@ struct Engine {
                 // patterns of length d0 end at the start, and their nodes' lists come out of the
                 // table sorted by row: the items go to the archive as they are (C5's 8-mers:
                 // ~1.5e5 intervals each, which the finisher path would append and radix-sort)
-                node_occ.ensure(M0); foff.ensure(M0); fend.ensure(M0); fin.ensure(M0);
-                launch(KC_FINISH, k_fin_flags, M0, M0, d0, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, fin.p);
+                // (only the finishing nodes' lists go to the archive: a batch with few patterns of
+                // length d0 among many longer ones archives few of the start's ~10^9 items)
+                node_occ.ensure(M0); foff.ensure(M0 + 1); fend.ensure(M0); fin.ensure(M0); fcnt.ensure(M0);
+                launch(KC_FINISH, k_fin_lt_cnt, M0, M0, d0, (const uint32_t*)node_first.p, (const uint32_t*)slen.p, (const uint32_t*)kt_cnt.p,
+                       fin.p, fcnt.p);
+                const uint32_t F = scan_u32(fcnt.p, foff, M0);
+                ab.grow_keep(abase + F, stream);
+                ae.grow_keep(abase + F, stream);
                 launch_grid(KC_FINISH, k_fin_lt, (unsigned)std::min<uint64_t>(((uint64_t)M0 + 3) / 4, 65536), M0, (const uint8_t*)fin.p,
                             (const uint32_t*)kt_pos.p, (const uint32_t*)kt_cnt.p, (const uint32_t*)ib[1].p, (const uint32_t*)ie[1].p,
-                            foff.p, fend.p, node_occ.p);
-                ab.grow_keep(abase + n0, stream);
-                ae.grow_keep(abase + n0, stream);
-                HIPCHK(hipMemcpyAsync(ab.p + abase, ib[1].p, (size_t)n0 * 4, hipMemcpyDeviceToDevice, stream));
-                HIPCHK(hipMemcpyAsync(ae.p + abase, ie[1].p, (size_t)n0 * 4, hipMemcpyDeviceToDevice, stream));
+                            (const uint32_t*)foff.p, fend.p, node_occ.p, abase, ab.p, ae.p);
                 launch(KC_FINISH, k_finish2, P, P, d0, (const uint32_t*)slen.p, (const uint32_t*)nid[1].p, (const uint32_t*)perm.p,
                        (const uint32_t*)foff.p, (const uint32_t*)fend.p, (const uint32_t*)node_occ.p, abase, r);
-                abase += n0;
+                abase += F;
             } else if (hist[d0]) {
                 // patterns of length d0 end at the start: their nodes' lists (sorted by row in the
                 // table) are finished as a depth's finishers are — k_fin_emit over the packed items

@@ -3061,23 +3061,41 @@ __global__ void k_fin_flags(uint32_t M, uint32_t D, const uint32_t* __restrict__
 
 // finishers at the level table's start (patterns of length L, engine.hip levels2): a node's items are
 // [kt_pos[u], + kt_cnt[u]) as k_ltab_emit wrote them, already sorted by row (the table's order), so
-// its archive range is that range (the items copied to the archive whole) and only its occurrence
-// total is summed — one wave per node, no emit, sort or bounds pass
+// its archive range is those items as they are.  k_fin_lt_cnt: the finishing nodes' item counts
+// (others 0), whose exclusive scan (foff) places each finishing node's list in the archive;
+// k_fin_lt copies the finishing lists there and sums their occurrences — one wave per node, no emit,
+// sort or bounds pass, and the lists of nodes that do not finish (only longer patterns pass them)
+// never reach the archive
+__global__ void k_fin_lt_cnt(uint32_t M, uint32_t D, const uint32_t* __restrict__ node_first, const uint32_t* __restrict__ slen,
+                             const uint32_t* __restrict__ kt_cnt, uint8_t* __restrict__ fin, uint32_t* __restrict__ fc) {
+    GRID_STRIDE(u, M) {
+        const bool f = slen[node_first[u]] == D;
+        fin[u] = f;
+        fc[u] = f ? kt_cnt[u] : 0u;
+    }
+}
 __global__ void __launch_bounds__(256) k_fin_lt(uint32_t M, const uint8_t* __restrict__ fin, const uint32_t* __restrict__ kt_pos,
                                                 const uint32_t* __restrict__ kt_cnt, const uint32_t* __restrict__ ib,
-                                                const uint32_t* __restrict__ ie, uint32_t* __restrict__ foff, uint32_t* __restrict__ fend,
-                                                uint32_t* __restrict__ node_occ) {
+                                                const uint32_t* __restrict__ ie, const uint32_t* __restrict__ foff, uint32_t* __restrict__ fend,
+                                                uint32_t* __restrict__ node_occ, uint64_t abase, uint32_t* __restrict__ ab,
+                                                uint32_t* __restrict__ ae) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t u = w0; u < M; u += nw) {  // (wave-uniform)
         if (!fin[u]) continue;
-        const uint32_t a = kt_pos[u], n = kt_cnt[u];
+        const uint32_t a = kt_pos[u], n = kt_cnt[u], o = foff[u];
+        uint32_t* db = ab + abase + o;
+        uint32_t* de = ae + abase + o;
         unsigned long long s = 0;
-        for (uint32_t t = lane; t < n; t += 64) s += (unsigned long long)(ie[a + t] - ib[a + t]) + 1;
+        for (uint32_t t = lane; t < n; t += 64) {
+            const uint32_t b = ib[a + t], e = ie[a + t];
+            db[t] = b;
+            de[t] = e;
+            s += (unsigned long long)(e - b) + 1;
+        }
         s = wave_sum(s);
         if (lane == 0) {
-            foff[u] = a;
-            fend[u] = a + n;
+            fend[u] = o + n;
             node_occ[u] = (uint32_t)s;
         }
     }
@@ -3276,9 +3294,9 @@ __device__ __forceinline__ uint32_t pat_id(const uint32_t* __restrict__ ids, uin
 // tasks (at most kLocRun + 1, from blk_first) are staged in LDS
 __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const uint64_t* __restrict__ tout, const uint32_t* __restrict__ trow,
                                                 const uint32_t* __restrict__ tpat, const uint64_t* __restrict__ blk_first, uint32_t first_id,
-                                                const uint32_t* __restrict__ ids, KIdx X, int mode, edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats,
-                                                const Res* __restrict__ res, const unsigned long long* __restrict__ tot_dev,
-                                                const uint32_t* __restrict__ oflow) {
+                                                const uint32_t* __restrict__ ids, KIdx X, int mode, edsbwt_occ* __restrict__ rec,
+                                                unsigned long long* __restrict__ stats, const Res* __restrict__ res,
+                                                const unsigned long long* __restrict__ tot_dev, const uint32_t* __restrict__ oflow) {
     // tot_dev (deferred checks): OCC and TT are the batch's totals on the device, the launch
     // arguments the buffers' capacities; nothing runs when k_tasks found them too small
     if (tot_dev) {
@@ -3289,11 +3307,16 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
     unsigned long long my_steps = 0, my_off = 0;
     __shared__ uint64_t s_out[kLocRun + 1];
     __shared__ uint32_t s_row[kLocRun + 1], s_pat[kLocRun + 1];
+    // the pass's kLocRun records are one contiguous 5 KB of the output (o0 is a multiple of kLocRun,
+    // so its start is 16-B aligned): staged here and written as 16-B stores instead of five strided
+    // 4-B stores per record from every lane
+    __shared__ uint32_t s_rec[kLocRun * 5];
+    uint32_t* recw = reinterpret_cast<uint32_t*>(rec);
     for (uint64_t o0 = (uint64_t)blockIdx.x * kLocRun; o0 < OCC; o0 += (uint64_t)gridDim.x * kLocRun) {  // block-uniform
         const uint64_t t0 = blk_first[o0 / kLocRun];
         if (t0 >= TT) continue;  // (block-uniform) only a batch that fails its deferred checks gets here
         const uint32_t nt = (uint32_t)min((uint64_t)kLocRun + 1, TT - t0);
-        __syncthreads();  // the previous pass is done with the staged tasks
+        __syncthreads();  // the previous pass is done with the staged tasks and records
         for (uint32_t j = threadIdx.x; j < nt; j += blockDim.x) {
             s_out[j] = tout[t0 + j];
             s_row[j] = trow[t0 + j];
@@ -3301,92 +3324,86 @@ __global__ void __launch_bounds__(256) k_locate(uint64_t OCC, uint64_t TT, const
         }
         __syncthreads();
         const uint64_t o = o0 + threadIdx.x;
-        if (o >= OCC) continue;
-        uint32_t lo = 0, hi = nt;  // last staged task with s_out <= o
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (s_out[mid] <= o) lo = mid; else hi = mid;
-        }
-        const uint32_t pat = s_pat[lo];
-        uint32_t word, off;
-        if (s_row[lo] == ~0u) {  // text-position result (kResPos): (word, offset) from the pattern's result
-            const Res rr = res[pat];
-            word = (uint32_t)rr.off;
-            off = (uint32_t)(rr.off >> 32);
-            my_off += off;
-            edsbwt_occ r;
-            r.pat = pat_id(ids, first_id, pat);
-            r.word = word;
-            r.seg = rr.occ;
-            r.word_in_seg = rr.cnt & kResCnt;
-            r.offset = off;
-            rec[o] = r;
-            continue;
-        }
-        uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
-        if (x >= X.N) continue;  // as above: rows of a valid task are < N
-        if (mode == 2 && X.samp_dense) {  // every row sampled: the record straight from row x's sample
-            const uint4 s = X.samples[x];
-            my_off += s.y;
-            edsbwt_occ r;
-            r.pat = pat_id(ids, first_id, pat);
-            r.word = s.x;
-            r.seg = s.z;
-            r.word_in_seg = s.w;
-            r.offset = s.y;
-            rec[o] = r;
-            continue;
-        }
-        if (mode == 1) {
-            word = X.da[x];
-            off = X.offt[x];
-        } else {
-            off = 0;
-            for (;;) {
+        // (pat, word, segment, word in segment, offset) of record o; zeros where no valid task holds it
+        uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0;
+        if (o < OCC) {
+            uint32_t lo = 0, hi = nt;  // last staged task with s_out <= o
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_out[mid] <= o) lo = mid; else hi = mid;
+            }
+            const uint32_t pat = s_pat[lo];
+            q0 = pat_id(ids, first_id, pat);
+            if (s_row[lo] == ~0u) {  // text-position result (kResPos): (word, offset) from the pattern's result
+                const Res rr = res[pat];
+                q1 = (uint32_t)rr.off;
+                q2 = rr.occ;
+                q3 = rr.cnt & kResCnt;
+                q4 = (uint32_t)(rr.off >> 32);
+                my_off += q4;
+            } else {
+                uint32_t x = s_row[lo] + (uint32_t)(o - s_out[lo]);
+                if (x >= X.N) {
+                    q0 = 0;  // as above: rows of a valid task are < N
+                } else if (mode == 2 && X.samp_dense) {  // every row sampled: the record straight from row x's sample
+                    const uint4 s = X.samples[x];
+                    q1 = s.x; q2 = s.z; q3 = s.w; q4 = s.y;
+                    my_off += s.y;
+                } else {
+                    uint32_t word = ~0u, off = 0;
+                    bool done = false;  // the record came from a sample met on the walk
+                    if (mode == 1) {
+                        word = X.da[x];
+                        off = X.offt[x];
+                    } else {
+                        for (;;) {
 #if EDSBWT_OCC_ROWS == 64
-                const OccV v = load_block(X.occ, x >> 6);
-                const uint32_t bit = x & 63u;
-                const uint64_t m = (1ull << bit) - 1ull;
-                if (mode == 2 && ((v.samp >> bit) & 1)) {  // (word, offset, segment, word in segment)
-                    const uint4 s = X.samples[v.cnt[7] + (uint32_t)__popcll(v.samp & m)];
-                    my_steps += off;
-                    my_off += off + s.y;
-                    edsbwt_occ r;
-                    r.pat = pat_id(ids, first_id, pat);
-                    r.word = s.x;
-                    r.seg = s.z;
-                    r.word_in_seg = s.w;
-                    r.offset = off + s.y;
-                    rec[o] = r;
-                    word = ~0u;
-                    break;
-                }
-                const uint32_t c = (uint32_t)((v.p0 >> bit) & 1) | (uint32_t)(((v.p1 >> bit) & 1) << 1) | (uint32_t)(((v.p2 >> bit) & 1) << 2);
-                uint32_t acc = 0;
+                            const OccV v = load_block(X.occ, x >> 6);
+                            const uint32_t bit = x & 63u;
+                            const uint64_t m = (1ull << bit) - 1ull;
+                            if (mode == 2 && ((v.samp >> bit) & 1)) {  // (word, offset, segment, word in segment)
+                                const uint4 s = X.samples[v.cnt[7] + (uint32_t)__popcll(v.samp & m)];
+                                my_steps += off;
+                                q1 = s.x; q2 = s.z; q3 = s.w; q4 = off + s.y;
+                                done = true;
+                                break;
+                            }
+                            const uint32_t c = (uint32_t)((v.p0 >> bit) & 1) | (uint32_t)(((v.p1 >> bit) & 1) << 1) | (uint32_t)(((v.p2 >> bit) & 1) << 2);
+                            uint32_t acc = 0;
 #pragma unroll
-                for (uint32_t cc = 0; cc < 8; cc++)
-                    if (cc == c) acc = v.cnt[cc];
-                const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
-                const uint32_t rk = acc + (uint32_t)__popcll(e & m);
+                            for (uint32_t cc = 0; cc < 8; cc++)
+                                if (cc == c) acc = v.cnt[cc];
+                            const uint64_t e = ((c & 1) ? v.p0 : ~v.p0) & ((c & 2) ? v.p1 : ~v.p1) & ((c & 4) ? v.p2 : ~v.p2);
+                            const uint32_t rk = acc + (uint32_t)__popcll(e & m);
 #else
-                uint32_t rk;
-                const uint32_t c = sym_rank(X.occ, x, &rk);
+                            uint32_t rk;
+                            const uint32_t c = sym_rank(X.occ, x, &rk);
 #endif
-                if (c == 0) { word = X.eof_word[rk]; my_steps += off; break; }
-                x = X.C[c] + rk;
-                off++;
+                            if (c == 0) { word = X.eof_word[rk]; my_steps += off; break; }
+                            x = X.C[c] + rk;
+                            off++;
+                        }
+                    }
+                    if (!done) {
+                        const uint32_t seg = X.seg_of_word[word];
+                        q1 = word; q2 = seg; q3 = word - X.seg_start[seg]; q4 = off;
+                    }
+                    my_off += q4;
+                }
             }
         }
-        if (word == ~0u) continue;  // written from its sample
-        my_off += off;
-        const uint32_t seg = X.seg_of_word[word];
-        edsbwt_occ r;
-        r.pat = pat_id(ids, first_id, pat);
-        r.word = word;
-        r.seg = seg;
-        r.word_in_seg = word - X.seg_start[seg];
-        r.offset = off;
-        rec[o] = r;
+        uint32_t* d = s_rec + threadIdx.x * 5;
+        d[0] = q0; d[1] = q1; d[2] = q2; d[3] = q3; d[4] = q4;
+        __syncthreads();
+        // words [o0*5, (o0 + n)*5) of the output, n = the pass's records: 16-B stores and a 4-B tail
+        const uint32_t n = (uint32_t)min((uint64_t)kLocRun, OCC - o0);
+        const uint32_t nw = n * 5, nq = nw / 4;
+        uint4* dst = reinterpret_cast<uint4*>(recw + o0 * 5);
+        for (uint32_t k = threadIdx.x; k < nq; k += blockDim.x) {
+            const uint32_t* s4 = s_rec + 4 * k;
+            dst[k] = make_uint4(s4[0], s4[1], s4[2], s4[3]);
+        }
+        if (threadIdx.x < nw - nq * 4) recw[o0 * 5 + nq * 4 + threadIdx.x] = s_rec[nq * 4 + threadIdx.x];
     }
     __shared__ unsigned long long sh[4];
     stat_add(stats, ST_LOC_STEPS, my_steps, sh);

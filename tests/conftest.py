@@ -12,6 +12,9 @@ TESTS = os.path.dirname(os.path.abspath(__file__))
 if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 GOLDEN = os.path.join(TESTS, "golden")
+# a host fault inside libedsbwt.so prints its native frames before Python's faulthandler dump
+# (engine.hip segv_trace; read when the library loads, so set before any test imports it)
+os.environ.setdefault("EDSBWT_SEGV_TRACE", "1")
 
 
 def pytest_configure(config):
