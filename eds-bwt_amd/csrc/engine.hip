@@ -588,6 +588,9 @@ struct Engine {
     // k_deep, which cost more than the k_count_tiles pass they save — C3 1.85 / 1.83 ms fused against
     // 1.69 ms with k_count_tiles, k_deep_direct 1.11 against 0.96 ms, profiles/r05_ab_c3_tile_fuse_*.json)
     bool tile_fuse = env_double("EDSBWT_TILE_FUSE", 0) != 0;
+    // the level walk's located results with dense samples: k_locate_lists (a wave per pattern, records
+    // from the lists directly); EDSBWT_LOCATE_LISTS=0: tasks + k_locate (C5 located step: see DESIGN §6)
+    bool locate_lists = env_double("EDSBWT_LOCATE_LISTS", 1) != 0;
     bool fc_tiles_want = false, tiles_done = false;
     uint32_t* fc_locate_counts = nullptr;
     bool fc_done = false;           // ... and k_deep_direct took them
@@ -2940,7 +2943,14 @@ struct Engine {
                 inclusive_scan_u64(tc64.p, tscan64, P);
                 tsc = tscan64.p;
             }
-            if (OCC) {
+            if (OCC && loc_mode == 2 && X.samp_dense && locate_lists) {
+                // dense samples: each pattern's records straight from its list (k_locate_lists), no tasks
+                rec.ensure(OCC);
+                launch_grid(KC_LOCATE, k_locate_lists, (unsigned)std::min<uint64_t>((P + 3) / 4, 65536), P, (const Res*)res.p,
+                            (const uint64_t*)oscan.p, tsc ? 0u : 1u, first_id, pat_ids, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p,
+                            rec.p, stats.p);
+                if (flags & EDSBWT_LEGACY_ORDER) legacy_order(OCC, P, first_id);
+            } else if (OCC) {
                 trow.ensure(TT); tout.ensure(TT); tpat.ensure(TT);
                 blk_first.ensure(OCC / kLocRun + 1);
                 if (TT <= 0x7fffffffull && (tasks_wave == 2 || (tasks_wave == 1 && TT > kTasksWaveRatio * P))) {

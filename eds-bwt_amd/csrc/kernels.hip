@@ -3425,6 +3425,64 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
     r.offset = off;
     rec[o] = r;
 }
+// Dense samples, the level walk's results (C5's 8-mer lists: ~1.5e5 intervals each, nearly all one row
+// wide): one wave per pattern, its lanes taking 64 of the pattern's intervals at a time; a wave scan of
+// their widths places each interval's records after the pattern's offset (oscan: exclusive, packed =
+// occurrences << 32 | tasks or the occurrences alone), and each row's record comes straight from its
+// sample — no task arrays (k_tasks / k_tasks_wave), no scan over the tasks, no per-record task search
+// (k_locate).  Same records in the same order as k_tasks + k_locate.
+__global__ void __launch_bounds__(256) k_locate_lists(uint64_t P, const Res* __restrict__ res, const uint64_t* __restrict__ oscan,
+                                                      uint32_t packed, uint32_t first_id, const uint32_t* __restrict__ ids, KIdx X,
+                                                      const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
+                                                      edsbwt_occ* __restrict__ rec, unsigned long long* __restrict__ stats) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long my_off = 0;
+    for (uint64_t i = w0; i < P; i += nw) {  // (wave-uniform)
+        const Res r = res[i];
+        const uint32_t occ = res_occ(r);
+        if (!occ) continue;
+        const uint64_t ps = oscan[i];
+        uint64_t base = packed ? ps >> 32 : ps;
+        const uint32_t pat = pat_id(ids, first_id, i);
+        if (r.cnt & kResPos) {  // the text position itself
+            if (lane == 0) {
+                const uint32_t off = (uint32_t)(r.off >> 32);
+                put_rec(rec, base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
+                my_off += off;
+            }
+            continue;
+        }
+        if (r.cnt & kResRow) {  // one interval [off, off + occ), not in the archive
+            for (uint32_t q = lane; q < occ; q += 64) {
+                const uint4 sm = X.samples[(uint32_t)r.off + q];
+                put_rec(rec, base + q, pat, sm.x, sm.z, sm.w, sm.y);
+                my_off += sm.y;
+            }
+            continue;
+        }
+        const uint32_t n = r.cnt & kResCnt;
+        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+            const uint32_t t = c0 + lane;
+            uint32_t b = 0, wd = 0;
+            if (t < n) {
+                b = ab[r.off + t];
+                wd = ae[r.off + t] - b + 1;
+            }
+            uint32_t tot;
+            const uint64_t o = base + wave_excl_scan(wd, lane, tot);
+            for (uint32_t k = 0; k < wd; k++) {
+                const uint4 sm = X.samples[b + k];
+                put_rec(rec, o + k, pat, sm.x, sm.z, sm.w, sm.y);
+                my_off += sm.y;
+            }
+            base += tot;
+        }
+    }
+    __shared__ unsigned long long sh[4];
+    stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
+}
+
 // records of one block's 256 patterns are one contiguous range of the output: staged in LDS
 // (up to kLocStage records) and written out as 16-B stores, instead of five strided 4-B stores
 // per record from every lane (records of patterns left to k_locate_big, which runs next on the

@@ -207,10 +207,12 @@ def test_level_table_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         gs, gso = idx.search((sbuf, soffs))
         assert idx.stats()["start_depth"] == 3
         assert np.array_equal(gs, soc) and np.array_equal(gso, soo)
-    # ... and the located finishers at the table's start through the emit + sort path, locate tasks
-    # one wave per pattern (the path of C5's long 8-mer lists) and one lane per pattern
+    # ... and the located finishers at the table's start through the emit + sort path, and the records
+    # through locate tasks (one wave or one lane per pattern, then k_locate) instead of straight from
+    # the lists (k_locate_lists, the default with dense samples)
     for env in ({"EDSBWT_NO_LTAB": "1"}, {"EDSBWT_FORCE_GROUPS": "2"}, {"EDSBWT_FORCE_GROUPS": "1", "EDSBWT_TEXT_STOP": "32"},
-                {"EDSBWT_LT_FIN_DIRECT": "0"}, {"EDSBWT_TASKS_WAVE": "2"}, {"EDSBWT_TASKS_WAVE": "0", "EDSBWT_LT_FIN_DIRECT": "0"}):
+                {"EDSBWT_LT_FIN_DIRECT": "0"}, {"EDSBWT_TASKS_WAVE": "2", "EDSBWT_LOCATE_LISTS": "0"},
+                {"EDSBWT_TASKS_WAVE": "0", "EDSBWT_LT_FIN_DIRECT": "0", "EDSBWT_LOCATE_LISTS": "0"}, {"EDSBWT_LOCATE_LISTS": "0"}):
         for k_, v_ in env.items():
             monkeypatch.setenv(k_, v_)
         with edsbwt.Index(base) as idx:
