@@ -150,6 +150,11 @@ def cpu_baseline(base: str, buf, offs, first_id: int, sample: int, threads: int,
     return {"value": sample / dt, "seconds": dt, "open_s": t_open, "counts": counts, "occ": occ, "ctr": ctr}
 
 
+# HIP-event times of the timed steps' kernel classes: the light set (deep, step, locate, link sort)
+# by default; EDSBWT_BENCH_PROFILE=full times every class (diagnostics: more events in the step)
+PROFILE_TIMED = True if os.environ.get("EDSBWT_BENCH_PROFILE") == "full" else "light"
+
+
 def record_chunks(counts, budget: float) -> list:
     """Cut points [0, ..., n] of contiguous pattern ranges holding at most `budget` records each
     (greedy; a single pattern above the budget is a chunk of its own)."""
@@ -240,7 +245,7 @@ def located_pass(idx, chunks, counts, stream, torch, kacc=None, check=False) -> 
     for sel, db, do, di, dc in chunks:
         t = time.perf_counter()
         p_occ, n = idx.search_device(db.data_ptr(), do.data_ptr(), sel.size, dc.data_ptr(), ids=di.data_ptr(), locate=True,
-                                     stream=stream, profile="light" if kacc is not None else False)
+                                     stream=stream, profile=PROFILE_TIMED if kacc is not None else False)
         if kacc is not None:
             idx.add_kernel_stats(kacc)
         recs += n
@@ -536,7 +541,7 @@ def main():
                 lp = located_pass(idx, chunks, counts_c, stream, torch, kacc=kacc)
                 exchange(lp["records"])
             else:
-                _, dn = dev_step(profile="light")
+                _, dn = dev_step(profile=PROFILE_TIMED)
                 exchange(dn, d_counts)
                 idx.add_kernel_stats(kacc)  # HIP-event times of this call's kernel classes, summed in place
         torch.cuda.synchronize()

@@ -3431,6 +3431,7 @@ __device__ __forceinline__ void put_rec(edsbwt_occ* __restrict__ rec, uint64_t o
 // occurrences << 32 | tasks or the occurrences alone), and each row's record comes straight from its
 // sample — no task arrays (k_tasks / k_tasks_wave), no scan over the tasks, no per-record task search
 // (k_locate).  Same records in the same order as k_tasks + k_locate.
+constexpr uint32_t kLocU = 4;
 __global__ void __launch_bounds__(256) k_locate_lists(uint64_t P, const Res* __restrict__ res, const uint64_t* __restrict__ oscan,
                                                       uint32_t packed, uint32_t first_id, const uint32_t* __restrict__ ids, KIdx X,
                                                       const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
@@ -3461,20 +3462,42 @@ __global__ void __launch_bounds__(256) k_locate_lists(uint64_t P, const Res* __r
             }
             continue;
         }
+        // kLocU consecutive intervals per lane per round (kLocU x 64 per wave): a lane's sample reads
+        // are independent, so a long list keeps kLocU gathers in flight per lane instead of one
         const uint32_t n = r.cnt & kResCnt;
-        for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-            const uint32_t t = c0 + lane;
-            uint32_t b = 0, wd = 0;
-            if (t < n) {
-                b = ab[r.off + t];
-                wd = ae[r.off + t] - b + 1;
+        for (uint32_t c0 = 0; c0 < n; c0 += 64 * kLocU) {
+            const uint32_t t0 = c0 + lane * kLocU;
+            uint32_t b[kLocU], wd[kLocU], lt = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < kLocU; j++) {
+                b[j] = 0;
+                wd[j] = 0;
+                if (t0 + j < n) {
+                    b[j] = ab[r.off + t0 + j];
+                    wd[j] = ae[r.off + t0 + j] - b[j] + 1;
+                }
+                lt += wd[j];
             }
+            // every interval's first sample read before any record store (nearly every interval of a
+            // long list is one row wide: that read is its only one)
+            uint4 s0[kLocU];
+#pragma unroll
+            for (uint32_t j = 0; j < kLocU; j++) s0[j] = wd[j] ? X.samples[b[j]] : make_uint4(0, 0, 0, 0);
             uint32_t tot;
-            const uint64_t o = base + wave_excl_scan(wd, lane, tot);
-            for (uint32_t k = 0; k < wd; k++) {
-                const uint4 sm = X.samples[b + k];
-                put_rec(rec, o + k, pat, sm.x, sm.z, sm.w, sm.y);
-                my_off += sm.y;
+            uint64_t o = base + wave_excl_scan(lt, lane, tot);
+#pragma unroll
+            for (uint32_t j = 0; j < kLocU; j++) {
+                if (wd[j] == 1) {
+                    put_rec(rec, o, pat, s0[j].x, s0[j].z, s0[j].w, s0[j].y);
+                    my_off += s0[j].y;
+                } else {
+                    for (uint32_t k = 0; k < wd[j]; k++) {
+                        const uint4 sm = X.samples[b[j] + k];
+                        put_rec(rec, o + k, pat, sm.x, sm.z, sm.w, sm.y);
+                        my_off += sm.y;
+                    }
+                }
+                o += wd[j];
             }
             base += tot;
         }
