@@ -3462,44 +3462,41 @@ __global__ void __launch_bounds__(256) k_locate_lists(uint64_t P, const Res* __r
             }
             continue;
         }
-        // kLocU consecutive intervals per lane per round (kLocU x 64 per wave): a lane's sample reads
-        // are independent, so a long list keeps kLocU gathers in flight per lane instead of one
+        // kLocU rounds of 64 intervals at once (interval c0 + 64 j + lane in lane's slot j, so each load
+        // instruction reads 64 neighbouring intervals, as one round would): the kLocU sample reads of a
+        // lane are issued together, before any record store, and each slot's records are placed by a
+        // wave scan of its widths after the previous slot's
         const uint32_t n = r.cnt & kResCnt;
         for (uint32_t c0 = 0; c0 < n; c0 += 64 * kLocU) {
-            const uint32_t t0 = c0 + lane * kLocU;
-            uint32_t b[kLocU], wd[kLocU], lt = 0;
+            uint32_t b[kLocU], wd[kLocU];
 #pragma unroll
             for (uint32_t j = 0; j < kLocU; j++) {
+                const uint32_t t = c0 + 64 * j + lane;
                 b[j] = 0;
                 wd[j] = 0;
-                if (t0 + j < n) {
-                    b[j] = ab[r.off + t0 + j];
-                    wd[j] = ae[r.off + t0 + j] - b[j] + 1;
+                if (t < n) {
+                    b[j] = ab[r.off + t];
+                    wd[j] = ae[r.off + t] - b[j] + 1;
                 }
-                lt += wd[j];
             }
-            // every interval's first sample read before any record store (nearly every interval of a
-            // long list is one row wide: that read is its only one)
-            uint4 s0[kLocU];
+            uint4 s0[kLocU];  // each interval's first row's sample (nearly every interval of a long list is one row wide)
 #pragma unroll
             for (uint32_t j = 0; j < kLocU; j++) s0[j] = wd[j] ? X.samples[b[j]] : make_uint4(0, 0, 0, 0);
-            uint32_t tot;
-            uint64_t o = base + wave_excl_scan(lt, lane, tot);
 #pragma unroll
             for (uint32_t j = 0; j < kLocU; j++) {
-                if (wd[j] == 1) {
+                uint32_t tot;
+                const uint64_t o = base + wave_excl_scan(wd[j], lane, tot);
+                if (wd[j]) {
                     put_rec(rec, o, pat, s0[j].x, s0[j].z, s0[j].w, s0[j].y);
                     my_off += s0[j].y;
-                } else {
-                    for (uint32_t k = 0; k < wd[j]; k++) {
-                        const uint4 sm = X.samples[b[j] + k];
-                        put_rec(rec, o + k, pat, sm.x, sm.z, sm.w, sm.y);
-                        my_off += sm.y;
-                    }
                 }
-                o += wd[j];
+                for (uint32_t k = 1; k < wd[j]; k++) {
+                    const uint4 sm = X.samples[b[j] + k];
+                    put_rec(rec, o + k, pat, sm.x, sm.z, sm.w, sm.y);
+                    my_off += sm.y;
+                }
+                base += tot;
             }
-            base += tot;
         }
     }
     __shared__ unsigned long long sh[4];
