@@ -187,11 +187,17 @@ def suffix_order(buf, offs, k: int = 8) -> np.ndarray:
     return np.argsort(key, kind="stable")
 
 
+# HBM per located record when sizing C5's batches (k_locate_lists needs no task arrays: round 5 sized
+# at 64 B with them, 12 batches; EDSBWT_LOCATED_BPR overrides)
+LOCATED_BYTES_PER_RECORD = float(os.environ.get("EDSBWT_LOCATED_BPR", "40"))
+
+
 def located_chunks(buf, offs, counts, dev, budget: float, torch, first_id: int, order: str = "suffix") -> tuple:
     """C5's located search: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
     and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so the
     batch is searched WITH locate in batches (chunks) whose records fit `budget` (at most what the
-    free HBM holds at ~64 B of locate workspace per record); each chunk's counts + records are left
+    free HBM holds at ~40 B of locate workspace per record: the 20-B record, its interval in the archive and
+    the walk's share); each chunk's counts + records are left
     in HBM and the next chunk reuses the buffers.  The chunks are cut in suffix_order(), not in line
     order: contiguous line ranges share the shallow trie nodes (C5: ~62K depth-8 nodes whose lists
     hold ~1.5e5 intervals each), which every range would walk again (round 5: 12 line-range chunks
@@ -202,7 +208,7 @@ def located_chunks(buf, offs, counts, dev, budget: float, torch, first_id: int, 
     t = time.perf_counter()
     c64 = counts.astype(np.int64)
     free_b, _ = torch.cuda.mem_get_info(dev)
-    budget = min(budget, 0.6 * free_b / 64.0)
+    budget = min(budget, 0.6 * free_b / LOCATED_BYTES_PER_RECORD)
     order = suffix_order(buf, offs) if order == "suffix" else np.arange(c64.size)
     cuts = record_chunks(c64[order], budget)
     lens = np.diff(offs.astype(np.int64))
@@ -287,7 +293,7 @@ def main():
     ap.add_argument("--dist-self", action="store_true",
                     help="run the N>1 exchange path (process group, RCCL gather of the device counts) with one rank too "
                          "(launch with torchrun --nproc-per-node 1): exercises RCCL on a one-GPU box")
-    ap.add_argument("--located-budget", type=float, default=1.0e9,
+    ap.add_argument("--located-budget", type=float, default=2.0e9,
                     help="C5 located leg: most records per pattern-range chunk (20 B each, left in HBM)")
     ap.add_argument("--located-order", default="suffix", choices=("suffix", "lines"),
                     help="C5 located leg: batches cut in the patterns' suffix order (default) or in line order")

@@ -3541,7 +3541,10 @@ struct Engine {
     // EDSBWT_PACK_LINES=0 turns it off.
     bool pack_lines = env_double("EDSBWT_PACK_LINES", 1) != 0;
     bool pack_single = env_double("EDSBWT_PACK_SINGLE", 1) != 0;
-    bool pack_streamed = env_double("EDSBWT_PACK_STREAMED", 1) != 0;  // (one-chunk batches: pack_chunk_streamed)
+    // one-chunk batches packed in sub-blocks, each uploaded when ready (pack_chunk_streamed): off by
+    // default — C2's 5 MB upload is shorter than the packing, 0.661 against 0.639 ms median call with
+    // the whole chunk packed first (profiles/r05_ab_c2_counts_pack_*.json); EDSBWT_PACK_STREAMED=1
+    bool pack_streamed = env_double("EDSBWT_PACK_STREAMED", 0) != 0;
     uint64_t pack_threads = 64;  // per call: EDSBWT_PACK_THREADS (at most the pool's)
     uint64_t pack_chunk(const uint8_t* s, uint64_t nb, const uint8_t* end, int sl, uint32_t* L_out) {
         if (!pack_lines) return 0;

@@ -712,8 +712,10 @@ def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
             buf, offs = _pack(lines)
             oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=5)
             text = ("\n".join(lines) + ("\n" if trailing else "")).encode()
-            for pack, mb in (("1", "0.02"), ("0", "0.02"), ("1", "")):  # "": one chunk, its line blocks streamed
+            # "": one chunk, packed whole (the default) or its line blocks streamed (EDSBWT_PACK_STREAMED=1)
+            for pack, mb, streamed in (("1", "0.02", "0"), ("0", "0.02", "0"), ("1", "", "0"), ("1", "", "1")):
                 monkeypatch.setenv("EDSBWT_PACK_LINES", pack)
+                monkeypatch.setenv("EDSBWT_PACK_STREAMED", streamed)
                 if mb:
                     monkeypatch.setenv("EDSBWT_CHUNK_MB", mb)
                     monkeypatch.setenv("EDSBWT_CHUNK_SINGLE_MB", "0")
@@ -723,7 +725,7 @@ def test_search_lines_packed_gpu(oracle, edsbwt, tmp_path, monkeypatch, pinned):
                 with edsbwt.Index(base) as idx:
                     gc, go = _lines_search(edsbwt, idx, text, first_id=5, pinned=pinned)
                     st = idx.stats()
-                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack, mb)
+                assert np.array_equal(gc, oc) and np.array_equal(go, oo), (L, trailing, pack, mb, streamed)
                 if not mb:
                     assert st["chunks"] == 1
                     continue
