@@ -1,0 +1,13 @@
+# round-5 GPU pass s: the whole GPU suite + smoke on the final tree, then the C5 located line with
+# batches sized at 40 B per record and a C2 line (whole-chunk packing by default)
+export TMPDIR=/tmp
+bash tools/gpu.sh r5s suite || exit 1
+bash tools/gpu.sh r5s quick:c5:2 quick:c2:20 || exit 2
+python3 - <<'PY'
+import json
+d = json.load(open('gpurun_out/r5s_quick_c5.json'))
+l = d.get('located', {})
+print({k: l.get(k) for k in ('chunks', 'records_per_step', 'seconds_per_step', 'records_per_sec', 'records_equal_counts')}, d.get('ms_per_step'))
+d = json.load(open('gpurun_out/r5s_quick_c2.json'))
+print(d['ms_per_step'], d['e2e']['ms_wall_median'])
+PY
