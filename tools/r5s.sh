@@ -11,3 +11,7 @@ print({k: l.get(k) for k in ('chunks', 'records_per_step', 'seconds_per_step', '
 d = json.load(open('gpurun_out/r5s_quick_c2.json'))
 print(d['ms_per_step'], d['e2e']['ms_wall_median'])
 PY
+# k_deep_direct's load kinds on C3 (the clock build): how many patterns the wide entry's text
+# window finishes, and how many go on to per-row text entries, segment rows and rank steps
+EDSBWT_LIB=$PWD/eds-bwt_amd/_build/libedsbwt_clk.so EDSBWT_TRACE=1 timeout -k 10 300 python3 bench.py --no-cpu --no-e2e --steps 2 --warmup 1 --config c3 > gpurun_out/r5s_clk_c3.json 2> gpurun_out/r5s_clk_c3.log || exit 3
+grep -a "k_deep_direct loads\|deep from depth\|k_deep lane-steps" gpurun_out/r5s_clk_c3.log | tail -4
