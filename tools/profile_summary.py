@@ -38,7 +38,7 @@ CLASSES = {
     "deep": ("k_deep_direct", "k_deep_fast"),
     "deep_list": ("k_deep",),
     "deep_wide": ("k_deep_wave", "k_deep_wide"),
-    "locate": ("k_locate", "k_locate_pp", "k_locate_big"),
+    "locate": ("k_locate", "k_locate_pp", "k_locate_big", "k_locate_lists"),
     # the link key sort (KC_LINKSORT, hipcub SortKeys on u64 keys: the only keys-only radix sort
     # the engine runs); one "launch" = one sort = one global-offsets kernel + its onesweep passes
     "link_sort": ("rocprim_sortkeys_offsets", "rocprim_sortkeys"),
