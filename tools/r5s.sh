@@ -1,8 +1,8 @@
 # round-5 GPU pass s: the whole GPU suite + smoke on the final tree, then the C5 located line with
-# batches sized at 40 B per record and a C2 line (whole-chunk packing by default)
+# batches sized at 40 B per record, a C2 line (whole-chunk packing by default), the split direct walk A/B
 export TMPDIR=/tmp
 bash tools/gpu.sh r5s suite || exit 1
-bash tools/gpu.sh r5s quick:c5:2 quick:c2:20 || exit 2
+bash tools/gpu.sh r5s quick:c5:2 quick:c2:20 ab:c3:EDSBWT_DIRECT_SPLIT=0:EDSBWT_DIRECT_SPLIT=1:EDSBWT_DIRECT_SPLIT=0 || exit 2
 python3 - <<'PY'
 import json
 d = json.load(open('gpurun_out/r5s_quick_c5.json'))
