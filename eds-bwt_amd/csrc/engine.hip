@@ -328,6 +328,7 @@ struct Engine {
     bool keys_swar = env_double("EDSBWT_KEYS_SWAR", 1) != 0;
     bool locate_pp = env_double("EDSBWT_LOCATE_TASKS", 0) == 0;  // deferred path: per-pattern locate
     DBuf<uint32_t> lbig;  // patterns with more than kLocBig records (k_locate_big)
+    DBuf<uint2> segtab3;  // KIdx::segtab3: {b, e} per (segment, c, c2, c3)
     // the split direct walk's continuation queue (k_deep_direct phases 1 -> 2): entries, packed starts, shard counters
     DBuf<uint4> dcq;
     DBuf<uint64_t> dcq2;
@@ -671,6 +672,7 @@ struct Engine {
         X.samples = samples.p;
         X.samp_dense = have_samples && samp_shift == 0 ? 1u : 0u;
         X.segtab = segtab.p;
+        X.segtab3 = segtab3.p ? (const uint2*)segtab3.p : nullptr;
         X.seg_stride = (sigma <= 7 && !segtab_wide) ? 16u : 32u;
         X.seg_hi = sigma <= 7 ? 8u : 9u;
         X.segtext = have_segtext ? 1u : 0u;
@@ -1132,6 +1134,14 @@ struct Engine {
                 eofrow.ensure((size_t)W * 16);
                 launch(KC_TABLE, k_eofrow, (size_t)W * 16, W, (const uint32_t*)eof_seg.p, (const uint32_t*)segtab.p, X0.seg_stride, eofrow.p);
                 device_bytes += (size_t)W * 64;
+            }
+            // the link and the next two characters in one read (k_deep_direct; 512 B per segment, C3: 0.97 GB;
+            // sigma = 5; within 2% of the free HBM; EDSBWT_SEGTAB3=0: off)
+            const double seg3_b = (double)(S + 2) * 512.0;
+            if (sigma == 5 && env_double("EDSBWT_SEGTAB3", 1) != 0 && seg3_b <= 0.02 * (double)hbm_free()) {
+                segtab3.ensure((size_t)(S + 2) * 64);
+                device_bytes += (size_t)(S + 2) * 512;
+                launch(KC_TABLE, k_segtab3, ((size_t)S + 2) * 4, S, kidx(), (uint2*)segtab3.p);
             }
             HIPCHK(hipStreamSynchronize(stream));
         }

@@ -1777,6 +1777,24 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                     d = L;
                     break;
                 }
+                if (X.segtab3 && d + 2 < L) {  // the link and the next two characters from one read
+                    const uint32_t c2 = code_at(d + 1), c3 = code_at(d + 2);
+                    const uint2 v = X.segtab3[(((size_t)s.z * 4 + (c - 1)) * 4 + (c2 - 1)) * 4 + (c3 - 1)];
+                    n_blk++;
+                    DD_CNT(c_seg);
+                    if (v.x != ~0u) {
+                        if (v.x > v.y) {
+                            alive = false;
+                            d = L;
+                            break;
+                        }
+                        n_steps += 3;
+                        b = v.x;
+                        e = v.y;
+                        d += 3;
+                        continue;
+                    }
+                }
                 const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
                 const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
                 n_blk++;
@@ -3963,6 +3981,48 @@ __global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
         for (uint32_t c = 0; c < X.sigma; c++) {
             e[1 + c] = r0[c];
             e[X.seg_hi + c] = r1[c];
+        }
+    }
+}
+
+// KIdx::segtab3: one thread per (segment, c); the link interval of c from the segment link table's
+// ranks, then every c2 and c3 step from two all-symbol ranks per interval
+__global__ void k_segtab3(uint32_t S, KIdx X, uint2* __restrict__ out) {
+    const uint2 kSeg3Dead = make_uint2(1u, 0u), kSeg3Fallback = make_uint2(~0u, ~0u);
+    GRID_STRIDE(t, ((size_t)S + 2) * 4) {
+        const size_t s = t >> 2;
+        const uint32_t c = 1u + (uint32_t)(t & 3u);
+        uint2* o = out + t * 16;
+        const uint32_t* et = X.segtab + s * X.seg_stride;
+        const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
+        if (s < 2 || ry <= rx) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) o[k] = kSeg3Dead;
+            continue;
+        }
+        const uint32_t b0 = X.C[c] + rx, e0 = X.C[c] + ry - 1;
+        uint32_t p0[8], p1[8];
+        rank_all(X.occ, b0, X.sigma, p0);
+        rank_all(X.occ, e0 + 1, X.sigma, p1);
+        for (uint32_t c2 = 1; c2 <= 4; c2++) {
+            uint2* o2 = o + (c2 - 1) * 4;
+            if (p1[0] > p0[0]) {  // '#' rows in the link interval
+                for (int k = 0; k < 4; k++) o2[k] = kSeg3Fallback;
+                continue;
+            }
+            if (p1[c2] <= p0[c2]) {
+                for (int k = 0; k < 4; k++) o2[k] = kSeg3Dead;
+                continue;
+            }
+            const uint32_t b1 = X.C[c2] + p0[c2], e1 = X.C[c2] + p1[c2] - 1;
+            uint32_t q0[8], q1[8];
+            rank_all(X.occ, b1, X.sigma, q0);
+            rank_all(X.occ, e1 + 1, X.sigma, q1);
+            for (uint32_t c3 = 1; c3 <= 4; c3++) {
+                if (q1[0] > q0[0]) o2[c3 - 1] = kSeg3Fallback;
+                else if (q1[c3] <= q0[c3]) o2[c3 - 1] = kSeg3Dead;
+                else o2[c3 - 1] = make_uint2(X.C[c3] + q0[c3], X.C[c3] + q1[c3] - 1);
+            }
         }
     }
 }

@@ -550,19 +550,23 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
         # ... each also as the split walk (EDSBWT_DIRECT_SPLIT=1: the walks the wide entry does not
         # finish go on in k_deep_direct's second phase) and with the record-offset tiles fused in
-        for fused, split, tiles in (("1", "0", "0"), ("0", "0", "0"), ("1", "1", "0"), ("0", "1", "0"), ("1", "1", "1")):
+        # ... and with the links past a matched word taken from the segment rows (EDSBWT_SEGTAB3=0)
+        # instead of the link + two characters table
+        for fused, split, tiles, seg3 in (("1", "0", "0", "1"), ("0", "0", "0", "1"), ("1", "1", "0", "1"), ("0", "1", "0", "1"),
+                                          ("1", "1", "1", "1"), ("1", "0", "0", "0")):
             monkeypatch.setenv("EDSBWT_FUSED_KEYS", fused)
             monkeypatch.setenv("EDSBWT_DIRECT_SPLIT", split)
             monkeypatch.setenv("EDSBWT_TILE_FUSE", tiles)
+            monkeypatch.setenv("EDSBWT_SEGTAB3", seg3)
             for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED"):
                 monkeypatch.delenv(k_, raising=False)
             with edsbwt.Index(base) as idx:
                 for kw in ({}, {"locate": False}):
                     gc, go = idx.search((buf, offs), **kw)
-                    assert np.array_equal(gc, oc), (fused, split, tiles, kw, len(pats))
+                    assert np.array_equal(gc, oc), (fused, split, tiles, seg3, kw, len(pats))
                     if kw.get("locate", True):
-                        assert np.array_equal(go, oo), (fused, split, tiles, kw, len(pats))
-    for k_ in ("EDSBWT_FUSED_KEYS", "EDSBWT_DIRECT_SPLIT", "EDSBWT_TILE_FUSE"):
+                        assert np.array_equal(go, oo), (fused, split, tiles, seg3, kw, len(pats))
+    for k_ in ("EDSBWT_FUSED_KEYS", "EDSBWT_DIRECT_SPLIT", "EDSBWT_TILE_FUSE", "EDSBWT_SEGTAB3"):
         monkeypatch.delenv(k_)
     E = (4 ** D0) + 1
     assert sizes["11"] - sizes["01"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
