@@ -1136,9 +1136,11 @@ struct Engine {
                 device_bytes += (size_t)W * 64;
             }
             // the link and the next two characters in one read (k_deep_direct; 512 B per segment, C3: 0.97 GB;
-            // sigma = 5; within 2% of the free HBM; EDSBWT_SEGTAB3=0: off)
+            // sigma = 5; within 2% of the free HBM).  Off by default (EDSBWT_SEGTAB3=1): at C3 a link
+            // mostly lands on one row, whose text compare follows anyway — 1.759 / 1.751 against 1.741 ms
+            // (profiles/r05_ab_c3_segtab3_*.json)
             const double seg3_b = (double)(S + 2) * 512.0;
-            if (sigma == 5 && env_double("EDSBWT_SEGTAB3", 1) != 0 && seg3_b <= 0.02 * (double)hbm_free()) {
+            if (sigma == 5 && env_double("EDSBWT_SEGTAB3", 0) != 0 && seg3_b <= 0.02 * (double)hbm_free()) {
                 segtab3.ensure((size_t)(S + 2) * 64);
                 device_bytes += (size_t)(S + 2) * 512;
                 launch(KC_TABLE, k_segtab3, ((size_t)S + 2) * 4, S, kidx(), (uint2*)segtab3.p);

@@ -550,10 +550,10 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
         # ... each also as the split walk (EDSBWT_DIRECT_SPLIT=1: the walks the wide entry does not
         # finish go on in k_deep_direct's second phase) and with the record-offset tiles fused in
-        # ... and with the links past a matched word taken from the segment rows (EDSBWT_SEGTAB3=0)
-        # instead of the link + two characters table
-        for fused, split, tiles, seg3 in (("1", "0", "0", "1"), ("0", "0", "0", "1"), ("1", "1", "0", "1"), ("0", "1", "0", "1"),
-                                          ("1", "1", "1", "1"), ("1", "0", "0", "0")):
+        # ... and with the links past a matched word and their next two characters from the segment
+        # link + two characters table (EDSBWT_SEGTAB3=1) instead of the segment rows
+        for fused, split, tiles, seg3 in (("1", "0", "0", "0"), ("0", "0", "0", "0"), ("1", "1", "0", "0"), ("0", "1", "0", "1"),
+                                          ("1", "1", "1", "0"), ("1", "0", "0", "1")):
             monkeypatch.setenv("EDSBWT_FUSED_KEYS", fused)
             monkeypatch.setenv("EDSBWT_DIRECT_SPLIT", split)
             monkeypatch.setenv("EDSBWT_TILE_FUSE", tiles)
