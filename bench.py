@@ -187,16 +187,16 @@ def suffix_order(buf, offs, k: int = 8) -> np.ndarray:
     return np.argsort(key, kind="stable")
 
 
-# HBM per located record when sizing C5's batches (k_locate_lists needs no task arrays: round 5 sized
-# at 64 B with them, 12 batches; EDSBWT_LOCATED_BPR overrides)
-LOCATED_BYTES_PER_RECORD = float(os.environ.get("EDSBWT_LOCATED_BPR", "40"))
+# HBM per located record when sizing C5's batches (k_locate_lists needs no task arrays): 30 B — 6 batches,
+# 1.189 s, against 8 at 40 B (1.229 s) and 12 at round 5's first 64 B (1.305 s); EDSBWT_LOCATED_BPR overrides
+LOCATED_BYTES_PER_RECORD = float(os.environ.get("EDSBWT_LOCATED_BPR", "30"))
 
 
 def located_chunks(buf, offs, counts, dev, budget: float, torch, first_id: int, order: str = "suffix") -> tuple:
     """C5's located search: the reference always recovers positions (MOVE_EDSBWTSearch.cpp:328-369),
     and C5's 8.7e9 occurrences (20-B records: ~174 GB) do not fit in HBM beside the index, so the
     batch is searched WITH locate in batches (chunks) whose records fit `budget` (at most what the
-    free HBM holds at ~40 B of locate workspace per record: the 20-B record, its interval in the archive and
+    free HBM holds at ~30 B of locate workspace per record: the 20-B record, its interval in the archive and
     the walk's share); each chunk's counts + records are left
     in HBM and the next chunk reuses the buffers.  The chunks are cut in suffix_order(), not in line
     order: contiguous line ranges share the shallow trie nodes (C5: ~62K depth-8 nodes whose lists
