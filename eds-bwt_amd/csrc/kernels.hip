@@ -1614,24 +1614,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         cq += (size_t)sh * qcap;
         cq2 += (size_t)sh * qcap;
     }
-    // FUSED: each lane's next pattern offsets are loaded one iteration ahead (the chain to a pattern's
-    // wide entry is offsets -> bytes -> entry; the offsets then arrive while this pattern walks)
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    uint64_t pf_a = 0, pf_b = 0;
-    if (FUSED && cmode != 2) {
-        const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (i0 < P) {
-            pf_a = off[i0];
-            pf_b = off[i0 + 1];
-        }
-    }
     UNIFORM_STRIDE(j, valid, nloop) {
         size_t i = j;
-        uint64_t cur_a = pf_a, cur_b = pf_b;
-        if (FUSED && cmode != 2 && j + stride < P) {
-            pf_a = off[j + stride];
-            pf_b = off[j + stride + 1];
-        }
         uint32_t want = 0, defer = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
         uint32_t pi = 0, L = 0, kx = 0;
@@ -1661,8 +1645,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             rem = 0;
             L = 0;
             if (valid) {
-                const uint64_t a = cur_a;
-                const uint32_t Lp = (uint32_t)(cur_b - a);
+                const uint64_t a = off[i];
+                const uint32_t Lp = (uint32_t)(off[i + 1] - a);
                 bool term;
                 if (Lp <= 32 && ((uintptr_t)bytes & 15) == 0) {
                     const uint4* src = reinterpret_cast<const uint4*>(bytes + (a & ~15ull));
