@@ -328,11 +328,6 @@ struct Engine {
     bool keys_swar = env_double("EDSBWT_KEYS_SWAR", 1) != 0;
     bool locate_pp = env_double("EDSBWT_LOCATE_TASKS", 0) == 0;  // deferred path: per-pattern locate
     DBuf<uint32_t> lbig;  // patterns with more than kLocBig records (k_locate_big)
-    DBuf<uint2> segtab3;  // KIdx::segtab3: {b, e} per (segment, c, c2, c3)
-    // the split direct walk's continuation queue (k_deep_direct phases 1 -> 2): entries, packed starts, shard counters
-    DBuf<uint4> dcq;
-    DBuf<uint64_t> dcq2;
-    DBuf<uint32_t> dccnt;
     // edsbwt_search_device_ids: the #Pat of batch pattern i is pat_ids[i] (device; null: first_id + i)
     const uint32_t* pat_ids = nullptr;
     DBuf<uint64_t> pv_in, pv_out;
@@ -596,9 +591,6 @@ struct Engine {
     // the level walk's located results with dense samples: k_locate_lists (a wave per pattern, records
     // from the lists directly); EDSBWT_LOCATE_LISTS=0: tasks + k_locate (C5 located step: see DESIGN §6)
     bool locate_lists = env_double("EDSBWT_LOCATE_LISTS", 1) != 0;
-    // k_deep_direct in two phases (EDSBWT_DIRECT_SPLIT=1): the walks its wide entry does not finish go
-    // on in a second grid of full waves (kernels.hip k_deep_direct cmode)
-    bool direct_split = env_double("EDSBWT_DIRECT_SPLIT", 0) != 0;
     bool fc_tiles_want = false, tiles_done = false;
     uint32_t* fc_locate_counts = nullptr;
     bool fc_done = false;           // ... and k_deep_direct took them
@@ -672,7 +664,6 @@ struct Engine {
         X.samples = samples.p;
         X.samp_dense = have_samples && samp_shift == 0 ? 1u : 0u;
         X.segtab = segtab.p;
-        X.segtab3 = segtab3.p ? (const uint2*)segtab3.p : nullptr;
         X.seg_stride = (sigma <= 7 && !segtab_wide) ? 16u : 32u;
         X.seg_hi = sigma <= 7 ? 8u : 9u;
         X.segtext = have_segtext ? 1u : 0u;
@@ -1134,16 +1125,6 @@ struct Engine {
                 eofrow.ensure((size_t)W * 16);
                 launch(KC_TABLE, k_eofrow, (size_t)W * 16, W, (const uint32_t*)eof_seg.p, (const uint32_t*)segtab.p, X0.seg_stride, eofrow.p);
                 device_bytes += (size_t)W * 64;
-            }
-            // the link and the next two characters in one read (k_deep_direct; 512 B per segment, C3: 0.97 GB;
-            // sigma = 5; within 2% of the free HBM).  Off by default (EDSBWT_SEGTAB3=1): at C3 a link
-            // mostly lands on one row, whose text compare follows anyway — 1.759 / 1.751 against 1.741 ms
-            // (profiles/r05_ab_c3_segtab3_*.json)
-            const double seg3_b = (double)(S + 2) * 512.0;
-            if (sigma == 5 && env_double("EDSBWT_SEGTAB3", 0) != 0 && seg3_b <= 0.02 * (double)hbm_free()) {
-                segtab3.ensure((size_t)(S + 2) * 64);
-                device_bytes += (size_t)(S + 2) * 512;
-                launch(KC_TABLE, k_segtab3, ((size_t)S + 2) * 4, S, kidx(), (uint2*)segtab3.p);
             }
             HIPCHK(hipStreamSynchronize(stream));
         }
@@ -1997,11 +1978,7 @@ struct Engine {
         ab.grow_keep(abase + (uint64_t)P * K, stream);
         ae.grow_keep(abase + (uint64_t)P * K, stream);
         // single-interval walks first; patterns needing lists or links are queued for k_deep
-        const uint64_t* kt1w_probe = goff == ktab_off.p && ktab_wide.p ? (const uint64_t*)ktab_wide.p : nullptr;
-        // the split walk (k_deep_direct phases 1 and 2) fills the k_deep queue from two grids: room for
-        // both in every shard
-        const bool split = direct_split && pv && kt1w_probe && !kidx().rent3 && deep_direct && !(fc_tiles_want && defer);
-        const size_t qcap = std::max<size_t>(shard_bound(P, 1), 1024) * (split ? 2 : 1);
+        const size_t qcap = std::max<size_t>(shard_bound(P, 1), 1024);
         dq.ensure(qcap * NSHARD);
         if (pv) dq2.ensure(qcap * NSHARD);
         dqpre.ensure(NSHARD + 1);
@@ -2033,36 +2010,20 @@ struct Engine {
             tiles_done = true;
         }
         if (fc) fc_done = true;
-        const bool spl = split && kdd && !ts;
-        if (spl) {
-            dcq.ensure(qcap * NSHARD);
-            dcq2.ensure(qcap * NSHARD);
-            dccnt.ensure(NSHARD * 32);
-            zero(dccnt.p, NSHARD * 32 * 4);
-        }
-        uint4* cq = spl ? (uint4*)dcq.p : (uint4*)nullptr;
-        uint64_t* cq2 = spl ? dcq2.p : (uint64_t*)nullptr;
-        uint32_t* cc = spl ? dccnt.p : (uint32_t*)nullptr;
         if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
             // written there, for k_deep and k_deep_wave)
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8, true> : direct_waves >= 7 ? k_deep_direct<7, true>
                      : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
-                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, ts,
-                   spl ? 1u : 0u, cq, cq2, cc);
-            if (spl)  // phase 2: the deferred walks, in full waves (the grid's blocks past them return)
-                launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
-                       fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc,
-                       (unsigned long long*)nullptr, 2u, cq, cq2, cc);
+                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, ts);
             fk_now.on = false;
         } else if (kdd) {
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
                                                                                                         : k_deep_direct<1>;
-            for (uint32_t ph = spl ? 1u : 0u; ph <= (spl ? 2u : 0u); ph++)  // (phase 2 of the split walk: the deferred walks)
-                launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
-                       (const uint8_t*)nullptr, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned long long*)nullptr,
-                       0u, 0u, 0u, fc, (unsigned long long*)nullptr, ph, cq, cq2, cc);
+            launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
+                   (const uint8_t*)nullptr, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned long long*)nullptr, 0u,
+                   0u, 0u, fc, (unsigned long long*)nullptr);
         } else {
             auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
             launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,

@@ -125,13 +125,6 @@ struct KIdx {
     // kTextItem) of the ONE word of [seg_lo[s], s - 1] ending with c, when there is one: the dollar
     // step then hands that single row on as a text item (no srow read at the next depth)
     uint32_t segtext;
-    // segtab3 (sigma = 5, nullptr: not built): per segment s >= 2 and codes c, c2, c3 (1..4) at
-    // [((s * 4 + c - 1) * 4 + c2 - 1) * 4 + c3 - 1], the interval after the link from s with c and
-    // the steps by c2 then c3 — {b, e}, or {1, 0} when it is empty at either step, or {~0, ~0}
-    // when either step's interval holds '#' rows (the link needs the general walk): k_deep_direct's
-    // link past a matched word start and its next two characters from ONE 8-B read instead of the
-    // segment row and a rank entry per end
-    const uint2* segtab3;
     // the k-mer start table's D-mers (B^depth; entry kt_E is the empty list of D-mers outside the
     // alphabet) and intervals: the bounds a queued direct-start list is checked against in the
     // debug build (-DEDSBWT_DEBUG_CHECKS)

@@ -1567,15 +1567,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                                                            const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                            uint32_t* __restrict__ len_out, uint32_t* __restrict__ kid_out,
                                                            unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax,
-                                                           uint32_t* __restrict__ counts, unsigned long long* __restrict__ tsum,
-                                                           uint32_t cmode, uint4* __restrict__ cq, uint64_t* __restrict__ cq2,
-                                                           uint32_t* __restrict__ ccnt) {
-    // cmode (the split walk, EDSBWT_DIRECT_SPLIT): 0 — every lane walks its pattern to the end; 1 — a
-    // lane whose walk needs more than its D-mer's wide entry (a multi-row interval, or a link past the
-    // entry's word) leaves (i, d, b, e) + its packed start in the continuation queue cq / cq2 (sharded
-    // as q, counters ccnt) instead of walking on; 2 — the lanes take those entries (P ignored) and walk
-    // them to the end.  A wave of phase 1 then ends with its short walks, and the long ones fill the
-    // waves of phase 2 instead of idling 63 finished lanes beside one walking lane
+                                                           uint32_t* __restrict__ counts, unsigned long long* __restrict__ tsum) {
     uint32_t n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;  // per lane: < 2^32 (widened at the end)
     CountSums cs;  // counts != nullptr: each final count written here (fused counts)
     // tsum (input order, FUSED): each wave's 64 patterns are one record-offset tile; its sum of the
@@ -1587,57 +1579,13 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
-    // phase 2: the shards' prefix sums of phase 1's continuation counters, by the block's first wave
-    __shared__ uint32_t cpre[NSHARD + 1];
-    uint64_t nloop = P;
-    if (cmode == 2) {
-        if (threadIdx.x < 64) {
-            const uint32_t lane = threadIdx.x;
-            uint32_t carry = 0;
-            for (uint32_t b0 = 0; b0 < NSHARD; b0 += 64) {
-                const uint32_t t = b0 + lane;
-                const uint32_t v = t < NSHARD ? ccnt[t * 32] : 0u;
-                uint32_t inc = v;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = __shfl_up(inc, (unsigned)o, 64);
-                    if (lane >= (uint32_t)o) inc += y;
-                }
-                if (t < NSHARD) cpre[t] = carry + inc - v;
-                carry += __shfl(inc, 63, 64);
-            }
-            if (lane == 0) cpre[NSHARD] = carry;
-        }
-        __syncthreads();
-        nloop = cpre[NSHARD];
-    } else if (cmode == 1) {
-        cq += (size_t)sh * qcap;
-        cq2 += (size_t)sh * qcap;
-    }
-    UNIFORM_STRIDE(j, valid, nloop) {
-        size_t i = j;
-        uint32_t want = 0, defer = 0;
+    UNIFORM_STRIDE(i, valid, P) {
+        uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
-        uint32_t pi = 0, L = 0, kx = 0;
-        uint64_t rem = 0;
-        uint4 cw = make_uint4(0, 0, 0, 0);  // phase 2: the continuation (i, d, b, e)
+        uint32_t pi, L, kx = 0;
+        uint64_t rem;
         cs.last = 0;
-        if (cmode == 2) {
-            if (valid) {
-                uint32_t lo = 0, hi = NSHARD;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (cpre[mid] <= (uint32_t)j) lo = mid; else hi = mid;
-                }
-                const size_t qi = (size_t)lo * qcap + ((uint32_t)j - cpre[lo]);
-                cw = cq[qi];
-                const uint64_t v = cq2[qi];
-                i = cw.x;
-                pi = (uint32_t)(v & 0x7fffffffu);
-                rem = v >> 31;
-                L = pk_len(D0, rem);
-            }
-        } else if constexpr (FUSED) {
+        if constexpr (FUSED) {
             // each lane loads its own pattern's bytes: the three 16-B words from a & ~15 cover
             // L <= 32 bytes (the wave's 64 patterns are consecutive, so those loads share lines);
             // no LDS stage, no block barrier between the lanes' walks
@@ -1676,13 +1624,13 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             rem = v >> 31;
             L = valid ? pk_len(D0, rem) : 0u;
         }
-        if (valid && cmode != 2) perm_out[i] = pi;
+        if (valid) perm_out[i] = pi;
         // the D-mer's wide entry: its one interval inline (or its list's length), and for one
         // row with its text position, the row's sample and the 32 text characters before it
         uint64_t ent = 0, win1 = 0;
         uint4 s1 = make_uint4(0, 0, 0, 0);
         uint32_t u = 0;
-        if (L > D0 && cmode != 2) {
+        if (L > D0) {
             u = FUSED ? kx : nid[i];
             const uint4 w0 = kt1w[2 * (size_t)u];
             s1 = kt1w[2 * (size_t)u + 1];
@@ -1690,7 +1638,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             win1 = (uint64_t)w0.w << 32 | w0.z;
             n_blk++;  // the entry's 32 B: one line
         }
-        const uint32_t n0 = cmode == 2 ? (valid ? 1u : 0u) : L <= D0 ? 0u : (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
+        const uint32_t n0 = L <= D0 ? 0u : (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
         if (n0 > 1) {
             want = 1;
             w = make_uint4((uint32_t)i, D0, kQWide, u);
@@ -1711,20 +1659,13 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             auto code_at = [&](uint32_t dd) -> uint32_t { return 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u); };
             bool alive = true, pair_skip = false, posres = false;
             uint32_t d = D0;
-            if (cmode == 2) {  // phase 2: the walk goes on from the continuation
-                d = cw.y;
-                b = cw.z;
-                e = cw.w;
-                g1 = ~0u;
-            }
             if (g1 != ~0u) DD_CNT(c_one);
             // the row's sample and text window: the wide entry's for the first row (have), loaded
             // for rows reached through a link
             uint4 s = s1;
             uint64_t tw = win1;
             bool have = g1 != ~0u;
-            if (cmode == 1 && !have) defer = 1;  // a multi-row interval (or a row without its text): phase 2
-            while (!defer && X.rtext && b == e && d < L) {
+            while (X.rtext && b == e && d < L) {
                 // one row = one text position: the next k = min(o, m) <= 16 characters against the
                 // text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row), as in k_deep_fast
                 uint32_t g = 0;
@@ -1777,24 +1718,6 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                     d = L;
                     break;
                 }
-                if (X.segtab3 && d + 2 < L) {  // the link and the next two characters from one read
-                    const uint32_t c2 = code_at(d + 1), c3 = code_at(d + 2);
-                    const uint2 v = X.segtab3[(((size_t)s.z * 4 + (c - 1)) * 4 + (c2 - 1)) * 4 + (c3 - 1)];
-                    n_blk++;
-                    DD_CNT(c_seg);
-                    if (v.x != ~0u) {
-                        if (v.x > v.y) {
-                            alive = false;
-                            d = L;
-                            break;
-                        }
-                        n_steps += 3;
-                        b = v.x;
-                        e = v.y;
-                        d += 3;
-                        continue;
-                    }
-                }
                 const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
                 const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
                 n_blk++;
@@ -1808,12 +1731,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 b = X.C[c] + rx;
                 e = X.C[c] + ry - 1;
                 d++;
-                if (cmode == 1) {  // past the entry's word: phase 2 walks on from the link
-                    defer = 1;
-                    break;
-                }
             }
-            for (; !defer && d < L; d++) {
+            for (; d < L; d++) {
                 const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
                 // two characters from one rank entry per interval end (rent2), else one step
@@ -1851,7 +1770,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 b = X.C[c] + sb;
                 e = X.C[c] + se - 1;
             }
-            if (want || defer) {
+            if (want) {
                 w = make_uint4((uint32_t)i, d, b, e);
             } else if (!posres) {
                 if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
@@ -1859,18 +1778,11 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 cs.put(counts, pi, alive ? e - b + 1 : 0u);
             }
         }
-        if (want || defer) put_res(res, pi, 0, 0u, 0u);  // the zeroed result the later walks expect
+        if (want) put_res(res, pi, 0, 0u, 0u);  // the zeroed result the later walks expect
         const uint32_t at = wave_append(qcnt + sh * 32, want);
         if (want && at < qcap) {
             q[at] = w;
             q2[at] = rem << 31 | pi;  // the packed start: k_deep reads it instead of perm, slen and the key chunks
-        }
-        if (cmode == 1) {  // (a kernel argument: uniform)
-            const uint32_t cat = wave_append(ccnt + sh * 32, defer);
-            if (defer && cat < qcap) {
-                cq[cat] = w;
-                cq2[cat] = rem << 31 | pi;
-            }
         }
         if (tsum) {  // (a kernel argument: uniform)
             const unsigned long long t = wave_sum((unsigned long long)cs.last);
@@ -3981,48 +3893,6 @@ __global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
         for (uint32_t c = 0; c < X.sigma; c++) {
             e[1 + c] = r0[c];
             e[X.seg_hi + c] = r1[c];
-        }
-    }
-}
-
-// KIdx::segtab3: one thread per (segment, c); the link interval of c from the segment link table's
-// ranks, then every c2 and c3 step from two all-symbol ranks per interval
-__global__ void k_segtab3(uint32_t S, KIdx X, uint2* __restrict__ out) {
-    const uint2 kSeg3Dead = make_uint2(1u, 0u), kSeg3Fallback = make_uint2(~0u, ~0u);
-    GRID_STRIDE(t, ((size_t)S + 2) * 4) {
-        const size_t s = t >> 2;
-        const uint32_t c = 1u + (uint32_t)(t & 3u);
-        uint2* o = out + t * 16;
-        const uint32_t* et = X.segtab + s * X.seg_stride;
-        const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
-        if (s < 2 || ry <= rx) {
-#pragma unroll
-            for (int k = 0; k < 16; k++) o[k] = kSeg3Dead;
-            continue;
-        }
-        const uint32_t b0 = X.C[c] + rx, e0 = X.C[c] + ry - 1;
-        uint32_t p0[8], p1[8];
-        rank_all(X.occ, b0, X.sigma, p0);
-        rank_all(X.occ, e0 + 1, X.sigma, p1);
-        for (uint32_t c2 = 1; c2 <= 4; c2++) {
-            uint2* o2 = o + (c2 - 1) * 4;
-            if (p1[0] > p0[0]) {  // '#' rows in the link interval
-                for (int k = 0; k < 4; k++) o2[k] = kSeg3Fallback;
-                continue;
-            }
-            if (p1[c2] <= p0[c2]) {
-                for (int k = 0; k < 4; k++) o2[k] = kSeg3Dead;
-                continue;
-            }
-            const uint32_t b1 = X.C[c2] + p0[c2], e1 = X.C[c2] + p1[c2] - 1;
-            uint32_t q0[8], q1[8];
-            rank_all(X.occ, b1, X.sigma, q0);
-            rank_all(X.occ, e1 + 1, X.sigma, q1);
-            for (uint32_t c3 = 1; c3 <= 4; c3++) {
-                if (q1[0] > q0[0]) o2[c3 - 1] = kSeg3Fallback;
-                else if (q1[c3] <= q0[c3]) o2[c3 - 1] = kSeg3Dead;
-                else o2[c3 - 1] = make_uint2(X.C[c3] + q0[c3], X.C[c3] + q1[c3] - 1);
-            }
         }
     }
 }

@@ -76,7 +76,7 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # character per step (no pair entries)
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "6"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
-                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0"), ("EDSBWT_DIRECT_SPLIT", "1")):
+                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -548,26 +548,20 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     for pats in (short, short + ["ACGT" * 4, "A" * (D0 + 17)]):
         buf, offs = _pack(pats)
         oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
-        # ... each also as the split walk (EDSBWT_DIRECT_SPLIT=1: the walks the wide entry does not
-        # finish go on in k_deep_direct's second phase) and with the record-offset tiles fused in
-        # ... and with the links past a matched word and their next two characters from the segment
-        # link + two characters table (EDSBWT_SEGTAB3=1) instead of the segment rows
-        for fused, split, tiles, seg3 in (("1", "0", "0", "0"), ("0", "0", "0", "0"), ("1", "1", "0", "0"), ("0", "1", "0", "1"),
-                                          ("1", "1", "1", "0"), ("1", "0", "0", "1")):
+        # (and the record-offset tiles summed inside the deep kernels, EDSBWT_TILE_FUSE=1)
+        for fused, tiles in (("1", "0"), ("0", "0"), ("1", "1")):
             monkeypatch.setenv("EDSBWT_FUSED_KEYS", fused)
-            monkeypatch.setenv("EDSBWT_DIRECT_SPLIT", split)
             monkeypatch.setenv("EDSBWT_TILE_FUSE", tiles)
-            monkeypatch.setenv("EDSBWT_SEGTAB3", seg3)
             for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED"):
                 monkeypatch.delenv(k_, raising=False)
             with edsbwt.Index(base) as idx:
                 for kw in ({}, {"locate": False}):
                     gc, go = idx.search((buf, offs), **kw)
-                    assert np.array_equal(gc, oc), (fused, split, tiles, seg3, kw, len(pats))
+                    assert np.array_equal(gc, oc), (fused, tiles, kw, len(pats))
                     if kw.get("locate", True):
-                        assert np.array_equal(go, oo), (fused, split, tiles, seg3, kw, len(pats))
-    for k_ in ("EDSBWT_FUSED_KEYS", "EDSBWT_DIRECT_SPLIT", "EDSBWT_TILE_FUSE", "EDSBWT_SEGTAB3"):
-        monkeypatch.delenv(k_)
+                        assert np.array_equal(go, oo), (fused, tiles, kw, len(pats))
+    monkeypatch.delenv("EDSBWT_FUSED_KEYS")
+    monkeypatch.delenv("EDSBWT_TILE_FUSE")
     E = (4 ** D0) + 1
     assert sizes["11"] - sizes["01"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
     assert sizes["11"] > sizes["10"]  # ... and the per-row entries
