@@ -591,6 +591,9 @@ struct Engine {
     // the level walk's located results with dense samples: k_locate_lists (a wave per pattern, records
     // from the lists directly); EDSBWT_LOCATE_LISTS=0: tasks + k_locate (C5 located step: see DESIGN §6)
     bool locate_lists = env_double("EDSBWT_LOCATE_LISTS", 1) != 0;
+    // k_deep_direct's per-lane work counters (steps, lines, text rows: the line model of bench.py's
+    // roofline); EDSBWT_DEEP_STATS=0 runs its build without them (8 waves per SIMD, fused keys)
+    bool deep_stats = env_double("EDSBWT_DEEP_STATS", 1) != 0;
     bool fc_tiles_want = false, tiles_done = false;
     uint32_t* fc_locate_counts = nullptr;
     bool fc_done = false;           // ... and k_deep_direct took them
@@ -2013,8 +2016,8 @@ struct Engine {
         if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
             // written there, for k_deep and k_deep_wave)
-            auto kd0 = direct_waves >= 8 ? k_deep_direct<8, true> : direct_waves >= 7 ? k_deep_direct<7, true>
-                     : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
+            auto kd0 = direct_waves >= 8 ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
+                     : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
                    fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, ts);
             fk_now.on = false;

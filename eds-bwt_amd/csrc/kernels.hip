@@ -1558,7 +1558,21 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
 // C3 stream traffic less.  kid and len are still written for every pattern (k_deep and
 // k_deep_wave read the queued ones'), and '#' / unexpected lengths counted into n_term for the
 // deferred check.
-template <int MINW, bool FUSED = false>
+// per-lane statistics counter that compiles away when the kernel is built without statistics
+template <bool ON>
+struct LaneCtr {
+    uint32_t v = 0;
+    __device__ __forceinline__ void operator+=(uint32_t x) {
+        if constexpr (ON) v += x;
+    }
+    __device__ __forceinline__ void operator++(int) {
+        if constexpr (ON) v++;
+    }
+};
+
+// STATS = false (EDSBWT_DEEP_STATS=0): no per-lane work counters (steps, lines, text rows) — five
+// registers fewer in a kernel whose time follows its register pressure
+template <int MINW, bool FUSED = false, bool STATS = true>
 __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
                                                            uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
                                                            uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
@@ -1568,7 +1582,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                                                            uint32_t* __restrict__ len_out, uint32_t* __restrict__ kid_out,
                                                            unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax,
                                                            uint32_t* __restrict__ counts, unsigned long long* __restrict__ tsum) {
-    uint32_t n_steps = 0, n_blk = 0, n_pl = 0, n_text = 0, n_trow = 0;  // per lane: < 2^32 (widened at the end)
+    LaneCtr<STATS> n_steps, n_blk, n_pl, n_text, n_trow;  // per lane: < 2^32 (widened at the end)
     CountSums cs;  // counts != nullptr: each final count written here (fused counts)
     // tsum (input order, FUSED): each wave's 64 patterns are one record-offset tile; its sum of the
     // counts written here is stored, k_deep / k_deep_wave add their patterns' counts after it
@@ -1790,11 +1804,11 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         }
     }
     __shared__ unsigned long long ssum[4];
-    stat_add(ctr, ST_DEEP_STEPS, n_steps, ssum);
-    stat_add(ctr, ST_DEEP_BLOCKS, n_blk, ssum);
-    stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl, ssum);
-    stat_add(ctr, ST_TEXT_CHARS, n_text, ssum);
-    stat_add(ctr, ST_TEXT_ROWS, n_trow, ssum);
+    stat_add(ctr, ST_DEEP_STEPS, n_steps.v, ssum);
+    stat_add(ctr, ST_DEEP_BLOCKS, n_blk.v, ssum);
+    stat_add(ctr, ST_DEEP_PAIR_LINES, n_pl.v, ssum);
+    stat_add(ctr, ST_TEXT_CHARS, n_text.v, ssum);
+    stat_add(ctr, ST_TEXT_ROWS, n_trow.v, ssum);
     cs.flush(counts, ctr, ssum);
 #ifdef EDSBWT_DEEP_CLOCKS
     stat_add(ctr, ST_CLK_DD_SROW, c_srow, ssum);
