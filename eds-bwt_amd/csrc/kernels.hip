@@ -1593,7 +1593,12 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
-    UNIFORM_STRIDE(i, valid, P) {
+    // 32-bit pattern indices (the engine keeps a search's batch below 2^31 patterns): fewer registers
+    // and no 64-bit index arithmetic in a kernel whose time follows its register pressure
+    const uint32_t P32 = (uint32_t)P, stride32 = gridDim.x * blockDim.x;
+    for (uint32_t i_b = blockIdx.x * blockDim.x; i_b < P32; i_b += stride32) {
+        const uint32_t i = i_b + threadIdx.x;
+        const bool valid = i < P32;
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
         uint32_t pi, L, kx = 0;
@@ -1788,7 +1793,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 w = make_uint4((uint32_t)i, d, b, e);
             } else if (!posres) {
                 if (alive) put_res(res, pi, b, 1u | kResRow, e - b + 1);
-                else put_res(res, pi, abase + i * K, 0u, 0u);
+                else put_res(res, pi, abase + (uint64_t)i * K, 0u, 0u);
                 cs.put(counts, pi, alive ? e - b + 1 : 0u);
             }
         }
