@@ -1589,7 +1589,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
 #ifdef EDSBWT_DEEP_CLOCKS
     uint32_t c_srow = 0, c_seg = 0, c_wrow = 0, c_one = 0;
 #endif
-    unsigned long long nt = 0;
+    uint32_t nt = 0;  // patterns holding '#' or of unexpected lengths (per lane)
     const uint32_t sh = blockIdx.x % NSHARD;
     q += (size_t)sh * qcap;
     q2 += (size_t)sh * qcap;
@@ -1822,8 +1822,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     stat_add(ctr, ST_CLK_DD_ONE, c_one, ssum);
 #endif
     if constexpr (FUSED) {
-        nt = block_sum(nt, ssum);
-        if (threadIdx.x == 0 && nt) atomicAdd(n_term, nt);
+        const unsigned long long ntb = block_sum((unsigned long long)nt, ssum);
+        if (threadIdx.x == 0 && ntb) atomicAdd(n_term, ntb);
     }
 }
 
@@ -1883,7 +1883,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
     }
     __syncthreads();
     const uint32_t total = spre[NSHARD];
-    GRID_STRIDE(j, total) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {  // (32-bit: fewer registers)
         uint32_t lo = 0, hi = NSHARD;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
