@@ -623,7 +623,9 @@ struct Engine {
     // k_deep<4, 3> likewise (5 or 6; C3 0.371 / 0.478 ms against 0.369 unbounded, profiles/r03_ab_occupancy.txt);
     // 1: the unbounded builds (k_deep<4, 3, 1>, <4, 4, 1>, the '#'-row link rows' <4, 3, 1, true>) —
     // every build is run through the parity tests (tests/test_gpu_parity.py::test_k_deep_builds_gpu)
-    int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 5);
+    // (round 5, 32-bit queue indices: 6 waves 0.294-0.301 ms against 0.310-0.316 at 5 and 0.71 at 8,
+    // profiles/r05_ab_c3_deepq_waves_568.txt)
+    int deepq_waves = (int)env_double("EDSBWT_DEEPQ_WAVES", 6);
     // locate tasks one wave per pattern when lists average more than kTasksWaveRatio intervals
     // (EDSBWT_TASKS_WAVE=0: k_tasks, one lane per pattern, always)
     static constexpr uint64_t kTasksWaveRatio = 8;
@@ -2041,7 +2043,7 @@ struct Engine {
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? (X.eofrow ? (unb ? k_deep<4, 3, 1, true> : k_deep<4, 3, 5, true>)
-                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 8 ? k_deep<4, 3, 8> : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
+                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
                                        : unb ? k_deep<4, 4, 1> : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,

@@ -70,12 +70,12 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # the defaults' A/B fallbacks (read when an index opens): the finisher pass instead of the
     # fused count (k_fin_flags / k_fin_emit), no text items, eof_seg link keys without the chain
     # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
-    # the dollar step's text-item entries, k_deep's other dispatched build (6 waves per SIMD), the
+    # the dollar step's text-item entries, k_deep's other dispatched build (5 waves per SIMD), the
     # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
     # counts instead of per-tile record offsets, the locate kernel's own counts, and k_deep one
     # character per step (no pair entries)
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
-                     ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "6"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
+                     ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "5"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
                      ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
@@ -1127,7 +1127,7 @@ def test_counts_mirror_gpu(oracle, edsbwt, tmp_path, monkeypatch):
 # every k_deep build the engine can dispatch (engine.hip run_deep): the register-list lengths
 # (EDSBWT_DEEP_K 2 / 3 / 4 / 8), the 4-interval build unbounded (EDSBWT_DEEPQ_WAVES=1) and held to
 # 5 / 6 waves per SIMD, and the '#'-row link-row variant (EDSBWT_EOF_ROWS=1) unbounded and at 5 waves
-K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDSBWT_DEEPQ_WAVES": "6"}, {"EDSBWT_DEEPQ_WAVES": "8"},
+K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDSBWT_DEEPQ_WAVES": "6"},
                  {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "5"},
                  {"EDSBWT_DEEP_K": "2"}, {"EDSBWT_DEEP_K": "3"}, {"EDSBWT_DEEP_K": "8"}]
 
