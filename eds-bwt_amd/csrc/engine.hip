@@ -583,19 +583,15 @@ struct Engine {
     uint32_t loc_stage = (uint32_t)env_double("EDSBWT_LOC_STAGE", 1024);
     DBuf<uint64_t> tile_sum, tile_pre;  // per-pattern locate: occurrences per 64-pattern tile, and their exclusive scan
     uint32_t* fc_counts = nullptr;  // this search's counts when the deep kernels write them
-    // ... and on the per-pattern locate's fused direct start with the record-offset tile sums
-    // (EDSBWT_TILE_FUSE=1; off by default: the tiles need the input-order start and per-put atomics in
-    // k_deep, which cost more than the k_count_tiles pass they save — C3 1.85 / 1.83 ms fused against
-    // 1.69 ms with k_count_tiles, k_deep_direct 1.11 against 0.96 ms, profiles/r05_ab_c3_tile_fuse_*.json)
-    bool tile_fuse = env_double("EDSBWT_TILE_FUSE", 0) != 0;
+    // (round 5 also summed the per-pattern locate's record-offset tiles inside the deep kernels: C3 1.85 /
+    // 1.83 ms against 1.69 ms with k_count_tiles, k_deep_direct 1.11 against 0.96 ms —
+    // profiles/r05_ab_c3_tile_fuse_*.json — so that path was removed)
     // the level walk's located results with dense samples: k_locate_lists (a wave per pattern, records
     // from the lists directly); EDSBWT_LOCATE_LISTS=0: tasks + k_locate (C5 located step: see DESIGN §6)
     bool locate_lists = env_double("EDSBWT_LOCATE_LISTS", 1) != 0;
     // k_deep_direct's per-lane work counters (steps, lines, text rows: the line model of bench.py's
     // roofline); EDSBWT_DEEP_STATS=0 runs its build without them (8 waves per SIMD, fused keys)
     bool deep_stats = env_double("EDSBWT_DEEP_STATS", 1) != 0;
-    bool fc_tiles_want = false, tiles_done = false;
-    uint32_t* fc_locate_counts = nullptr;
     bool fc_done = false;           // ... and k_deep_direct took them
     static constexpr uint32_t kWideCap = 16384;
     static constexpr uint32_t kWaveGrid = 2048;  // k_deep_wave's waves (each strides over the wide list)
@@ -2004,16 +2000,6 @@ struct Engine {
         if (!kdd) settle_res(r);  // (k_deep_direct writes every result; the other walks need zeros)
         // fused counts: only on the deferred direct start (its three kernels write every final count)
         uint32_t* fc = kdd && defer ? fc_counts : nullptr;
-        // per-pattern locate on the fused (input-order) direct start: the deep kernels also write the
-        // counts and each 64-pattern tile's record total (k_deep_direct per wave, k_deep / k_deep_wave
-        // by atomics), so finish_deferred runs no k_count_tiles pass over the results
-        unsigned long long* ts = nullptr;
-        if (!fc && kdd && defer && fk_now.on && fc_tiles_want) {
-            fc = fc_locate_counts;
-            tile_sum.ensure((P + 63) / 64);
-            ts = (unsigned long long*)tile_sum.p;
-            tiles_done = true;
-        }
         if (fc) fc_done = true;
         if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
@@ -2021,14 +2007,14 @@ struct Engine {
             auto kd0 = direct_waves >= 8 ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
                      : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
-                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, ts);
+                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc);
             fk_now.on = false;
         } else if (kdd) {
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
                                                                                                         : k_deep_direct<1>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
                    (const uint8_t*)nullptr, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned long long*)nullptr, 0u,
-                   0u, 0u, fc, (unsigned long long*)nullptr);
+                   0u, 0u, fc);
         } else {
             auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
             launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
@@ -2048,7 +2034,7 @@ struct Engine {
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
-               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc, deepq_pairs, ts);
+               pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc, deepq_pairs);
         tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
@@ -2071,7 +2057,7 @@ struct Engine {
                 if (deep_wave)
                     launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(wcap, kWaveGrid) * 64, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
                            d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
-                           (const uint32_t*)ovf.p, stats.p, fc, ts);
+                           (const uint32_t*)ovf.p, stats.p, fc);
                 else
                     launch(KC_DEEPW, k_deep_wide<kDeepWide>, wcap, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
                            d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
@@ -2095,7 +2081,7 @@ struct Engine {
             if (deep_wave)
                 launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(nw, kWaveGrid) * 64, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
-                       (const uint32_t*)nullptr, stats.p, (uint32_t*)nullptr, (unsigned long long*)nullptr);
+                       (const uint32_t*)nullptr, stats.p, (uint32_t*)nullptr);
             else
                 launch(KC_DEEPW, k_deep_wide<kDeepWide>, nw, P, d, list, nw, lens, (const uint32_t*)perm.p, ind,
                        d_off, d_bytes, (const uint8_t*)code_of.p, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf2.p,
@@ -2819,17 +2805,8 @@ struct Engine {
         defer_call = defer_ok && !(flags & (kFlagNoDefer | EDSBWT_LEGACY_ORDER)) && !force_groups && !sticky_groups;
         fc_done = false;
         fc_counts = nullptr;
-        // (count-only; the per-pattern locate writes them in k_locate_pp instead, finish_deferred —
-        // or, on the fused direct start, in the deep kernels with the record-offset tile sums: run_deep)
-        fc_tiles_want = false;
-        fc_locate_counts = nullptr;
-        tiles_done = false;
+        // (count-only; the per-pattern locate writes them in k_count_tiles or k_locate_pp instead, finish_deferred)
         if (defer_call && fused_counts && (deep_wave || no_wide) && !locate) fc_counts = d_counts;
-        if (defer_call && fused_counts && (deep_wave || no_wide) && locate && tile_fuse && tile_scan && loc_mode == 2 &&
-            kidx().samp_dense && locate_pp && !locate_counts) {
-            fc_tiles_want = true;
-            fc_locate_counts = d_counts;
-        }
         if (P == 0) return 0;
         struct EvPair {  // released on every exit, including exceptions
             hipEvent_t a = nullptr, b = nullptr;
@@ -3112,8 +3089,7 @@ struct Engine {
         if (tiles) {
             tile_sum.ensure(ntile);
             tile_pre.ensure(ntile);
-            if (!tiles_done)  // (else written by the deep kernels, with the counts: run_deep)
-                launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
+            launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
         } else if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);

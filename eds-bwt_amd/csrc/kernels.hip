@@ -388,21 +388,17 @@ __device__ __forceinline__ void stat_add(unsigned long long* __restrict__ stats,
 // a final result's count into counts[o] (fused counts), and the lane's found / occurrence sums in
 // two u32 registers: the occurrence sum saturates at 2^32 - 1, which fails the deferred checks'
 // record-capacity test (a batch with that many records is searched again on the checked path).
-// The interval total is not kept: the deferred path that fuses counts (per-pattern locate or
-// count-only) never builds the task list it bounds
-// tile (the per-pattern locate's record offsets fused in, engine.hip finish_deferred): each put adds
-// its count into the pattern's 64-pattern tile sum (k_deep, k_deep_wave: atomics after
-// k_deep_direct's per-wave stores); last = the last put's count (k_deep_direct sums its wave's)
+// The interval total is not kept: the deferred path that fuses counts (count-only) never builds
+// the task list it bounds.  (Round 5 also summed the per-pattern locate's 64-pattern record tiles
+// here — a register and an atomic per put in every deep kernel — and measured it slower than
+// k_count_tiles' pass: removed)
 struct CountSums {
-    uint32_t f = 0, occ = 0, last = 0;
-    unsigned long long* tile = nullptr;
+    uint32_t f = 0, occ = 0;
     __device__ __forceinline__ void put(uint32_t* __restrict__ counts, size_t o, uint32_t occ_) {
         if (!counts) return;
         counts[o] = occ_;
         f += occ_ > 0;
         occ = occ + occ_ < occ ? 0xFFFFFFFFu : occ + occ_;
-        last = occ_;
-        if (tile && occ_) atomicAdd(tile + (o >> 6), (unsigned long long)occ_);
     }
     // every thread of the block
     __device__ __forceinline__ void flush(const uint32_t* counts, unsigned long long* __restrict__ ctr, unsigned long long* sh) {
@@ -1581,11 +1577,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                                                            const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                            uint32_t* __restrict__ len_out, uint32_t* __restrict__ kid_out,
                                                            unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax,
-                                                           uint32_t* __restrict__ counts, unsigned long long* __restrict__ tsum) {
+                                                           uint32_t* __restrict__ counts) {
     LaneCtr<STATS> n_steps, n_blk, n_pl, n_text, n_trow;  // per lane: < 2^32 (widened at the end)
     CountSums cs;  // counts != nullptr: each final count written here (fused counts)
-    // tsum (input order, FUSED): each wave's 64 patterns are one record-offset tile; its sum of the
-    // counts written here is stored, k_deep / k_deep_wave add their patterns' counts after it
 #ifdef EDSBWT_DEEP_CLOCKS
     uint32_t c_srow = 0, c_seg = 0, c_wrow = 0, c_one = 0;
 #endif
@@ -1603,7 +1597,6 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         uint4 w = make_uint4(0, 0, 0, 0);
         uint32_t pi, L, kx = 0;
         uint64_t rem;
-        cs.last = 0;
         if constexpr (FUSED) {
             // each lane loads its own pattern's bytes: the three 16-B words from a & ~15 cover
             // L <= 32 bytes (the wave's 64 patterns are consecutive, so those loads share lines);
@@ -1803,10 +1796,6 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             q[at] = w;
             q2[at] = rem << 31 | pi;  // the packed start: k_deep reads it instead of perm, slen and the key chunks
         }
-        if (tsum) {  // (a kernel argument: uniform)
-            const unsigned long long t = wave_sum((unsigned long long)cs.last);
-            if ((threadIdx.x & 63) == 0 && valid) tsum[i >> 6] = t;
-        }
     }
     __shared__ unsigned long long ssum[4];
     stat_add(ctr, ST_DEEP_STEPS, n_steps.v, ssum);
@@ -1850,11 +1839,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2,
-                                              const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts, uint32_t qpairs,
-                                              unsigned long long* __restrict__ tsum) {
+                                              const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts, uint32_t qpairs) {
     uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;
     CountSums cs;  // n_blk: occ blocks read (per lane, widened at the end)
-    cs.tile = tsum;
 #ifdef EDSBWT_DEBUG_CHECKS
     uint32_t dbg_q = 0, dbg_p = 0, dbg_w = 0, dbg_l = 0;
 #endif
@@ -2404,11 +2391,9 @@ __global__ void __launch_bounds__(256) k_deep_wave(uint64_t P, uint32_t D0, cons
                                                   const uint32_t* __restrict__ ib, const uint32_t* __restrict__ ie, KIdx X, uint64_t abase,
                                                   uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                                   uint32_t* __restrict__ ovf2, const uint32_t* __restrict__ ntodo_dev,
-                                                  unsigned long long* __restrict__ ctr, uint32_t* __restrict__ counts,
-                                                  unsigned long long* __restrict__ tsum) {
+                                                  unsigned long long* __restrict__ ctr, uint32_t* __restrict__ counts) {
     (void)P;
     CountSums cs;  // (lane 0 of each wave puts its patterns' counts)
-    cs.tile = tsum;
     __shared__ uint32_t s_seg[4][kWaveHash], s_tmp[4][kWaveHash];
     __shared__ uint32_t s_b[4][192], s_e[4][192];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;

@@ -548,21 +548,19 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     for pats in (short, short + ["ACGT" * 4, "A" * (D0 + 17)]):
         buf, offs = _pack(pats)
         oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
-        # (and the record-offset tiles summed inside the deep kernels, EDSBWT_TILE_FUSE=1, and
-        # k_deep_direct's build without work counters, EDSBWT_DEEP_STATS=0)
-        for fused, tiles, stats in (("1", "0", "1"), ("0", "0", "1"), ("1", "1", "1"), ("1", "0", "0")):
+        # (and k_deep_direct's build without work counters, EDSBWT_DEEP_STATS=0)
+        for fused, stats in (("1", "1"), ("0", "1"), ("1", "0")):
             monkeypatch.setenv("EDSBWT_FUSED_KEYS", fused)
-            monkeypatch.setenv("EDSBWT_TILE_FUSE", tiles)
             monkeypatch.setenv("EDSBWT_DEEP_STATS", stats)
             for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED"):
                 monkeypatch.delenv(k_, raising=False)
             with edsbwt.Index(base) as idx:
                 for kw in ({}, {"locate": False}):
                     gc, go = idx.search((buf, offs), **kw)
-                    assert np.array_equal(gc, oc), (fused, tiles, stats, kw, len(pats))
+                    assert np.array_equal(gc, oc), (fused, stats, kw, len(pats))
                     if kw.get("locate", True):
-                        assert np.array_equal(go, oo), (fused, tiles, stats, kw, len(pats))
-    for k_ in ("EDSBWT_FUSED_KEYS", "EDSBWT_TILE_FUSE", "EDSBWT_DEEP_STATS"):
+                        assert np.array_equal(go, oo), (fused, stats, kw, len(pats))
+    for k_ in ("EDSBWT_FUSED_KEYS", "EDSBWT_DEEP_STATS"):
         monkeypatch.delenv(k_)
     E = (4 ** D0) + 1
     assert sizes["11"] - sizes["01"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
