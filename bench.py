@@ -286,6 +286,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=0)
     ap.add_argument("--no-device", action="store_true", help="skip the device-resident leg")
+    ap.add_argument("--timed-counters", action="store_true",
+                    help="run the timed steps with the deep kernels' work counters (rounds 1-5); default: the timed "
+                         "steps pass EDSBWT_NO_COUNTERS and one untimed counted step gives the line model")
     ap.add_argument("--no-e2e", action="store_true",
                     help="profiling runs: only the device-resident leg (its kernel averages then match a rocprofv3 "
                          "trace of the whole run); the line's value is then the device-resident rate")
@@ -511,10 +514,22 @@ def main():
         d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
         d_counts = torch.zeros(npat, dtype=torch.int32, device=dev)
 
-        def dev_step(profile=False):
-            return idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(), first_pattern_id=first_id,
-                                     locate=locate, profile=profile, stream=stream, **flags_kw)
+        # the timed steps run the deep kernels' builds without their work counters (EDSBWT_NO_COUNTERS:
+        # same results, fewer registers); the line model (bytes / lines per launch, intervals stepped)
+        # comes from one counted step, untimed, before the warm-up
+        counted = args.timed_counters or located_timed
 
+        def dev_step(profile=False, counters=counted):
+            return idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(), first_pattern_id=first_id,
+                                     locate=locate, profile=profile, stream=stream, counters=counters, **flags_kw)
+
+        kacc_c = stats_c = None
+        if not counted:
+            kacc_c = idx.kernel_acc()
+            _, dn = dev_step(profile=PROFILE_TIMED, counters=True)
+            exchange(dn, d_counts)
+            idx.add_kernel_stats(kacc_c)
+            stats_c = idx.stats()
         for _ in range(max(1, args.warmup)):
             _, dn = dev_step()
             exchange(dn, d_counts)
@@ -560,8 +575,15 @@ def main():
             tt = torch.tensor([d_elapsed], dtype=torch.float64, device=gdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             d_elapsed = float(tt.item())
+        dstats = idx.stats()
+        if kacc_c is not None:
+            # the timed steps' HIP-event times and launches; bytes and lines per step from the counted
+            # step (a step's work is the same every step); its statistics for the interval steps
+            kacc[2:4] = kacc_c[2:4] * args.steps
+            dstats = stats_c
         kstats = idx.kernel_acc_dict(kacc)
-        dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": idx.stats(), "d_counts": d_counts}
+        dres = {"elapsed": d_elapsed, "kstats": kstats, "stats": dstats, "d_counts": d_counts,
+                "counters": "timed" if counted else "one untimed counted step (timed steps: EDSBWT_NO_COUNTERS)"}
         if not located_timed and not args.no_e2e and not np.array_equal(d_counts.cpu().numpy().view(np.uint32), counts_last):
             raise SystemExit("bench.py: device-resident counts differ from the end-to-end counts")
         if located is not None:
@@ -705,6 +727,7 @@ def main():
                                                     "intervals) over the whole device-resident step; omits the text "
                                                     "compares, table entries, link sorts and stores"},
                 "from": "device_resident leg (HIP events on the library stream, EDSBWT_PROFILE_LIGHT)",
+                "counters": dres["counters"],
             }
             out["device_resident"] = {
                 "value": round(total_pats * args.steps / dres["elapsed"], 1), "ms_per_step": round(d_ms, 3),

@@ -40,6 +40,7 @@ NO_KTAB = 0x400
 NO_DIRECT = 0x800
 NO_PAIRS = 0x1000
 NO_TEXT = 0x2000
+NO_COUNTERS = 0x4000
 
 # edsbwt_last_paths bits (EDSBWT_PATH_TAGS=1): the kernels a pattern went through
 PATH_DEEP = 0x1
@@ -274,7 +275,7 @@ class Index:
     def search(self, patterns: Sequence[bytes | str] | tuple[np.ndarray, np.ndarray], *, first_pattern_id: int = 1,
                locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
                ordered: bool = False, wide: bool = True, walk: bool = False, legacy: bool = False,
-               ktab: bool = True, direct: bool = True, pairs: bool = True, text: bool = True):
+               ktab: bool = True, direct: bool = True, pairs: bool = True, text: bool = True, counters: bool = True):
         """Search a batch.  Returns (counts u32[npat], occ OCC_DTYPE[nocc]).
         ``table``: (word, offset) per row from the full table; ``walk``: the reference's
         full LF walk to '#'; default: walk to the first sampled row.  ``legacy``: records in
@@ -287,7 +288,8 @@ class Index:
         flags = ((LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | (PROFILE if profile else 0)
                  | (0 if deep else NO_DEEP) | (ORDERED if ordered else 0) | (0 if wide else NO_WIDE)
                  | (LOCATE_WALK if walk else 0) | (LEGACY_ORDER if legacy else 0) | (0 if ktab else NO_KTAB)
-                 | (0 if direct else NO_DIRECT) | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT))
+                 | (0 if direct else NO_DIRECT) | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT)
+                 | (0 if counters else NO_COUNTERS))
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         bp = buf.ctypes.data if buf.size else None
@@ -340,14 +342,15 @@ class Index:
     def search_device(self, d_bytes: int, d_offsets: int, npat: int, d_counts: int, *, first_pattern_id: int = 1,
                       locate: bool = True, table: bool = False, profile: bool = False, deep: bool = True,
                       stream: int = 0, walk: bool = False, ktab: bool = True, direct: bool = True,
-                      pairs: bool = True, text: bool = True, ids: int = 0):
+                      pairs: bool = True, text: bool = True, ids: int = 0, counters: bool = True):
         """Device-resident batch (pointers are device addresses, e.g. torch data_ptr()).
         ids: device array of npat u32 — pattern i is reported as #Pat ids[i] (edsbwt_search_device_ids)
-        instead of first_pattern_id + i.  Returns (device pointer of the records, number of records)."""
+        instead of first_pattern_id + i.  counters=False: EDSBWT_NO_COUNTERS (the deep kernels' work
+        statistics read 0; same results).  Returns (device pointer of the records, number of records)."""
         pflag = {False: 0, True: PROFILE, "light": PROFILE_LIGHT}[profile]
         flags = (LOCATE if locate else COUNT_ONLY) | (LOCATE_TABLE if table else 0) | pflag | (0 if deep else NO_DEEP) \
             | (LOCATE_WALK if walk else 0) | (0 if ktab else NO_KTAB) | (0 if direct else NO_DIRECT) \
-            | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT)
+            | (0 if pairs else NO_PAIRS) | (0 if text else NO_TEXT) | (0 if counters else NO_COUNTERS)
         occ_p = ctypes.c_void_p()
         nocc = ctypes.c_uint64()
         if ids:

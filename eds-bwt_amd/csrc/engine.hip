@@ -589,9 +589,11 @@ struct Engine {
     // the level walk's located results with dense samples: k_locate_lists (a wave per pattern, records
     // from the lists directly); EDSBWT_LOCATE_LISTS=0: tasks + k_locate (C5 located step: see DESIGN §6)
     bool locate_lists = env_double("EDSBWT_LOCATE_LISTS", 1) != 0;
-    // k_deep_direct's per-lane work counters (steps, lines, text rows: the line model of bench.py's
-    // roofline); EDSBWT_DEEP_STATS=0 runs its build without them (8 waves per SIMD, fused keys)
-    bool deep_stats = env_double("EDSBWT_DEEP_STATS", 1) != 0;
+    // the direct start's deep kernels with their per-lane work counters (steps, lines, text rows: the
+    // line model of bench.py's roofline); off for a call with EDSBWT_NO_COUNTERS (or every call with
+    // EDSBWT_DEEP_STATS=0): the builds without them (k_deep_direct 8 waves fused, k_deep 6 waves)
+    bool deep_stats_env = env_double("EDSBWT_DEEP_STATS", 1) != 0;
+    bool deep_stats = true;  // (this call's)
     bool fc_done = false;           // ... and k_deep_direct took them
     static constexpr uint32_t kWideCap = 16384;
     static constexpr uint32_t kWaveGrid = 2048;  // k_deep_wave's waves (each strides over the wide list)
@@ -2029,7 +2031,7 @@ struct Engine {
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? (X.eofrow ? (unb ? k_deep<4, 3, 1, true> : k_deep<4, 3, 5, true>)
-                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? k_deep<4, 3, 6> : k_deep<4, 3, 5>)
+                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>) : k_deep<4, 3, 5>)
                                        : unb ? k_deep<4, 4, 1> : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
@@ -2786,6 +2788,7 @@ struct Engine {
         prof_mask = (flags & EDSBWT_PROFILE) ? ~0u
                                              : ((1u << KC_STEP) | (1u << KC_DEEP) | (1u << KC_DEEPQ) | (1u << KC_DEEPW) | (1u << KC_LOCATE) |
                                                 (1u << KC_LINKSORT));
+        deep_stats = deep_stats_env && !(flags & EDSBWT_NO_COUNTERS);
         const bool locate = (flags & EDSBWT_LOCATE) && !(flags & EDSBWT_COUNT_ONLY);
         const bool use_table = locate && (flags & EDSBWT_LOCATE_TABLE);
         count_only = !locate;

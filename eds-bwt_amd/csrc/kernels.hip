@@ -1830,7 +1830,7 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
 
 // EOFROW: links from '#' rows through KIdx::eofrow (one line per row; costs k_deep 6 VGPRs and a
 // wave per SIMD: C3 0.355 against 0.304 ms, profiles/r04_ab_c3_*.json — off by default)
-template <int K, int BPS, int MINW = 1, bool EOFROW = false>  // MINW: waves per SIMD the register budget is held to (1: no bound)
+template <int K, int BPS, int MINW = 1, bool EOFROW = false, bool STATS = true>  // MINW: waves per SIMD the register budget is held to (1: no bound)
 __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qcnt, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
                                               const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind, uint64_t P,
@@ -1840,7 +1840,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                                               uint32_t* __restrict__ ab, uint32_t* __restrict__ ae, Res* __restrict__ res,
                                               uint32_t* __restrict__ ovf, unsigned long long* __restrict__ ctr, const uint64_t* __restrict__ q2,
                                               const uint4* __restrict__ kt1w, uint32_t* __restrict__ counts, uint32_t qpairs) {
-    uint32_t n_steps = 0, n_hash = 0, n_blk = 0, n_text = 0, n_trow = 0, n_q = 0;
+    LaneCtr<STATS> n_steps, n_hash, n_blk, n_text, n_trow, n_q;  // (STATS = false: compiled away)
     CountSums cs;  // n_blk: occ blocks read (per lane, widened at the end)
 #ifdef EDSBWT_DEBUG_CHECKS
     uint32_t dbg_q = 0, dbg_p = 0, dbg_w = 0, dbg_l = 0;
@@ -2217,12 +2217,12 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         cs.put(counts, o, occ);
     }
     __shared__ unsigned long long sh[4];
-    stat_add(ctr, ST_DEEPQ_STEPS, n_steps, sh);
-    stat_add(ctr, ST_DEEP_HASH, n_hash, sh);
-    stat_add(ctr, ST_DEEPQ_BLOCKS, n_blk, sh);
-    stat_add(ctr, ST_DEEPQ_PATS, n_q, sh);
-    stat_add(ctr, ST_TEXT_CHARS, n_text, sh);
-    stat_add(ctr, ST_TEXT_ROWS, n_trow, sh);
+    stat_add(ctr, ST_DEEPQ_STEPS, n_steps.v, sh);
+    stat_add(ctr, ST_DEEP_HASH, n_hash.v, sh);
+    stat_add(ctr, ST_DEEPQ_BLOCKS, n_blk.v, sh);
+    stat_add(ctr, ST_DEEPQ_PATS, n_q.v, sh);
+    stat_add(ctr, ST_TEXT_CHARS, n_text.v, sh);
+    stat_add(ctr, ST_TEXT_ROWS, n_trow.v, sh);
     cs.flush(counts, ctr, sh);
 #ifdef EDSBWT_DEBUG_CHECKS
     stat_add(ctr, ST_DBG_QUEUE, dbg_q, sh);

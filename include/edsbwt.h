@@ -61,6 +61,10 @@ enum {
                                     pair blocks (sigma <= 5; tests: same results) */
 #define EDSBWT_NO_TEXT      0x2000u/* step single-row intervals through the rank entries instead of
                                     comparing the pattern with the words' text (tests: same results) */
+#define EDSBWT_NO_COUNTERS  0x4000u/* the direct start's deep kernels without their per-lane work
+                                    counters (steps, lines, text rows): the same results, those
+                                    statistics read 0 for them, and the kernels run with fewer
+                                    registers (C3: k_deep_direct 0.816 against 0.850 ms) */
 
 typedef struct edsbwt_index edsbwt_index;
 

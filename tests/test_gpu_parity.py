@@ -555,7 +555,8 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
             for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED"):
                 monkeypatch.delenv(k_, raising=False)
             with edsbwt.Index(base) as idx:
-                for kw in ({}, {"locate": False}):
+                # (counters=False: the per-call EDSBWT_NO_COUNTERS, bench.py's timed steps)
+                for kw in ({}, {"locate": False}, {"counters": False}, {"locate": False, "counters": False}):
                     gc, go = idx.search((buf, offs), **kw)
                     assert np.array_equal(gc, oc), (fused, stats, kw, len(pats))
                     if kw.get("locate", True):
@@ -1126,6 +1127,7 @@ def test_counts_mirror_gpu(oracle, edsbwt, tmp_path, monkeypatch):
 # (EDSBWT_DEEP_K 2 / 3 / 4 / 8), the 4-interval build unbounded (EDSBWT_DEEPQ_WAVES=1) and held to
 # 5 / 6 waves per SIMD, and the '#'-row link-row variant (EDSBWT_EOF_ROWS=1) unbounded and at 5 waves
 K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDSBWT_DEEPQ_WAVES": "6"},
+                 {"EDSBWT_DEEPQ_WAVES": "6", "EDSBWT_DEEP_STATS": "0"},  # (the build without work counters)
                  {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "5"},
                  {"EDSBWT_DEEP_K": "2"}, {"EDSBWT_DEEP_K": "3"}, {"EDSBWT_DEEP_K": "8"}]
 
