@@ -2031,7 +2031,7 @@ struct Engine {
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? (X.eofrow ? (unb ? k_deep<4, 3, 1, true> : k_deep<4, 3, 5, true>)
-                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>) : k_deep<4, 3, 5>)
+                                          : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>) : deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>)
                                        : unb ? k_deep<4, 4, 1> : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
