@@ -1127,7 +1127,8 @@ def test_counts_mirror_gpu(oracle, edsbwt, tmp_path, monkeypatch):
 # (EDSBWT_DEEP_K 2 / 3 / 4 / 8), the 4-interval build unbounded (EDSBWT_DEEPQ_WAVES=1) and held to
 # 5 / 6 waves per SIMD, and the '#'-row link-row variant (EDSBWT_EOF_ROWS=1) unbounded and at 5 waves
 K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDSBWT_DEEPQ_WAVES": "6"},
-                 {"EDSBWT_DEEPQ_WAVES": "6", "EDSBWT_DEEP_STATS": "0"},  # (the build without work counters)
+                 {"EDSBWT_DEEPQ_WAVES": "6", "EDSBWT_DEEP_STATS": "0"}, {"EDSBWT_DEEPQ_WAVES": "5", "EDSBWT_DEEP_STATS": "0"},
+                 # (the builds without work counters)
                  {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "5"},
                  {"EDSBWT_DEEP_K": "2"}, {"EDSBWT_DEEP_K": "3"}, {"EDSBWT_DEEP_K": "8"}]
 
