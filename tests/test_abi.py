@@ -78,3 +78,19 @@ def test_write_csv(edsbwt, tmp_path):
     p = tmp_path / "empty.csv"
     with open(p, "wb") as f:
         assert edsbwt.write_csv(occ[:0], f.fileno(), 0, 4) == 0
+
+
+def test_header_flags_match_python(edsbwt):
+    """Every EDSBWT_* search flag and path tag include/edsbwt.h defines has the same value in the
+    Python host (eds-bwt_amd/__init__.py), and no two search flags share a bit."""
+    hdr = open(os.path.join(ROOT, "include", "edsbwt.h")).read()
+    defs = {m.group(1): int(m.group(2), 16) for m in re.finditer(r"#define EDSBWT_([A-Z_0-9]+)\s+(0x[0-9a-fA-F]+)u?", hdr)}
+    flags = {k: v for k, v in defs.items() if not k.startswith(("PATH_", "E_"))}
+    assert "NO_COUNTERS" in flags and "NO_TEXT" in flags
+    for k, v in flags.items():
+        if hasattr(edsbwt, k):
+            assert getattr(edsbwt, k) == v, k
+    for k in ("COUNT_ONLY", "LOCATE", "NO_TEXT", "NO_COUNTERS", "NO_PAIRS"):
+        assert hasattr(edsbwt, k), k
+    bits = [v for v in flags.values() if v and (v & (v - 1)) == 0]
+    assert len(bits) == len(set(bits))
