@@ -72,11 +72,11 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
     # the dollar step's text-item entries, k_deep's other dispatched build (5 waves per SIMD), the
     # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
-    # counts instead of per-tile record offsets, the locate kernel's own counts, and k_deep one
-    # character per step (no pair entries)
+    # counts instead of per-chunk record offsets, the locate kernel's own counts, k_deep one
+    # character per step (no pair entries), and the tile sums + scan instead of the look-back
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "5"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
-                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0")):
+                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0"), ("EDSBWT_LOC_LOOKBACK", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -1395,3 +1395,43 @@ def test_search_device_ids_gpu(oracle, edsbwt, tmp_path, monkeypatch, shape):
         occ_p, nocc = ctypes.c_void_p(), ctypes.c_uint64()
         assert L.edsbwt_search_device_ids(idx._h, None, None, 0, None, edsbwt.LOCATE | edsbwt.LEGACY_ORDER, None,
                                           ctypes.byref(occ_p), ctypes.byref(nocc), None) == -5
+
+
+def test_locate_lookback_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The per-pattern locate's record offsets by the decoupled look-back (k_locate_pp, the default)
+    over a batch of ~1200 256-pattern chunks — look-back windows past 64 chunks, chunks of 0 and of
+    more than the LDS stage's records, patterns left to k_locate_big: records and counts identical
+    to the tile sums + scan (EDSBWT_LOC_LOOKBACK=0) and to the per-pattern scan (EDSBWT_TILE_SCAN=0),
+    and the first patterns' records identical to the oracle's, three times over."""
+    rng = random.Random(4242)
+    segs = _covid_like(rng, 900)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs), "lb")
+    pats = []
+    for k in range(300_000):
+        m = rng.choice((6, 9, 16, 24, 31))
+        if (k // 256) % 7 == 3:  # whole chunks of patterns that occur nowhere (0-record chunks)
+            pats.append("N" * m)
+        else:
+            pats.append(edsgen.planted(rng, segs, m) or "ACGT" * 8)
+    buf, offs = _pack(pats)
+    n0 = 3000
+    b0, o0 = _pack(pats[:n0])
+    oc0, oo0, _ = oracle.Engine(base, 8).search(b0, o0)
+    got = {}
+    for lbk, tsc in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("EDSBWT_LOC_LOOKBACK", lbk)
+        monkeypatch.setenv("EDSBWT_TILE_SCAN", tsc)
+        with edsbwt.Index(base) as idx:
+            for rep in range(3):
+                gc, go = idx.search((buf, offs))
+                assert np.array_equal(gc[:n0], oc0), (lbk, tsc, rep)
+                assert np.array_equal(go[:oo0.size], oo0), (lbk, tsc, rep)
+                assert int(gc.astype(np.int64).sum()) == go.size
+                if lbk + tsc in got:
+                    assert np.array_equal(gc, got[lbk + tsc][0]) and np.array_equal(go, got[lbk + tsc][1])
+                got[lbk + tsc] = (gc, go)
+    assert np.array_equal(got["11"][0], got["01"][0]) and np.array_equal(got["11"][1], got["01"][1])
+    assert np.array_equal(got["11"][0], got["00"][0]) and np.array_equal(got["11"][1], got["00"][1])
+    assert got["11"][1].size > 300_000 * 2  # (records well past the chunks' stage sizes)
