@@ -582,7 +582,7 @@ struct Engine {
     // k_count_tiles pass, no scan launch); EDSBWT_LOC_LOOKBACK=0: the tile sums + scan (EDSBWT_TILE_SCAN=0:
     // a scan of every pattern's count, either way)
     bool loc_lookback = env_double("EDSBWT_LOC_LOOKBACK", 1) != 0;
-    DBuf<unsigned long long> lbst;  // its chunk ticket + one word per 256-pattern chunk
+    DBuf<unsigned long long> lbst;  // its chunk ticket + one word per chunk of kLbSub x 256 patterns
     // k_locate_pp's LDS record stage (512 or 1024 records; 512 lets 8 blocks share a CU: the
     // locate class 0.190 against 0.189 ms at C3, profiles/r04_ab_locstage_c3_*.json — not the bound)
     uint32_t loc_stage = (uint32_t)env_double("EDSBWT_LOC_STAGE", 1024);
@@ -2844,7 +2844,7 @@ struct Engine {
             const uint64_t nb = direct_buckets();
             if (nb) bhist.ensure(nb + 1);
             lbig.ensure(P + 1);  // (the per-pattern locate's big list: its counter is zeroed here)
-            const uint64_t nlb = locate && loc_lookback ? (P + 255) / 256 + 1 : 0;  // (k_locate_pp's look-back words)
+            const uint64_t nlb = locate && loc_lookback ? (P + kLbSub * 256 - 1) / (kLbSub * 256) + 1 : 0;  // (k_locate_pp's look-back words)
             if (nlb) lbst.ensure(nlb);
             // (the result array only when the search does not turn out to be k_deep_direct's, which
             // writes every result: res_unzeroed, settled by run_batch / run_deep)
@@ -3095,7 +3095,7 @@ struct Engine {
         // the offsets inside a tile in k_locate_pp) instead of a scan over every pattern's count
         // (EDSBWT_TILE_SCAN=0: the latter; C3 1.607 / 1.610 against 1.635 ms with 256-pattern
         // tiles, profiles/r04_ab5_c3_*.json)
-        const bool lookback = per_pattern && !loc_counts && tile_scan && loc_lookback && lbst.p && lbst.cap >= (P + 255) / 256 + 1;
+        const bool lookback = per_pattern && !loc_counts && tile_scan && loc_lookback && lbst.p && lbst.cap >= (P + kLbSub * 256 - 1) / (kLbSub * 256) + 1;
         const bool tiles = per_pattern && !loc_counts && tile_scan && !lookback;
         const uint64_t ntile = (P + 63) / 64;
         if (lookback) {
