@@ -578,11 +578,6 @@ struct Engine {
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
     bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
     bool tile_scan = env_double("EDSBWT_TILE_SCAN", 1) != 0;
-    // the per-pattern locate's record offsets by a decoupled look-back inside k_locate_pp (no
-    // k_count_tiles pass, no scan launch); EDSBWT_LOC_LOOKBACK=0: the tile sums + scan (EDSBWT_TILE_SCAN=0:
-    // a scan of every pattern's count, either way)
-    bool loc_lookback = env_double("EDSBWT_LOC_LOOKBACK", 1) != 0;
-    DBuf<unsigned long long> lbst;  // its chunk ticket + one word per chunk of kLbSub x 256 patterns
     // k_locate_pp's LDS record stage (512 or 1024 records; 512 lets 8 blocks share a CU: the
     // locate class 0.190 against 0.189 ms at C3, profiles/r04_ab_locstage_c3_*.json — not the bound)
     uint32_t loc_stage = (uint32_t)env_double("EDSBWT_LOC_STAGE", 1024);
@@ -810,7 +805,7 @@ struct Engine {
         uint64_t mx = 0;
         for (auto& r : rs) {
             if (!r.second) continue;
-            if (n == 10) throw Fail(EDSBWT_E_ARG, "zero_many: more than 10 ranges");
+            if (n == 8) throw Fail(EDSBWT_E_ARG, "zero_many: more than 8 ranges");
             z.p[n] = static_cast<uint32_t*>(r.first);
             z.n4[n] = r.second / 4;
             mx = std::max<uint64_t>(mx, z.n4[n]);
@@ -2844,13 +2839,10 @@ struct Engine {
             const uint64_t nb = direct_buckets();
             if (nb) bhist.ensure(nb + 1);
             lbig.ensure(P + 1);  // (the per-pattern locate's big list: its counter is zeroed here)
-            const uint64_t nlb = locate && loc_lookback ? (P + kLbSub * 256 - 1) / (kLbSub * 256) + 1 : 0;  // (k_locate_pp's look-back words)
-            if (nlb) lbst.ensure(nlb);
             // (the result array only when the search does not turn out to be k_deep_direct's, which
             // writes every result: res_unzeroed, settled by run_batch / run_deep)
             zero_many({{stats.p, kStatSlots * 8}, {counters.p, 24 * 8}, {tflag.p, 4}, {hcnt.p, 4},
-                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}, {lbig.p, 4},
-                       {lbst.p, nlb * 8}});
+                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}, {lbig.p, 4}});
             res_unzeroed = true;
         } else {
             zero(res.p, P * sizeof(Res));
@@ -3095,19 +3087,16 @@ struct Engine {
         // the offsets inside a tile in k_locate_pp) instead of a scan over every pattern's count
         // (EDSBWT_TILE_SCAN=0: the latter; C3 1.607 / 1.610 against 1.635 ms with 256-pattern
         // tiles, profiles/r04_ab5_c3_*.json)
-        const bool lookback = per_pattern && !loc_counts && tile_scan && loc_lookback && lbst.p && lbst.cap >= (P + kLbSub * 256 - 1) / (kLbSub * 256) + 1;
-        const bool tiles = per_pattern && !loc_counts && tile_scan && !lookback;
+        const bool tiles = per_pattern && !loc_counts && tile_scan;
         const uint64_t ntile = (P + 63) / 64;
-        if (lookback) {
-            // (k_locate_pp writes the counts and sums them, as k_count_tiles would)
-        } else if (tiles) {
+        if (tiles) {
             tile_sum.ensure(ntile);
             tile_pre.ensure(ntile);
             launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
         } else if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
-        if (!loc_counts && !lookback) emit_c8(P, d_counts);
+        if (!loc_counts) emit_c8(P, d_counts);
         uint32_t* oflow = reinterpret_cast<uint32_t*>(counters.p + 20);
         if (per_pattern) {
             // record offsets: a u32 scan of the counts themselves (a total past 2^32 fails the
@@ -3115,9 +3104,7 @@ struct Engine {
             oscan.ensure(P + 1);
             uint32_t* o32 = reinterpret_cast<uint32_t*>(oscan.p);
             size_t tb = 0;
-            if (lookback) {
-                // (none: k_locate_pp's look-back)
-            } else if (tiles) {
+            if (tiles) {
                 HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tile_sum.p, tile_pre.p, cub_n(ntile), stream));
                 tmp.ensure(tb);
                 timed(KC_SCAN, [&] { HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, tile_sum.p, tile_pre.p, cub_n(ntile), stream)); });
@@ -3138,16 +3125,15 @@ struct Engine {
             // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
             launch(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>, P, P, (const Res*)res.p, o32, first_id, pat_ids, X,
                    (const uint32_t*)ab.p,
-                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts || lookback ? d_counts : (uint32_t*)nullptr,
-                   tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr,
-                   lookback ? lbst.p : (unsigned long long*)nullptr);
+                   (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
+                   tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);
             timed(KC_LOCATE, [&] {
                 hipLaunchKernelGGL(k_locate_big, dim3(256), dim3(256), 0, stream, (const uint32_t*)lbig.p, (const Res*)res.p,
                                    (const uint32_t*)o32, first_id, pat_ids, X, (const uint32_t*)ab.p, (const uint32_t*)ae.p, rec.p, stats.p);
             });
             HIPCHK(hipGetLastError());
             task_cap = ~0ull;  // no task buffers in this path
-            if (loc_counts || lookback) emit_c8(P, d_counts);
+            if (loc_counts) emit_c8(P, d_counts);
         } else if (locate) {
             inclusive_scan_u64(occ64.p, oscan, P, false);  // packed: occurrences << 32 | tasks (totals checked below)
             hmark("locate scan");

@@ -3512,122 +3512,38 @@ __global__ void __launch_bounds__(256) k_locate_lists(uint64_t P, const Res* __r
 // per record from every lane (records of patterns left to k_locate_big, which runs next on the
 // stream, are written over by it)
 constexpr uint32_t kLocStage = 1024;
-// the per-pattern locate's record offsets by a decoupled look-back (EDSBWT_LOC_LOOKBACK): each
-// chunk of kLbSub x 256 patterns, taken in ticket order, publishes its record total (kLbAgg) at
-// once, then its first wave reads the 256 chunks before it per round (4 per lane, loads issued
-// together), adding totals back to the first chunk that holds its inclusive prefix (kLbInc) — no
-// tile-sum pass and no scan launch.  (256-pattern chunks and a 64-chunk window: the inclusive
-// prefixes advanced ~64 chunks per round, locate 0.67 against 0.22 ms, profiles/r05_ab_c3_loc_lookback_v1.txt.)
-// A chunk waits only on chunks with lower tickets, taken by blocks already running, which publish
-// before they wait.  Flag and value share one 64-bit word (relaxed agent-scope atomics: nothing
-// else is read through it); the words are zeroed with the search's counters.
-constexpr uint32_t kLbSub = 4;
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
-__device__ __forceinline__ unsigned long long lb_lookback(const unsigned long long* __restrict__ st, uint64_t c, uint32_t lane) {
-    unsigned long long excl = 0;
-    int64_t j = (int64_t)c - 1;  // this round's window: chunks j - 255 .. j (sub-window k, lane l: j - 64k - l)
-    while (true) {
-        unsigned long long v[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int64_t idx = j - 64 * k - (int64_t)lane;
-            v[k] = idx >= 0 ? __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbInc;  // (before chunk 0: 0)
-        }
-        bool wait = false;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t f = (uint32_t)(v[k] >> 62);
-            const unsigned long long zero = __ballot(f == 0), inc = __ballot(f == 2);
-            const unsigned long long need = inc ? (inc ^ (inc - 1)) : ~0ull;  // lanes up to the first inclusive one
-            if (zero & need) {  // a chunk not yet published: read again from this sub-window
-                wait = true;
-                break;
-            }
-            excl += wave_sum(((need >> lane) & 1ull) ? (v[k] & kLbVal) : 0ull);
-            if (inc) return excl;
-            j -= 64;
-        }
-        if (wait) __builtin_amdgcn_s_sleep(1);
-    }
-}
 template <uint32_t STAGE = kLocStage>  // records staged per block (STAGE x 20 B of LDS: 1024 -> 7 blocks per CU)
 __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, uint32_t* __restrict__ oscan, uint32_t first_id,
                                                    const uint32_t* __restrict__ ids, KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
                                                    uint32_t* __restrict__ oflow, unsigned long long* __restrict__ stats,
-                                                   uint32_t* __restrict__ counts, const unsigned long long* __restrict__ tile_pre,
-                                                   unsigned long long* __restrict__ lb) {
+                                                   uint32_t* __restrict__ counts, const unsigned long long* __restrict__ tile_pre) {
     // counts != nullptr (the deferred per-pattern locate): each pattern's count is written here and
     // found / occurrences summed (fused counts), the scan having read the results directly.
     // tile_pre != nullptr: each 64-pattern tile's first record (k_count_tiles + a scan over tiles);
     // the offsets inside a tile come from a wave scan here, and oscan is written only for the
-    // patterns k_locate_big takes.  lb != nullptr: the offsets by the look-back above (lb[0]: the
-    // chunk ticket, lb[1 + c]: chunk c's word; blockDim 256), counts written here
+    // patterns k_locate_big takes
     CountSums cs;
     __shared__ uint32_t sw[STAGE * 5];
-    __shared__ uint64_t s_lo, s_hi, s_p0;
-    __shared__ unsigned long long sh[4], s_wt[kLbSub * 4], s_excl;
+    __shared__ uint64_t s_lo, s_hi;
+    __shared__ unsigned long long sh[4];
     unsigned long long my_off = 0;
     uint32_t* recw = reinterpret_cast<uint32_t*>(rec);
-    uint32_t* ticket = reinterpret_cast<uint32_t*>(lb);
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t span = lb ? kLbSub * 256u : 256u;  // patterns per chunk (lb) or per block step
-    uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x;
-    if (lb) {
-        if (threadIdx.x == 0) s_p0 = (uint64_t)atomicAdd(ticket, 1u) * span;
-        __syncthreads();
-        p0 = s_p0;
-    }
-    while (p0 < P) {  // block-uniform
-      if (lb) {
-        // the chunk's record total: per sub-chunk wave totals, then the look-back by wave 0
-#pragma unroll
-        for (uint32_t sb = 0; sb < kLbSub; sb++) {
-            const uint64_t i = p0 + sb * 256u + threadIdx.x;
-            const uint32_t oc = i < P ? res_occ(res[i]) : 0u;
-            const unsigned long long inw = wave_excl_scan(oc);
-            if (lane == 63) s_wt[sb * 4 + wv] = inw + oc;
-        }
-        __syncthreads();
-        if (wv == 0) {
-            unsigned long long T = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < kLbSub * 4; k++) T += s_wt[k];
-            const uint64_t c = p0 / span;
-            unsigned long long* st = lb + 1;
-            unsigned long long excl = 0;
-            if (c == 0) {
-                if (lane == 0) __hip_atomic_store(st, kLbInc | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                if (lane == 0) __hip_atomic_store(st + c, kLbAgg | T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                excl = lb_lookback(st, c, lane);
-                if (lane == 0) __hip_atomic_store(st + c, kLbInc | (excl + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (lane == 0) s_excl = excl;
-        }
-        __syncthreads();
-      }
-      for (uint32_t sb = 0; sb < span / 256u; sb++) {  // (one step without lb)
-        const uint64_t q0 = p0 + sb * 256u;
-        if (q0 >= P) break;  // (uniform)
-        const uint64_t i = q0 + threadIdx.x, plast = min(P, q0 + blockDim.x) - 1;
+    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < P; p0 += (uint64_t)gridDim.x * blockDim.x) {  // block-uniform
+        const uint64_t i = p0 + threadIdx.x, plast = min(P, p0 + blockDim.x) - 1;
         Res r{};
         uint32_t occ = 0;
         uint64_t base = 0;
         if (i < P) {
             r = res[i];
             occ = res_occ(r);
-            if (!tile_pre && !lb) base = oscan[i];  // exclusive scan of the counts
+            if (!tile_pre) base = oscan[i];  // exclusive scan of the counts
             cs.put(counts, i, occ);
         }
         if (tile_pre) {  // (a uniform branch) the wave's tile: its first record + the offsets inside it
-            const uint64_t w0 = q0 + (threadIdx.x & ~63u);
+            const uint64_t w0 = p0 + (threadIdx.x & ~63u);
             const unsigned long long inw = wave_excl_scan(occ);
             if (w0 < P) base = tile_pre[w0 >> 6] + inw;
-        } else if (lb) {  // (uniform) the chunk's first record + the waves before this one in the chunk
-            unsigned long long woff = s_excl;
-            for (uint32_t k = 0; k < sb * 4 + wv; k++) woff += s_wt[k];
-            base = woff + wave_excl_scan(occ);
         }
         if (threadIdx.x == 0) s_lo = base;
         if (i == plast) s_hi = base + occ;
@@ -3651,7 +3567,7 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
                 emit(base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
                 my_off += off;
             } else if (occ > kLocBig) {
-                if (tile_pre || lb) oscan[i] = (uint32_t)base;  // (< occ_cap < 2^32) k_locate_big's offset
+                if (tile_pre) oscan[i] = (uint32_t)base;  // (< occ_cap < 2^32) k_locate_big's offset
                 flag_push(big, (uint32_t)i);
             } else {
                 uint64_t o = base;
@@ -3683,14 +3599,6 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
             if (threadIdx.x < nw - t0) recw[g0 + t0 + threadIdx.x] = sw[t0 + threadIdx.x];
         }
         __syncthreads();
-      }
-        if (lb) {
-            if (threadIdx.x == 0) s_p0 = (uint64_t)atomicAdd(ticket, 1u) * span;
-            __syncthreads();
-            p0 = s_p0;
-        } else {
-            p0 += (uint64_t)gridDim.x * blockDim.x;
-        }
     }
     stat_add(stats, ST_LOC_OFFSETS, my_off, sh);
     cs.flush(counts, stats, sh);
@@ -4484,8 +4392,8 @@ constexpr uint32_t kLineBlk = 4096;
 // small host<->device transfers on the engine stream (engine.hip small_copy)
 // zero up to 8 ranges (byte sizes multiples of 4, 4-B aligned) in one launch: blockIdx.y = range
 struct ZeroSet {
-    uint32_t* p[10];
-    uint64_t n4[10];
+    uint32_t* p[8];
+    uint64_t n4[8];
 };
 __global__ void __launch_bounds__(256) k_zero_multi(ZeroSet z) {
     uint32_t* p = z.p[blockIdx.y];

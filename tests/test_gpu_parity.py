@@ -72,11 +72,11 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # bit (also taken when S >= 2^31), one lane per wide list (k_deep_wide), 64-B segment rows without
     # the dollar step's text-item entries, k_deep's other dispatched build (5 waves per SIMD), the
     # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
-    # counts instead of per-chunk record offsets, the locate kernel's own counts, k_deep one
-    # character per step (no pair entries), and the tile sums + scan instead of the look-back
+    # counts instead of per-tile record offsets, the locate kernel's own counts, and k_deep one
+    # character per step (no pair entries)
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "5"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
-                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0"), ("EDSBWT_LOC_LOOKBACK", "0")):
+                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -1397,12 +1397,13 @@ def test_search_device_ids_gpu(oracle, edsbwt, tmp_path, monkeypatch, shape):
                                           ctypes.byref(occ_p), ctypes.byref(nocc), None) == -5
 
 
-def test_locate_lookback_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
-    """The per-pattern locate's record offsets by the decoupled look-back (k_locate_pp, the default)
-    over a batch of ~1200 256-pattern chunks — look-back windows past 64 chunks, chunks of 0 and of
-    more than the LDS stage's records, patterns left to k_locate_big: records and counts identical
-    to the tile sums + scan (EDSBWT_LOC_LOOKBACK=0) and to the per-pattern scan (EDSBWT_TILE_SCAN=0),
-    and the first patterns' records identical to the oracle's, three times over."""
+def test_locate_many_tiles_gpu(oracle, edsbwt, tmp_path, monkeypatch):
+    """The per-pattern locate's record offsets over a batch of ~4700 64-pattern tiles (k_count_tiles,
+    the scan over tiles, k_locate_pp's wave scans) — blocks of 0 records and of more than the LDS
+    stage's records, patterns left to k_locate_big: records and counts identical to the per-pattern
+    scan (EDSBWT_TILE_SCAN=0) and the first patterns' records identical to the oracle's, three
+    times over.  (Round 5 also ran this against a decoupled look-back inside k_locate_pp: exact,
+    but slower — profiles/r05_ab_c3_loc_lookback_v*.txt.)"""
     rng = random.Random(4242)
     segs = _covid_like(rng, 900)
     if any(w == "" for w in segs[1]):
@@ -1411,7 +1412,7 @@ def test_locate_lookback_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     pats = []
     for k in range(300_000):
         m = rng.choice((6, 9, 16, 24, 31))
-        if (k // 256) % 7 == 3:  # whole chunks of patterns that occur nowhere (0-record chunks)
+        if (k // 256) % 7 == 3:  # whole blocks of patterns that occur nowhere (0-record blocks)
             pats.append("N" * m)
         else:
             pats.append(edsgen.planted(rng, segs, m) or "ACGT" * 8)
@@ -1420,18 +1421,16 @@ def test_locate_lookback_many_chunks_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     b0, o0 = _pack(pats[:n0])
     oc0, oo0, _ = oracle.Engine(base, 8).search(b0, o0)
     got = {}
-    for lbk, tsc in (("1", "1"), ("0", "1"), ("0", "0")):
-        monkeypatch.setenv("EDSBWT_LOC_LOOKBACK", lbk)
+    for tsc in ("1", "0"):
         monkeypatch.setenv("EDSBWT_TILE_SCAN", tsc)
         with edsbwt.Index(base) as idx:
             for rep in range(3):
                 gc, go = idx.search((buf, offs))
-                assert np.array_equal(gc[:n0], oc0), (lbk, tsc, rep)
-                assert np.array_equal(go[:oo0.size], oo0), (lbk, tsc, rep)
+                assert np.array_equal(gc[:n0], oc0), (tsc, rep)
+                assert np.array_equal(go[:oo0.size], oo0), (tsc, rep)
                 assert int(gc.astype(np.int64).sum()) == go.size
-                if lbk + tsc in got:
-                    assert np.array_equal(gc, got[lbk + tsc][0]) and np.array_equal(go, got[lbk + tsc][1])
-                got[lbk + tsc] = (gc, go)
-    assert np.array_equal(got["11"][0], got["01"][0]) and np.array_equal(got["11"][1], got["01"][1])
-    assert np.array_equal(got["11"][0], got["00"][0]) and np.array_equal(got["11"][1], got["00"][1])
-    assert got["11"][1].size > 300_000 * 2  # (records well past the chunks' stage sizes)
+                if tsc in got:
+                    assert np.array_equal(gc, got[tsc][0]) and np.array_equal(go, got[tsc][1])
+                got[tsc] = (gc, go)
+    assert np.array_equal(got["1"][0], got["0"][0]) and np.array_equal(got["1"][1], got["0"][1])
+    assert got["1"][1].size > 300_000 * 2  # (records well past the blocks' stage sizes)
