@@ -338,7 +338,8 @@ struct Engine {
     bool split_scans = env_double("EDSBWT_SPLIT_SCANS", 0) != 0;  // tests: locate offsets by two scans
     DBuf<uint32_t> ktab_off, ktab_b, ktab_e;
     DBuf<uint64_t> ktab_one;  // per D-mer: its one interval inline, else list length and offset (k_ktab_one)
-    DBuf<uint4> ktab_wide;    // ... or the wide form, 32 B per D-mer (k_ktab_wide; replaces ktab_one)
+    DBuf<uint4> ktab_wide;    // ... or the wide form, 32 or 64 B per D-mer (k_ktab_wide; replaces ktab_one)
+    uint32_t kt1_ws = 2;      // its uint4s per D-mer (KIdx::kt1_ws)
     DBuf<uint4> srow;         // per-row text-compare entries, 32 B per row (k_srow; KIdx::srow)
     // deep level start table (build_ltab; kernels.hip k_ltab_*): every L-mer's walk items after
     // its L characters, in lt_G groups by the L-mer's last characters (x mod lt_G); a level walk
@@ -689,6 +690,7 @@ struct Engine {
         X.srow = txt && srow.p ? (const uint4*)srow.p : nullptr;
         X.text_deep = text_deep ? 1u : 0u;
         X.kt1_pos = kt1_pos ? 1u : 0u;
+        X.kt1_ws = kt1_ws;
         X.rk16 = use_rk16 ? rk16.p : nullptr;
         X.rk16sup = use_rk16 ? rk16sup.p : nullptr;
         X.kt_E = (uint32_t)std::min<uint64_t>(ktab_entries, 0xffffffffu);
@@ -1490,16 +1492,22 @@ struct Engine {
             // the wide form when a one-row entry can carry its sample and text window (dense
             // samples, the text) and HBM holds 32 B per D-mer with room to spare (C3: 4^15 D-mers,
             // 34 GB); EDSBWT_KT1_WIDE=0: the 8-B entries
+            // (64 B per D-mer when HBM also holds that: a one-row entry then carries the link ranks of
+            // its word's segment, KIdx::kt1_ws; EDSBWT_KT1_LINK=0: 32 B)
             size_t fb = 0, tb_ = 0;
             fb = hbm_free(&tb_);
-            const uint64_t wide_b = (E + 1) * 32;
+            const KIdx X0 = kidx();
+            const bool link = sigma <= 5 && X0.segtab && env_double("EDSBWT_KT1_LINK", 1) != 0 &&
+                              (double)fb > kKt1WideHbmShare * (double)((E + 1) * 64);
+            kt1_ws = link ? 4u : 2u;
+            const uint64_t wide_b = (E + 1) * 16 * kt1_ws;
             const bool wide = kt1_pos && have_samples && samp_shift == 0 && samples.p && rtext.p &&
                               (double)fb > kKt1WideHbmShare * (double)wide_b && env_double("EDSBWT_KT1_WIDE", 1) != 0;
             if (wide) {
-                ktab_wide.ensure(2 * (E + 1));
+                ktab_wide.ensure((size_t)kt1_ws * (E + 1));
                 launch(KC_TABLE, k_ktab_wide, E + 1, E, (const uint32_t*)ktab_off.p, (const uint32_t*)ktab_b.p,
                        (const uint32_t*)ktab_e.p, (const uint32_t*)gpos.p, (const uint4*)samples.p, (const uint64_t*)rtext.p,
-                       (uint64_t)tlen, ktab_wide.p);
+                       (uint64_t)tlen, ktab_wide.p, kt1_ws, X0.segtab, X0.seg_stride, X0.seg_hi, (uint32_t)sigma);
                 device_bytes += wide_b;
             } else {
                 ktab_one.ensure(E + 1);

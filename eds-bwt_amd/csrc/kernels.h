@@ -129,6 +129,11 @@ struct KIdx {
     // alphabet) and intervals: the bounds a queued direct-start list is checked against in the
     // debug build (-DEDSBWT_DEBUG_CHECKS)
     uint32_t kt_E, kt_n;
+    // uint4s per wide D-mer entry (kt1w): 2, or 4 when a one-row entry also holds the link ranks of
+    // its row's word's segment for c = 1..4 (rx at uint4 2, ry at uint4 3: segtab's [1 + c] and
+    // [seg_hi + c]) — the first link after the entry's text compare then reads the entry's own
+    // 128-B DRAM line instead of a segment row (sigma <= 5)
+    uint32_t kt1_ws;
 };
 
 }  // namespace edsbwt

@@ -1315,8 +1315,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_fast(uint64_t P, uint32_t D0
         uint64_t ent = 0, win1 = 0;
         uint4 s1 = make_uint4(0, 0, 0, 0);
         if (L > D0 && kt1w) {
-            const uint4 w0 = kt1w[2 * (size_t)u];
-            s1 = kt1w[2 * (size_t)u + 1];
+            const uint4 w0 = kt1w[(size_t)X.kt1_ws * u];
+            s1 = kt1w[(size_t)X.kt1_ws * u + 1];
             ent = (uint64_t)w0.y << 32 | w0.x;
             win1 = (uint64_t)w0.w << 32 | w0.z;
         } else if (L > D0 && kt1) {
@@ -1644,11 +1644,11 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         uint32_t u = 0;
         if (L > D0) {
             u = FUSED ? kx : nid[i];
-            const uint4 w0 = kt1w[2 * (size_t)u];
-            s1 = kt1w[2 * (size_t)u + 1];
+            const uint4 w0 = kt1w[(size_t)X.kt1_ws * u];
+            s1 = kt1w[(size_t)X.kt1_ws * u + 1];
             ent = (uint64_t)w0.y << 32 | w0.x;
             win1 = (uint64_t)w0.w << 32 | w0.z;
-            n_blk++;  // the entry's 32 B: one line
+            n_blk++;  // the entry's 32 or 64 B: one line
         }
         const uint32_t n0 = L <= D0 ? 0u : (ent >> 63) ? 1u : (uint32_t)(ent >> 32);
         if (n0 > 1) {
@@ -1677,6 +1677,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             uint4 s = s1;
             uint64_t tw = win1;
             bool have = g1 != ~0u;
+            bool ent_row = have && X.kt1_ws == 4;  // s is the entry's row: its link ranks are in the entry
             while (X.rtext && b == e && d < L) {
                 // one row = one text position: the next k = min(o, m) <= 16 characters against the
                 // text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row), as in k_deep_fast
@@ -1730,11 +1731,20 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                     d = L;
                     break;
                 }
-                const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
-                const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
-                n_blk++;
+                uint32_t rx, ry;
+                if (ent_row) {  // (the entry's 128-B line, already fetched)
+                    const uint32_t* lk = reinterpret_cast<const uint32_t*>(kt1w + 4 * (size_t)u + 2);
+                    rx = lk[c - 1];
+                    ry = lk[4 + c - 1];
+                } else {
+                    const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
+                    rx = et[1 + c];
+                    ry = et[X.seg_hi + c];
+                    n_blk++;
+                    DD_CNT(c_seg);
+                }
+                ent_row = false;
                 n_steps++;
-                DD_CNT(c_seg);
                 if (ry <= rx) {
                     alive = false;
                     d = L;
@@ -1908,7 +1918,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             // another kind, or a D-mer past the table, goes to the wide-list walk (node lists)
             DBG_CHECK(w.z == kQWide && w.w <= X.kt_E, dbg_w);
             if (w.z != kQWide || w.w > X.kt_E) { flag_push(ovf, (uint32_t)i); continue; }
-            const uint4 a0 = kt1w[2 * (size_t)w.w], a1 = kt1w[2 * (size_t)w.w + 1];
+            const uint4 a0 = kt1w[(size_t)X.kt1_ws * w.w], a1 = kt1w[(size_t)X.kt1_ws * w.w + 1];
             n_blk++;
             cn = a0.y;
             // a queued D-mer has a list of >= 2 intervals (one interval is never queued from the
@@ -4184,7 +4194,9 @@ __global__ void k_ktab_one(uint64_t E, const uint32_t* __restrict__ off, const u
 // before the row's suffix (rtext_window at tlen - g) and the row's sample
 __global__ void k_ktab_wide(uint64_t E, const uint32_t* __restrict__ off, const uint32_t* __restrict__ b, const uint32_t* __restrict__ e,
                             const uint32_t* __restrict__ gpos, const uint4* __restrict__ samples, const uint64_t* __restrict__ rtext,
-                            uint64_t tlen, uint4* __restrict__ w) {
+                            uint64_t tlen, uint4* __restrict__ w, uint32_t ws, const uint32_t* __restrict__ segtab, uint32_t seg_stride,
+                            uint32_t seg_hi, uint32_t sigma) {
+    // ws = 4 (KIdx::kt1_ws): a one-row entry also gets its word's segment's link ranks for c = 1..4
     GRID_STRIDE(u, E + 1) {
         const uint32_t o = off[u], n = off[u + 1] - o;
         uint64_t ent, win = 0;
@@ -4201,8 +4213,22 @@ __global__ void k_ktab_wide(uint64_t E, const uint32_t* __restrict__ off, const 
                 s = make_uint4(b[o + 1], e[o + 1], n > 2 ? b[o + 2] : 0u, n > 2 ? e[o + 2] : 0u);
             }
         }
-        w[2 * u] = make_uint4((uint32_t)ent, (uint32_t)(ent >> 32), (uint32_t)win, (uint32_t)(win >> 32));
-        w[2 * u + 1] = s;
+        w[(size_t)ws * u] = make_uint4((uint32_t)ent, (uint32_t)(ent >> 32), (uint32_t)win, (uint32_t)(win >> 32));
+        w[(size_t)ws * u + 1] = s;
+        if (ws == 4) {
+            uint32_t rx[4] = {0, 0, 0, 0}, ry[4] = {0, 0, 0, 0};  // (s.z < 2: no link, as the walk decides)
+            if ((ent >> 62) == 3ull && s.z >= 2) {
+                const uint32_t* et = segtab + (size_t)s.z * seg_stride;
+#pragma unroll
+                for (uint32_t c = 1; c <= 4; c++)
+                    if (c < sigma) {
+                        rx[c - 1] = et[1 + c];
+                        ry[c - 1] = et[seg_hi + c];
+                    }
+            }
+            w[4 * (size_t)u + 2] = make_uint4(rx[0], rx[1], rx[2], rx[3]);
+            w[4 * (size_t)u + 3] = make_uint4(ry[0], ry[1], ry[2], ry[3]);
+        }
     }
 }
 

@@ -527,12 +527,15 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         monkeypatch.setenv("EDSBWT_DIRECT_PACKED", packed)
         monkeypatch.setenv("EDSBWT_DIRECT_SORT_MIN", "0")  # the D-mer sort even for this small batch, when on
         # -1: the default sort (input order when wide); srow: the per-row text-compare entries
-        for wide, sort_bits, srow in (("1", "-1", "1"), ("1", "16", "1"), ("0", "-1", "1"), ("1", "-1", "0"), ("0", "-1", "0")):
+        # link "0": 32-B wide entries without the first link's segment ranks (EDSBWT_KT1_LINK=0)
+        for wide, sort_bits, srow, link in (("1", "-1", "1", "1"), ("1", "16", "1", "1"), ("0", "-1", "1", "1"), ("1", "-1", "0", "1"),
+                                            ("0", "-1", "0", "1"), ("1", "-1", "1", "0")):
             monkeypatch.setenv("EDSBWT_KT1_WIDE", wide)
             monkeypatch.setenv("EDSBWT_DIRECT_SORT_BITS", sort_bits)
             monkeypatch.setenv("EDSBWT_SROW", srow)
+            monkeypatch.setenv("EDSBWT_KT1_LINK", link)
             with edsbwt.Index(base) as idx:
-                sizes[wide + srow] = idx.device_bytes
+                sizes[wide + srow + ("" if link == "1" else "n")] = idx.device_bytes
                 for kw in ({}, {"locate": False}, {"text": False}):
                     gc, go = idx.search((buf, offs), **kw)
                     st = idx.stats()
@@ -552,7 +555,7 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         for fused, stats in (("1", "1"), ("0", "1"), ("1", "0")):
             monkeypatch.setenv("EDSBWT_FUSED_KEYS", fused)
             monkeypatch.setenv("EDSBWT_DEEP_STATS", stats)
-            for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED"):
+            for k_ in ("EDSBWT_KT1_WIDE", "EDSBWT_DIRECT_SORT_BITS", "EDSBWT_SROW", "EDSBWT_DIRECT_PACKED", "EDSBWT_KT1_LINK"):
                 monkeypatch.delenv(k_, raising=False)
             with edsbwt.Index(base) as idx:
                 # (counters=False: the per-call EDSBWT_NO_COUNTERS, bench.py's timed steps)
@@ -564,7 +567,8 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     for k_ in ("EDSBWT_FUSED_KEYS", "EDSBWT_DEEP_STATS"):
         monkeypatch.delenv(k_)
     E = (4 ** D0) + 1
-    assert sizes["11"] - sizes["01"] == 24 * E  # the wide table was built (32 B instead of 8 per D-mer)
+    assert sizes["11"] - sizes["01"] == 56 * E  # the wide table was built (64 B instead of 8 per D-mer) ...
+    assert sizes["11n"] - sizes["01"] == 24 * E  # ... or 32 B without the link ranks
     assert sizes["11"] > sizes["10"]  # ... and the per-row entries
 
 
