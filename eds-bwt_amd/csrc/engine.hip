@@ -1492,12 +1492,14 @@ struct Engine {
             // the wide form when a one-row entry can carry its sample and text window (dense
             // samples, the text) and HBM holds 32 B per D-mer with room to spare (C3: 4^15 D-mers,
             // 34 GB); EDSBWT_KT1_WIDE=0: the 8-B entries
-            // (64 B per D-mer when HBM also holds that: a one-row entry then carries the link ranks of
-            // its word's segment, KIdx::kt1_ws; EDSBWT_KT1_LINK=0: 32 B)
+            // (EDSBWT_KT1_LINK=1: 64 B per D-mer when HBM also holds that, a one-row entry then carrying
+            // the link ranks of its word's segment, KIdx::kt1_ws — C3 1.434-1.446 against 1.438-1.475 ms
+            // for 34 GB more index, profiles/r05_ab_c3_kt1_link.txt: the segment rows mostly hit the
+            // cache; off by default)
             size_t fb = 0, tb_ = 0;
             fb = hbm_free(&tb_);
             const KIdx X0 = kidx();
-            const bool link = sigma <= 5 && X0.segtab && env_double("EDSBWT_KT1_LINK", 1) != 0 &&
+            const bool link = sigma <= 5 && X0.segtab && env_double("EDSBWT_KT1_LINK", 0) != 0 &&
                               (double)fb > kKt1WideHbmShare * (double)((E + 1) * 64);
             kt1_ws = link ? 4u : 2u;
             const uint64_t wide_b = (E + 1) * 16 * kt1_ws;

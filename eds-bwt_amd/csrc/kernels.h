@@ -132,7 +132,7 @@ struct KIdx {
     // uint4s per wide D-mer entry (kt1w): 2, or 4 when a one-row entry also holds the link ranks of
     // its row's word's segment for c = 1..4 (rx at uint4 2, ry at uint4 3: segtab's [1 + c] and
     // [seg_hi + c]) — the first link after the entry's text compare then reads the entry's own
-    // 128-B DRAM line instead of a segment row (sigma <= 5)
+    // 128-B DRAM line instead of a segment row (sigma <= 5; EDSBWT_KT1_LINK=1)
     uint32_t kt1_ws;
 };
 

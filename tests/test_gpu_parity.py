@@ -527,7 +527,8 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
         monkeypatch.setenv("EDSBWT_DIRECT_PACKED", packed)
         monkeypatch.setenv("EDSBWT_DIRECT_SORT_MIN", "0")  # the D-mer sort even for this small batch, when on
         # -1: the default sort (input order when wide); srow: the per-row text-compare entries
-        # link "0": 32-B wide entries without the first link's segment ranks (EDSBWT_KT1_LINK=0)
+        # link "1": 64-B wide entries with the first link's segment ranks (EDSBWT_KT1_LINK=1; "0", the
+        # default: 32 B)
         for wide, sort_bits, srow, link in (("1", "-1", "1", "1"), ("1", "16", "1", "1"), ("0", "-1", "1", "1"), ("1", "-1", "0", "1"),
                                             ("0", "-1", "0", "1"), ("1", "-1", "1", "0")):
             monkeypatch.setenv("EDSBWT_KT1_WIDE", wide)
