@@ -117,16 +117,27 @@ static inline int cub_n(uint64_t n) {
             throw Fail(EDSBWT_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));          \
     } while (0)
 
-// device bytes the engines' DBufs hold (this process), and the most held at once since the last
-// reset: index_open reports the peak of its builds (edsbwt_index_info::open_peak_bytes)
+// device bytes the engines' DBufs hold (this process), and per index_open the most that open held
+// at once (edsbwt_index_info::open_peak_bytes): the open running on a thread tracks its own
+// allocations and frees (thread_local), so concurrent opens on other threads (the CLI's --gpus N
+// opens its indexes in parallel) neither inflate nor hide it
+struct MemTrack {
+    int64_t live = 0, peak = 0;
+};
 struct DevMem {
-    static inline std::atomic<uint64_t> live{0}, peak{0};
+    static inline std::atomic<uint64_t> live{0};
+    static inline thread_local MemTrack* track = nullptr;
     static void add(uint64_t n) {
-        const uint64_t v = live.fetch_add(n) + n;
-        uint64_t p = peak.load();
-        while (v > p && !peak.compare_exchange_weak(p, v)) {}
+        live.fetch_add(n);
+        if (track) {
+            track->live += (int64_t)n;
+            track->peak = std::max(track->peak, track->live);
+        }
     }
-    static void sub(uint64_t n) { live.fetch_sub(n); }
+    static void sub(uint64_t n) {
+        live.fetch_sub(n);
+        if (track) track->live -= (int64_t)n;
+    }
 };
 
 template <class T>
@@ -986,8 +997,11 @@ struct Engine {
     // ------------------------------------------------------------ index
     void open(const std::string& base, int dev) {
         const auto t_open = std::chrono::steady_clock::now();
-        const uint64_t live0 = DevMem::live.load();
-        DevMem::peak.store(live0);
+        MemTrack mt;
+        struct TrackScope {
+            explicit TrackScope(MemTrack* m) { DevMem::track = m; }
+            ~TrackScope() { DevMem::track = nullptr; }
+        } track_scope(&mt);
         device = dev;
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -1142,7 +1156,7 @@ struct Engine {
         build_segtext();
         // after the per-row entries: the level table's budget is a share of what HBM has left
         build_ltab();
-        open_peak_bytes = DevMem::peak.load() - live0;
+        open_peak_bytes = (uint64_t)std::max<int64_t>(0, mt.peak);
         open_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_open).count();
         if (trace)
             std::fprintf(stderr, "[edsbwt] index open: %.2f s, %llu device bytes held, peak %llu while building\n", open_seconds,

@@ -2032,8 +2032,10 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             // of (c, c2) and of the rows coded '#' or (c, '#'); when no interval holds such a row,
             // neither step links (MOVE_EDSBWTSearch.cpp:512-563 is not reached) and every interval
             // maps to [PC[p] + rank_p(b), PC[p] + rank_p(e + 1)) — DESIGN.md §3.  Else (or after a
-            // failed try: pskip) one step as below.  The list order is kept, so merges are the same
-            if (qpairs && X.rent2 && !pskip && d + 1 < L) {
+            // failed try: pskip) one step as below.  The list order is kept, so merges are the same.
+            // c = '#' (code 0: a pattern holding '#' on the ordered path) has no pair code — p would
+            // wrap below 1 — so it always takes the single step, as in k_deep_fast
+            if (qpairs && X.rent2 && !pskip && d + 1 < L && c != 0) {
                 const uint32_t c2 = code_at(d + 1);
                 if (c2 != 0 && c2 < X.sigma) {
                     const uint32_t p = 1 + (c - 1) * X.sigma + c2;

@@ -26,7 +26,8 @@
 // per device (opened in parallel), contiguous line ranges searched concurrently with
 // first_pattern_id = first line + 1 so #Pat stays the file's line number, and each shard's CSV
 // rows written at its byte offset of the one output file: the same bytes
-// as --gpus 1.  With fewer devices than N the shards share them (device k mod count).
+// as --gpus 1.  With fewer devices than N the shards share them (device k mod count), opened one
+// after another on a shared device, each sizing its tables for its share (EDSBWT_HBM_SHARE).
 // The search itself runs on the GPU through libedsbwt.so (include/edsbwt.h).
 #include <algorithm>
 #include <chrono>
@@ -114,11 +115,28 @@ int main(int argc, char** argv) {
             x.idx = nullptr;
         }
     };
-    // one index per device, opened in parallel (each builds its device tables)
-    each(N, [&](size_t k) {
-        sh[k].device = devs[k];
-        sh[k].rc = edsbwt_index_open(base.c_str(), devs[k], 8, &sh[k].idx);
-        if (sh[k].rc) sh[k].err = edsbwt_last_error();
+    // one index per shard, the devices' opens in parallel (each builds its device tables).  Shards
+    // that share a device (--gpus N above the device count, or a repeated --devices entry) open one
+    // after another on it, each sizing its optional tables for its share of that device's HBM
+    // (EDSBWT_HBM_SHARE, unless the caller set it): opened together, each would size them from the
+    // whole device's free memory and the device would be oversubscribed
+    std::vector<int> udev;
+    size_t per_dev = 0;
+    for (int d : devs)
+        if (std::find(udev.begin(), udev.end(), d) == udev.end()) udev.push_back(d);
+    for (int d : udev) per_dev = std::max<size_t>(per_dev, (size_t)std::count(devs.begin(), devs.end(), d));
+    if (per_dev > 1 && !std::getenv("EDSBWT_HBM_SHARE")) {
+        char share[32];
+        std::snprintf(share, sizeof share, "%.4f", 0.9 / (double)per_dev);
+        setenv("EDSBWT_HBM_SHARE", share, 1);
+    }
+    each(udev.size(), [&](size_t g) {
+        for (size_t k = 0; k < N; k++) {
+            if (devs[k] != udev[g]) continue;
+            sh[k].device = devs[k];
+            sh[k].rc = edsbwt_index_open(base.c_str(), devs[k], 8, &sh[k].idx);
+            if (sh[k].rc) sh[k].err = edsbwt_last_error();
+        }
     });
     for (auto& x : sh)
         if (x.rc) {

@@ -64,7 +64,11 @@ enum {
 #define EDSBWT_NO_COUNTERS  0x4000u/* the direct start's deep kernels without their per-lane work
                                     counters (steps, lines, text rows): the same results, those
                                     statistics read 0 for them, and the kernels run with fewer
-                                    registers (C3: k_deep_direct 0.816 against 0.850 ms) */
+                                    registers (C3: k_deep_direct 0.816 against 0.850 ms).  Only the
+                                    default builds have counter-free instantiations — k_deep_direct
+                                    at 8 waves per SIMD and k_deep<4 intervals> at 5 or 6 waves;
+                                    the builds chosen by EDSBWT_DIRECT_WAVES < 8, EDSBWT_DEEPQ_WAVES=1,
+                                    EDSBWT_EOF_ROWS=1 or EDSBWT_DEEP_K != 4 keep their counters */
 
 typedef struct edsbwt_index edsbwt_index;
 

@@ -1180,6 +1180,47 @@ def test_k_deep_builds_gpu(oracle, edsbwt, tmp_path, monkeypatch, build):
         monkeypatch.delenv("EDSBWT_DIRECT_ITEMS", raising=False)
 
 
+@pytest.mark.parametrize("build", [{}, {"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEP_STATS": "0"}],
+                         ids=lambda b: ",".join(f"{k[7:]}={v}" for k, v in b.items()) or "default")
+def test_hash_pattern_pair_step_in_k_deep_gpu(oracle, edsbwt, tmp_path, monkeypatch, build):
+    """Patterns holding '#' that are still alive when k_deep reaches the '#' (ADVICE r5, high):
+    X + '#' + Y with Y a word's head and X a word's tail, so Y's rows survive and the '#' step
+    (code 0) is taken inside k_deep with pair entries on (rent2, EDSBWT_DEEPQ_PAIRS default).  A
+    pair code for c = '#' would wrap below 1 and index rent2 ~2^32 entries away; the single step is
+    the reference's (MOVE_EDSBWTSearch.cpp:376-422 with c = '#').  Such patterns take the ordered
+    path (levels()); EDSBWT_DEEP_SHARE=0 cuts over to k_deep at depth 2, so the '#' is met there."""
+    for k, v in build.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("EDSBWT_DEEP_SHARE", "0")
+    rng = random.Random(2323)
+    segs = edsgen.random_eds(rng, 600, lmax=9, p_empty=0.2)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    words = [w for s in segs for w in s if len(w) >= 4]
+    assert words
+    pats = []
+    for _ in range(1500):
+        a, b = rng.choice(words), rng.choice(words)
+        pats.append(a[-rng.randint(1, 3):] + "#" + b[: rng.randint(2, 4)])      # '#' at depth 2..4
+    pats += [rng.choice(words)[-2:] + "#" + "".join(rng.choice("ACGT") for _ in range(3)) for _ in range(300)]
+    pats += ["#" + rng.choice(words)[:3] for _ in range(50)] + [rng.choice(words)[-3:] + "#" for _ in range(50)]
+    pats += [edsgen.planted(rng, segs, rng.randint(4, 20)) or "ACGT" for _ in range(1000)]  # the same batch, no '#'
+    buf, offs = _pack(pats)
+    eng = oracle.Engine(base, 8)
+    oc, oo, _ = eng.search(buf, offs)
+    # every head Y after the '#' occurs (a word's prefix): each such pattern is alive at the '#'
+    ybuf, yoffs = _pack([p.split("#", 1)[1] for p in pats[:1500]])
+    assert (eng.search(ybuf, yoffs)[0] > 0).all()
+    with edsbwt.Index(base) as idx:
+        assert idx.pair_blocks
+        for kw in ({}, {"locate": False}, {"ktab": False}, {"ordered": True}):
+            gc, go = idx.search((buf, offs), **kw)
+            assert np.array_equal(gc, oc), (build, kw, np.flatnonzero(gc != oc)[:8].tolist())
+            if kw.get("locate", True):
+                assert np.array_equal(go, oo), (build, kw)
+            if kw.get("ktab") is False:
+                assert idx.stats()["deep_from_depth"] == 2  # k_deep walked from depth 2: it met every '#'
+
+
 @pytest.mark.parametrize("gpus", [2, 3, 5])
 def test_cli_gpus_shards(oracle, tmp_path, gpus):
     """EDSBWTsearch --gpus N (the pattern loop MOVE_EDSBWTSearch.cpp:111-136 sharded into N

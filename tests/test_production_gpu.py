@@ -93,18 +93,30 @@ def _d2h(ptr, nbytes):
     return out[:nbytes]
 
 
-def _device_tags(edsbwt, idx, buf, offs, first_id, locate):
-    """search_device over the whole batch (no chunking): counts, records, path tags."""
+def _device_search(edsbwt, idx, buf, offs, first_id, locate, counters=True, repeat=1):
+    """search_device over the whole batch (no chunking) on torch's current stream, as bench.py's
+    device-resident leg calls it; repeat > 1 calls it again on the same buffers (the timed steps'
+    reuse) and returns the last call's counts and records."""
     torch = pytest.importorskip("torch")
     npat = offs.size - 1
     d_bytes = torch.from_numpy(buf.copy()).cuda()
     d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
     d_counts = torch.zeros(npat, dtype=torch.int32, device="cuda")
-    ptr, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(), first_pattern_id=first_id,
-                               locate=locate)
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(repeat):
+        d_counts.fill_(-1)
+        ptr, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, d_counts.data_ptr(), first_pattern_id=first_id,
+                                   locate=locate, stream=stream, counters=counters)
+    torch.cuda.synchronize()
     counts = d_counts.cpu().numpy().view(np.uint32).copy()
     occ = _d2h(ptr, n * 20).view(edsbwt.OCC_DTYPE) if locate else np.zeros(0, edsbwt.OCC_DTYPE)
-    tags = idx.path_tags(npat)
+    return counts, occ
+
+
+def _device_tags(edsbwt, idx, buf, offs, first_id, locate):
+    """search_device over the whole batch (no chunking): counts, records, path tags."""
+    counts, occ = _device_search(edsbwt, idx, buf, offs, first_id, locate)
+    tags = idx.path_tags(offs.size - 1)
     return counts, occ, tags, idx.stats()
 
 
@@ -142,6 +154,19 @@ def _check_production(oracle, edsbwt, monkeypatch, name, expect_direct):
         assert np.array_equal(c2, counts) and o2.size == 0
         dc, do, tags, dst = _device_tags(edsbwt, idx, buf, offs, lo + 1, locate=True)
         assert np.array_equal(dc, counts) and np.array_equal(do, occ)
+    # the exact build bench.py times: a fresh index without path tags, the
+    # device-resident call with EDSBWT_NO_COUNTERS (the counter-free k_deep_direct / k_deep
+    # instantiations), three calls on the same buffers as the timed steps make them; its counts and
+    # every record equal the counted device run and the host path above
+    monkeypatch.delenv("EDSBWT_PATH_TAGS")
+    with edsbwt.Index(base) as idx:
+        fc, fo = _device_search(edsbwt, idx, buf, offs, lo + 1, locate=True, counters=False, repeat=3)
+        fst = idx.stats()
+        assert fst["redo_searches"] == 0 and (not expect_direct or fst["start_depth"] == 15)
+        assert np.array_equal(fc, counts) and np.array_equal(fo, occ)
+        if name == "c2":  # C2's timed step is count-only
+            fc2, fo2 = _device_search(edsbwt, idx, buf, offs, lo + 1, locate=False, counters=False, repeat=2)
+            assert np.array_equal(fc2, counts) and fo2.size == 0
     # whole-batch properties
     assert int(counts.astype(np.uint64).sum()) == occ.size
     assert (counts[planted] > 0).all()
@@ -164,6 +189,8 @@ def _check_production(oracle, edsbwt, monkeypatch, name, expect_direct):
                    "tagged_levels": int((tags & edsbwt.PATH_LEVELS).astype(bool).sum()),
                    "tagged_redo": int((tags & edsbwt.PATH_REDO).astype(bool).sum()), "rare_in_sample": int(rare.size),
                    "device_stats": {k2: dst[k2] for k2 in ("deep_overflow", "deep_level_rerun", "redo_searches", "start_depth")},
+                   "timed_build_checked": "search_device with EDSBWT_NO_COUNTERS (bench.py's timed build), 3 calls, no path "
+                                          "tags: counts and every record equal to the counted device run and the host path",
                    "match": True})
     return counts, occ
 

@@ -20,6 +20,11 @@
 #   rccl:<cfg>[:<patterns>] one rank through the exchange path over RCCL (bench.py --dist-self)
 #   cli:<cfg>               the EDSBWTsearch CLI timed on the config's index and pattern file
 #   ab:<cfg>:<VAR=a,VAR2=b>[:<VAR=c>...] A/B bench lines (no CPU leg) under env settings
+#   abi:<cfg>:<reps>:<VAR=a,..>:<VAR=b,..>  interleaved A/B: reps x (A, B) device-resident lines (no e2e,
+#                           no CPU leg), one summary line each (round 5's one-off r5*.sh passes, folded in)
+#   stress:<args>           tools/kdeep_stress.py (every k_deep build, repeated searches) with <args> (',' = ' ')
+#   dist:<cfg>              the exchange path with one rank (--dist-self) and the same line without it,
+#                           interleaved twice: the step with and without the exchange
 # Outputs: gpurun_out/<tag>_<task>*.{json,log}.
 export TMPDIR=/tmp
 TAG=$1; shift
@@ -108,6 +113,29 @@ for task in "$@"; do
         i=$((i+1))
         env ${spec//,/ } timeout -k 10 600 python bench.py --no-cpu --no-located --config $cfg --steps 5 --warmup 2 > ${out}_$i.json 2> ${out}_$i.log || fail ab ${out}_$i.log
         python3 -c "import json;d=json.load(open('${out}_$i.json'));r=d.get('device_resident',{});e=d.get('e2e') or {};print('$spec', d['value'], d['ms_per_step'], r.get('kernel_ms_per_step'), 'e2e median', e.get('ms_wall_median'))"
+      done ;;
+    abi)
+      cfg=${a:-c3}; reps=${b:-3}
+      for k in $(seq 1 $reps); do
+        for spec in "$c" "$d"; do
+          [ -z "$spec" ] && continue
+          sid=${spec//[^A-Za-z0-9]/_}
+          env ${spec//,/ } timeout -k 10 300 python3 bench.py --no-cpu --no-e2e --no-located --config $cfg --steps 20 --warmup 3 > ${out}_${k}_${sid}.json 2>> ${out}.log || fail abi ${out}.log
+          python3 -c "import json;d=json.load(open('${out}_${k}_${sid}.json'));print('$k', '$spec', d['ms_per_step'], d['device_resident']['kernel_ms_per_step'])" | tee -a ${out}_summary.txt
+        done
+      done ;;
+    stress)
+      timeout -k 10 900 python3 tools/kdeep_stress.py ${a//,/ } > ${out}.json 2> ${out}.log || fail stress ${out}.log
+      tail -5 ${out}.json ;;
+    dist)
+      cfg=${a:-c3}
+      for k in 1 2; do
+        timeout -k 10 600 python bench.py --dist-self --config $cfg --steps 20 --warmup 3 --no-cpu > ${out}_self_$k.json 2>> ${out}.log || fail dist ${out}.log
+        timeout -k 10 600 python bench.py --config $cfg --steps 20 --warmup 3 --no-cpu > ${out}_plain_$k.json 2>> ${out}.log || fail dist ${out}.log
+        python3 -c "
+import json
+a=json.load(open('${out}_self_$k.json'));b=json.load(open('${out}_plain_$k.json'))
+print('$k', 'exchange', a['ms_per_step'], a['e2e']['per_rank_search_exchange_ms'], 'plain', b['ms_per_step'], b['e2e']['per_rank_search_exchange_ms'])" | tee -a ${out}_summary.txt
       done ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
