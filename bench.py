@@ -343,9 +343,9 @@ def main():
     ap.add_argument("--workdir", default=workloads.default_workdir())
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on GPU nodes; gloo to rehearse ranks on one GPU")
     ap.add_argument("--gather", default="auto", choices=("auto", "none", "counts"),
-                    help="N>1 exchange: the (patterns, records) sizes are all-gathered (each rank's output offsets: every "
-                         "rank keeps its counts and records as its slice of the output); 'counts' (the default when N>1) "
-                         "also gathers the per-pattern counts to rank 0 over RCCL inside the timed step")
+                    help="N>1 exchange: 'counts' (the default when N>1) gathers the per-pattern counts to rank 0 over "
+                         "RCCL inside the timed step (every rank's (patterns, records) offsets follow from them); 'none': "
+                         "no exchange, every rank keeps its counts and records")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -443,64 +443,70 @@ def main():
     flags_kw = dict(table=args.locate == "table", walk=args.locate == "walk")
     rccl = multi and args.dist_backend == "nccl"
 
-    # ---- the exchange step (N > 1), set up once per batch shape (shard.SizesExchange / CountsGather):
-    # every rank's shard size follows from the static split, so no size is read back to the host and
-    # nothing is allocated per step; on RCCL both collectives are asynchronous and the counts of step
-    # i are gathered from one of two alternating device buffers while step i + 1 searches into the other
+    # ---- the exchange step (N > 1), set up once per batch shape: the per-pattern counts gathered to
+    # rank 0 (shard.CountsGather over RCCL/xGMI).  Every rank's shard size follows from the static split
+    # and its records are the sum of its counts, so rank 0 has every rank's (patterns, records) offsets
+    # from the gather itself: one collective per step, no size read back to the host, nothing
+    # allocated per step.  On RCCL the gather runs from a side stream (shard.StepExchange) over two
+    # alternating count buffers: step i's gather beside step i + 1's search, whose stream never waits
     shard_sizes = [b_ - a_ for a_, b_ in (workloads.shard(w, r, world, args.patterns) for r in range(world))]
     assert shard_sizes[rank] == npat
-    sx = shard.SizesExchange(gdev) if multi else None
     cg = shard.CountsGather(shard_sizes, gdev) if multi and args.gather == "counts" else None
     # e2e leg: the engine leaves each call's u32 counts in a device mirror too (a device-to-device copy
-    # per chunk): RCCL gathers them from HBM, no second upload.  Two mirrors, alternated per call; a
-    # mirror is written again only after the host saw its gather end (xev, recorded two calls earlier)
-    d_counts_x = [torch.zeros(npat, dtype=torch.int32, device=dev) for _ in range(2 if rccl and cg else 0)]
-    xev = [None, None]
-    n_e2e = [0]
+    # per chunk): RCCL gathers them from HBM, no second upload
+    xe_e2e = shard.StepExchange(cg, 2, npat, dev) if rccl and cg else None
+    # the last exchanged step's record count per leg (checked against rank 0's view after the timing)
+    last_nocc = {}
 
     def e2e_step(keep=False):
-        if d_counts_x:
-            k = n_e2e[0] % 2
-            if xev[k] is not None:
-                xev[k].synchronize()
-            idx.set_counts_mirror(d_counts_x[k].data_ptr(), npat)
+        if xe_e2e is not None:
+            k, buf_ = xe_e2e.buffer()
+            idx.set_counts_mirror(buf_.data_ptr(), npat)
         n, ptr, nocc = idx.search_lines(text.ptr, text.nbytes, counts_hb.ptr, npat + 1, first_pattern_id=first_id,
                                         locate=locate, keep=keep)
         assert n == npat, (n, npat)
         return ptr, nocc
 
-    def exchange(nocc, d_src=None):
-        # the path's exchange step: every rank's (patterns, records) all-gathered — its offsets in
-        # the output (each rank writes its slice); --gather counts also gathers the
-        # per-pattern counts to rank 0 (RCCL/xGMI).  d_src: the device-resident leg's counts.
-        if not multi:
+    def exchange(nocc, xe=None, d_src=None, leg="e2e"):
+        # the path's exchange step: the per-pattern counts to rank 0, where they also
+        # give every rank's (patterns, records) — its offsets in the output.  xe: the leg's StepExchange
+        # (RCCL; its current buffer was just written); else gloo: counts staged through host memory
+        if not multi or cg is None:
             return
-        sx.start(npat, nocc, async_op=rccl)
-        if cg is None:
-            return
-        if rccl:
-            if d_src is not None:
-                cg.start(d_src, async_op=True)  # the next start() (after the next search) makes the stream wait
-            else:
-                k = n_e2e[0] % 2
-                cg.start(d_counts_x[k], async_op=True)
-                cg.wait()  # (the current stream waits; the engine's own streams do not)
-                xev[k] = torch.cuda.Event()
-                xev[k].record()
-                n_e2e[0] += 1
-        else:  # gloo rehearsal: counts staged through host memory, synchronous
+        last_nocc[leg] = nocc
+        if xe is not None:
+            xe.send((xe.k) % len(xe.bufs), after=torch.cuda.current_stream(dev) if leg == "device" else None)
+        else:
             cg.start(d_src.cpu() if d_src is not None else torch.from_numpy(counts[:npat].view(np.int32)))
 
     def exchange_drain():
-        if sx is not None:
-            sx.result()
+        for xe in (xe_e2e, xe_dev):
+            if xe is not None:
+                xe.drain()
         if cg is not None:
             cg.wait()
+
+    def exchange_check(leg):
+        """Outside the timed region: rank 0's per-rank records from the gathered counts == every
+        rank's own record count of its last exchanged step."""
+        if not multi or cg is None or leg not in last_nocc:
+            return None
+        mine = torch.tensor([last_nocc[leg]], dtype=torch.int64, device=gdev)
+        allr = torch.empty(world, dtype=torch.int64, device=gdev)
+        dist.all_gather_into_tensor(allr, mine)
+        got = cg.result()
+        if rank != 0:
+            return None
+        sums = [int(t_.cpu().numpy().view(np.uint32).astype(np.int64).sum()) for t_ in torch.split(got, shard_sizes)]
+        return {"records_per_rank_from_counts": sums, "records_per_rank_reported": [int(x) for x in allr.tolist()],
+                "match": sums == [int(x) for x in allr.tolist()]}
+
+    xe_dev = None
 
     # ---- timed: end-to-end (host memory -> host memory)
     for _ in range(0 if args.no_e2e else args.warmup):
         _, nocc = e2e_step()
-        exchange(nocc)
+        exchange(nocc, xe_e2e)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -517,7 +523,7 @@ def main():
         if last:
             held = (ptr, nocc)
         tb = time.perf_counter()
-        exchange(nocc)
+        exchange(nocc, xe_e2e)
         search_ms += 1e3 * (tb - ta)
         exch_ms += 1e3 * (time.perf_counter() - tb)
         st_call = idx.stats_struct()  # one preallocated struct: no per-step dict building in the timed loop
@@ -528,6 +534,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    xchk = {"e2e": exchange_check("e2e")}
     host_cores = (time.process_time() - c0) / max(1e-9, elapsed)  # host CPU the pipeline kept busy
     e2e_stats = idx.stats()
     if args.no_e2e:
@@ -560,11 +567,10 @@ def main():
         buf, offs = pkg.read_pattern_file(pats_path)
         d_bytes = torch.from_numpy(buf).to(dev)
         d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
-        # two count buffers when the counts are gathered (RCCL): step i's gather reads one while
-        # step i + 1 searches into the other (shard.CountsGather); else one
-        d_counts_b = [torch.zeros(npat, dtype=torch.int32, device=dev) for _ in range(2 if rccl and cg else 1)]
-        d_counts = d_counts_b[0]
-        n_dev = [0]
+        # two count buffers when the counts are gathered (RCCL, shard.StepExchange): step i's gather
+        # reads one while step i + 1 searches into the other; else one
+        xe_dev = shard.StepExchange(cg, 2, npat, dev) if rccl and cg else None
+        d_counts = torch.zeros(npat, dtype=torch.int32, device=dev)
 
         # the timed steps run the deep kernels' builds without their work counters (EDSBWT_NO_COUNTERS:
         # same results, fewer registers); the line model (bytes / lines per launch, intervals stepped)
@@ -573,8 +579,7 @@ def main():
 
         def dev_step(profile=False, counters=counted):
             # returns (records pointer, records, the counts buffer this step wrote)
-            dc = d_counts_b[n_dev[0] % len(d_counts_b)]
-            n_dev[0] += 1
+            dc = xe_dev.buffer()[1] if xe_dev is not None else d_counts
             p_, n_ = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, dc.data_ptr(), first_pattern_id=first_id,
                                        locate=locate, profile=profile, stream=stream, counters=counters, **flags_kw)
             return p_, n_, dc
@@ -583,12 +588,12 @@ def main():
         if not counted:
             kacc_c = idx.kernel_acc()
             _, dn, dc = dev_step(profile=PROFILE_TIMED, counters=True)
-            exchange(dn, dc)
+            exchange(dn, xe_dev, dc, "device")
             idx.add_kernel_stats(kacc_c)
             stats_c = idx.stats()
         for _ in range(max(1, args.warmup)):
             _, dn, dc = dev_step()
-            exchange(dn, dc)
+            exchange(dn, xe_dev, dc, "device")
         exchange_drain()
         d_counts = dc
         located = None
@@ -596,6 +601,10 @@ def main():
             # C5: the timed step is the located search (the reference always locates), in record-budget
             # chunks; the count-only warm-up above gave the counts the chunks are cut by
             counts_c = d_counts.cpu().numpy().view(np.uint32)[:npat].copy()
+            if xe_dev is not None:
+                xe_dev.drain()
+                for b_ in xe_dev.bufs:  # (each located step gathers the batch's counts, in line order)
+                    b_.copy_(d_counts)
             chunks, budget, setup_s = located_chunks(buf, offs, counts_c, dev, args.located_budget, torch, first_id,
                                                       order=args.located_order)
             chk = located_pass(idx, chunks, counts_c, stream, torch, check=True)  # warm-up pass, checked
@@ -619,15 +628,16 @@ def main():
         for _ in range(args.steps):
             if located_timed:
                 lp = located_pass(idx, chunks, counts_c, stream, torch, kacc=kacc)
-                exchange(lp["records"])
+                exchange(lp["records"], xe_dev, d_counts, "device")  # (the batch's counts, line order)
             else:
                 p_last, n_last, d_counts = dev_step(profile=PROFILE_TIMED)
-                exchange(n_last, d_counts)
+                exchange(n_last, xe_dev, d_counts, "device")
                 idx.add_kernel_stats(kacc)  # HIP-event times of this call's kernel classes, summed in place
         exchange_drain()
         torch.cuda.synchronize()
         barrier()
         d_elapsed = time.perf_counter() - t1
+        xchk["device_resident"] = exchange_check("device")
         # the last TIMED step's results (its build: counter-free unless --timed-counters), kept for the
         # oracle sample below (the records the headline times are the ones compared)
         timed_counts = d_counts.cpu().numpy().view(np.uint32)[:npat].copy()
@@ -732,11 +742,13 @@ def main():
                                         "(--no-device) edsbwt_search_lines: page-locked pattern-file bytes H2D -> search -> "
                                         "counts + records D2H (SURVEY §8(d)), plus the exchange step when N>1"),
                        "exchange": ("none (one GPU)" if not multi else
-                                    "sizes all-gathered (each rank keeps its counts + records as its output slice)"
-                                    + ((" + counts gathered to rank 0 over RCCL (device counts mirror, xGMI)"
-                                        if args.dist_backend == "nccl" else
-                                        f" + counts gathered to rank 0 over {args.dist_backend} (rehearsal: counts staged "
-                                        "through host memory)") if args.gather == "counts" else "")),
+                                    "none (--gather none: every rank keeps its counts + records)" if args.gather != "counts" else
+                                    ("per-pattern counts gathered to rank 0 over RCCL (xGMI) from a side stream, two "
+                                     "alternating count buffers (the gather of step i beside the search of step i + 1); "
+                                     "every rank's (patterns, records) offsets follow from the gathered counts"
+                                     if args.dist_backend == "nccl" else
+                                     f"per-pattern counts gathered to rank 0 over {args.dist_backend} (rehearsal: counts "
+                                     "staged through host memory, synchronous)")),
                        "dist_backend": args.dist_backend if multi else None,
                        "ktab_depth": idx.ktab_depth, "ltab_depth": idx.ltab_depth, "ltab_items": idx.ltab_items,
                        "index_device_bytes": idx.device_bytes,
@@ -831,7 +843,7 @@ def main():
             out["device_resident"] = {
                 "value": round(total_pats * args.steps / dres["elapsed"], 1), "ms_per_step": round(d_ms, 3),
                 "what": "pattern bytes + u64 offsets resident in HBM before the timed region; counts + records left in HBM"
-                        + ("; the exchange step (sizes all-gathered, counts gathered to rank 0) in every step" if multi else ""),
+                        + ("; the exchange step (counts gathered to rank 0) in every step" if multi else ""),
                 "kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in sorted(kstats.items()) if v["ms"]},
                 "kernel_lines_per_s": {k: round((v["lines"] / (v["ms"] * 1e-3)) if v["ms"] > 0 else 0.0, 1)
                                        for k, v in sorted(kstats.items()) if v["lines"]},
@@ -852,6 +864,9 @@ def main():
                                     "oracle-counted reference M_LF moves per pattern x value (SURVEY §8(d)), a model, not executed")
         if rank_parity is not None:
             out["parity_sample"] = rank_parity
+        if multi and cg is not None:
+            out["exchange_check"] = dict(xchk, what="rank 0: every rank's records of its last exchanged step from the "
+                                                    "gathered counts (sum per rank) == the record count each rank reported")
         if world == 1 and not args.no_cpu:
             buf, offs = pkg.read_pattern_file(pats_path)
             threads = cpu_threads

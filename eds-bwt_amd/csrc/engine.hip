@@ -646,6 +646,15 @@ struct Engine {
     // k_deep takes two characters per rank entry when no interval of its list meets a link
     // (rent2, as k_deep_direct; EDSBWT_DEEPQ_PAIRS=0: one character per step)
     uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
+    // the deferred direct start in pieces (EDSBWT_DEEP_PIECES, batches of at least
+    // EDSBWT_DEEP_PIECE_MIN patterns): k_deep_direct over piece j + 1 runs while k_deep walks piece
+    // j's queue on a second stream (an event per piece), so k_deep's long-tailed lanes share the
+    // GPU with the next piece's direct walk instead of running after the whole batch
+    uint32_t deep_pieces = std::max(1u, std::min(16u, (uint32_t)env_double("EDSBWT_DEEP_PIECES", 1)));
+    uint64_t deep_piece_min = (uint64_t)env_double("EDSBWT_DEEP_PIECE_MIN", 1 << 20);
+    hipStream_t stream2 = nullptr;  // (created on first use)
+    std::vector<hipEvent_t> piece_ev;
+    DBuf<uint32_t> pcnt;  // queue counters of the pieces (NSHARD * 32 per piece)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
     uint64_t defer_cap = (uint64_t)env_double("EDSBWT_DEFER_CAP", 0);        // (tests: record / task buffer caps)
     // pinned + 32..: the deferred checks' landing slots (u32 words)
@@ -2027,20 +2036,25 @@ struct Engine {
         // fused counts: only on the deferred direct start (its three kernels write every final count)
         uint32_t* fc = kdd && defer ? fc_counts : nullptr;
         if (fc) fc_done = true;
-        if (kdd && fk_now.on) {
+        const uint32_t np = kdd && fk_now.on && defer && deep_pieces > 1 && P >= deep_piece_min && K == 4 && bps == 3 &&
+                                    !X.eofrow && deepq_waves >= 5
+                                ? deep_pieces : 1u;
+        if (np > 1) {
+            run_deep_pieces(np, d, P, nid_d, goff, gend, gb, gee, lens, k0, krest, ind, X, abase, K, r, kt1w, fc);
+        } else if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
             // written there, for k_deep and k_deep_wave)
             auto kd0 = direct_waves >= 8 ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
                      : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
-                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc);
+                   fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, 0u);
             fk_now.on = false;
         } else if (kdd) {
             auto kd0 = direct_waves >= 8 ? k_deep_direct<8> : direct_waves >= 7 ? k_deep_direct<7> : direct_waves >= 6 ? k_deep_direct<6>
                                                                                                         : k_deep_direct<1>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
                    (const uint8_t*)nullptr, (const uint64_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (unsigned long long*)nullptr, 0u,
-                   0u, 0u, fc);
+                   0u, 0u, fc, 0u);
         } else {
             auto kf = bps == 4 ? k_deep_fast<4> : deep_waves >= 8 ? k_deep_fast<3, 8> : deep_waves >= 6 ? k_deep_fast<3, 6> : k_deep_fast<3>;
             launch(KC_DEEP, kf, P, P, d, lens, (const uint32_t*)perm.p, k0, krest, ind,
@@ -2052,6 +2066,9 @@ struct Engine {
             HIPCHK(hipGetLastError());
         }
         const bool unb = deepq_waves <= 1;
+        if (np > 1) {
+            // (run_deep_pieces walked every piece's queue)
+        } else {
         auto kd = K == 2   ? (bps == 3 ? k_deep<2, 3> : k_deep<2, 4>)
                   : K == 3 ? (bps == 3 ? k_deep<3, 3> : k_deep<3, 4>)
                   : K == 4 ? (bps == 3 ? (X.eofrow ? (unb ? k_deep<4, 3, 1, true> : k_deep<4, 3, 5, true>)
@@ -2062,6 +2079,7 @@ struct Engine {
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
                pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc, deepq_pairs);
         tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
+        }
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;
         if (trace)
@@ -2126,6 +2144,56 @@ struct Engine {
         if (no_wide) st.deep_overflow += nw;
         st.deep_level_rerun += novf;
         return novf;
+    }
+
+    // The fused, deferred direct start in np pieces of the batch (EDSBWT_DEEP_PIECES): piece j's
+    // k_deep_direct on the library stream, then an event, and k_deep over piece j's own queue on a
+    // second stream, so it runs beside piece j + 1's k_deep_direct; the library stream waits for the
+    // last k_deep before what follows (k_deep_wave, locate).  Each piece has its own queue slots and
+    // shard counters (pcnt), its k_deep the queue's capacity of its piece; results, counts, the
+    // overflow list and the statistics are shared (device atomics).  Same work, same results as one
+    // piece: only the order in which the GPU runs it changes
+    void run_deep_pieces(uint32_t np, uint32_t d, uint64_t P, const uint32_t* nid_d, const uint32_t* goff, const uint32_t* gend,
+                         const uint32_t* gb, const uint32_t* gee, const uint32_t* lens, const uint64_t* k0, const uint64_t* krest,
+                         uint32_t ind, const KIdx& X, uint64_t abase, uint32_t K, Res* r, const uint4* kt1w, uint32_t* fc) {
+        if (!stream2) HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+        while (piece_ev.size() < np + 1) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            piece_ev.push_back(e);
+        }
+        DBuf<uint32_t>& ovf = tflag;
+        const size_t pq = std::max<size_t>(shard_bound((P + np - 1) / np, 1), 1024);  // each piece's queue capacity per shard
+        dq.ensure(pq * NSHARD * np);
+        dq2.ensure(pq * NSHARD * np);
+        pcnt.ensure((size_t)NSHARD * 32 * np);
+        // stream2 starts after everything already on the library stream (the zeroing, the keys' inputs)
+        HIPCHK(hipEventRecord(piece_ev[np], stream));
+        HIPCHK(hipStreamWaitEvent(stream2, piece_ev[np], 0));
+        auto kd0 = direct_waves >= 8 ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
+                 : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
+        auto kd = deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>)
+                                   : (deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>);
+        for (uint32_t j = 0; j < np; j++) {
+            const uint64_t lo = P * j / np, hi = P * (j + 1) / np;
+            uint4* qj = (uint4*)dq.p + (size_t)j * pq * NSHARD;
+            uint64_t* q2j = dq2.p + (size_t)j * pq * NSHARD;
+            uint32_t* cj = pcnt.p + (size_t)j * NSHARD * 32;
+            launch(KC_DEEP, kd0, hi - lo, hi, d, nid_d, X, abase, K, r, qj, (uint32_t)pq, cj, stats.p, (const uint64_t*)nullptr, perm.p,
+                   kt1w, q2j, fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin,
+                   fk_now.lmax, fc, (uint32_t)lo);
+            HIPCHK(hipEventRecord(piece_ev[j], stream));
+            HIPCHK(hipStreamWaitEvent(stream2, piece_ev[j], 0));
+            std::swap(stream, stream2);  // (launch() and its timing events on the second stream)
+            launch(KC_DEEPQ, kd, hi - lo, (const uint4*)qj, (const uint32_t*)cj, (uint32_t)pq, d, lens, (const uint32_t*)perm.p, k0,
+                   krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p, (const uint64_t*)q2j, kt1w, fc,
+                   deepq_pairs);
+            std::swap(stream, stream2);
+            tag_queue((const uint4*)qj, (const uint32_t*)cj, (uint32_t)pq, EDSBWT_PATH_DEEP);
+        }
+        fk_now.on = false;
+        HIPCHK(hipEventRecord(piece_ev[np], stream2));
+        HIPCHK(hipStreamWaitEvent(stream, piece_ev[np], 0));
     }
 
     // Direct start: when every pattern is longer than the k-mer table's depth D0 and the
@@ -2865,8 +2933,10 @@ struct Engine {
             lbig.ensure(P + 1);  // (the per-pattern locate's big list: its counter is zeroed here)
             // (the result array only when the search does not turn out to be k_deep_direct's, which
             // writes every result: res_unzeroed, settled by run_batch / run_deep)
+            if (deep_pieces > 1) pcnt.ensure((size_t)NSHARD * 32 * deep_pieces);
             zero_many({{stats.p, kStatSlots * 8}, {counters.p, 24 * 8}, {tflag.p, 4}, {hcnt.p, 4},
-                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}, {lbig.p, 4}});
+                       {lcnt.p, NSHARD * 32 * 4}, {oscan.p, 8}, {bhist.p, nb ? (nb + 1) * 4 : 0}, {lbig.p, 4},
+                       {pcnt.p, deep_pieces > 1 ? (size_t)NSHARD * 32 * deep_pieces * 4 : 0}});
             res_unzeroed = true;
         } else {
             zero(res.p, P * sizeof(Res));
@@ -4492,6 +4562,9 @@ struct Engine {
 
     ~Engine() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (stream2) (void)hipStreamSynchronize(stream2);
+        for (auto e : piece_ev) (void)hipEventDestroy(e);
+        if (stream2) (void)hipStreamDestroy(stream2);
         if (up) (void)hipStreamSynchronize(up);
         if (down) (void)hipStreamSynchronize(down);
         for (auto e : chunk_ev) (void)hipEventDestroy(e);

@@ -1577,7 +1577,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                                                            const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                            uint32_t* __restrict__ len_out, uint32_t* __restrict__ kid_out,
                                                            unsigned long long* __restrict__ n_term, uint32_t E, uint32_t lmin, uint32_t lmax,
-                                                           uint32_t* __restrict__ counts) {
+                                                           uint32_t* __restrict__ counts, uint32_t i0) {
+    // patterns [i0, P) (i0 > 0: one piece of the batch, engine.hip run_deep_pieces)
     LaneCtr<STATS> n_steps, n_blk, n_pl, n_text, n_trow;  // per lane: < 2^32 (widened at the end)
     CountSums cs;  // counts != nullptr: each final count written here (fused counts)
 #ifdef EDSBWT_DEEP_CLOCKS
@@ -1590,7 +1591,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     // 32-bit pattern indices (the engine keeps a search's batch below 2^31 patterns): fewer registers
     // and no 64-bit index arithmetic in a kernel whose time follows its register pressure
     const uint32_t P32 = (uint32_t)P, stride32 = gridDim.x * blockDim.x;
-    for (uint32_t i_b = blockIdx.x * blockDim.x; i_b < P32; i_b += stride32) {
+    for (uint32_t i_b = i0 + blockIdx.x * blockDim.x; i_b < P32; i_b += stride32) {
         const uint32_t i = i_b + threadIdx.x;
         const bool valid = i < P32;
         uint32_t want = 0;

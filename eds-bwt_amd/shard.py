@@ -180,6 +180,56 @@ class CountsGather:
         return torch.cat([r[:n] for r, n in zip(self.recv, self.sizes)])
 
 
+class StepExchange:
+    """The per-step counts gather of a timed loop on GPUs (RCCL), kept off the search's stream:
+    `nbuf` device count buffers written in turn by the searches; send(k) orders a gather of buffer k
+    after the work already queued on `after` (an event), issues it from a side stream and records its
+    end there; buffer(k) hands a buffer out again only after the host saw its previous gather end
+    (with two buffers: the gather of step i runs beside the search of step i + 1, and the search's
+    stream never waits for a collective).  The per-rank (patterns, records) offsets follow from the
+    gathered counts on rank dst (patterns per rank are static; records = the sum of a rank's counts),
+    so no separate sizes collective runs per step."""
+
+    def __init__(self, cg: "CountsGather", nbuf: int, n: int, device):
+        import torch
+
+        self.cg = cg
+        self.side = torch.cuda.Stream(device)
+        self.bufs = [torch.zeros(max(n, 1), dtype=torch.int32, device=device)[:n] for _ in range(nbuf)]
+        self.ev_src = torch.cuda.Event()
+        self.ev_done = [torch.cuda.Event() for _ in range(nbuf)]
+        self.pending = [False] * nbuf
+        self.k = 0
+
+    def buffer(self):
+        """(k, tensor): the next buffer to write, free of its previous gather."""
+        k = self.k % len(self.bufs)
+        if self.pending[k]:
+            self.ev_done[k].synchronize()
+            self.pending[k] = False
+        return k, self.bufs[k]
+
+    def send(self, k: int, after=None) -> None:
+        """Gather buffer k to dst once the work queued so far on stream `after` (None: already done) ends."""
+        import torch
+
+        if after is not None:
+            self.ev_src.record(after)
+            self.side.wait_event(self.ev_src)
+        with torch.cuda.stream(self.side):
+            self.cg.start(self.bufs[k], async_op=True)
+            self.cg.wait()  # (the side stream waits for the collective; the host does not)
+            self.ev_done[k].record(self.side)
+        self.pending[k] = True
+        self.k += 1
+
+    def drain(self) -> None:
+        for k, p in enumerate(self.pending):
+            if p:
+                self.ev_done[k].synchronize()
+                self.pending[k] = False
+
+
 def gather_records(occ, sizes: list[int], dst: int = 0, group=None):
     """Every rank's occurrence records to rank dst in rank order.  `occ` is an int32/uint32
     tensor of n x 5 words (edsbwt_occ, e.g. a view of the engine's device records) or a

@@ -220,7 +220,7 @@ int orc_transform(const char* eds_path, const char* base) {
     uint32_t* sa = xmalloc((size_t)tot * 4);
     for (uint32_t i = 0; i < tot; i++) sa[i] = i;
     gsa_ctx G = {T, wid};
-    qsort_r(sa, tot, 4, gsa_cmp, &G);
+    if (tot > 1) qsort_r(sa, tot, 4, gsa_cmp, &G);
 
     /* .bwt + .4.da → remove_empty_symbols (da_to_everything.cpp:371-486) */
     uint32_t N = tot - E.empty; /* toKeep */
@@ -583,7 +583,7 @@ orc_engine* orc_open(const char* base, uint32_t a, int from_runs_files) {
     if (load_runs(E, base, from_runs_files, L, E->n, &v, &let, &k)) { free(L); orc_close(E); return NULL; }
     E->runs = k;
     pq_t* heads = xmalloc((size_t)k * sizeof(pq_t));
-    memcpy(heads, v, (size_t)k * sizeof(pq_t));
+    if (k) memcpy(heads, v, (size_t)k * sizeof(pq_t));
     mlf_balance(&v, &k, E->n, a);
     E->r = k;
     E->p = xmalloc((size_t)(k + 1) * 4);
@@ -752,7 +752,7 @@ static void link_(const orc_engine* E, ctx_t* X) {
         uint32_t b_ = X->other.v[it].bi, e_ = X->other.v[it].ei;
         if (b_ <= e_) dollars_in_interval(E, X, b_, e_);
     }
-    qsort(X->d.v, X->d.n, 4, u32_cmp);
+    if (X->d.n > 1) qsort(X->d.v, X->d.n, 4, u32_cmp); /* (n = 0: v may be NULL — qsort's argument must not be) */
     rvec* D = &X->dollar;
     while (X->d.n) {
         uint32_t x = X->d.v[--X->d.n];
@@ -903,7 +903,10 @@ static int search_batch(orc_engine* E, const char* bytes, const uint64_t* offset
     if (occ) {
         *occ = xmalloc((size_t)tot * sizeof(orc_occ) + sizeof(orc_occ));
         uint64_t at = 0;
-        for (int t = 0; t < threads; t++) { memcpy(*occ + at, J[t].X.out.v, J[t].X.out.n * sizeof(orc_occ)); at += J[t].X.out.n; }
+        for (int t = 0; t < threads; t++) {
+            if (J[t].X.out.n) memcpy(*occ + at, J[t].X.out.v, J[t].X.out.n * sizeof(orc_occ));
+            at += J[t].X.out.n;
+        }
     }
     if (nocc) *nocc = tot;
     for (int t = 0; t < threads; t++) { if (ctr) add_ctr(ctr, &J[t].X.c); ctx_free(&J[t].X); }
@@ -1025,7 +1028,7 @@ int orc_search_batch_trie(orc_engine* E, const char* bytes, const uint64_t* offs
     uint8_t* owner = xmalloc((size_t)npat + 1);
     for (uint64_t i = 0; i < npat; i++) order[i] = i;
     rsort_arg A = {(const uint8_t*)bytes, offsets};
-    qsort_r(order, npat, 8, rev_cmp, &A);
+    if (npat > 1) qsort_r(order, npat, 8, rev_cmp, &A);
     tjob_t* J = xcalloc((size_t)threads, sizeof(tjob_t));
     pthread_t* th = xcalloc((size_t)threads, sizeof(pthread_t));
     for (int t = 0; t < threads; t++) {
@@ -1047,7 +1050,7 @@ int orc_search_batch_trie(orc_engine* E, const char* bytes, const uint64_t* offs
         *occ = xmalloc((size_t)tot * sizeof(orc_occ) + sizeof(orc_occ));
         uint64_t at = 0;
         for (uint64_t i = 0; i < npat; i++) {
-            memcpy(*occ + at, J[owner[i]].X.out.v + rec_at[i], (size_t)counts[i] * sizeof(orc_occ));
+            if (counts[i]) memcpy(*occ + at, J[owner[i]].X.out.v + rec_at[i], (size_t)counts[i] * sizeof(orc_occ));
             at += counts[i];
         }
     }

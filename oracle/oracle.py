@@ -14,8 +14,10 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
-CLI_PATH = os.path.join(HERE, "_build", "edsbwt_oracle")
+# EDSBWT_ORACLE_BUILD: another build directory of this Makefile (the sanitizer build, _build_asan)
+_BUILD = os.environ.get("EDSBWT_ORACLE_BUILD") or os.path.join(HERE, "_build")
+LIB_PATH = os.path.join(_BUILD, "liboracle.so")
+CLI_PATH = os.path.join(_BUILD, "edsbwt_oracle")
 
 OCC_DTYPE = np.dtype([("pat", "<u4"), ("word", "<u4"), ("seg", "<u4"), ("word_in_seg", "<u4"), ("offset", "<u4")])
 

@@ -573,6 +573,52 @@ def test_wide_kmer_entries_gpu(oracle, edsbwt, tmp_path, monkeypatch):
     assert sizes["11"] > sizes["10"]  # ... and the per-row entries
 
 
+@pytest.mark.parametrize("pieces", ["2", "3", "5"])
+def test_deep_pieces_gpu(oracle, edsbwt, tmp_path, monkeypatch, pieces):
+    """The deferred direct start in pieces (engine.hip run_deep_pieces, EDSBWT_DEEP_PIECES): each
+    piece's k_deep_direct, then k_deep over that piece's own queue on a second stream beside the
+    next piece's k_deep_direct.  Same counts and records as one piece and as the oracle, located
+    and count-only, with and without work counters, through search() and the device-resident call,
+    and the queue's patterns really walked by k_deep (path tags)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
+    monkeypatch.setenv("EDSBWT_DEEP_PIECE_MIN", "1")
+    monkeypatch.setenv("EDSBWT_PATH_TAGS", "1")
+    rng = random.Random(4242)
+    segs = _covid_like(rng, 900)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(7000)]
+    pats = [p[: D0 + 16] if len(p) > D0 + 16 else p for p in pats]
+    pats += [rng.choice("ACGT") + p[1:] for p in pats[:500]]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=3)
+    for np_ in ("1", pieces):
+        monkeypatch.setenv("EDSBWT_DEEP_PIECES", np_)
+        with edsbwt.Index(base) as idx:
+            for kw in ({}, {"locate": False}, {"counters": False}):
+                gc, go = idx.search((buf, offs), first_pattern_id=3, **kw)
+                assert idx.stats()["start_depth"] == D0 and idx.stats()["redo_searches"] == 0
+                assert np.array_equal(gc, oc), (np_, kw)
+                if kw.get("locate", True):
+                    assert np.array_equal(go, oo), (np_, kw)
+            d_bytes = torch.from_numpy(buf.copy()).cuda()
+            d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+            d_counts = torch.zeros(len(pats), dtype=torch.int32, device="cuda")
+            for counters in (True, False):
+                ptr, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), len(pats), d_counts.data_ptr(), first_pattern_id=3,
+                                           counters=counters)
+                torch.cuda.synchronize()
+                assert np.array_equal(d_counts.cpu().numpy().view(np.uint32), oc) and n == oo.size
+            tags = idx.path_tags(len(pats))
+            assert (tags & edsbwt.PATH_DEEP).sum() > 50  # queued patterns walked by k_deep in every piece
+            deep = np.flatnonzero(tags & edsbwt.PATH_DEEP)
+            assert deep.min() < len(pats) // int(pieces) and deep.max() >= len(pats) - len(pats) // int(pieces)
+
+
 @pytest.mark.parametrize("direct", [True, False])
 def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, direct):
     """Single-row intervals decided by comparing the pattern with the words' text: patterns

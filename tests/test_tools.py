@@ -10,7 +10,7 @@ import pytest
 from conftest import ROOT, GOLDEN
 import edsgen
 
-BUILD = os.path.join(ROOT, "eds-bwt_amd", "_build")
+BUILD = os.environ.get("EDSBWT_BUILD_DIR") or os.path.join(ROOT, "eds-bwt_amd", "_build")  # (tools/asan_suite.sh)
 FILES = [".ebwt", "_info.aux", ".bitvector", "_runs.aux", "_runs.txt"]
 
 
