@@ -475,7 +475,7 @@ def main():
             return
         last_nocc[leg] = nocc
         if xe is not None:
-            xe.send((xe.k) % len(xe.bufs), after=torch.cuda.current_stream(dev) if leg == "device" else None)
+            xe.send(xe.k % len(xe.bufs))  # (the search returned: its counts are complete)
         else:
             cg.start(d_src.cpu() if d_src is not None else torch.from_numpy(counts[:npat].view(np.int32)))
 
@@ -597,6 +597,19 @@ def main():
         exchange_drain()
         d_counts = dc
         located = None
+        count_only = None
+        if located_timed:
+            # the count-only device-resident step (C5's timed step through round 4), timed on its own so
+            # the C5 series stays comparable across rounds: same batch, counts left in HBM
+            torch.cuda.synchronize()
+            tc = time.perf_counter()
+            for _ in range(args.steps):
+                dev_step(counters=False)
+            torch.cuda.synchronize()
+            dt_c = (time.perf_counter() - tc) / args.steps
+            count_only = {"value": round(npat / dt_c, 1), "ms_per_step": round(1e3 * dt_c, 3), "steps": args.steps,
+                          "what": "the count-only device-resident search of the same batch (C5's timed step through "
+                                  "round 4), timed separately; `value` is the located step since round 5"}
         if located_timed:
             # C5: the timed step is the located search (the reference always locates), in record-budget
             # chunks; the count-only warm-up above gave the counts the chunks are cut by
@@ -668,6 +681,7 @@ def main():
             if not located["records_equal_counts"]:
                 raise SystemExit("bench.py: located chunks' records differ from the count-only counts")
             dres["located"] = located
+            dres["count_only"] = count_only
 
     # ---- N > 1: every rank's first patterns against the oracle, outside the timed region: the e2e
     # leg's results and the last timed device-resident step's (the counter-free build the line times)
@@ -857,6 +871,7 @@ def main():
             }
             if "located" in dres:
                 out["located"] = dres["located"]
+                out["device_resident_count_only"] = dres.get("count_only")
             # the LF steps the device executed (measured: 2 rank queries per interval step + locate moves)
             out["lf_steps_per_sec"] = out["device_resident"]["device_lf_steps_per_sec"]
             out["lf_steps_note"] = ("lf_steps_per_sec: LF steps the device executed (2 per interval step + locate walk moves), "
@@ -938,6 +953,9 @@ def main():
             except Exception as e:  # the GPU line is still valid
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), file=json_out, flush=True)
+    for xe in (xe_e2e, xe_dev):
+        if xe is not None:
+            xe.close()
     text.free()
     counts_hb.free()
     idx.close()

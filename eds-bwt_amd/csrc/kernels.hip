@@ -1911,8 +1911,14 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         uint32_t cn;
         // a list start (kQWide / kQNode) or one interval: the only divergent branch on the entry's
         // kind; wide or node list is the uniform kt1w (a kernel argument).  (A divergent three-way
-        // branch on the kind here made the unbounded build fault — rounds 4 and 5)
+        // branch on the kind here made the unbounded build fault — rounds 4 and 5, DESIGN.md §0;
+        // EDSBWT_KDEEP_THREEWAY compiles that shape back in for the test-only libedsbwt_3way.so)
+#ifdef EDSBWT_KDEEP_THREEWAY
+        if (w.z == kQWide) {  // (acac474: the table's presence checked inside the arm)
+            if (!kt1w) { flag_push(ovf, (uint32_t)i); continue; }
+#else
         if (w.z >= kQWide && kt1w) {
+#endif
             // the list's length, offset and (<= 3 intervals) the intervals themselves from the
             // D-mer's 32-B wide entry, w.w = the D-mer (k_ktab_wide) — one line instead of the nid,
             // ioff / iend, ib and ie reads below.  Producers given the wide table write kQWide;
@@ -1935,7 +1941,11 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 cb[t] = !on ? 0u : inl && t < kWideInline ? lb[t < kWideInline ? t : 0] : ib[a0.x + t];
                 ce[t] = !on ? 0u : inl && t < kWideInline ? le[t < kWideInline ? t : 0] : ie[a0.x + t];
             }
+#ifdef EDSBWT_KDEEP_THREEWAY
+        } else if (w.z == kQNode) {  // (acac474's second divergent arm)
+#else
         } else if (w.z >= kQWide) {  // from the node's items at the cutover depth
+#endif
             DBG_CHECK(w.z == kQNode, dbg_q);
             const uint32_t u = nid[i];
             cn = iend[u] - ioff[u];
