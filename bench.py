@@ -444,69 +444,80 @@ def main():
     rccl = multi and args.dist_backend == "nccl"
 
     # ---- the exchange step (N > 1), set up once per batch shape: the per-pattern counts gathered to
-    # rank 0 (shard.CountsGather over RCCL/xGMI).  Every rank's shard size follows from the static split
-    # and its records are the sum of its counts, so rank 0 has every rank's (patterns, records) offsets
-    # from the gather itself: one collective per step, no size read back to the host, nothing
-    # allocated per step.  On RCCL the gather runs from a side stream (shard.StepExchange) over two
-    # alternating count buffers: step i's gather beside step i + 1's search, whose stream never waits
+    # rank 0.  Every rank's shard size follows from the static split and its records are the sum of
+    # its counts, so rank 0 has every rank's (patterns, records) offsets from the gather itself: one
+    # collective per step, no size read back to the host, nothing allocated per step.  On GPUs the
+    # gather is the library's own (edsbwt_gather_counts, ABI 7: an RCCL communicator per index, the
+    # gather queued on the library's exchange stream with no Python or host wait on the search's
+    # path); the searches alternate two count buffers and the library orders a search that writes a
+    # buffer after the gather still reading it, so the gather of step i overlaps step i + 1.  gloo
+    # (rehearsal): counts staged through host memory (shard.CountsGather), synchronous
     shard_sizes = [b_ - a_ for a_, b_ in (workloads.shard(w, r, world, args.patterns) for r in range(world))]
     assert shard_sizes[rank] == npat
-    cg = shard.CountsGather(shard_sizes, gdev) if multi and args.gather == "counts" else None
+    native = rccl and args.gather == "counts"
+    cg = shard.CountsGather(shard_sizes, gdev) if multi and args.gather == "counts" and not native else None
+    sizes_np = np.array(shard_sizes, np.uint64)
+    d_gather_out = None
+    if native:
+        uid = [idx.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        idx.comm_init(uid[0], world, rank)
+        d_gather_out = torch.zeros(max(1, sum(shard_sizes)), dtype=torch.int32, device=dev) if rank == 0 else None
     # e2e leg: the engine leaves each call's u32 counts in a device mirror too (a device-to-device copy
-    # per chunk): RCCL gathers them from HBM, no second upload
-    xe_e2e = shard.StepExchange(cg, 2, npat, dev) if rccl and cg else None
+    # per chunk): the gather reads them from HBM, no second upload; two mirrors, alternated per call
+    d_counts_x = [torch.zeros(max(1, npat), dtype=torch.int32, device=dev) for _ in range(2 if native else 0)]
+    n_e2e = [0]
     # the last exchanged step's record count per leg (checked against rank 0's view after the timing)
     last_nocc = {}
 
     def e2e_step(keep=False):
-        if xe_e2e is not None:
-            k, buf_ = xe_e2e.buffer()
-            idx.set_counts_mirror(buf_.data_ptr(), npat)
+        if d_counts_x:
+            idx.set_counts_mirror(d_counts_x[n_e2e[0] % 2].data_ptr(), npat)
         n, ptr, nocc = idx.search_lines(text.ptr, text.nbytes, counts_hb.ptr, npat + 1, first_pattern_id=first_id,
                                         locate=locate, keep=keep)
         assert n == npat, (n, npat)
         return ptr, nocc
 
-    def exchange(nocc, xe=None, d_src=None, leg="e2e"):
+    def exchange(nocc, d_src=None, leg="e2e"):
         # the path's exchange step: the per-pattern counts to rank 0, where they also
-        # give every rank's (patterns, records) — its offsets in the output.  xe: the leg's StepExchange
-        # (RCCL; its current buffer was just written); else gloo: counts staged through host memory
-        if not multi or cg is None:
+        # give every rank's (patterns, records) — its offsets in the output.  d_src: the device leg's
+        # counts (else the e2e leg's mirror / host counts)
+        if not multi or args.gather != "counts":
             return
         last_nocc[leg] = nocc
-        if xe is not None:
-            xe.send(xe.k % len(xe.bufs))  # (the search returned: its counts are complete)
+        if native:
+            if d_src is None:
+                d_src = d_counts_x[n_e2e[0] % 2]
+                n_e2e[0] += 1
+            idx.gather_counts(d_src.data_ptr(), npat, d_gather_out.data_ptr() if d_gather_out is not None else 0, sizes_np, 0)
         else:
             cg.start(d_src.cpu() if d_src is not None else torch.from_numpy(counts[:npat].view(np.int32)))
 
     def exchange_drain():
-        for xe in (xe_e2e, xe_dev):
-            if xe is not None:
-                xe.drain()
-        if cg is not None:
+        if native:
+            idx.comm_sync()
+        elif cg is not None:
             cg.wait()
 
     def exchange_check(leg):
         """Outside the timed region: rank 0's per-rank records from the gathered counts == every
         rank's own record count of its last exchanged step."""
-        if not multi or cg is None or leg not in last_nocc:
+        if not multi or args.gather != "counts" or leg not in last_nocc:
             return None
         mine = torch.tensor([last_nocc[leg]], dtype=torch.int64, device=gdev)
         allr = torch.empty(world, dtype=torch.int64, device=gdev)
         dist.all_gather_into_tensor(allr, mine)
-        got = cg.result()
+        got = d_gather_out if native else cg.result()
         if rank != 0:
             return None
-        sums = [int(t_.cpu().numpy().view(np.uint32).astype(np.int64).sum()) for t_ in torch.split(got, shard_sizes)]
+        sums = [int(t_.cpu().numpy().view(np.uint32).astype(np.int64).sum()) for t_ in torch.split(got[:sum(shard_sizes)], shard_sizes)]
         return {"records_per_rank_from_counts": sums, "records_per_rank_reported": [int(x) for x in allr.tolist()],
                 "match": sums == [int(x) for x in allr.tolist()]}
-
-    xe_dev = None
 
     # ---- timed: end-to-end (host memory -> host memory)
     for _ in range(0 if args.no_e2e else args.warmup):
         _, nocc = e2e_step()
-        exchange(nocc, xe_e2e)
+        exchange(nocc)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -523,7 +534,7 @@ def main():
         if last:
             held = (ptr, nocc)
         tb = time.perf_counter()
-        exchange(nocc, xe_e2e)
+        exchange(nocc)
         search_ms += 1e3 * (tb - ta)
         exch_ms += 1e3 * (time.perf_counter() - tb)
         st_call = idx.stats_struct()  # one preallocated struct: no per-step dict building in the timed loop
@@ -535,6 +546,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     xchk = {"e2e": exchange_check("e2e")}
+    if d_counts_x:
+        idx.set_counts_mirror(0, 0)
     host_cores = (time.process_time() - c0) / max(1e-9, elapsed)  # host CPU the pipeline kept busy
     e2e_stats = idx.stats()
     if args.no_e2e:
@@ -567,10 +580,11 @@ def main():
         buf, offs = pkg.read_pattern_file(pats_path)
         d_bytes = torch.from_numpy(buf).to(dev)
         d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
-        # two count buffers when the counts are gathered (RCCL, shard.StepExchange): step i's gather
-        # reads one while step i + 1 searches into the other; else one
-        xe_dev = shard.StepExchange(cg, 2, npat, dev) if rccl and cg else None
-        d_counts = torch.zeros(npat, dtype=torch.int32, device=dev)
+        # two count buffers when the counts are gathered natively: step i's gather reads one while
+        # step i + 1 searches into the other; else one
+        d_counts_b = [torch.zeros(max(1, npat), dtype=torch.int32, device=dev) for _ in range(2 if native else 1)]
+        d_counts = d_counts_b[0]
+        n_dev = [0]
 
         # the timed steps run the deep kernels' builds without their work counters (EDSBWT_NO_COUNTERS:
         # same results, fewer registers); the line model (bytes / lines per launch, intervals stepped)
@@ -579,7 +593,8 @@ def main():
 
         def dev_step(profile=False, counters=counted):
             # returns (records pointer, records, the counts buffer this step wrote)
-            dc = xe_dev.buffer()[1] if xe_dev is not None else d_counts
+            dc = d_counts_b[n_dev[0] % len(d_counts_b)]
+            n_dev[0] += 1
             p_, n_ = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), npat, dc.data_ptr(), first_pattern_id=first_id,
                                        locate=locate, profile=profile, stream=stream, counters=counters, **flags_kw)
             return p_, n_, dc
@@ -588,12 +603,12 @@ def main():
         if not counted:
             kacc_c = idx.kernel_acc()
             _, dn, dc = dev_step(profile=PROFILE_TIMED, counters=True)
-            exchange(dn, xe_dev, dc, "device")
+            exchange(dn, dc, "device")
             idx.add_kernel_stats(kacc_c)
             stats_c = idx.stats()
         for _ in range(max(1, args.warmup)):
             _, dn, dc = dev_step()
-            exchange(dn, xe_dev, dc, "device")
+            exchange(dn, dc, "device")
         exchange_drain()
         d_counts = dc
         located = None
@@ -614,9 +629,9 @@ def main():
             # C5: the timed step is the located search (the reference always locates), in record-budget
             # chunks; the count-only warm-up above gave the counts the chunks are cut by
             counts_c = d_counts.cpu().numpy().view(np.uint32)[:npat].copy()
-            if xe_dev is not None:
-                xe_dev.drain()
-                for b_ in xe_dev.bufs:  # (each located step gathers the batch's counts, in line order)
+            exchange_drain()
+            for b_ in d_counts_b:  # (each located step gathers the batch's counts, in line order)
+                if b_.data_ptr() != d_counts.data_ptr():
                     b_.copy_(d_counts)
             chunks, budget, setup_s = located_chunks(buf, offs, counts_c, dev, args.located_budget, torch, first_id,
                                                       order=args.located_order)
@@ -641,10 +656,11 @@ def main():
         for _ in range(args.steps):
             if located_timed:
                 lp = located_pass(idx, chunks, counts_c, stream, torch, kacc=kacc)
-                exchange(lp["records"], xe_dev, d_counts, "device")  # (the batch's counts, line order)
+                exchange(lp["records"], d_counts_b[n_dev[0] % len(d_counts_b)], "device")  # (the batch's counts, line order)
+                n_dev[0] += 1
             else:
                 p_last, n_last, d_counts = dev_step(profile=PROFILE_TIMED)
-                exchange(n_last, xe_dev, d_counts, "device")
+                exchange(n_last, d_counts, "device")
                 idx.add_kernel_stats(kacc)  # HIP-event times of this call's kernel classes, summed in place
         exchange_drain()
         torch.cuda.synchronize()
@@ -757,9 +773,10 @@ def main():
                                         "counts + records D2H (SURVEY §8(d)), plus the exchange step when N>1"),
                        "exchange": ("none (one GPU)" if not multi else
                                     "none (--gather none: every rank keeps its counts + records)" if args.gather != "counts" else
-                                    ("per-pattern counts gathered to rank 0 over RCCL (xGMI) from a side stream, two "
-                                     "alternating count buffers (the gather of step i beside the search of step i + 1); "
-                                     "every rank's (patterns, records) offsets follow from the gathered counts"
+                                    ("per-pattern counts gathered to rank 0 over RCCL (xGMI) by the library itself "
+                                     "(edsbwt_gather_counts: its own communicator and exchange stream), two alternating "
+                                     "count buffers (the gather of step i beside the search of step i + 1); every rank's "
+                                     "(patterns, records) offsets follow from the gathered counts"
                                      if args.dist_backend == "nccl" else
                                      f"per-pattern counts gathered to rank 0 over {args.dist_backend} (rehearsal: counts "
                                      "staged through host memory, synchronous)")),
@@ -953,9 +970,6 @@ def main():
             except Exception as e:  # the GPU line is still valid
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), file=json_out, flush=True)
-    for xe in (xe_e2e, xe_dev):
-        if xe is not None:
-            xe.close()
     text.free()
     counts_hb.free()
     idx.close()

@@ -144,6 +144,15 @@ def lib() -> ctypes.CDLL:
     L.edsbwt_occ_free.restype = None
     L.edsbwt_set_counts_mirror.argtypes = [vp, vp, u64]
     L.edsbwt_set_counts_mirror.restype = i32
+    if hasattr(L, "edsbwt_comm_init"):  # (ABI 7: the native RCCL exchange)
+        L.edsbwt_comm_unique_id.argtypes = [vp, u64]
+        L.edsbwt_comm_unique_id.restype = i32
+        L.edsbwt_comm_init.argtypes = [vp, vp, u64, i32, i32]
+        L.edsbwt_comm_init.restype = i32
+        L.edsbwt_gather_counts.argtypes = [vp, vp, u64, vp, vp, i32]
+        L.edsbwt_gather_counts.restype = i32
+        L.edsbwt_comm_sync.argtypes = [vp]
+        L.edsbwt_comm_sync.restype = i32
     L.edsbwt_last_paths.argtypes = [vp, vp, u64]
     L.edsbwt_last_paths.restype = i32
     L.edsbwt_last_stats.argtypes = [vp, ctypes.POINTER(_Stats)]
@@ -365,6 +374,29 @@ class Index:
         """Host-pipeline calls also leave the u32 counts in device array d_counts[cap] (the
         multi-GPU exchange gathers them over RCCL); 0 turns it off."""
         _check(lib().edsbwt_set_counts_mirror(self._h, d_counts or None, int(cap) if d_counts else 0))
+
+    # ---- the native RCCL exchange (ABI 7, include/edsbwt.h): one process per GPU
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """rank 0: a new RCCL unique id (128 bytes) to hand to every rank's comm_init."""
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().edsbwt_comm_unique_id(buf, 128))
+        return buf.raw
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
+        """An RCCL communicator on this index's device (edsbwt_comm_init)."""
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        _check(lib().edsbwt_comm_init(self._h, buf, len(uid), int(nranks), int(rank)))
+
+    def gather_counts(self, d_counts: int, n: int, d_out: int, sizes: np.ndarray, dst: int = 0) -> None:
+        """Queue the gather of every rank's counts to rank dst (device pointers; sizes: uint64 per
+        rank, kept alive by the caller); returns at once (edsbwt_gather_counts)."""
+        sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        _check(lib().edsbwt_gather_counts(self._h, d_counts or None, int(n), d_out or None, sizes.ctypes.data, int(dst)))
+
+    def comm_sync(self) -> None:
+        """Wait until every queued gather is done (edsbwt_comm_sync)."""
+        _check(lib().edsbwt_comm_sync(self._h))
 
     def path_tags(self, n: int) -> np.ndarray:
         """PATH_* bits per pattern of the last search_device call (the process must run with

@@ -16,6 +16,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <dlfcn.h>
+#include <rccl/rccl.h>  // (types only: librccl.so is dlopen'ed by the native exchange, edsbwt_comm_init)
 #include <execinfo.h>
 #include <signal.h>
 #include <sys/syscall.h>
@@ -279,6 +280,45 @@ static OccRegistry& occ_registry() {
     static OccRegistry r;
     return r;
 }
+
+// ---- RCCL, loaded on first use (edsbwt_comm_init): dlopen'ed with local binding, so a process that
+// already holds another RCCL (PyTorch's own) keeps its symbols apart from this library's calls
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+    bool ok = false;
+    static Rccl& get() {
+        static Rccl r = [] {
+            Rccl x;
+            void* h = nullptr;
+            for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+                if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+            if (!h) return x;
+            x.get_id = (decltype(x.get_id))dlsym(h, "ncclGetUniqueId");
+            x.init = (decltype(x.init))dlsym(h, "ncclCommInitRank");
+            x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+            x.send = (decltype(x.send))dlsym(h, "ncclSend");
+            x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
+            x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+            x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+            x.err = (decltype(x.err))dlsym(h, "ncclGetErrorString");
+            x.ok = x.get_id && x.init && x.destroy && x.send && x.recv && x.group_start && x.group_end && x.err;
+            return x;
+        }();
+        return r;
+    }
+};
+#define NCCLCHK(x)                                                                                        \
+    do {                                                                                                  \
+        ncclResult_t r_ = (x);                                                                            \
+        if (r_ != ncclSuccess) throw Fail(EDSBWT_E_DEVICE, std::string(#x) + ": " + Rccl::get().err(r_)); \
+    } while (0)
 
 struct Engine {
     int device = 0;
@@ -653,6 +693,25 @@ struct Engine {
     uint32_t deep_pieces = std::max(1u, std::min(16u, (uint32_t)env_double("EDSBWT_DEEP_PIECES", 1)));
     uint64_t deep_piece_min = (uint64_t)env_double("EDSBWT_DEEP_PIECE_MIN", 1 << 20);
     hipStream_t stream2 = nullptr;  // (created on first use)
+    // native RCCL exchange (edsbwt_comm_init / edsbwt_gather_counts): the communicator, its stream,
+    // and the gathers still reading a count buffer (a search writing that buffer waits for them)
+    ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_size = 0;
+    hipStream_t xs = nullptr;
+    struct PendingGather {
+        const void* p = nullptr;
+        hipEvent_t ev = nullptr;
+    };
+    PendingGather gathers[4];
+    uint32_t gather_next = 0;
+    hipEvent_t xs_after = nullptr;
+    // the search stream waits for the queued gathers that read buffer p (the caller alternates
+    // buffers, so normally for one that ended a step ago)
+    void wait_gathers_on(const void* p) {
+        if (!p) return;
+        for (auto& g : gathers)
+            if (g.p == p) HIPCHK(hipStreamWaitEvent(stream, g.ev, 0));
+    }
     std::vector<hipEvent_t> piece_ev;
     DBuf<uint32_t> pcnt;  // queue counters of the pieces (NSHARD * 32 per piece)
     uint32_t wide_cap = (uint32_t)env_double("EDSBWT_WIDE_CAP", kWideCap);  // (tests: small caps force redos)
@@ -4561,6 +4620,12 @@ struct Engine {
     }
 
     ~Engine() {
+        if (xs) (void)hipStreamSynchronize(xs);
+        if (comm) (void)Rccl::get().destroy(comm);
+        for (auto& g : gathers)
+            if (g.ev) (void)hipEventDestroy(g.ev);
+        if (xs_after) (void)hipEventDestroy(xs_after);
+        if (xs) (void)hipStreamDestroy(xs);
         if (stream) (void)hipStreamSynchronize(stream);
         if (stream2) (void)hipStreamSynchronize(stream2);
         for (auto e : piece_ev) (void)hipEventDestroy(e);
@@ -4648,6 +4713,7 @@ static void occ_free_any(edsbwt_occ* p) {
 
 using edsbwt::Engine;
 using edsbwt::Fail;
+using edsbwt::Rccl;
 
 struct edsbwt_index {
     std::unique_ptr<Engine> eng;
@@ -4844,6 +4910,7 @@ static int search_device_impl(edsbwt_index* idx, const uint8_t* d_bytes, const u
     HIPCHK(hipEventRecord(ev, (hipStream_t)stream));
     HIPCHK(hipStreamWaitEvent(E.stream, ev, 0));
     (void)hipEventDestroy(ev);
+    E.wait_gathers_on(d_counts);  // (a gather of the previous use of this buffer must end first)
     struct TagReset { bool& t; ~TagReset() { t = false; } } tr{E.tag_now};
     if (E.tag_paths) {
         E.ptag.ensure(npat + 1);
@@ -4884,6 +4951,7 @@ int edsbwt_search(edsbwt_index* idx, const char* pat_bytes, const uint64_t* pat_
     Engine& E = *idx->eng;
     HIPCHK(hipSetDevice(E.device));
     if (npat && !pat_bytes && pat_offsets[npat]) throw Fail(EDSBWT_E_ARG, "null pattern bytes");
+    E.wait_gathers_on(E.counts_mirror);
     uint64_t n = E.search_host((const uint8_t*)pat_bytes, npat ? pat_offsets[npat] : 0, pat_offsets, npat, false, first_pattern_id, flags,
                                counts, npat, occ, nullptr);
     if (nocc) *nocc = n;
@@ -4900,6 +4968,7 @@ int edsbwt_search_lines(edsbwt_index* idx, const char* text, uint64_t len, uint3
     ABI_TRY
     Engine& E = *idx->eng;
     HIPCHK(hipSetDevice(E.device));
+    E.wait_gathers_on(E.counts_mirror);
     uint64_t n = E.search_host((const uint8_t*)text, len, nullptr, 0, true, first_pattern_id, flags, counts, counts_cap, occ, npat);
     if (nocc) *nocc = n;
     return 0;
@@ -4934,6 +5003,90 @@ void edsbwt_host_free(void* p) {
 const char* edsbwt_build_id(void) { return EDSBWT_BUILD_ID; }
 
 void edsbwt_occ_free(edsbwt_occ* occ) { edsbwt::occ_free_any(occ); }
+
+int edsbwt_comm_unique_id(void* id_out, uint64_t cap) {
+    if (!id_out || cap < sizeof(ncclUniqueId)) { edsbwt::g_err = "id buffer smaller than 128 bytes"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    Rccl& R = Rccl::get();
+    if (!R.ok) throw Fail(EDSBWT_E_UNSUPPORTED, "librccl.so not found");
+    ncclUniqueId id;
+    NCCLCHK(R.get_id(&id));
+    std::memcpy(id_out, &id, sizeof id);
+    return 0;
+    ABI_CATCH
+}
+
+int edsbwt_comm_init(edsbwt_index* idx, const void* id, uint64_t id_bytes, int nranks, int rank) {
+    if (!idx || !id || id_bytes != sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks) {
+        edsbwt::g_err = "bad argument";
+        return EDSBWT_E_ARG;
+    }
+    ABI_TRY
+    Engine& E = *idx->eng;
+    Rccl& R = Rccl::get();
+    if (!R.ok) throw Fail(EDSBWT_E_UNSUPPORTED, "librccl.so not found");
+    if (E.comm) throw Fail(EDSBWT_E_ARG, "the index already has a communicator");
+    HIPCHK(hipSetDevice(E.device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    NCCLCHK(R.init(&E.comm, nranks, uid, rank));
+    E.comm_rank = rank;
+    E.comm_size = nranks;
+    if (!E.xs) HIPCHK(hipStreamCreateWithFlags(&E.xs, hipStreamNonBlocking));
+    if (!E.xs_after) HIPCHK(hipEventCreateWithFlags(&E.xs_after, hipEventDisableTiming));
+    for (auto& g : E.gathers)
+        if (!g.ev) HIPCHK(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming));
+    return 0;
+    ABI_CATCH
+}
+
+int edsbwt_gather_counts(edsbwt_index* idx, const uint32_t* d_counts, uint64_t n, uint32_t* d_out, const uint64_t* sizes, int dst) {
+    if (!idx || !sizes || (n && !d_counts)) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    Engine& E = *idx->eng;
+    Rccl& R = Rccl::get();
+    if (!E.comm) throw Fail(EDSBWT_E_ARG, "no communicator: edsbwt_comm_init first");
+    if (dst < 0 || dst >= E.comm_size) throw Fail(EDSBWT_E_ARG, "dst outside the communicator");
+    if (sizes[E.comm_rank] != n) throw Fail(EDSBWT_E_ARG, "n differs from sizes[rank]");
+    if (E.comm_rank == dst && !d_out) throw Fail(EDSBWT_E_ARG, "null d_out on the receiving rank");
+    HIPCHK(hipSetDevice(E.device));
+    // after everything queued on the search stream (the search that wrote d_counts)
+    HIPCHK(hipEventRecord(E.xs_after, E.stream));
+    HIPCHK(hipStreamWaitEvent(E.xs, E.xs_after, 0));
+    NCCLCHK(R.group_start());
+    if (E.comm_rank == dst) {
+        uint64_t at = 0;
+        for (int r = 0; r < E.comm_size; r++) {
+            if (r == dst) {
+                if (n) HIPCHK(hipMemcpyAsync(d_out + at, d_counts, n * 4, hipMemcpyDeviceToDevice, E.xs));
+            } else if (sizes[r]) {
+                NCCLCHK(R.recv(d_out + at, sizes[r], ncclUint32, r, E.comm, E.xs));
+            }
+            at += sizes[r];
+        }
+    } else if (n) {
+        NCCLCHK(R.send(d_counts, n, ncclUint32, dst, E.comm, E.xs));
+    }
+    NCCLCHK(R.group_end());
+    // the gather's end, for the next search that writes d_counts (wait_gathers_on)
+    Engine::PendingGather* g = nullptr;
+    for (auto& x : E.gathers)
+        if (x.p == d_counts) g = &x;
+    if (!g) g = &E.gathers[E.gather_next++ % 4];
+    g->p = d_counts;
+    HIPCHK(hipEventRecord(g->ev, E.xs));
+    return 0;
+    ABI_CATCH
+}
+
+int edsbwt_comm_sync(edsbwt_index* idx) {
+    if (!idx) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }
+    ABI_TRY
+    Engine& E = *idx->eng;
+    if (E.xs) HIPCHK(hipStreamSynchronize(E.xs));
+    return 0;
+    ABI_CATCH
+}
 
 int edsbwt_set_counts_mirror(edsbwt_index* idx, uint32_t* d_counts, uint64_t cap) {
     if (!idx) { edsbwt::g_err = "null argument"; return EDSBWT_E_ARG; }

@@ -180,91 +180,6 @@ class CountsGather:
         return torch.cat([r[:n] for r, n in zip(self.recv, self.sizes)])
 
 
-class StepExchange:
-    """The per-step counts gather of a timed loop on GPUs (RCCL), off the search's stream and off the
-    search's host thread: `nbuf` device count buffers written in turn by the searches; send(k)
-    hands buffer k (just written by a search that has returned) to an exchange thread, which issues
-    the gather from a side stream and records its end there, while the calling thread already
-    starts the next search (a search call waits for its results, so a gather issued from the
-    calling thread would add its host time to every step); buffer() hands a buffer out again only
-    after the host saw its previous gather end.  With two buffers the gather of step i runs beside
-    the search of step i + 1, and the search's stream never waits for a collective.  The per-rank
-    (patterns, records) offsets follow from the gathered counts on rank dst (patterns per rank are
-    static; records = the sum of a rank's counts), so no separate sizes collective runs per step.
-    The exchange thread is the only one issuing collectives while the loop runs; drain() before
-    any other collective."""
-
-    def __init__(self, cg: "CountsGather", nbuf: int, n: int, device):
-        import queue
-        import threading
-
-        import torch
-
-        self.cg = cg
-        self.device = torch.device(device)
-        self.side = torch.cuda.Stream(self.device)
-        self.bufs = [torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)[:n] for _ in range(nbuf)]
-        self.ev_done = [torch.cuda.Event() for _ in range(nbuf)]
-        self.sent = [0] * nbuf      # gathers handed over, per buffer
-        self.issued = [0] * nbuf    # ... and issued by the exchange thread (their end event recorded)
-        self.k = 0
-        self.cv = threading.Condition()
-        self.q = queue.Queue()
-        self.err = None
-        self.th = threading.Thread(target=self._run, daemon=True)
-        self.th.start()
-
-    def _run(self):
-        import torch
-
-        torch.cuda.set_device(self.device)
-        while True:
-            k = self.q.get()
-            if k is None:
-                return
-            try:
-                with torch.cuda.stream(self.side):
-                    self.cg.start(self.bufs[k], async_op=True)
-                    self.cg.wait()  # (the side stream waits for the collective; no host wait)
-                    self.ev_done[k].record(self.side)
-            except Exception as e:  # noqa: BLE001 - re-raised on the calling thread
-                self.err = e
-            with self.cv:
-                self.issued[k] += 1
-                self.cv.notify_all()
-
-    def _wait_issued(self, k):
-        with self.cv:
-            self.cv.wait_for(lambda: self.issued[k] >= self.sent[k])
-        if self.err is not None:
-            raise self.err
-
-    def buffer(self):
-        """(k, tensor): the next buffer to write, free of its previous gather."""
-        k = self.k % len(self.bufs)
-        if self.sent[k]:
-            self._wait_issued(k)
-            self.ev_done[k].synchronize()
-        return k, self.bufs[k]
-
-    def send(self, k: int) -> None:
-        """Gather buffer k to dst (its search has returned: its counts are complete)."""
-        self.sent[k] += 1
-        self.k += 1
-        self.q.put(k)
-
-    def drain(self) -> None:
-        for k in range(len(self.bufs)):
-            if self.sent[k]:
-                self._wait_issued(k)
-                self.ev_done[k].synchronize()
-
-    def close(self) -> None:
-        self.drain()
-        self.q.put(None)
-        self.th.join()
-
-
 def gather_records(occ, sizes: list[int], dst: int = 0, group=None):
     """Every rank's occurrence records to rank dst in rank order.  `occ` is an int32/uint32
     tensor of n x 5 words (edsbwt_occ, e.g. a view of the engine's device records) or a

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EDSBWT_ABI_VERSION 6
+#define EDSBWT_ABI_VERSION 7
 
 enum {
     EDSBWT_OK = 0,
@@ -222,6 +222,26 @@ int edsbwt_last_paths(const edsbwt_index* idx, uint8_t* out, uint64_t n);
  * line count is known chunk by chunk, before the first chunk that would overflow it (the
  * mirror then holds the earlier chunks' counts). */
 int edsbwt_set_counts_mirror(edsbwt_index* idx, uint32_t* d_counts, uint64_t cap);
+
+/* Native RCCL exchange (ABI 7): the per-step gather of every rank's per-pattern
+ * counts to one rank over RCCL/xGMI, issued by the library on its own exchange stream — no Python
+ * and no host wait on the search's thread.  One process per GPU, one index per process:
+ *   rank 0: edsbwt_comm_unique_id(id, 128); broadcast the 128 bytes to the other ranks (any channel);
+ *   every rank: edsbwt_comm_init(idx, id, 128, nranks, rank) — an RCCL communicator on the index's
+ *   device (librccl.so is loaded on first use; E_UNSUPPORTED without it).
+ * edsbwt_gather_counts(idx, d_counts, n, d_out, sizes, dst): after the work already queued on the
+ * index's stream (the search that wrote d_counts), rank `dst` receives every rank's counts into
+ * d_out in rank order (rank r's n_r = sizes[r] counts at offset sizes[0] + .. + sizes[r-1]; d_out is
+ * ignored elsewhere); this rank's n must equal sizes[rank].  Returns once the gather is queued; the
+ * library orders any later search that writes d_counts (or a counts mirror at d_counts) after the
+ * gather that reads it, so callers alternate two count buffers and the gather of step i overlaps
+ * step i + 1.  edsbwt_comm_sync waits (host) until every queued gather is done.  The
+ * communicator is destroyed with the index.  (Replaces the reference's single-process output
+ * loop, MOVE_EDSBWTSearch.cpp:111-136, gathered in file order.) */
+int edsbwt_comm_unique_id(void* id_out, uint64_t cap);
+int edsbwt_comm_init(edsbwt_index* idx, const void* id, uint64_t id_bytes, int nranks, int rank);
+int edsbwt_gather_counts(edsbwt_index* idx, const uint32_t* d_counts, uint64_t n, uint32_t* d_out, const uint64_t* sizes, int dst);
+int edsbwt_comm_sync(edsbwt_index* idx);
 
 /* Setup for a following edsbwt_search_lines of ~text_bytes bytes in npat lines (flags as that
  * call's): the host pipeline's threads, streams and copy engines, every slot's page-locked and

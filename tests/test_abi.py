@@ -21,7 +21,7 @@ def test_header_symbols_exported(edsbwt):
     assert "edsbwt_search" in names and "edsbwt_index_open" in names
     for n in names:
         assert hasattr(L, n), n
-    assert L.edsbwt_abi_version() == 6
+    assert L.edsbwt_abi_version() == 7
     assert L.edsbwt_device_count() >= 0  # (0 without a GPU: no compute)
 
 

@@ -1526,3 +1526,43 @@ def test_locate_many_tiles_gpu(oracle, edsbwt, tmp_path, monkeypatch):
                 got[tsc] = (gc, go)
     assert np.array_equal(got["1"][0], got["0"][0]) and np.array_equal(got["1"][1], got["0"][1])
     assert got["1"][1].size > 300_000 * 2  # (records well past the blocks' stage sizes)
+
+
+def test_native_gather_counts_gpu(oracle, edsbwt, tmp_path):
+    """The library's own RCCL exchange (edsbwt_comm_init / edsbwt_gather_counts, ABI 7) with one
+    rank: counts of alternating device-resident searches gathered into rank 0's output, the
+    host pipeline's counts mirror gathered too, in step order (a search writing a buffer waits
+    for the gather still reading it), every gather equal to the oracle's counts."""
+    torch = pytest.importorskip("torch")
+    rng = random.Random(717)
+    segs = _covid_like(rng, 300)
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    pats = [edsgen.planted(rng, segs, rng.randint(4, 40)) or "ACGT" for _ in range(5000)]
+    buf, offs = _pack(pats)
+    oc, _, _ = oracle.Engine(base, 8).search(buf, offs)
+    n = len(pats)
+    sizes = np.array([n], np.uint64)
+    with edsbwt.Index(base) as idx:
+        idx.comm_init(edsbwt.Index.comm_unique_id(), 1, 0)
+        d_bytes = torch.from_numpy(buf.copy()).cuda()
+        d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+        bufs = [torch.full((n,), -1, dtype=torch.int32, device="cuda") for _ in range(2)]
+        out = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        for step in range(6):
+            b = bufs[step % 2]
+            idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), n, b.data_ptr(), locate=step % 3 != 0)
+            idx.gather_counts(b.data_ptr(), n, out.data_ptr(), sizes, 0)
+        idx.comm_sync()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), oc)
+        # the host pipeline's counts mirror, gathered the same way
+        out.fill_(-1)
+        text = ("\n".join(pats) + "\n").encode()
+        for step in range(3):
+            idx.set_counts_mirror(bufs[step % 2].data_ptr(), n)
+            gc, _ = _lines_search(edsbwt, idx, text)
+            idx.gather_counts(bufs[step % 2].data_ptr(), n, out.data_ptr(), sizes, 0)
+        idx.comm_sync()
+        idx.set_counts_mirror(0, 0)
+        assert np.array_equal(gc, oc) and np.array_equal(out.cpu().numpy().view(np.uint32), oc)
+        with pytest.raises(edsbwt.EdsBwtError):
+            idx.gather_counts(bufs[0].data_ptr(), n - 1, out.data_ptr(), sizes, 0)  # n differs from sizes[rank]

@@ -23,6 +23,8 @@
 #   abi:<cfg>:<reps>:<VAR=a,..>:<VAR=b,..>  interleaved A/B: reps x (A, B) device-resident lines (no e2e,
 #                           no CPU leg), one summary line each (round 5's one-off r5*.sh passes, folded in)
 #   stress:<args>           tools/kdeep_stress.py (every k_deep build, repeated searches) with <args> (',' = ' ')
+#   probe3:<lib>[:<waves>]  tools/threeway_probe.py: the README KAT through eds-bwt_amd/_build/<lib> (k_deep's
+#                           three-way list start variants), EDSBWT_DEEPQ_WAVES=<waves> (default 1), traced
 #   dist:<cfg>              the exchange path with one rank (--dist-self) and the same line without it,
 #                           interleaved twice: the step with and without the exchange
 # Outputs: gpurun_out/<tag>_<task>*.{json,log}.
@@ -137,6 +139,12 @@ import json
 a=json.load(open('${out}_self_$k.json'));b=json.load(open('${out}_plain_$k.json'))
 print('$k', 'exchange', a['ms_per_step'], a['e2e']['per_rank_search_exchange_ms'], 'plain', b['ms_per_step'], b['e2e']['per_rank_search_exchange_ms'])" | tee -a ${out}_summary.txt
       done ;;
+    probe3)
+      # k_deep's three-way list start: the README KAT through the library named by
+      # <a> (a file under eds-bwt_amd/_build/), unbounded k_deep build, traced; one process
+      EDSBWT_LIB=$PWD/eds-bwt_amd/_build/${a:-libedsbwt_3way.so} EDSBWT_DEEPQ_WAVES=${b:-1} EDSBWT_TRACE=1 EDSBWT_PATH_TAGS=1 \
+        timeout -k 10 120 python3 tools/threeway_probe.py > ${out}_${b:-1}.json 2> ${out}_${b:-1}.log || fail probe3 ${out}_${b:-1}.log
+      python3 -c "import json;d=json.load(open('${out}_${b:-1}.json'));print(d['lib'][-24:], d['oracle_counts'], [(r['kw'], r['counts'], r['stats']['deep_from_depth'], r['stats']['start_depth']) for r in d['runs']])" ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done
