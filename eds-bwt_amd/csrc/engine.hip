@@ -5004,6 +5004,15 @@ const char* edsbwt_build_id(void) { return EDSBWT_BUILD_ID; }
 
 void edsbwt_occ_free(edsbwt_occ* occ) { edsbwt::occ_free_any(occ); }
 
+#ifdef EDSBWT_KDEEP_DUMP
+// diagnostic builds only (not in the header): k_deep's dumped list starts of the last launch
+extern "C" int edsbwt_debug_kdeep_dump(uint32_t* out, uint32_t n) {
+    if (!out) return EDSBWT_E_ARG;
+    n = std::min<uint32_t>(n, edsbwt::kDumpMax * 16);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(edsbwt::g_kdeep_dump), n * 4, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : EDSBWT_E_DEVICE;
+}
+#endif
+
 int edsbwt_comm_unique_id(void* id_out, uint64_t cap) {
     if (!id_out || cap < sizeof(ncclUniqueId)) { edsbwt::g_err = "id buffer smaller than 128 bytes"; return EDSBWT_E_ARG; }
     ABI_TRY

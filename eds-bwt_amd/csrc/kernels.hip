@@ -1839,6 +1839,10 @@ __global__ void k_queue_prefix(const uint32_t* __restrict__ qcnt, uint32_t* __re
     }
 }
 
+#ifdef EDSBWT_KDEEP_DUMP
+constexpr uint32_t kDumpMax = 64;
+__device__ uint32_t g_kdeep_dump[kDumpMax * 16];
+#endif
 // EOFROW: links from '#' rows through KIdx::eofrow (one line per row; costs k_deep 6 VGPRs and a
 // wave per SIMD: C3 0.355 against 0.304 ms, profiles/r04_ab_c3_*.json — off by default)
 template <int K, int BPS, int MINW = 1, bool EOFROW = false, bool STATS = true>  // MINW: waves per SIMD the register budget is held to (1: no bound)
@@ -1907,12 +1911,24 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             pi = ind ? perm[i] : i;  // slen and key chunks in input order (k_deep_fast)
             L = slen[pi];
         }
+        // the entry as one interval [w.z, w.w], assigned BEFORE the branch on the entry's kind: the
+        // list arms below only override it, and the interval case writes nothing at the join.  (Round
+        // 6, DESIGN.md §0: with the interval's values assigned in its own arm of a three-way branch,
+        // this compiler lowered the kind test to a signed range split and wrote those values only on
+        // the w.z <= -2 side, so a row entry — w.z < 2^31 — started from stale registers: the round-4
+        // miscount and round-5 fault of the unbounded build, profiles/r06_isa_kdeep431_threeway_*.txt)
         uint32_t cb[K], ce[K];
-        uint32_t cn;
-        // a list start (kQWide / kQNode) or one interval: the only divergent branch on the entry's
-        // kind; wide or node list is the uniform kt1w (a kernel argument).  (A divergent three-way
-        // branch on the kind here made the unbounded build fault — rounds 4 and 5, DESIGN.md §0;
-        // EDSBWT_KDEEP_THREEWAY compiles that shape back in for the test-only libedsbwt_3way.so)
+        uint32_t cn = 1;
+#pragma unroll
+        for (int t = 0; t < K; t++) cb[t] = ce[t] = 0;
+        cb[0] = w.z;
+        ce[0] = w.w;
+#ifdef EDSBWT_KDEEP_DUMP
+        uint32_t dump_u = 0xFFFFFFFFu;
+#endif
+        // a list start (kQWide / kQNode) or the interval above: the only divergent branch on the
+        // entry's kind; wide or node list is the uniform kt1w (a kernel argument).
+        // EDSBWT_KDEEP_THREEWAY compiles round 5's three-way shape for the test-only libedsbwt_3way.so
 #ifdef EDSBWT_KDEEP_THREEWAY
         if (w.z == kQWide) {  // (acac474: the table's presence checked inside the arm)
             if (!kt1w) { flag_push(ovf, (uint32_t)i); continue; }
@@ -1948,6 +1964,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
 #endif
             DBG_CHECK(w.z == kQNode, dbg_q);
             const uint32_t u = nid[i];
+#ifdef EDSBWT_KDEEP_DUMP
+            dump_u = u;
+#endif
             cn = iend[u] - ioff[u];
             n_blk += 4;  // nid, ioff / iend, and the list's lines in ib and ie
             if (cn > K) { flag_push(ovf, (uint32_t)i); continue; }
@@ -1956,16 +1975,24 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                 cb[t] = (uint32_t)t < cn ? ib[ioff[u] + t] : 0u;
                 ce[t] = (uint32_t)t < cn ? ie[ioff[u] + t] : 0u;
             }
-        } else {
-            cn = 1;
-#pragma unroll
-            for (int t = 0; t < K; t++) cb[t] = ce[t] = 0;
-            cb[0] = w.z;
-            ce[0] = w.w;
         }
 #ifdef EDSBWT_DEBUG_CHECKS
         for (int t = 0; t < K; t++)
             if ((uint32_t)t < cn && !(cb[t] <= ce[t] && ce[t] < X.N)) dbg_l++;
+#endif
+#ifdef EDSBWT_KDEEP_DUMP
+        // (diagnostic builds: the first kDumpMax queue entries' list starts, read back by
+        // edsbwt_debug_kdeep_dump — DESIGN.md §0, the three-way list start)
+        if (j < kDumpMax) {
+            uint32_t* dd = g_kdeep_dump + (size_t)j * 16;
+            dd[0] = w.x; dd[1] = w.y; dd[2] = w.z; dd[3] = w.w; dd[4] = cn; dd[5] = dump_u;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                dd[6 + t] = t < K ? cb[t < K ? t : 0] : 0u;
+                dd[10 + t] = t < K ? ce[t < K ? t : 0] : 0u;
+            }
+            dd[14] = pi; dd[15] = 0xD0D0D0D0u;
+        }
 #endif
         SymReader<BPS> sym{k0, krest, P, pi};
         auto code_at = [&](uint32_t dd) -> uint32_t { return q2 ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };

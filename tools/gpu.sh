@@ -144,7 +144,7 @@ print('$k', 'exchange', a['ms_per_step'], a['e2e']['per_rank_search_exchange_ms'
       # <a> (a file under eds-bwt_amd/_build/), unbounded k_deep build, traced; one process
       EDSBWT_LIB=$PWD/eds-bwt_amd/_build/${a:-libedsbwt_3way.so} EDSBWT_DEEPQ_WAVES=${b:-1} EDSBWT_TRACE=1 EDSBWT_PATH_TAGS=1 \
         timeout -k 10 120 python3 tools/threeway_probe.py > ${out}_${b:-1}.json 2> ${out}_${b:-1}.log || fail probe3 ${out}_${b:-1}.log
-      python3 -c "import json;d=json.load(open('${out}_${b:-1}.json'));print(d['lib'][-24:], d['oracle_counts'], [(r['kw'], r['counts'], r['stats']['deep_from_depth'], r['stats']['start_depth']) for r in d['runs']])" ;;
+        python3 -c "import json;d=json.load(open('${out}_${b:-1}.json'));print(d['lib'][-24:], d['oracle_counts'], [(r['kw'], r.get('counts', r.get('error'))) for r in d['runs']]);[print(x) for x in d.get('kdeep_dump', [])]" ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done

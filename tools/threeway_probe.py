@@ -28,10 +28,25 @@ with tempfile.TemporaryDirectory() as d:
         out["index"] = {"rows": idx.n_rows, "ktab_depth": idx.ktab_depth, "pair_blocks": idx.pair_blocks}
         runs = []
         for kw in ({}, {"locate": False}, {"ktab": False}, {"direct": False}, {"pairs": False}, {"text": False}, {"deep": False}):
-            c, o = idx.search((buf, offs), **kw)
+            try:
+                c, o = idx.search((buf, offs), **kw)
+            except pkg.EdsBwtError as e:  # (a debug build's failed check) reported, the probe goes on
+                runs.append({"kw": kw, "error": str(e)})
+                continue
             st = idx.stats()
             runs.append({"kw": kw, "counts": c.tolist(), "match": bool(np.array_equal(c, oc)),
                          "stats": {k: st[k] for k in ("start_depth", "depths", "trie_nodes", "deep_from_depth", "deep_overflow",
                                                       "deep_level_rerun", "redo_searches", "intervals_stepped", "link_hash_rows")}})
         out["runs"] = runs
+        L = pkg.lib()
+        if hasattr(L, "edsbwt_debug_kdeep_dump"):
+            # the first search again, then k_deep's dumped list starts (diagnostic builds)
+            import ctypes
+            idx.search((buf, offs))
+            d = np.zeros(64 * 16, np.uint32)
+            L.edsbwt_debug_kdeep_dump.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+            assert L.edsbwt_debug_kdeep_dump(d.ctypes.data, d.size) == 0
+            rows = d.reshape(64, 16)
+            out["kdeep_dump"] = [{"w": r[0:4].tolist(), "cn": int(r[4]), "u": int(r[5]), "cb": r[6:10].tolist(), "ce": r[10:14].tolist(),
+                                  "pi": int(r[14])} for r in rows if r[15] == 0xD0D0D0D0]
 print(json.dumps(out))
