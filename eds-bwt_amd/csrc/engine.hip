@@ -630,6 +630,10 @@ struct Engine {
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
     bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
     bool tile_scan = env_double("EDSBWT_TILE_SCAN", 1) != 0;
+    // located searches: the deep kernels write the counts too (as count-only searches do), so the
+    // record-offset tiles are summed from the 4-B counts (k_tile_sums) instead of the 16-B results
+    // (k_count_tiles); EDSBWT_LOC_FC=0: k_count_tiles
+    bool loc_fc = env_double("EDSBWT_LOC_FC", 1) != 0;
     // k_locate_pp's LDS record stage (512 or 1024 records; 512 lets 8 blocks share a CU: the
     // locate class 0.190 against 0.189 ms at C3, profiles/r04_ab_locstage_c3_*.json — not the bound)
     uint32_t loc_stage = (uint32_t)env_double("EDSBWT_LOC_STAGE", 1024);
@@ -2960,7 +2964,10 @@ struct Engine {
         fc_done = false;
         fc_counts = nullptr;
         // (count-only; the per-pattern locate writes them in k_count_tiles or k_locate_pp instead, finish_deferred)
-        if (defer_call && fused_counts && (deep_wave || no_wide) && !locate) fc_counts = d_counts;
+        // (located: only when finish_deferred takes the per-pattern locate with record-offset tiles —
+        // the path whose k_tile_sums reads these counts; every other located path sums them itself)
+        const bool loc_tiles = locate && loc_mode == 2 && have_samples && samp_shift == 0 && locate_pp && !locate_counts && tile_scan;
+        if (defer_call && fused_counts && (deep_wave || no_wide) && (!locate || (loc_fc && loc_tiles))) fc_counts = d_counts;
         if (P == 0) return 0;
         struct EvPair {  // released on every exit, including exceptions
             hipEvent_t a = nullptr, b = nullptr;
@@ -3245,7 +3252,10 @@ struct Engine {
         if (tiles) {
             tile_sum.ensure(ntile);
             tile_pre.ensure(ntile);
-            launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
+            if (fc_done)  // (the deep kernels wrote every count and their sums)
+                launch(KC_FINISH, k_tile_sums, P, (const uint32_t*)d_counts, P, (unsigned long long*)tile_sum.p);
+            else
+                launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
         } else if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);

@@ -4092,6 +4092,17 @@ __global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res
     cs.flush(counts, stats, sh);
 }
 
+// the same tile sums from the counts the deep kernels wrote (fused counts on a located search):
+// 4 B per pattern read instead of the 16-B result, nothing else written
+__global__ void __launch_bounds__(256) k_tile_sums(const uint32_t* __restrict__ counts, uint64_t P, unsigned long long* __restrict__ tile_sum) {
+    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < P; p0 += (uint64_t)gridDim.x * blockDim.x) {  // block-uniform
+        const uint64_t i = p0 + threadIdx.x;
+        const uint32_t oc = i < P ? counts[i] : 0u;
+        const unsigned long long t = wave_sum(oc);
+        if ((threadIdx.x & 63) == 0 && i < P) tile_sum[i >> 6] = t;  // (p0 is a multiple of 64)
+    }
+}
+
 // per depth D: trie nodes M_D = #{i : lcp[i] < D <= slen[i]} (difference array over D)
 // and patterns per length, in one pass (LDS bins, Lmax < 1023)
 __global__ void __launch_bounds__(256) k_trie_counts(const uint32_t* __restrict__ slen, const uint32_t* __restrict__ lcp, uint64_t P,
