@@ -630,10 +630,11 @@ struct Engine {
     bool fused_counts = env_double("EDSBWT_FUSED_COUNTS", 1) != 0;
     bool locate_counts = env_double("EDSBWT_LOCATE_COUNTS", 0) != 0;
     bool tile_scan = env_double("EDSBWT_TILE_SCAN", 1) != 0;
-    // located searches: the deep kernels write the counts too (as count-only searches do), so the
-    // record-offset tiles are summed from the 4-B counts (k_tile_sums) instead of the 16-B results
-    // (k_count_tiles); EDSBWT_LOC_FC=0: k_count_tiles
-    bool loc_fc = env_double("EDSBWT_LOC_FC", 1) != 0;
+    // EDSBWT_LOC_FC=1: located searches have the deep kernels write the counts too (as count-only
+    // searches do), and sum the record-offset tiles from those 4-B counts (k_tile_sums) instead of
+    // the 16-B results (k_count_tiles) — slower at C3: 1.459-1.467 against 1.443-1.461 ms, the deep
+    // kernels' count stores cost 0.035 ms, the tile pass saves less (profiles/r06_ab_c3_loc_fc.txt)
+    bool loc_fc = env_double("EDSBWT_LOC_FC", 0) != 0;
     // k_locate_pp's LDS record stage (512 or 1024 records; 512 lets 8 blocks share a CU: the
     // locate class 0.190 against 0.189 ms at C3, profiles/r04_ab_locstage_c3_*.json — not the bound)
     uint32_t loc_stage = (uint32_t)env_double("EDSBWT_LOC_STAGE", 1024);
