@@ -1566,3 +1566,26 @@ def test_native_gather_counts_gpu(oracle, edsbwt, tmp_path):
         assert np.array_equal(gc, oc) and np.array_equal(out.cpu().numpy().view(np.uint32), oc)
         with pytest.raises(edsbwt.EdsBwtError):
             idx.gather_counts(bufs[0].data_ptr(), n - 1, out.data_ptr(), sizes, 0)  # n differs from sizes[rank]
+
+
+def test_three_way_list_start_gpu():
+    """Round 5's fault, kept reproducible: k_deep with the three-way divergent branch on
+    the queue entry's kind (libedsbwt_3way.so, built by `make all` from the same sources with
+    -DEDSBWT_KDEEP_THREEWAY), unbounded build (EDSBWT_DEEPQ_WAVES=1), over the README KAT in every
+    search variant (tools/threeway_probe.py, its own process).  Before the fix (the interval assigned
+    in its own arm) this build returned [0, 0, 0] for [4, 0, 3]; with the interval assigned before the
+    branch every variant equals the oracle."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    lib3 = os.path.join(ROOT, "eds-bwt_amd", "_build", "libedsbwt_3way.so")
+    if not os.path.exists(lib3):
+        pytest.skip("libedsbwt_3way.so not built (make -C eds-bwt_amd all)")
+    env = dict(os.environ, EDSBWT_LIB=lib3, EDSBWT_DEEPQ_WAVES="1", EDSBWT_PATH_TAGS="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "threeway_probe.py")], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["oracle_counts"] == [4, 0, 3]
+    assert all(run.get("match") for run in d["runs"]), d["runs"]
