@@ -454,15 +454,33 @@ def main():
     # (rehearsal): counts staged through host memory (shard.CountsGather), synchronous
     shard_sizes = [b_ - a_ for a_, b_ in (workloads.shard(w, r, world, args.patterns) for r in range(world))]
     assert shard_sizes[rank] == npat
-    native = rccl and args.gather == "counts"
-    cg = shard.CountsGather(shard_sizes, gdev) if multi and args.gather == "counts" and not native else None
+    # (EDSBWT_BENCH_TORCH_EXCHANGE=1: torch.distributed's gather instead — the fallback, tested)
+    native = rccl and args.gather == "counts" and os.environ.get("EDSBWT_BENCH_TORCH_EXCHANGE") != "1"
+    native_err = None if native or not rccl else "EDSBWT_BENCH_TORCH_EXCHANGE=1"
     sizes_np = np.array(shard_sizes, np.uint64)
     d_gather_out = None
     if native:
-        uid = [idx.comm_unique_id() if rank == 0 else None]
+        # every rank tries; if any rank's communicator fails (no librccl, an init error) all fall back to
+        # torch.distributed's gather (shard.CountsGather over the same RCCL process group) together
+        try:
+            uid = [idx.comm_unique_id() if rank == 0 else None]
+        except Exception as e:  # noqa: BLE001
+            uid, native_err = [None], repr(e)
         dist.broadcast_object_list(uid, src=0)
-        idx.comm_init(uid[0], world, rank)
-        d_gather_out = torch.zeros(max(1, sum(shard_sizes)), dtype=torch.int32, device=dev) if rank == 0 else None
+        ok = torch.tensor([0 if (uid[0] is None or native_err) else 1], dtype=torch.int32, device=gdev)
+        if ok.item():
+            try:
+                idx.comm_init(uid[0], world, rank)
+            except Exception as e:  # noqa: BLE001
+                native_err = repr(e)
+                ok.fill_(0)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not ok.item():
+            log(f"[bench] rank {rank}: the library's RCCL exchange is unavailable ({native_err}); torch.distributed gather instead")
+            native = False
+        else:
+            d_gather_out = torch.zeros(max(1, sum(shard_sizes)), dtype=torch.int32, device=dev) if rank == 0 else None
+    cg = shard.CountsGather(shard_sizes, gdev) if multi and args.gather == "counts" and not native else None
     # e2e leg: the engine leaves each call's u32 counts in a device mirror too (a device-to-device copy
     # per chunk): the gather reads them from HBM, no second upload; two mirrors, alternated per call
     d_counts_x = [torch.zeros(max(1, npat), dtype=torch.int32, device=dev) for _ in range(2 if native else 0)]
@@ -490,6 +508,9 @@ def main():
                 d_src = d_counts_x[n_e2e[0] % 2]
                 n_e2e[0] += 1
             idx.gather_counts(d_src.data_ptr(), npat, d_gather_out.data_ptr() if d_gather_out is not None else 0, sizes_np, 0)
+        elif rccl:  # (fallback) torch.distributed's gather over RCCL, from device tensors, synchronous
+            cg.start(d_src if d_src is not None else torch.from_numpy(counts[:npat].view(np.int32)).to(dev))
+            cg.wait()
         else:
             cg.start(d_src.cpu() if d_src is not None else torch.from_numpy(counts[:npat].view(np.int32)))
 
@@ -773,7 +794,9 @@ def main():
                                         "counts + records D2H (SURVEY §8(d)), plus the exchange step when N>1"),
                        "exchange": ("none (one GPU)" if not multi else
                                     "none (--gather none: every rank keeps its counts + records)" if args.gather != "counts" else
-                                    ("per-pattern counts gathered to rank 0 over RCCL (xGMI) by the library itself "
+                                    ("per-pattern counts gathered to rank 0 over RCCL by torch.distributed (the library's "
+                                     f"exchange was unavailable: {native_err})" if rccl and not native else
+                                     "per-pattern counts gathered to rank 0 over RCCL (xGMI) by the library itself "
                                      "(edsbwt_gather_counts: its own communicator and exchange stream), two alternating "
                                      "count buffers (the gather of step i beside the search of step i + 1); every rank's "
                                      "(patterns, records) offsets follow from the gathered counts"
