@@ -2123,8 +2123,8 @@ struct Engine {
                 HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
                 direct_dyn_grid = (unsigned)std::max(1, nb * cus);
             }
-            const uint64_t nrun = ((P + 63) / 64 + kDynSub - 1) / kDynSub;  // counter fetches: kDynSub chunks each
-            const size_t qcap_d = std::max<size_t>(qcap, (nrun + NSHARD - 1) / NSHARD * 64 * kDynSub);
+            const uint64_t nchunk = (P + 63) / 64;
+            const size_t qcap_d = std::max<size_t>(qcap, (nchunk + NSHARD - 1) / NSHARD * 64);
             dq.ensure(qcap_d * NSHARD);
             dq2.ensure(qcap_d * NSHARD);
             if (!defer) zero(counters.p + kWorkCtrSlot, 4);

@@ -1571,7 +1571,6 @@ struct LaneCtr {
 // DYN: each wave takes 64-pattern chunks from a device counter (X.work_ctr, zeroed per search) on a
 // persistent grid, instead of a fixed grid-stride share — no tail of waves that drew slow patterns;
 // a chunk's queue entries go to shard chunk % NSHARD (the engine sizes qcap for that)
-constexpr uint32_t kDynSub = 8;  // DYN: 64-pattern chunks per counter fetch
 template <int MINW, bool FUSED = false, bool STATS = true, bool DYN = false>
 __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
                                                            uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
@@ -1593,20 +1592,15 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     // 32-bit pattern indices (the engine keeps a search's batch below 2^31 patterns): fewer registers
     // and no 64-bit index arithmetic in a kernel whose time follows its register pressure
     const uint32_t P32 = (uint32_t)P, stride32 = gridDim.x * blockDim.x;
-    uint32_t dyn_c0 = 0, dyn_sub = kDynSub;  // (DYN: the wave's current run of kDynSub chunks)
     for (uint32_t i_b = i0 + blockIdx.x * blockDim.x;; i_b += stride32) {
         uint32_t i;
         if constexpr (DYN) {  // (the loop is wave-uniform: every lane of the wave takes the same chunk)
-            if (dyn_sub == kDynSub) {  // one atomic per kDynSub chunks: a single hot counter serialises
-                uint32_t c = 0;
-                if ((threadIdx.x & 63) == 0) c = atomicAdd(X.work_ctr, 1u);
-                dyn_c0 = __shfl(c, 0, 64);
-                dyn_sub = 0;
-            }
-            const uint32_t c = dyn_c0 * kDynSub + dyn_sub++;
+            uint32_t c = 0;
+            if ((threadIdx.x & 63) == 0) c = atomicAdd(X.work_ctr, 1u);
+            c = __shfl(c, 0, 64);
             if (c >= (P32 - i0 + 63) / 64) break;
             i = i0 + c * 64 + (threadIdx.x & 63);
-            sh = dyn_c0 % NSHARD;
+            sh = c % NSHARD;
         } else {
             if (i_b >= P32) break;
             i = i_b + threadIdx.x;
