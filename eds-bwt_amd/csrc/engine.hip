@@ -691,11 +691,6 @@ struct Engine {
     // k_deep takes two characters per rank entry when no interval of its list meets a link
     // (rent2, as k_deep_direct; EDSBWT_DEEPQ_PAIRS=0: one character per step)
     uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
-    // k_deep_direct's chunk scheduling (EDSBWT_DIRECT_DYN=1): each wave takes 64-pattern chunks from
-    // a counter (counters slot kWorkCtrSlot, zeroed per search) on a persistent grid
-    bool direct_dyn = env_double("EDSBWT_DIRECT_DYN", 0) != 0;
-    static constexpr int kWorkCtrSlot = 22;
-    unsigned direct_dyn_grid = 0;  // (blocks resident at once, measured on first use)
     // the deferred direct start in pieces (EDSBWT_DEEP_PIECES, batches of at least
     // EDSBWT_DEEP_PIECE_MIN patterns): k_deep_direct over piece j + 1 runs while k_deep walks piece
     // j's queue on a second stream (an event per piece), so k_deep's long-tailed lanes share the
@@ -742,7 +737,6 @@ struct Engine {
     }
     KIdx kidx() const {
         KIdx X{};  // (every field set below; value-initialised so a new one cannot reach a kernel unset)
-        X.work_ctr = counters.p ? reinterpret_cast<uint32_t*>(counters.p + kWorkCtrSlot) : nullptr;
         X.occ = occ.p;
         X.eof_seg = eof_seg.p;
         X.eofrow = eofrow.p;
@@ -2085,7 +2079,6 @@ struct Engine {
         ae.grow_keep(abase + (uint64_t)P * K, stream);
         // single-interval walks first; patterns needing lists or links are queued for k_deep
         const size_t qcap = std::max<size_t>(shard_bound(P, 1), 1024);
-        size_t qcap_used = qcap;  // (the DYN direct start sizes its shards by chunks: k_deep reads them with its qcap)
         dq.ensure(qcap * NSHARD);
         if (pv) dq2.ensure(qcap * NSHARD);
         dqpre.ensure(NSHARD + 1);
@@ -2112,27 +2105,6 @@ struct Engine {
                                 ? deep_pieces : 1u;
         if (np > 1) {
             run_deep_pieces(np, d, P, nid_d, goff, gend, gb, gee, lens, k0, krest, ind, X, abase, K, r, kt1w, fc);
-        } else if (kdd && fk_now.on && direct_dyn && direct_waves >= 8) {
-            // the fused direct start on a persistent grid, waves taking 64-pattern chunks (DYN): a
-            // chunk's entries go to shard chunk % NSHARD, so a shard holds at most ceil(chunks /
-            // NSHARD) * 64 of them
-            auto kd0 = deep_stats ? k_deep_direct<8, true, true, true> : k_deep_direct<8, true, false, true>;
-            if (!direct_dyn_grid) {
-                int nb = 0, cus = 0;
-                HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kd0, 256, 0));
-                HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-                direct_dyn_grid = (unsigned)std::max(1, nb * cus);
-            }
-            const uint64_t nchunk = (P + 63) / 64;
-            const size_t qcap_d = std::max<size_t>(qcap, (nchunk + NSHARD - 1) / NSHARD * 64);
-            dq.ensure(qcap_d * NSHARD);
-            dq2.ensure(qcap_d * NSHARD);
-            if (!defer) zero(counters.p + kWorkCtrSlot, 4);
-            launch_grid(KC_DEEP, kd0, (unsigned)std::min<uint64_t>(direct_dyn_grid, (P + 255) / 256), P, d, nid_d, X, abase, K, r, dq.p,
-                        (uint32_t)qcap_d, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p, fk_now.bytes, fk_now.off, len.p,
-                        const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, 0u);
-            fk_now.on = false;
-            qcap_used = qcap_d;
         } else if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
             // written there, for k_deep and k_deep_wave)
@@ -2167,10 +2139,10 @@ struct Engine {
                                           : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>) : deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>)
                                        : unb ? k_deep<4, 4, 1> : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
-        launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap_used, d, lens,
+        launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
                pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc, deepq_pairs);
-        tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap_used, EDSBWT_PATH_DEEP);
+        tag_queue((const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, EDSBWT_PATH_DEEP);
         }
         abase += (uint64_t)P * K;
         st.deep_from_depth = D;

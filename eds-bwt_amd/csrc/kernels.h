@@ -134,9 +134,6 @@ struct KIdx {
     // [seg_hi + c]) — the first link after the entry's text compare then reads the entry's own
     // 128-B DRAM line instead of a segment row (sigma <= 5; EDSBWT_KT1_LINK=1)
     uint32_t kt1_ws;
-    // the direct start's chunk counter (k_deep_direct<.., DYN = true>: each wave takes 64-pattern
-    // chunks from it), a u32 of the search's zeroed counters
-    uint32_t* work_ctr;
 };
 
 }  // namespace edsbwt

@@ -1568,10 +1568,7 @@ struct LaneCtr {
 
 // STATS = false (EDSBWT_DEEP_STATS=0): no per-lane work counters (steps, lines, text rows) — five
 // registers fewer in a kernel whose time follows its register pressure
-// DYN: each wave takes 64-pattern chunks from a device counter (X.work_ctr, zeroed per search) on a
-// persistent grid, instead of a fixed grid-stride share — no tail of waves that drew slow patterns;
-// a chunk's queue entries go to shard chunk % NSHARD (the engine sizes qcap for that)
-template <int MINW, bool FUSED = false, bool STATS = true, bool DYN = false>
+template <int MINW, bool FUSED = false, bool STATS = true>
 __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
                                                            uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
                                                            uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
@@ -1588,23 +1585,14 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
     uint32_t c_srow = 0, c_seg = 0, c_wrow = 0, c_one = 0;
 #endif
     uint32_t nt = 0;  // patterns holding '#' or of unexpected lengths (per lane)
-    uint32_t sh = blockIdx.x % NSHARD;
+    const uint32_t sh = blockIdx.x % NSHARD;
+    q += (size_t)sh * qcap;
+    q2 += (size_t)sh * qcap;
     // 32-bit pattern indices (the engine keeps a search's batch below 2^31 patterns): fewer registers
     // and no 64-bit index arithmetic in a kernel whose time follows its register pressure
     const uint32_t P32 = (uint32_t)P, stride32 = gridDim.x * blockDim.x;
-    for (uint32_t i_b = i0 + blockIdx.x * blockDim.x;; i_b += stride32) {
-        uint32_t i;
-        if constexpr (DYN) {  // (the loop is wave-uniform: every lane of the wave takes the same chunk)
-            uint32_t c = 0;
-            if ((threadIdx.x & 63) == 0) c = atomicAdd(X.work_ctr, 1u);
-            c = __shfl(c, 0, 64);
-            if (c >= (P32 - i0 + 63) / 64) break;
-            i = i0 + c * 64 + (threadIdx.x & 63);
-            sh = c % NSHARD;
-        } else {
-            if (i_b >= P32) break;
-            i = i_b + threadIdx.x;
-        }
+    for (uint32_t i_b = i0 + blockIdx.x * blockDim.x; i_b < P32; i_b += stride32) {
+        const uint32_t i = i_b + threadIdx.x;
         const bool valid = i < P32;
         uint32_t want = 0;
         uint4 w = make_uint4(0, 0, 0, 0);
@@ -1816,8 +1804,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
         if (want) put_res(res, pi, 0, 0u, 0u);  // the zeroed result the later walks expect
         const uint32_t at = wave_append(qcnt + sh * 32, want);
         if (want && at < qcap) {
-            q[(size_t)sh * qcap + at] = w;
-            q2[(size_t)sh * qcap + at] = rem << 31 | pi;  // the packed start: k_deep reads it instead of perm, slen and the key chunks
+            q[at] = w;
+            q2[at] = rem << 31 | pi;  // the packed start: k_deep reads it instead of perm, slen and the key chunks
         }
     }
     __shared__ unsigned long long ssum[4];

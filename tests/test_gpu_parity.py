@@ -619,45 +619,6 @@ def test_deep_pieces_gpu(oracle, edsbwt, tmp_path, monkeypatch, pieces):
             assert deep.min() < len(pats) // int(pieces) and deep.max() >= len(pats) - len(pats) // int(pieces)
 
 
-def test_direct_dyn_gpu(oracle, edsbwt, tmp_path, monkeypatch):
-    """k_deep_direct on a persistent grid, each wave taking 64-pattern chunks from a device counter
-    (EDSBWT_DIRECT_DYN=1; a chunk's queue entries in shard chunk % NSHARD): counts and records equal
-    to the oracle, located and count-only, counted and counter-free, with a batch that is not a
-    multiple of 64 and one smaller than a chunk, and k_deep's queue walked (path tags)."""
-    monkeypatch.setenv("EDSBWT_DIRECT_ITEMS", "1e9")
-    monkeypatch.setenv("EDSBWT_DIRECT_DYN", "1")
-    monkeypatch.setenv("EDSBWT_PATH_TAGS", "1")
-    torch = pytest.importorskip("torch")
-    rng = random.Random(5151)
-    segs = _covid_like(rng, 900)
-    if any(w == "" for w in segs[1]):
-        segs[1] = ["A"]
-    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
-    with edsbwt.Index(base) as idx:
-        D0 = idx.ktab_depth
-    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(9001)]
-    pats = [p[: D0 + 16] if len(p) > D0 + 16 else p for p in pats]
-    pats += [rng.choice("ACGT") + p[1:] for p in pats[:777]]
-    for batch in (pats, pats[:37]):
-        buf, offs = _pack(batch)
-        oc, oo, _ = oracle.Engine(base, 8).search(buf, offs)
-        with edsbwt.Index(base) as idx:
-            for kw in ({}, {"locate": False}, {"counters": False}):
-                gc, go = idx.search((buf, offs), **kw)
-                assert idx.stats()["start_depth"] == D0 and idx.stats()["redo_searches"] == 0
-                assert np.array_equal(gc, oc), (len(batch), kw)
-                if kw.get("locate", True):
-                    assert np.array_equal(go, oo), (len(batch), kw)
-            d_bytes = torch.from_numpy(buf.copy()).cuda()
-            d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
-            d_counts = torch.zeros(len(batch), dtype=torch.int32, device="cuda")
-            _, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), len(batch), d_counts.data_ptr(), counters=False)
-            torch.cuda.synchronize()
-            assert np.array_equal(d_counts.cpu().numpy().view(np.uint32), oc) and n == oo.size
-            if len(batch) > 1000:
-                assert (idx.path_tags(len(batch)) & edsbwt.PATH_DEEP).sum() > 50
-
-
 @pytest.mark.parametrize("direct", [True, False])
 def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, direct):
     """Single-row intervals decided by comparing the pattern with the words' text: patterns
