@@ -691,6 +691,8 @@ struct Engine {
     // k_deep takes two characters per rank entry when no interval of its list meets a link
     // (rent2, as k_deep_direct; EDSBWT_DEEPQ_PAIRS=0: one character per step)
     uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
+    // the packed direct start's k_deep build without the generic key reader (k_deep<.., PACKED>)
+    bool deepq_packed = env_double("EDSBWT_DEEPQ_PACKED", 1) != 0;
     // the deferred direct start in pieces (EDSBWT_DEEP_PIECES, batches of at least
     // EDSBWT_DEEP_PIECE_MIN patterns): k_deep_direct over piece j + 1 runs while k_deep walks piece
     // j's queue on a second stream (an event per piece), so k_deep's long-tailed lanes share the
@@ -2139,6 +2141,12 @@ struct Engine {
                                           : unb ? k_deep<4, 3, 1> : deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>) : deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>)
                                        : unb ? k_deep<4, 4, 1> : k_deep<4, 4, 5>)
                            : (bps == 3 ? k_deep<8, 3> : k_deep<8, 4>);
+        // the packed direct start's queue: the build without the key-chunk reader and the perm /
+        // slen reads (PACKED: 77 VGPRs and no scratch at 6 waves per SIMD, against 80 + 40 B of
+        // scratch; EDSBWT_DEEPQ_PACKED=0: the generic build; EDSBWT_DEEPQ_WAVES=7: 7 waves)
+        if (pv && deepq_packed && K == 4 && bps == 3 && !X.eofrow && !unb && deepq_waves >= 6)
+            kd = deepq_waves >= 7 ? (deep_stats ? k_deep<4, 3, 7, false, true, true> : k_deep<4, 3, 7, false, false, true>)
+                                  : (deep_stats ? k_deep<4, 3, 6, false, true, true> : k_deep<4, 3, 6, false, false, true>);
         launch(KC_DEEPQ, kd, P, (const uint4*)dq.p, (const uint32_t*)lcnt.p, (uint32_t)qcap, d, lens,
                (const uint32_t*)perm.p, k0, krest, ind, P, nid_d, goff, gend, gb, gee, X, abase, ab.p, ae.p, r, ovf.p, stats.p,
                pv ? (const uint64_t*)dq2.p : (const uint64_t*)nullptr, kt1w, fc, deepq_pairs);
@@ -2238,6 +2246,9 @@ struct Engine {
                  : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
         auto kd = deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>)
                                    : (deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>);
+        if (deepq_packed && deepq_waves >= 6)  // (the pieces are the packed start's: see run_deep)
+            kd = deepq_waves >= 7 ? (deep_stats ? k_deep<4, 3, 7, false, true, true> : k_deep<4, 3, 7, false, false, true>)
+                                  : (deep_stats ? k_deep<4, 3, 6, false, true, true> : k_deep<4, 3, 6, false, false, true>);
         for (uint32_t j = 0; j < np; j++) {
             const uint64_t lo = P * j / np, hi = P * (j + 1) / np;
             uint4* qj = (uint4*)dq.p + (size_t)j * pq * NSHARD;

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -185,6 +186,44 @@ __attribute__((target("avx2"))) int pack_avx2(const uint8_t* s, uint64_t nb, uin
     }
     return 1;
 }
+
+// the bulk of a range for L <= 31, where each line's '\n' falls inside its own 32-byte window: one
+// table lookup (pshufb on the low nibble: 'A' 'C' 'G' 'T' '\n' map to themselves, any other byte
+// to a value it is not) validates the L bases and the '\n' together, the two code bits come from
+// two movemasks spread by pdep, and the verdict is accumulated without a branch per line.  Covers
+// the lines [p0, the returned p) whose window lies inside the buffer and whose 8-byte store stays
+// inside the range; *bad is nonzero when one of them is not L A/C/G/T bytes then '\n'.
+__attribute__((target("avx2,bmi2"))) uint64_t pack_bulk_avx2(const uint8_t* s, uint64_t nb, uint32_t L, uint64_t p0, uint64_t p1,
+                                                            const uint8_t* end, uint8_t* out, uint32_t* bad) {
+    const char X = (char)0x80;
+    const __m256i lut = _mm256_setr_epi8(X, 'A', X, 'C', 'T', X, X, 'G', X, X, '\n', X, X, X, X, X,  //
+                                         X, 'A', X, 'C', 'T', X, X, 'G', X, X, '\n', X, X, X, X, X);
+    const __m256i nl = _mm256_set1_epi8('\n');
+    const uint32_t need = (2u << L) - 1u, nlbit = 1u << L;  // bytes 0..L; L = 31: all 32
+    const uint64_t cmask = (1ull << (2 * L)) - 1ull;
+    const uint64_t stride = L + 1, S = (L + 3) / 4;
+    const uint64_t room = (uint64_t)(end - s);
+    uint64_t pe = p1;
+    // window inside the buffer, the '\n' inside the chunk, the 8-byte store inside [p0, p1)
+    pe = std::min(pe, room >= 32 ? (room - 32) / stride + 1 : 0);
+    pe = std::min(pe, nb > L ? (nb - 1 - L) / stride + 1 : 0);
+    const uint64_t tail = (8 + S - 1) / S;
+    pe = p1 >= tail ? std::min(pe, p1 - tail + 1) : 0;
+    if (pe <= p0) return p0;
+    uint32_t acc = 0;
+    for (uint64_t p = p0; p < pe; p++) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + p * stride));
+        const uint32_t ok = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_shuffle_epi8(lut, v), v));
+        const uint32_t isnl = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, nl));
+        acc |= ((ok & need) ^ need) | ((isnl & need) ^ nlbit);
+        const uint64_t lo = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(v, 6));  // byte bit 1: code bit 0
+        const uint64_t hi = (uint32_t)_mm256_movemask_epi8(_mm256_slli_epi16(v, 5));  // byte bit 2: code bit 1
+        const uint64_t codes = (_pdep_u64(lo, 0x5555555555555555ull) | _pdep_u64(hi, 0xAAAAAAAAAAAAAAAAull)) & cmask;
+        std::memcpy(out + p * S, &codes, 8);
+    }
+    *bad = acc;
+    return pe;
+}
 }  // namespace
 
 // pack lines [p0, p1) of a chunk edsbwt_lines_fixed accepted (L bases each); `end` is the first
@@ -192,5 +231,15 @@ __attribute__((target("avx2"))) int pack_avx2(const uint8_t* s, uint64_t nb, uin
 // then '\n' (or the CPU lacks AVX2): the caller then sends the raw bytes.
 extern "C" int edsbwt_pack_lines(const uint8_t* s, uint64_t nb, uint32_t L, uint64_t p0, uint64_t p1, const uint8_t* end, uint8_t* out) {
     if (L == 0 || L > 32 || !__builtin_cpu_supports("avx2")) return 0;
+    // the bulk path where pdep is a fast instruction (not on the first two Zen generations)
+    // (EDSBWT_PACK_BULK=0: the per-line path only)
+    static const bool bulk = __builtin_cpu_supports("bmi2") && !__builtin_cpu_is("znver1") && !__builtin_cpu_is("znver2") &&
+                             !(std::getenv("EDSBWT_PACK_BULK") && std::atoi(std::getenv("EDSBWT_PACK_BULK")) == 0);
+    if (bulk && L <= 31) {
+        uint32_t bad = 0;
+        const uint64_t p = pack_bulk_avx2(s, nb, L, p0, p1, end, out, &bad);
+        if (bad) return 0;
+        p0 = p;
+    }
     return pack_avx2(s, nb, L, p0, p1, end, out);
 }

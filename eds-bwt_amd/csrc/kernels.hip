@@ -1845,7 +1845,9 @@ __device__ uint32_t g_kdeep_dump[kDumpMax * 16];
 #endif
 // EOFROW: links from '#' rows through KIdx::eofrow (one line per row; costs k_deep 6 VGPRs and a
 // wave per SIMD: C3 0.355 against 0.304 ms, profiles/r04_ab_c3_*.json — off by default)
-template <int K, int BPS, int MINW = 1, bool EOFROW = false, bool STATS = true>  // MINW: waves per SIMD the register budget is held to (1: no bound)
+// PACKED: the packed direct start's queue only (q2 != nullptr: each entry's pattern index and remaining
+// symbols travel in q2) — the key-chunk reader and the perm / slen reads are compiled out
+template <int K, int BPS, int MINW = 1, bool EOFROW = false, bool STATS = true, bool PACKED = false>  // MINW: waves per SIMD the register budget is held to (1: no bound)
 __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q, const uint32_t* __restrict__ qcnt, uint32_t qcap, uint32_t D0,
                                               const uint32_t* __restrict__ slen, const uint32_t* __restrict__ perm,
                                               const uint64_t* __restrict__ k0, const uint64_t* __restrict__ krest, uint32_t ind, uint64_t P,
@@ -1900,7 +1902,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         // q2 (packed direct start): input index and remaining symbols from the queue entry
         uint32_t pi, L;
         uint64_t rem = 0;
-        if (q2) {
+        if (PACKED || q2) {
             const uint64_t v = q2[qi];
             pi = (uint32_t)(v & 0x7fffffffu);
             rem = v >> 31;
@@ -1995,7 +1997,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
         }
 #endif
         SymReader<BPS> sym{k0, krest, P, pi};
-        auto code_at = [&](uint32_t dd) -> uint32_t { return q2 ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };
+        auto code_at = [&](uint32_t dd) -> uint32_t { return (PACKED || q2) ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };
         bool over = false, posres = false, pskip = false;
         for (uint32_t d = d0; d < L && cn; d++) {
             DEEP_CLK(t0);
@@ -2038,8 +2040,8 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                         if (s.w <= kResCnt) {  // else (a segment of 2^30 words) the walk below decides
                             n_text += m;
                             posres = true;
-                            put_res(res, q2 ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
-                            cs.put(counts, q2 ? pi : perm[i], 1u);
+                            put_res(res, (PACKED || q2) ? pi : perm[i], (uint64_t)(s.y - m) << 32 | s.x, kResRow | kResPos | s.w, s.z);
+                            cs.put(counts, (PACKED || q2) ? pi : perm[i], 1u);
                             break;
                         }
                     } else {
@@ -2248,7 +2250,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
                     uint32_t t0 = cb[b2]; cb[b2] = cb[b2 + 1]; cb[b2 + 1] = t0;
                     t0 = ce[b2]; ce[b2] = ce[b2 + 1]; ce[b2 + 1] = t0;
                 }
-        const uint32_t o = q2 ? pi : perm[i];
+        const uint32_t o = (PACKED || q2) ? pi : perm[i];
         uint32_t occ = 0;
         const uint64_t at = abase + (uint64_t)i * K;
         if (cn == 1) {

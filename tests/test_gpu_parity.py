@@ -1181,7 +1181,9 @@ K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDS
                  {"EDSBWT_DEEPQ_WAVES": "6", "EDSBWT_DEEP_STATS": "0"}, {"EDSBWT_DEEPQ_WAVES": "5", "EDSBWT_DEEP_STATS": "0"},
                  # (the builds without work counters)
                  {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_EOF_ROWS": "1", "EDSBWT_DEEPQ_WAVES": "5"},
-                 {"EDSBWT_DEEP_K": "2"}, {"EDSBWT_DEEP_K": "3"}, {"EDSBWT_DEEP_K": "8"}]
+                 {"EDSBWT_DEEP_K": "2"}, {"EDSBWT_DEEP_K": "3"}, {"EDSBWT_DEEP_K": "8"},
+                 # the packed direct start's queue: the generic build (not the PACKED one) and PACKED at 7 waves
+                 {"EDSBWT_DEEPQ_PACKED": "0"}, {"EDSBWT_DEEPQ_WAVES": "7"}, {"EDSBWT_DEEPQ_WAVES": "7", "EDSBWT_DEEP_STATS": "0"}]
 
 
 @pytest.mark.parametrize("build", K_DEEP_BUILDS, ids=lambda b: ",".join(f"{k[7:]}={v}" for k, v in b.items()))

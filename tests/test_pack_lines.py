@@ -132,3 +132,23 @@ def test_pack_parts_any_order(lib, L):
     for t in th:
         t.join()
     assert all(ok) and np.array_equal(out[:P * S], want)
+
+
+@pytest.mark.parametrize("L", [3, 20, 31])
+def test_pack_refuses_every_other_byte(lib, L):
+    """Every byte value other than A/C/G/T at a base, and every value other than '\\n' at a line's
+    end, in the middle of a chunk (the packer's bulk path: one table lookup validates a line's
+    bases and its '\\n' together), makes the packer refuse the chunk."""
+    rng = np.random.default_rng(L)
+    P = 3000
+    a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, (P, L))]
+    base = np.concatenate([a, np.full((P, 1), 10, np.uint8)], 1)
+    assert _pack(lib, base.tobytes(), 2) is not None
+    for b in range(256):
+        for col in (0, L // 2, L - 1, L):
+            good = (b == 10) if col == L else (b in b"ACGT")
+            if good:
+                continue
+            t = base.copy()
+            t[P // 3 + b, col] = b
+            assert _pack(lib, t.tobytes(), 2) is None, (b, col)
