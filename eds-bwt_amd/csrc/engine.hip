@@ -693,6 +693,7 @@ struct Engine {
     uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
     // the packed direct start's k_deep build without the generic key reader (k_deep<.., PACKED>)
     bool deepq_packed = env_double("EDSBWT_DEEPQ_PACKED", 1) != 0;
+    unsigned loc_blocks = (unsigned)env_double("EDSBWT_LOC_BLOCKS", 0);
     // the deferred direct start in pieces (EDSBWT_DEEP_PIECES, batches of at least
     // EDSBWT_DEEP_PIECE_MIN patterns): k_deep_direct over piece j + 1 runs while k_deep walks piece
     // j's queue on a second stream (an event per piece), so k_deep's long-tailed lanes share the
@@ -3298,7 +3299,9 @@ struct Engine {
             rec.ensure(occ_cap);
             lbig.ensure(P + 1);  // (its counter zeroed with the others at the search's start)
             // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
-            launch(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>, P, P, (const Res*)res.p, o32, first_id, pat_ids, X,
+            // (EDSBWT_LOC_BLOCKS: a smaller grid, so small tests take the kernel's later block-rounds)
+            launch_grid(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>,
+                        loc_blocks ? std::min<unsigned>(grid_for(P), loc_blocks) : grid_for(P), P, (const Res*)res.p, o32, first_id, pat_ids, X,
                    (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
                    tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);

@@ -73,10 +73,12 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # the dollar step's text-item entries, k_deep's other dispatched build (5 waves per SIMD), the
     # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
     # counts instead of per-tile record offsets, the locate kernel's own counts, and k_deep one
-    # character per step (no pair entries)
+    # character per step (no pair entries), k_locate_pp's block-rounds on a 1- and 3-block grid, and
+    # its 512-record stage
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "5"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
-                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0")):
+                     ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0"), ("EDSBWT_LOC_BLOCKS", "1"), ("EDSBWT_LOC_BLOCKS", "3"),
+                     ("EDSBWT_LOC_STAGE", "512")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -654,6 +656,37 @@ def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, dire
             assert np.array_equal(gc2, oc) and idx.stats()["text_rows"] == 0
             if locate:
                 assert np.array_equal(go2, oo)
+
+
+@pytest.mark.parametrize("env", [{"EDSBWT_LOC_BLOCKS": "1"}, {"EDSBWT_LOC_BLOCKS": "3"}, {"EDSBWT_LOC_BLOCKS": "5", "EDSBWT_LOC_STAGE": "512"}],
+                         ids=["1 block", "3 blocks", "5 blocks, stage 512"])
+def test_locate_block_rounds_gpu(oracle, edsbwt, tmp_path, monkeypatch, env):
+    """k_locate_pp over many block-rounds (a grid of 1-5 blocks for ~6000 patterns: the production
+    grid gives C3's 10M patterns 2-3 rounds per block): planted patterns ending in one row (records from the
+    result's text position), in a row range and in interval lists, misses; records identical to the
+    oracle's, count-only counts too."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = random.Random(4242)
+    segs = _covid_like(rng, 700)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(3000)]
+    pats += [edsgen.planted(rng, segs, rng.randint(4, D0)) or "ACG" for _ in range(2000)]        # short: many occurrences
+    pats += [rng.choice("ACGT") + p[1:] for p in pats[:1000]]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=5)
+    assert oo.size > 2 * len(pats)
+    with edsbwt.Index(base) as idx:
+        for kw in ({}, {"direct": False}, {"locate": False}):
+            gc, go = idx.search((buf, offs), first_pattern_id=5, **kw)
+            assert np.array_equal(gc, oc), kw
+            if kw.get("locate", True):
+                assert np.array_equal(go, oo), kw
+                assert idx.stats()["locate_offsets"] == int(oo["offset"].astype(np.uint64).sum())
 
 
 def test_split_locate_scans_gpu(oracle, edsbwt, tmp_path, monkeypatch):
