@@ -694,6 +694,24 @@ struct Engine {
     // the packed direct start's k_deep build without the generic key reader (k_deep<.., PACKED>)
     bool deepq_packed = env_double("EDSBWT_DEEPQ_PACKED", 1) != 0;
     unsigned loc_blocks = (unsigned)env_double("EDSBWT_LOC_BLOCKS", 0);
+    // a located deferred direct-start search sums its record-offset tiles (k_count_tiles) on a second
+    // stream beside k_deep_wave, leaving out the patterns k_deep_wave walks (a bitmap, k_mark_wide);
+    // k_tile_fix adds those after both (EDSBWT_WAVE_TILES=0: k_count_tiles after k_deep_wave)
+    bool wave_tiles = env_double("EDSBWT_WAVE_TILES", 1) != 0;
+    DBuf<uint32_t> wbits;           // the bitmap (zero between searches: k_count_tiles clears what it read)
+    uint64_t wbits_words = 0;
+    uint32_t* early_counts = nullptr;  // this search's counts when the early tiles may run (search())
+    bool in_direct = false;            // run_deep called from the direct start (nothing writes results after it)
+    bool tiles_early = false;          // the early tiles were queued (finish_deferred joins them)
+    hipEvent_t tiles_ev = nullptr, tiles_ev0 = nullptr;
+    // the library stream waits for the early tiles (before anything else may touch their outputs)
+    void join_early() {
+        if (!tiles_early) return;
+        HIPCHK(hipStreamWaitEvent(stream, tiles_ev, 0));
+        tiles_early = false;
+    }
+    const uint32_t* early_ovf = nullptr;
+    uint32_t early_cap = 0;
     // the deferred direct start in pieces (EDSBWT_DEEP_PIECES, batches of at least
     // EDSBWT_DEEP_PIECE_MIN patterns): k_deep_direct over piece j + 1 runs while k_deep walks piece
     // j's queue on a second stream (an event per piece), so k_deep's long-tailed lanes share the
@@ -2170,6 +2188,30 @@ struct Engine {
             if (!no_wide) {
                 ab.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
                 ae.grow_keep(abase + (uint64_t)wcap * kDeepWide, stream);
+                // the record-offset tiles of every other pattern beside k_deep_wave (early_counts: a
+                // located direct start; the results are final but for k_deep_wave's patterns)
+                if (deep_wave && early_counts && in_direct && r == res.p) {
+                    const uint64_t nwords = (P + 31) / 32;
+                    if (wbits_words < nwords) {
+                        wbits.ensure(nwords);
+                        zero(wbits.p, nwords * 4);
+                        wbits_words = nwords;
+                    }
+                    tile_sum.ensure((P + 63) / 64);
+                    if (!stream2) HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+                    if (!tiles_ev) HIPCHK(hipEventCreateWithFlags(&tiles_ev, hipEventDisableTiming));
+                    if (!tiles_ev0) HIPCHK(hipEventCreateWithFlags(&tiles_ev0, hipEventDisableTiming));
+                    HIPCHK(hipEventRecord(tiles_ev0, stream));
+                    HIPCHK(hipStreamWaitEvent(stream2, tiles_ev0, 0));
+                    std::swap(stream, stream2);  // (launch() and its timing events on the second stream)
+                    launch(KC_FINISH, k_mark_wide, wcap, (const uint32_t*)ovf.p, wcap, (const uint32_t*)perm.p, wbits.p);
+                    launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, early_counts, stats.p, (unsigned long long*)tile_sum.p, wbits.p);
+                    std::swap(stream, stream2);
+                    HIPCHK(hipEventRecord(tiles_ev, stream2));
+                    tiles_early = true;
+                    early_ovf = ovf.p;
+                    early_cap = wcap;
+                }
                 // (the waves stride over the list: 2048 of them, not one per possible pattern)
                 if (deep_wave)
                     launch(KC_DEEPW, k_deep_wave, (size_t)std::min<uint32_t>(wcap, kWaveGrid) * 64, P, d, (const uint32_t*)(ovf.p + 1), wcap, lens, (const uint32_t*)perm.p, ind,
@@ -2862,7 +2904,16 @@ struct Engine {
     // k_deep could not hold re-run through the unbounded level path.
     void run_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t P, bool allow_deep, bool ordered, Res* r, uint64_t& abase) {
         uint32_t novf = kNotDirect;
-        if (!ordered && allow_deep) novf = direct(d_off, d_bytes, P, r, abase, ovf_orig.p);
+        if (!ordered && allow_deep) {
+            in_direct = true;
+            try {
+                novf = direct(d_off, d_bytes, P, r, abase, ovf_orig.p);
+            } catch (...) {
+                in_direct = false;
+                throw;
+            }
+            in_direct = false;
+        }
         if (novf == kNotDirect || novf == kNeedOrdered) settle_res(r);
         if (novf == kNeedOrdered) ordered = true;
         if (!ordered && novf == kNotDirect) {
@@ -2981,6 +3032,10 @@ struct Engine {
         // the path whose k_tile_sums reads these counts; every other located path sums them itself)
         const bool loc_tiles = locate && loc_mode == 2 && have_samples && samp_shift == 0 && locate_pp && !locate_counts && tile_scan;
         if (defer_call && fused_counts && (deep_wave || no_wide) && (!locate || (loc_fc && loc_tiles))) fc_counts = d_counts;
+        // (the early tiles: exactly the path finish_deferred takes k_count_tiles on)
+        early_counts = defer_call && loc_tiles && !fc_counts && deep_wave && !no_wide && wave_tiles ? d_counts : nullptr;
+        join_early();  // (a previous search that failed after queueing them)
+        in_direct = false;
         if (P == 0) return 0;
         struct EvPair {  // released on every exit, including exceptions
             hipEvent_t a = nullptr, b = nullptr;
@@ -3030,6 +3085,7 @@ struct Engine {
             if (g0) run_grouped(d_bytes, d_off, P, allow_deep, ordered, g0, abase);
             else run_batch(d_bytes, d_off, P, allow_deep, ordered, res.p, abase);
         } catch (const TooBig&) {
+            join_early();  // (the early tiles of the failed attempt, if queued, end before anything is reused)
             // a depth outgrew 32-bit counts (e.g. a 1 Gchar EDS with many empty words):
             // search the batch as separate trie subtrees, grouped by the last k characters;
             // later batches on this index start grouped (sticky_groups)
@@ -3261,14 +3317,23 @@ struct Engine {
         // (EDSBWT_TILE_SCAN=0: the latter; C3 1.607 / 1.610 against 1.635 ms with 256-pattern
         // tiles, profiles/r04_ab5_c3_*.json)
         const bool tiles = per_pattern && !loc_counts && tile_scan;
+        if (tiles_early && !tiles) {
+            join_early();
+            throw std::logic_error("early record-offset tiles without the tile path");
+        }
         const uint64_t ntile = (P + 63) / 64;
         if (tiles) {
             tile_sum.ensure(ntile);
             tile_pre.ensure(ntile);
-            if (fc_done)  // (the deep kernels wrote every count and their sums)
+            if (tiles_early) {  // (summed beside k_deep_wave: join them, add k_deep_wave's patterns)
+                if (fc_done || d_counts != early_counts) throw std::logic_error("early record-offset tiles on another path");
+                join_early();
+                launch_grid(KC_FINISH, k_tile_fix, std::max(1u, std::min(grid_for(early_cap), 64u)), early_ovf, early_cap, (const uint32_t*)perm.p,
+                            (const Res*)res.p, d_counts, stats.p, (unsigned long long*)tile_sum.p);
+            } else if (fc_done)  // (the deep kernels wrote every count and their sums)
                 launch(KC_FINISH, k_tile_sums, P, (const uint32_t*)d_counts, P, (unsigned long long*)tile_sum.p);
             else
-                launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p);
+                launch(KC_FINISH, k_count_tiles, P, (const Res*)res.p, P, d_counts, stats.p, (unsigned long long*)tile_sum.p, (uint32_t*)nullptr);
         } else if (!fc_done && !loc_counts)
             launch_reduce(KC_FINISH, k_count_found, (const Res*)res.p, P, d_counts, counters.p + 1, counters.p + 12,
                           locate && !per_pattern ? occ64.p : (uint64_t*)nullptr);
@@ -4654,6 +4719,8 @@ struct Engine {
         if (stream) (void)hipStreamSynchronize(stream);
         if (stream2) (void)hipStreamSynchronize(stream2);
         for (auto e : piece_ev) (void)hipEventDestroy(e);
+        if (tiles_ev) (void)hipEventDestroy(tiles_ev);
+        if (tiles_ev0) (void)hipEventDestroy(tiles_ev0);
         if (stream2) (void)hipStreamDestroy(stream2);
         if (up) (void)hipStreamSynchronize(up);
         if (down) (void)hipStreamSynchronize(down);

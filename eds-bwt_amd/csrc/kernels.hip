@@ -4075,8 +4075,15 @@ __global__ void __launch_bounds__(256) k_count_found(const Res* __restrict__ res
 // of each 64-pattern tile (one wave of k_locate_pp), whose exclusive scan gives every tile its
 // first record — a scan over tiles instead of over patterns (C3: 156K entries against 10M), and
 // no block barrier per tile (wave shuffles)
+// wbits != nullptr (engine.hip run_deep: this pass runs beside k_deep_wave, on a second stream):
+// the patterns k_deep_wave still walks are marked there (k_mark_wide, by output index) and left
+// out — neither their results nor their counts are read or written here; k_tile_fix adds them once
+// both kernels are done.  Each marked word is cleared after it is read (the bitmap is zero again
+// for the next search): a word's two readers are lanes of one wave, and the store depends on the
+// loaded value, so it follows the loads.
 __global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res, uint64_t P, uint32_t* __restrict__ counts,
-                                                     unsigned long long* __restrict__ stats, unsigned long long* __restrict__ tile_sum) {
+                                                     unsigned long long* __restrict__ stats, unsigned long long* __restrict__ tile_sum,
+                                                     uint32_t* __restrict__ wbits) {
     // (a grid of up to 16384 blocks: the found / occurrence sums go to the sharded stats, folded by
     // k_gather_checks — the deferred path of this pass checks no interval total)
     __shared__ unsigned long long sh[4];
@@ -4085,11 +4092,42 @@ __global__ void __launch_bounds__(256) k_count_tiles(const Res* __restrict__ res
         const uint64_t i = p0 + threadIdx.x;
         uint32_t oc = 0;
         if (i < P) {
-            oc = res_occ(res[i]);
-            cs.put(counts, i, oc);
+            const uint32_t wb = wbits ? wbits[i >> 5] : 0u;
+            if (!((wb >> (i & 31)) & 1u)) {
+                oc = res_occ(res[i]);
+                cs.put(counts, i, oc);
+            }
+            if (wb && (i & 31) == 0) wbits[i >> 5] = 0u;
         }
         const unsigned long long t = wave_sum(oc);
         if ((threadIdx.x & 63) == 0 && i < P) tile_sum[i >> 6] = t;  // (p0 is a multiple of 64)
+    }
+    cs.flush(counts, stats, sh);
+}
+
+// the patterns k_deep_wave walks (its list: count at ovf[0], queue indices after it, at most cap of
+// them), marked by output index for k_count_tiles running beside it
+__global__ void k_mark_wide(const uint32_t* __restrict__ ovf, uint32_t cap, const uint32_t* __restrict__ perm, uint32_t* __restrict__ wbits) {
+    const uint32_t n = min(ovf[0], cap);
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const uint32_t o = perm[ovf[1 + j]];
+        atomicOr(&wbits[o >> 5], 1u << (o & 31));
+    }
+}
+
+// after k_count_tiles (without the marked patterns) and k_deep_wave: the walked patterns' counts into
+// the caller's array, their occurrences into their tiles' sums and into the fused sums
+__global__ void __launch_bounds__(256) k_tile_fix(const uint32_t* __restrict__ ovf, uint32_t cap, const uint32_t* __restrict__ perm,
+                                                  const Res* __restrict__ res, uint32_t* __restrict__ counts,
+                                                  unsigned long long* __restrict__ stats, unsigned long long* __restrict__ tile_sum) {
+    __shared__ unsigned long long sh[4];
+    CountSums cs;
+    const uint32_t n = min(ovf[0], cap);
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const uint32_t o = perm[ovf[1 + j]];
+        const uint32_t oc = res_occ(res[o]);
+        cs.put(counts, o, oc);
+        if (oc) atomicAdd(&tile_sum[o >> 6], (unsigned long long)oc);
     }
     cs.flush(counts, stats, sh);
 }

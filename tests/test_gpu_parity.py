@@ -621,6 +621,54 @@ def test_deep_pieces_gpu(oracle, edsbwt, tmp_path, monkeypatch, pieces):
             assert deep.min() < len(pats) // int(pieces) and deep.max() >= len(pats) - len(pats) // int(pieces)
 
 
+@pytest.mark.parametrize("env", [{}, {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7"},
+                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_WAVE_TILES": "0"},
+                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_DEEP_PIECES": "3"}],
+                         ids=["default", "K=2", "K=2, tiles after k_deep_wave", "K=2, 3 pieces"])
+def test_wave_tiles_gpu(oracle, edsbwt, tmp_path, monkeypatch, env):
+    """The located deferred direct start sums its record-offset tiles on a second stream beside
+    k_deep_wave (engine.hip run_deep: k_mark_wide + k_count_tiles without the patterns k_deep_wave
+    walks, then k_tile_fix): counts and every record equal to the oracle's, through search() and the
+    device-resident call (with and without work counters, repeated on the same buffers: the bitmap
+    must be clear again), with patterns really walked by k_deep_wave (7-mer start lists and K = 2:
+    many lists overflow k_deep's registers), and the same with the tiles summed after k_deep_wave."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("EDSBWT_PATH_TAGS", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = random.Random(9091)
+    segs = _covid_like(rng, 900)
+    if any(w == "" for w in segs[1]):
+        segs[1] = ["A"]
+    base = _build(oracle, tmp_path, edsgen.eds_text(segs))
+    with edsbwt.Index(base) as idx:
+        D0 = idx.ktab_depth
+    pats = [edsgen.planted(rng, segs, rng.randint(D0 + 1, D0 + 16)) or "ACGT" * 8 for _ in range(6000)]
+    pats = [p[: D0 + 16] if len(p) > D0 + 16 else p for p in pats]
+    pats += [rng.choice("ACGT") + p[1:] for p in pats[:800]]
+    buf, offs = _pack(pats)
+    oc, oo, _ = oracle.Engine(base, 8).search(buf, offs, first_pattern_id=2)
+    with edsbwt.Index(base) as idx:
+        gc, go = idx.search((buf, offs), first_pattern_id=2)
+        assert idx.stats()["start_depth"] == D0 and idx.stats()["redo_searches"] == 0
+        assert np.array_equal(gc, oc) and np.array_equal(go, oo)
+        d_bytes = torch.from_numpy(buf.copy()).cuda()
+        d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_counts = torch.zeros(len(pats), dtype=torch.int32, device="cuda")
+        for counters in (False, False, True):  # (path tags: of the last call, a counted one)
+            d_counts.fill_(-1)
+            ptr, n = idx.search_device(d_bytes.data_ptr(), d_offs.data_ptr(), len(pats), d_counts.data_ptr(), first_pattern_id=2,
+                                       counters=counters)
+            torch.cuda.synchronize()
+            assert np.array_equal(d_counts.cpu().numpy().view(np.uint32), oc) and n == oo.size
+            assert idx.stats()["redo_searches"] == 0
+        tags = idx.path_tags(len(pats))  # (of the last device-resident call)
+        if env.get("EDSBWT_DEEP_K") == "2":
+            assert (tags & edsbwt.PATH_WIDE).astype(bool).sum() > 20
+        gc2, go2 = idx.search((buf, offs), first_pattern_id=2)
+        assert np.array_equal(gc2, oc) and np.array_equal(go2, oo)
+
+
 @pytest.mark.parametrize("direct", [True, False])
 def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, direct):
     """Single-row intervals decided by comparing the pattern with the words' text: patterns
