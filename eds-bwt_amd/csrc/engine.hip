@@ -694,13 +694,13 @@ struct Engine {
     // the packed direct start's k_deep build without the generic key reader (k_deep<.., PACKED>)
     bool deepq_packed = env_double("EDSBWT_DEEPQ_PACKED", 1) != 0;
     unsigned loc_blocks = (unsigned)env_double("EDSBWT_LOC_BLOCKS", 0);
-    // EDSBWT_WAVE_TILES=1: a located deferred direct-start search sums its record-offset tiles
-    // (k_count_tiles) on a second stream beside k_deep_wave, leaving out the patterns k_deep_wave walks
-    // (a bitmap, k_mark_wide); k_tile_fix adds those after both.  Off by default: C3 1.412-1.424 against
-    // 1.425-1.442 ms in a process that only runs device-resident searches, but 1.55-1.70 against 1.43 ms
-    // once the host pipeline has run in the process (bench.py's e2e leg first; k_deep_direct and k_deep
-    // themselves read slower, not only the joined step — profiles/r06_ab_c3_wave_tiles.txt)
-    bool wave_tiles = env_double("EDSBWT_WAVE_TILES", 0) != 0;
+    // a located deferred direct-start search sums its record-offset tiles (k_count_tiles) on the second
+    // stream beside k_deep_wave, leaving out the patterns k_deep_wave walks (a bitmap, k_mark_wide);
+    // k_tile_fix adds those after both (EDSBWT_WAVE_TILES=0: k_count_tiles after k_deep_wave).  C3
+    // 1.373-1.387 against 1.392-1.396 ms with bench.py's e2e leg first in the process — with the second
+    // stream created at open; created on first use (inside the host pipeline, after its copy streams)
+    // it made the step 1.55-1.73 ms (profiles/r06_ab_c3_wave_tiles.txt)
+    bool wave_tiles = env_double("EDSBWT_WAVE_TILES", 1) != 0;
     DBuf<uint32_t> wbits;           // the bitmap (zero between searches: k_count_tiles clears what it read)
     uint64_t wbits_words = 0;
     uint32_t* early_counts = nullptr;  // this search's counts when the early tiles may run (search())
@@ -1102,6 +1102,9 @@ struct Engine {
         device = dev;
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        // the second stream (run_deep_pieces, the wave tiles) next to it, before the host pipeline's
+        // copy streams exist (EDSBWT_STREAM2_EARLY=0: created on first use)
+        if (env_double("EDSBWT_STREAM2_EARLY", 1) != 0) HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
         {
             const size_t a = 512, big = ((kCnt + 2 * (NSHARD + 8)) * 4 + 255) / 256 * 256, stb = kStatSlots * 8;
             hostblk_size = a + big + stb + kStageBytes;

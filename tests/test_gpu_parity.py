@@ -621,13 +621,14 @@ def test_deep_pieces_gpu(oracle, edsbwt, tmp_path, monkeypatch, pieces):
             assert deep.min() < len(pats) // int(pieces) and deep.max() >= len(pats) - len(pats) // int(pieces)
 
 
-@pytest.mark.parametrize("env", [{"EDSBWT_WAVE_TILES": "1"}, {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_WAVE_TILES": "1"},
-                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7"},
-                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_DEEP_PIECES": "3", "EDSBWT_WAVE_TILES": "1"}],
-                         ids=["wave tiles", "K=2, wave tiles", "K=2, tiles after k_deep_wave (default)", "K=2, 3 pieces, wave tiles"])
+@pytest.mark.parametrize("env", [{}, {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7"},
+                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_WAVE_TILES": "0"},
+                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_DEEP_PIECES": "3"},
+                                 {"EDSBWT_DEEP_K": "2", "EDSBWT_KTAB_K": "7", "EDSBWT_STREAM2_EARLY": "0"}],
+                         ids=["default", "K=2", "K=2, tiles after k_deep_wave", "K=2, 3 pieces", "K=2, second stream on first use"])
 def test_wave_tiles_gpu(oracle, edsbwt, tmp_path, monkeypatch, env):
-    """EDSBWT_WAVE_TILES=1 (opt-in): the located deferred direct start sums its record-offset tiles on
-    a second stream beside k_deep_wave (engine.hip run_deep: k_mark_wide + k_count_tiles without the patterns k_deep_wave
+    """The located deferred direct start sums its record-offset tiles on the second stream beside
+    k_deep_wave (engine.hip run_deep: k_mark_wide + k_count_tiles without the patterns k_deep_wave
     walks, then k_tile_fix): counts and every record equal to the oracle's, through search() and the
     device-resident call (with and without work counters, repeated on the same buffers: the bitmap
     must be clear again), with patterns really walked by k_deep_wave (7-mer start lists and K = 2:
