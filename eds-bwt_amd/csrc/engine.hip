@@ -392,6 +392,7 @@ struct Engine {
     DBuf<uint4> ktab_wide;    // ... or the wide form, 32 or 64 B per D-mer (k_ktab_wide; replaces ktab_one)
     uint32_t kt1_ws = 2;      // its uint4s per D-mer (KIdx::kt1_ws)
     DBuf<uint4> srow;         // per-row text-compare entries, 32 B per row (k_srow; KIdx::srow)
+    DBuf<uint4> seglink;      // k_deep_direct's link lines, 128 B per segment (k_seglink; KIdx::seglink)
     // deep level start table (build_ltab; kernels.hip k_ltab_*): every L-mer's walk items after
     // its L characters, in lt_G groups by the L-mer's last characters (x mod lt_G); a level walk
     // whose patterns are all at least L long starts at depth L from it (C5: L = 8)
@@ -796,6 +797,7 @@ struct Engine {
         X.gpos = gpos.p;
         X.wrow = wrow.p;
         X.srow = txt && srow.p ? (const uint4*)srow.p : nullptr;
+        X.seglink = X.srow && seglink.p ? (const uint4*)seglink.p : nullptr;
         X.text_deep = text_deep ? 1u : 0u;
         X.kt1_pos = kt1_pos ? 1u : 0u;
         X.kt1_ws = kt1_ws;
@@ -1254,6 +1256,7 @@ struct Engine {
         // per-row entries would take first (C5: 40 GB, the table then one depth shallower)
         build_srow();
         build_segtext();
+        build_seglink();
         // after the per-row entries: the level table's budget is a share of what HBM has left
         build_ltab();
         open_peak_bytes = (uint64_t)std::max<int64_t>(0, mt.peak);
@@ -1393,6 +1396,20 @@ struct Engine {
                              std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
             return;
         }
+    }
+
+    // KIdx::seglink: k_deep_direct's link from a word start reads the segment's ranks for the next
+    // character and, when they give one row, that row's text-compare entry from one 128-B line
+    // instead of the segment row and then the row's srow line (C3: 243 MB; EDSBWT_SEGLINK=0: off)
+    void build_seglink() {
+        if (!srow.p || sigma != 5 || !segtab.p || env_double("EDSBWT_SEGLINK", 1) == 0) return;
+        const size_t bytes = ((size_t)S + 2) * 128;
+        size_t tb_ = 0;
+        if ((double)hbm_free(&tb_) < 4.0 * (double)bytes) return;
+        seglink.ensure(((size_t)S + 2) * 8);
+        launch(KC_TABLE, k_seglink, ((size_t)S + 2) * 4, S, kidx(), seglink.p);
+        HIPCHK(hipStreamSynchronize(stream));
+        device_bytes += bytes;
     }
 
     // KIdx::segtext: each segment row's text-item entries, from the per-row text entries (k_segtext)

@@ -96,6 +96,12 @@ struct KIdx {
     const uint4* srow;         // nullptr, or [2N]: row x's sample (srow[2x]) and {gpos[x], 0, the 32
                                // reversed-text characters before its suffix} (srow[2x+1]): a single
                                // row's text compare from ONE line (k_srow; dense samples + text)
+    // the direct start's link from a word start (k_deep_direct; sigma = 5 with srow; nullptr: not
+    // built): per segment s, 128 B = one DRAM line, for c = 1..4 at seglink[8 s + 2 (c - 1)]:
+    // {rx, ry, sample.x, sample.y}, {sample.z, sample.w, window lo, window hi} — the segment link
+    // table's ranks (segtab [1 + c], [seg_hi + c]) and, when ry = rx + 1, the srow entry of the one
+    // row C[c] + rx, so a link that lands on one row needs no second line for its text compare
+    const uint4* seglink;
     uint32_t text_deep;        // k_deep compares single rows too (EDSBWT_TEXT_DEEP, A/B)
     uint32_t kt1_pos;          // the direct start's inline D-mer entries of ONE row hold that row's
                                // text position too (k_ktab_one): bit 62 set, gpos in bits [31, 62)

@@ -1737,6 +1737,18 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                     const uint32_t* lk = reinterpret_cast<const uint32_t*>(kt1w + 4 * (size_t)u + 2);
                     rx = lk[c - 1];
                     ry = lk[4 + c - 1];
+                } else if (X.seglink) {  // the ranks and, for one row, its text-compare entry: one line
+                    const uint4* sl = X.seglink + 8 * (size_t)s.z + 2 * (c - 1);
+                    const uint4 l0 = sl[0], l1 = sl[1];
+                    rx = l0.x;
+                    ry = l0.y;
+                    if (ry == rx + 1) {
+                        s = make_uint4(l0.z, l0.w, l1.x, l1.y);
+                        tw = (uint64_t)l1.w << 32 | l1.z;
+                        have = true;
+                    }
+                    n_blk++;
+                    DD_CNT(c_seg);
                 } else {
                     const uint32_t* et = X.segtab + (size_t)s.z * X.seg_stride;
                     rx = et[1 + c];
@@ -3950,6 +3962,28 @@ __global__ void k_segtab(uint32_t S, KIdx X, uint32_t* __restrict__ tab) {
             e[1 + c] = r0[c];
             e[X.seg_hi + c] = r1[c];
         }
+    }
+}
+
+// KIdx::seglink (k_deep_direct's links): per segment s and c = 1..4, the segment link table's ranks
+// and, when they give one row, that row's srow entry (sample, and the 32 reversed-text characters
+// before its suffix); one 128-B line per segment
+__global__ void k_seglink(uint32_t S, KIdx X, uint4* __restrict__ out) {
+    GRID_STRIDE(t, ((size_t)S + 2) * 4) {
+        const size_t s = t >> 2;
+        const uint32_t c = (uint32_t)(t & 3) + 1;
+        const uint32_t* et = X.segtab + s * X.seg_stride;
+        const uint32_t rx = et[1 + c], ry = et[X.seg_hi + c];
+        uint4 a = make_uint4(rx, ry, 0, 0), b = make_uint4(0, 0, 0, 0);
+        if (ry == rx + 1 && X.srow) {
+            const size_t row = (size_t)X.C[c] + rx;
+            const uint4 s0 = X.srow[2 * row], s1 = X.srow[2 * row + 1];
+            a.z = s0.x;
+            a.w = s0.y;
+            b = make_uint4(s0.z, s0.w, s1.z, s1.w);
+        }
+        out[2 * t] = a;
+        out[2 * t + 1] = b;
     }
 }
 

@@ -73,12 +73,12 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     # the dollar step's text-item entries, k_deep's other dispatched build (5 waves per SIMD), the
     # separate count pass instead of the deep kernels' fused counts, the per-pattern scan of the
     # counts instead of per-tile record offsets, the locate kernel's own counts, and k_deep one
-    # character per step (no pair entries), k_locate_pp's block-rounds on a 1- and 3-block grid, and
-    # its 512-record stage
+    # character per step (no pair entries), k_locate_pp's block-rounds on a 1- and 3-block grid, its
+    # 512-record stage, and k_deep_direct's links through the segment table and srow (no seglink lines)
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "5"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
                      ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0"), ("EDSBWT_LOC_BLOCKS", "1"), ("EDSBWT_LOC_BLOCKS", "3"),
-                     ("EDSBWT_LOC_STAGE", "512")):
+                     ("EDSBWT_LOC_STAGE", "512"), ("EDSBWT_SEGLINK", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -705,6 +705,14 @@ def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, dire
             assert np.array_equal(gc2, oc) and idx.stats()["text_rows"] == 0
             if locate:
                 assert np.array_equal(go2, oo)
+    # the same with k_deep_direct's links through the segment table, then the row's srow line
+    monkeypatch.setenv("EDSBWT_SEGLINK", "0")
+    with edsbwt.Index(base) as idx:
+        for locate in (True, False):
+            gc3, go3 = idx.search((buf, offs), direct=direct, locate=locate)
+            assert np.array_equal(gc3, oc)
+            if locate:
+                assert np.array_equal(go3, oo)
 
 
 @pytest.mark.parametrize("env", [{"EDSBWT_LOC_BLOCKS": "1"}, {"EDSBWT_LOC_BLOCKS": "3"}, {"EDSBWT_LOC_BLOCKS": "5", "EDSBWT_LOC_STAGE": "512"}],
