@@ -694,6 +694,8 @@ struct Engine {
     uint32_t deepq_pairs = env_double("EDSBWT_DEEPQ_PAIRS", 1) != 0 ? 1u : 0u;
     // the packed direct start's k_deep build without the generic key reader (k_deep<.., PACKED>)
     bool deepq_packed = env_double("EDSBWT_DEEPQ_PACKED", 1) != 0;
+    // k_deep_direct returns to the text compare when a rank step leaves one row (k_deep_direct<.., BACK>)
+    bool direct_back = env_double("EDSBWT_DIRECT_BACK", 1) != 0;
     unsigned loc_blocks = (unsigned)env_double("EDSBWT_LOC_BLOCKS", 0);
     // a located deferred direct-start search sums its record-offset tiles (k_count_tiles) on the second
     // stream beside k_deep_wave, leaving out the patterns k_deep_wave walks (a bitmap, k_mark_wide);
@@ -2152,7 +2154,8 @@ struct Engine {
         } else if (kdd && fk_now.on) {
             // the fused direct start: keys from the pattern bytes inside k_deep_direct (nid_d is
             // written there, for k_deep and k_deep_wave)
-            auto kd0 = direct_waves >= 8 ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
+            auto kd0 = direct_waves >= 8 ? (direct_back ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
+                                                        : (deep_stats ? k_deep_direct<8, true, true, false> : k_deep_direct<8, true, false, false>))
                      : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
                    fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, 0u);
@@ -2308,7 +2311,8 @@ struct Engine {
         // stream2 starts after everything already on the library stream (the zeroing, the keys' inputs)
         HIPCHK(hipEventRecord(piece_ev[np], stream));
         HIPCHK(hipStreamWaitEvent(stream2, piece_ev[np], 0));
-        auto kd0 = direct_waves >= 8 ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
+        auto kd0 = direct_waves >= 8 ? (direct_back ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
+                                                    : (deep_stats ? k_deep_direct<8, true, true, false> : k_deep_direct<8, true, false, false>))
                  : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
         auto kd = deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>)
                                    : (deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>);

@@ -1568,7 +1568,7 @@ struct LaneCtr {
 
 // STATS = false (EDSBWT_DEEP_STATS=0): no per-lane work counters (steps, lines, text rows) — five
 // registers fewer in a kernel whose time follows its register pressure
-template <int MINW, bool FUSED = false, bool STATS = true>
+template <int MINW, bool FUSED = false, bool STATS = true, bool BACK = true>
 __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t D0, const uint32_t* __restrict__ nid, KIdx X, uint64_t abase,
                                                            uint32_t K, Res* __restrict__ res, uint4* __restrict__ q, uint32_t qcap,
                                                            uint32_t* __restrict__ qcnt, unsigned long long* __restrict__ ctr,
@@ -1679,6 +1679,11 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
             uint64_t tw = win1;
             bool have = g1 != ~0u;
             bool ent_row = have && X.kt1_ws == 4;  // s is the entry's row: its link ranks are in the entry
+            // the text compare while the interval is one row, rank steps while it holds several, and
+            // back to the text compare when a rank step leaves one row (BACK; EDSBWT_DIRECT_BACK=0:
+            // rank steps to the end once the interval was wide) — a row's text-compare line replaces a
+            // rank-entry line per two characters
+            for (;;) {
             while (X.rtext && b == e && d < L) {
                 // one row = one text position: the next k = min(o, m) <= 16 characters against the
                 // text (MOVE_EDSBWTSearch.cpp:424-510 stepping one row), as in k_deep_fast
@@ -1767,6 +1772,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 e = X.C[c] + ry - 1;
                 d++;
             }
+            bool back = false;
             for (; d < L; d++) {
                 const uint32_t c = code_at(d);
                 if (c >= X.sigma) { alive = false; break; }
@@ -1788,6 +1794,7 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                             b = X.PC[p] + p0;
                             e = X.PC[p] + p1 - 1;
                             d++;
+                            if (BACK && b == e && X.rtext) { d++; back = true; break; }
                             continue;
                         }
                         pair_skip = true;
@@ -1804,6 +1811,9 @@ __global__ void __launch_bounds__(256, MINW) k_deep_direct(uint64_t P, uint32_t 
                 if (se <= sb) { alive = false; break; }
                 b = X.C[c] + sb;
                 e = X.C[c] + se - 1;
+                if (BACK && b == e && X.rtext) { d++; back = true; break; }
+            }
+            if (!back) break;
             }
             if (want) {
                 w = make_uint4((uint32_t)i, d, b, e);

@@ -78,7 +78,7 @@ def _compare(oracle, edsbwt, base, pats, table_too=True):
     for var, val in (("EDSBWT_FUSE_FINISH", "0"), ("EDSBWT_TEXT_ITEMS", "0"), ("EDSBWT_LINK_CB", "0"), ("EDSBWT_DEEP_WAVE", "0"),
                      ("EDSBWT_SEGTEXT", "0"), ("EDSBWT_DEEPQ_WAVES", "5"), ("EDSBWT_FUSED_COUNTS", "0"), ("EDSBWT_TILE_SCAN", "0"),
                      ("EDSBWT_LOCATE_COUNTS", "1"), ("EDSBWT_DEEPQ_PAIRS", "0"), ("EDSBWT_LOC_BLOCKS", "1"), ("EDSBWT_LOC_BLOCKS", "3"),
-                     ("EDSBWT_LOC_STAGE", "512"), ("EDSBWT_SEGLINK", "0")):
+                     ("EDSBWT_LOC_STAGE", "512"), ("EDSBWT_SEGLINK", "0"), ("EDSBWT_DIRECT_BACK", "0")):
         old = os.environ.get(var)
         os.environ[var] = val
         try:
@@ -705,14 +705,17 @@ def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, dire
             assert np.array_equal(gc2, oc) and idx.stats()["text_rows"] == 0
             if locate:
                 assert np.array_equal(go2, oo)
-    # the same with k_deep_direct's links through the segment table, then the row's srow line
-    monkeypatch.setenv("EDSBWT_SEGLINK", "0")
-    with edsbwt.Index(base) as idx:
-        for locate in (True, False):
-            gc3, go3 = idx.search((buf, offs), direct=direct, locate=locate)
-            assert np.array_equal(gc3, oc)
-            if locate:
-                assert np.array_equal(go3, oo)
+    # the same with k_deep_direct's links through the segment table, then the row's srow line, and
+    # with its rank steps kept to the end once an interval was wide (no return to the text compare)
+    for var in ("EDSBWT_SEGLINK", "EDSBWT_DIRECT_BACK"):
+        monkeypatch.setenv(var, "0")
+        with edsbwt.Index(base) as idx:
+            for locate in (True, False):
+                gc3, go3 = idx.search((buf, offs), direct=direct, locate=locate)
+                assert np.array_equal(gc3, oc), var
+                if locate:
+                    assert np.array_equal(go3, oo), var
+        monkeypatch.delenv(var)
 
 
 @pytest.mark.parametrize("env", [{"EDSBWT_LOC_BLOCKS": "1"}, {"EDSBWT_LOC_BLOCKS": "3"}, {"EDSBWT_LOC_BLOCKS": "5", "EDSBWT_LOC_STAGE": "512"}],
