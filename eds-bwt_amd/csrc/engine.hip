@@ -697,6 +697,7 @@ struct Engine {
     // k_deep_direct returns to the text compare when a rank step leaves one row (k_deep_direct<.., BACK>)
     bool direct_back = env_double("EDSBWT_DIRECT_BACK", 1) != 0;
     unsigned loc_blocks = (unsigned)env_double("EDSBWT_LOC_BLOCKS", 0);
+    unsigned loc_ppt = (unsigned)env_double("EDSBWT_LOC_PPT", 2);
     // a located deferred direct-start search sums its record-offset tiles (k_count_tiles) on the second
     // stream beside k_deep_wave, leaving out the patterns k_deep_wave walks (a bitmap, k_mark_wide);
     // k_tile_fix adds those after both (EDSBWT_WAVE_TILES=0: k_count_tiles after k_deep_wave).  C3
@@ -1402,10 +1403,13 @@ struct Engine {
 
     // KIdx::seglink: k_deep_direct's link from a word start reads the segment's ranks for the next
     // character and, when they give one row, that row's text-compare entry from one 128-B line
-    // instead of the segment row and then the row's srow line (C3: 243 MB; EDSBWT_SEGLINK=0: off)
+    // instead of the segment row and then the row's srow line (C3: 243 MB; EDSBWT_SEGLINK=0: off).
+    // At most EDSBWT_SEGLINK_GB (default 2) GB: it is built before the level start table, whose
+    // budget is a share of the HBM left (C5's 88M segments would take 11 GB of it)
     void build_seglink() {
         if (!srow.p || sigma != 5 || !segtab.p || env_double("EDSBWT_SEGLINK", 1) == 0) return;
         const size_t bytes = ((size_t)S + 2) * 128;
+        if ((double)bytes > env_double("EDSBWT_SEGLINK_GB", 2) * 1073741824.0) return;
         size_t tb_ = 0;
         if ((double)hbm_free(&tb_) < 4.0 * (double)bytes) return;
         seglink.ensure(((size_t)S + 2) * 8);
@@ -3392,8 +3396,12 @@ struct Engine {
             lbig.ensure(P + 1);  // (its counter zeroed with the others at the search's start)
             // (k_locate_pp's waves are k_count_tiles' tiles: both start every block at a multiple of 256)
             // (EDSBWT_LOC_BLOCKS: a smaller grid, so small tests take the kernel's later block-rounds)
-            launch_grid(KC_LOCATE, loc_stage <= 512 ? k_locate_pp<512> : k_locate_pp<kLocStage>,
-                        loc_blocks ? std::min<unsigned>(grid_for(P), loc_blocks) : grid_for(P), P, (const Res*)res.p, o32, first_id, pat_ids, X,
+            // (EDSBWT_LOC_PPT: patterns per thread and block-round, 1 or 2)
+            const uint64_t lppt = loc_ppt >= 2 ? 2 : 1;
+            const unsigned lgrid = grid_for((P + lppt - 1) / lppt);
+            launch_grid(KC_LOCATE, loc_stage <= 512 ? (lppt == 2 ? k_locate_pp<512, 2> : k_locate_pp<512>)
+                                                    : (lppt == 2 ? k_locate_pp<kLocStage, 2> : k_locate_pp<kLocStage>),
+                        loc_blocks ? std::min<unsigned>(lgrid, loc_blocks) : lgrid, P, (const Res*)res.p, o32, first_id, pat_ids, X,
                    (const uint32_t*)ab.p,
                    (const uint32_t*)ae.p, rec.p, occ_cap, lbig.p, oflow, stats.p, loc_counts ? d_counts : (uint32_t*)nullptr,
                    tiles ? (const unsigned long long*)tile_pre.p : (const unsigned long long*)nullptr);

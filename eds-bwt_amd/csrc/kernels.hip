@@ -3586,7 +3586,7 @@ __global__ void __launch_bounds__(256) k_locate_lists(uint64_t P, const Res* __r
 // per record from every lane (records of patterns left to k_locate_big, which runs next on the
 // stream, are written over by it)
 constexpr uint32_t kLocStage = 1024;
-template <uint32_t STAGE = kLocStage>  // records staged per block (STAGE x 20 B of LDS: 1024 -> 7 blocks per CU)
+template <uint32_t STAGE = kLocStage, int PPT = 1>  // records staged per block (STAGE x 20 B of LDS: 1024 -> 7 blocks per CU)
 __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __restrict__ res, uint32_t* __restrict__ oscan, uint32_t first_id,
                                                    const uint32_t* __restrict__ ids, KIdx X, const uint32_t* __restrict__ ab, const uint32_t* __restrict__ ae,
                                                    edsbwt_occ* __restrict__ rec, uint64_t occ_cap, uint32_t* __restrict__ big,
@@ -3603,24 +3603,39 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
     __shared__ unsigned long long sh[4];
     unsigned long long my_off = 0;
     uint32_t* recw = reinterpret_cast<uint32_t*>(rec);
-    for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < P; p0 += (uint64_t)gridDim.x * blockDim.x) {  // block-uniform
-        const uint64_t i = p0 + threadIdx.x, plast = min(P, p0 + blockDim.x) - 1;
-        Res r{};
-        uint32_t occ = 0;
-        uint64_t base = 0;
-        if (i < P) {
-            r = res[i];
-            occ = res_occ(r);
-            if (!tile_pre) base = oscan[i];  // exclusive scan of the counts
-            cs.put(counts, i, occ);
+    // PPT patterns per thread and block-round (p0 + h * 256 + thread): their loads issued together,
+    // so a round's chain of dependent loads (result, then samples) serves PPT x 256 patterns
+    const uint64_t span = (uint64_t)blockDim.x * PPT;
+    for (uint64_t p0 = (uint64_t)blockIdx.x * span; p0 < P; p0 += (uint64_t)gridDim.x * span) {  // block-uniform
+        const uint64_t plast = min(P, p0 + span) - 1;
+        Res r[PPT];
+        uint32_t occ[PPT];
+        uint64_t base[PPT];
+#pragma unroll
+        for (int h = 0; h < PPT; h++) {
+            const uint64_t i = p0 + (uint64_t)h * blockDim.x + threadIdx.x;
+            r[h] = Res{};
+            occ[h] = 0;
+            base[h] = 0;
+            if (i < P) {
+                r[h] = res[i];
+                occ[h] = res_occ(r[h]);
+                if (!tile_pre) base[h] = oscan[i];  // exclusive scan of the counts
+                cs.put(counts, i, occ[h]);
+            }
         }
-        if (tile_pre) {  // (a uniform branch) the wave's tile: its first record + the offsets inside it
-            const uint64_t w0 = p0 + (threadIdx.x & ~63u);
-            const unsigned long long inw = wave_excl_scan(occ);
-            if (w0 < P) base = tile_pre[w0 >> 6] + inw;
+        if (tile_pre) {  // (a uniform branch) each wave's tile: its first record + the offsets inside it
+#pragma unroll
+            for (int h = 0; h < PPT; h++) {
+                const uint64_t w0 = p0 + (uint64_t)h * blockDim.x + (threadIdx.x & ~63u);
+                const unsigned long long inw = wave_excl_scan(occ[h]);
+                if (w0 < P) base[h] = tile_pre[w0 >> 6] + inw;
+            }
         }
-        if (threadIdx.x == 0) s_lo = base;
-        if (i == plast) s_hi = base + occ;
+        if (threadIdx.x == 0) s_lo = base[0];
+#pragma unroll
+        for (int h = 0; h < PPT; h++)
+            if (p0 + (uint64_t)h * blockDim.x + threadIdx.x == plast) s_hi = base[h] + occ[h];
         __syncthreads();
         const uint64_t lo = s_lo, hi = min(s_hi, occ_cap);
         const bool stage = hi >= lo && hi - lo <= STAGE;
@@ -3632,27 +3647,31 @@ __global__ void __launch_bounds__(256) k_locate_pp(uint64_t P, const Res* __rest
                 put_rec(rec, o, pat, word, seg, wis, off);
             }
         };
-        if (i < P && occ) {
-            const uint32_t pat = pat_id(ids, first_id, i);
-            if (base + occ > occ_cap) {
-                atomicOr(oflow, 1u);
-            } else if (r.cnt & kResPos) {
-                const uint32_t off = (uint32_t)(r.off >> 32);
-                emit(base, pat, (uint32_t)r.off, r.occ, r.cnt & kResCnt, off);
-                my_off += off;
-            } else if (occ > kLocBig) {
-                if (tile_pre) oscan[i] = (uint32_t)base;  // (< occ_cap < 2^32) k_locate_big's offset
-                flag_push(big, (uint32_t)i);
-            } else {
-                uint64_t o = base;
-                const uint32_t n = (r.cnt & kResRow) ? 1u : (r.cnt & kResCnt);
-                for (uint32_t t = 0; t < n; t++) {
-                    const uint32_t b = (r.cnt & kResRow) ? (uint32_t)r.off : ab[r.off + t];
-                    const uint32_t e = (r.cnt & kResRow) ? (uint32_t)r.off + occ - 1 : ae[r.off + t];
-                    for (uint32_t x = b; x <= e; x++, o++) {
-                        const uint4 sm = X.samples[x];
-                        emit(o, pat, sm.x, sm.z, sm.w, sm.y);
-                        my_off += sm.y;
+#pragma unroll
+        for (int h = 0; h < PPT; h++) {
+            const uint64_t i = p0 + (uint64_t)h * blockDim.x + threadIdx.x;
+            if (i < P && occ[h]) {
+                const uint32_t pat = pat_id(ids, first_id, i);
+                if (base[h] + occ[h] > occ_cap) {
+                    atomicOr(oflow, 1u);
+                } else if (r[h].cnt & kResPos) {
+                    const uint32_t off = (uint32_t)(r[h].off >> 32);
+                    emit(base[h], pat, (uint32_t)r[h].off, r[h].occ, r[h].cnt & kResCnt, off);
+                    my_off += off;
+                } else if (occ[h] > kLocBig) {
+                    if (tile_pre) oscan[i] = (uint32_t)base[h];  // (< occ_cap < 2^32) k_locate_big's offset
+                    flag_push(big, (uint32_t)i);
+                } else {
+                    uint64_t o = base[h];
+                    const uint32_t n = (r[h].cnt & kResRow) ? 1u : (r[h].cnt & kResCnt);
+                    for (uint32_t t = 0; t < n; t++) {
+                        const uint32_t b = (r[h].cnt & kResRow) ? (uint32_t)r[h].off : ab[r[h].off + t];
+                        const uint32_t e = (r[h].cnt & kResRow) ? (uint32_t)r[h].off + occ[h] - 1 : ae[r[h].off + t];
+                        for (uint32_t x = b; x <= e; x++, o++) {
+                            const uint4 sm = X.samples[x];
+                            emit(o, pat, sm.x, sm.z, sm.w, sm.y);
+                            my_off += sm.y;
+                        }
                     }
                 }
             }

@@ -718,8 +718,9 @@ def test_single_row_text_compare_gpu(oracle, edsbwt, tmp_path, monkeypatch, dire
         monkeypatch.delenv(var)
 
 
-@pytest.mark.parametrize("env", [{"EDSBWT_LOC_BLOCKS": "1"}, {"EDSBWT_LOC_BLOCKS": "3"}, {"EDSBWT_LOC_BLOCKS": "5", "EDSBWT_LOC_STAGE": "512"}],
-                         ids=["1 block", "3 blocks", "5 blocks, stage 512"])
+@pytest.mark.parametrize("env", [{"EDSBWT_LOC_BLOCKS": "1"}, {"EDSBWT_LOC_BLOCKS": "3"}, {"EDSBWT_LOC_BLOCKS": "5", "EDSBWT_LOC_STAGE": "512"},
+                                 {"EDSBWT_LOC_BLOCKS": "3", "EDSBWT_LOC_PPT": "1"}, {"EDSBWT_LOC_PPT": "1"}],
+                         ids=["1 block", "3 blocks", "5 blocks, stage 512", "3 blocks, 1 pattern per thread", "1 pattern per thread"])
 def test_locate_block_rounds_gpu(oracle, edsbwt, tmp_path, monkeypatch, env):
     """k_locate_pp over many block-rounds (a grid of 1-5 blocks for ~6000 patterns: the production
     grid gives C3's 10M patterns 2-3 rounds per block): planted patterns ending in one row (records from the
