@@ -2160,7 +2160,8 @@ struct Engine {
             // written there, for k_deep and k_deep_wave)
             auto kd0 = direct_waves >= 8 ? (direct_back ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
                                                         : (deep_stats ? k_deep_direct<8, true, true, false> : k_deep_direct<8, true, false, false>))
-                     : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
+                     : direct_waves >= 7 ? (deep_stats ? k_deep_direct<7, true> : k_deep_direct<7, true, false>)
+                     : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
             launch(KC_DEEP, kd0, P, P, d, nid_d, X, abase, K, r, dq.p, (uint32_t)qcap, lcnt.p, stats.p, pv, perm.p, kt1w, dq2.p,
                    fk_now.bytes, fk_now.off, len.p, const_cast<uint32_t*>(nid_d), fk_now.n_term, fk_now.E, fk_now.lmin, fk_now.lmax, fc, 0u);
             fk_now.on = false;
@@ -2317,7 +2318,8 @@ struct Engine {
         HIPCHK(hipStreamWaitEvent(stream2, piece_ev[np], 0));
         auto kd0 = direct_waves >= 8 ? (direct_back ? (deep_stats ? k_deep_direct<8, true> : k_deep_direct<8, true, false>)
                                                     : (deep_stats ? k_deep_direct<8, true, true, false> : k_deep_direct<8, true, false, false>))
-                 : direct_waves >= 7 ? k_deep_direct<7, true> : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
+                 : direct_waves >= 7 ? (deep_stats ? k_deep_direct<7, true> : k_deep_direct<7, true, false>)
+                 : direct_waves >= 6 ? k_deep_direct<6, true> : k_deep_direct<1, true>;
         auto kd = deepq_waves >= 6 ? (deep_stats ? k_deep<4, 3, 6> : k_deep<4, 3, 6, false, false>)
                                    : (deep_stats ? k_deep<4, 3, 5> : k_deep<4, 3, 5, false, false>);
         if (deepq_packed && deepq_waves >= 6)  // (the pieces are the packed start's: see run_deep)
