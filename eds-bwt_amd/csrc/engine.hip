@@ -665,7 +665,9 @@ struct Engine {
     // the level step (k_lvl_items, k_lvl_dollar): 7 waves per SIMD (SGPR-bound) or 8 (arguments
     // spilled to VGPR lanes)
     int lvl_waves = (int)env_double("EDSBWT_LVL_WAVES", 7);
-    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 8);
+    // (7 since the walk returns to the text compare: 72 VGPRs against 64 + 9 spilled at 8; C3 1.246-1.250
+    // against 1.255 ms, C2 equal — profiles/r06_ab_direct_waves_back.txt)
+    int direct_waves = (int)env_double("EDSBWT_DIRECT_WAVES", 7);
     // ... and computes the pattern keys itself, no k_keys_acgt (EDSBWT_FUSED_KEYS=0: off, A/B); the
     // fused launch's inputs, set by direct() for run_deep
     bool fused_keys = env_double("EDSBWT_FUSED_KEYS", 1) != 0;
