@@ -698,6 +698,8 @@ struct Engine {
     bool deepq_packed = env_double("EDSBWT_DEEPQ_PACKED", 1) != 0;
     // k_deep_direct returns to the text compare when a rank step leaves one row (k_deep_direct<.., BACK>)
     bool direct_back = env_double("EDSBWT_DIRECT_BACK", 1) != 0;
+    // k_deep's packed build filters a list start of single rows by their text (KIdx::deep_filter)
+    bool deepq_filter = env_double("EDSBWT_DEEPQ_FILTER", 1) != 0;
     unsigned loc_blocks = (unsigned)env_double("EDSBWT_LOC_BLOCKS", 0);
     unsigned loc_ppt = (unsigned)env_double("EDSBWT_LOC_PPT", 2);
     // a located deferred direct-start search sums its record-offset tiles (k_count_tiles) on the second
@@ -804,6 +806,7 @@ struct Engine {
         X.srow = txt && srow.p ? (const uint4*)srow.p : nullptr;
         X.seglink = X.srow && seglink.p ? (const uint4*)seglink.p : nullptr;
         X.text_deep = text_deep ? 1u : 0u;
+        X.deep_filter = deepq_filter ? 1u : 0u;
         X.kt1_pos = kt1_pos ? 1u : 0u;
         X.kt1_ws = kt1_ws;
         X.rk16 = use_rk16 ? rk16.p : nullptr;

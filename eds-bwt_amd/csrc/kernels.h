@@ -103,6 +103,7 @@ struct KIdx {
     // row C[c] + rx, so a link that lands on one row needs no second line for its text compare
     const uint4* seglink;
     uint32_t text_deep;        // k_deep compares single rows too (EDSBWT_TEXT_DEEP, A/B)
+    uint32_t deep_filter;      // k_deep (packed build) filters a list start of single rows by their text (EDSBWT_DEEPQ_FILTER)
     uint32_t kt1_pos;          // the direct start's inline D-mer entries of ONE row hold that row's
                                // text position too (k_ktab_one): bit 62 set, gpos in bits [31, 62)
     // All-symbol rank entries (sigma <= 5; nullptr: not built or not used): the rank of every

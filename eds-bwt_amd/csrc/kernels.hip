@@ -2018,6 +2018,38 @@ __global__ void __launch_bounds__(256, MINW) k_deep(const uint4* __restrict__ q,
             dd[14] = pi; dd[15] = 0xD0D0D0D0u;
         }
 #endif
+        if (PACKED && X.deep_filter && X.srow && X.rtext && X.text_deep && cn > 1 && d0 < L) {
+            // a list start of single rows (a D-mer that occurs a few times): each row's text compared
+            // up to its word start, the lines issued together; the rows that mismatch leave the list
+            // before the first step (they would die in it), so a planted pattern usually goes on
+            // with one row — the text compare below — instead of stepping every row
+            const uint32_t m = L - d0;
+            const uint64_t want = rem >> (2 * (d0 - D0));
+            bool ok[K];
+#pragma unroll
+            for (int t = 0; t < K; t++) {
+                ok[t] = (uint32_t)t < cn;
+                if ((uint32_t)t < cn && cb[t] == ce[t]) {
+                    const uint4 s0 = X.srow[2 * (size_t)cb[t]];
+                    const uint4 t2 = X.srow[2 * (size_t)cb[t] + 1];
+                    const uint32_t k = min(s0.y, m);  // (<= 16: the packed start's patterns)
+                    const uint64_t mask = (1ull << (2 * k)) - 1ull;
+                    ok[t] = ((((uint64_t)t2.w << 32 | t2.z) ^ want) & mask) == 0;
+                    n_blk++;
+                }
+            }
+            uint32_t keep = 0;
+#pragma unroll
+            for (int t = 0; t < K; t++) {
+                if (ok[t]) {
+#pragma unroll
+                    for (int v = 0; v <= t; v++)
+                        if ((uint32_t)v == keep) { cb[v] = cb[t]; ce[v] = ce[t]; }
+                    keep++;
+                }
+            }
+            cn = keep;
+        }
         SymReader<BPS> sym{k0, krest, P, pi};
         auto code_at = [&](uint32_t dd) -> uint32_t { return (PACKED || q2) ? 1u + (uint32_t)((rem >> (2 * (dd - D0))) & 3u) : sym.code(dd); };
         bool over = false, posres = false, pskip = false;

@@ -1279,7 +1279,9 @@ K_DEEP_BUILDS = [{"EDSBWT_DEEPQ_WAVES": "1"}, {"EDSBWT_DEEPQ_WAVES": "5"}, {"EDS
                  # the packed direct start's queue: the generic build (not the PACKED one) and PACKED at 7 waves
                  {"EDSBWT_DEEPQ_PACKED": "0"}, {"EDSBWT_DEEPQ_WAVES": "7"}, {"EDSBWT_DEEPQ_WAVES": "7", "EDSBWT_DEEP_STATS": "0"},
                  # k_deep_direct at 8 waves per SIMD (the default is 7), and without the return to the text compare
-                 {"EDSBWT_DIRECT_WAVES": "8"}, {"EDSBWT_DIRECT_BACK": "0", "EDSBWT_DEEP_STATS": "0"}]
+                 {"EDSBWT_DIRECT_WAVES": "8"}, {"EDSBWT_DIRECT_BACK": "0", "EDSBWT_DEEP_STATS": "0"},
+                 # k_deep's packed build without the text filter of a list start
+                 {"EDSBWT_DEEPQ_FILTER": "0"}]
 
 
 @pytest.mark.parametrize("build", K_DEEP_BUILDS, ids=lambda b: ",".join(f"{k[7:]}={v}" for k, v in b.items()))
